@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""Benchmark of the Haar LL ("icon") hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--depth D] [--images B]
+
+Workload (BASELINE.json configs[2], the roofline run, at the metric's depth 5):
+a batch of B = 128 synthetic 8K RGB images (7680x4320x3 uint8) per GPU,
+generated on device and resident in HBM before timing.  One step = one pass
+of HaarCoder.get_small_copy's work over the whole batch through the C ABI
+(``wicca_haar_ll_u8_uniform``: ONE kernel launch, no host copies).
+
+Multi-GPU (``torch.distributed.run``, one rank per GPU): images shard
+image-parallel with no data-path collective (weak scaling: B images per
+rank).  A barrier + device sync brackets the K timed steps and the maximum
+over ranks is reported.
+
+Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (HIP
+events on the launch stream) and, at N=1, the CPU baseline: the NumPy port of
+the reference (oracle/haar_numpy.py) timed on a bounded sample of the same
+workload on this host.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+BASELINE = json.load(open(os.path.join(REPO, "BASELINE.json")))
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--depth", type=int, default=5)
+    ap.add_argument("--images", type=int, default=128, help="images per GPU")
+    ap.add_argument("--height", type=int, default=4320)
+    ap.add_argument("--width", type=int, default=7680)
+    ap.add_argument("--channels", type=int, default=3)
+    ap.add_argument("--border", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="budget of the CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
+                    help="PMC summary (rocprofv3 FETCH_SIZE/WRITE_SIZE) for roofline.traffic")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, budget_s: float):
+    """NumPy port of the reference on this host (oracle/haar_numpy.py)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import haar_numpy
+    from wicca_amd.synth import synth_image
+
+    H, W, C, d = args.height, args.width, args.channels, args.depth
+    mp = H * W / 1e6
+    pool_imgs = [synth_image(1234, i, H, W, C) for i in range(4)]
+    # single thread, as ClassifierProcessor runs it in one worker
+    t0 = time.perf_counter()
+    n1 = 0
+    while True:
+        haar_numpy.get_small_copy(pool_imgs[n1 % 4], d, args.border)
+        n1 += 1
+        if time.perf_counter() - t0 > budget_s / 3 or n1 >= 64:
+            break
+    single = n1 * mp / (time.perf_counter() - t0)
+    # image-parallel thread pool on this process's CPU share
+    threads = max(1, min(16, os.cpu_count() or 1))
+    n_par = max(threads, int(single * budget_s * 0.66 * min(threads, 8) / mp / 4) // threads
+                * threads)
+    n_par = min(n_par, 4 * threads)
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda i: haar_numpy.get_small_copy(pool_imgs[i % 4], d, args.border),
+                    range(threads)))  # warm
+        t0 = time.perf_counter()
+        list(ex.map(lambda i: haar_numpy.get_small_copy(pool_imgs[i % 4], d, args.border),
+                    range(n_par)))
+        par = n_par * mp / (time.perf_counter() - t0)
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
+    return {
+        "value": round(par, 2), "unit": "MP/s", "cores": threads, "kind": "port",
+        "sample": f"{n_par} synthetic {W}x{H}x{C} images (seed 1234) at depth {d}, "
+                  f"ThreadPoolExecutor({threads}); single-thread {n1} images",
+        "single_thread_value": round(single, 2),
+        "host_cpus": os.cpu_count(), "cpu_model": model,
+    }
+
+
+def read_pmc(path: str, workload_key: str):
+    try:
+        with open(path) as f:
+            data = json.load(f)
+        return data.get(workload_key)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    torch.cuda.set_device(local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from wicca_amd import _lib
+    lib = _lib.load()
+    if _lib.device_count() < 1:
+        raise SystemExit("no HIP device visible")
+
+    B, H, W, C, D = args.images, args.height, args.width, args.channels, args.depth
+    pitch = (W * C + 15) // 16 * 16
+    r = 1 << D
+    oh, ow = -(-H // r), -(-W // r)
+    opitch = (ow * C + 15) // 16 * 16
+    src = torch.empty(B * H * pitch, dtype=torch.uint8, device="cuda")
+    dst = torch.empty(B * oh * opitch, dtype=torch.uint8, device="cuda")
+    # a dedicated (non-null) stream: the C ABI launches on it and the HIP
+    # events below are recorded on the same stream
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    assert sh.value, "expected a non-null HIP stream"
+    # device-resident synthetic batch; rank r owns images [r*B, (r+1)*B)
+    _lib.check(lib.wicca_synth_u8(ctypes.c_void_p(src.data_ptr()), B, H, W, C, pitch, H * pitch,
+                                  args.seed * 1000003 + rank, -1, sh))
+
+    def step():
+        _lib.check(lib.wicca_haar_ll_u8_uniform(
+            ctypes.c_void_p(src.data_ptr()), B, H, W, C, pitch, H * pitch, D, args.border, 0,
+            ctypes.c_void_p(dst.data_ptr()), opitch, oh * opitch, -1, sh))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    barrier()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one kernel launch per step
+
+    if dist is not None:
+        t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall, kernel_ms = float(t[0]), float(t[1])
+
+    verified = None
+    if not args.no_verify and rank == 0:
+        from oracle import haar_numpy
+        from wicca_amd.synth import synth_image
+        i = B - 1
+        img = synth_image(args.seed * 1000003 + rank, i, H, W, C)
+        ref = haar_numpy.get_small_copy(img, D, args.border)
+        got = dst.view(B, oh, opitch)[i, :, :ow * C].cpu().numpy().reshape(oh, ow, C)
+        verified = bool(np.array_equal(got, ref))
+        if not verified:
+            raise SystemExit("bench verification FAILED: icon differs from the NumPy port")
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    ms_per_step = wall / args.steps * 1e3
+    mpix = world * B * H * W / 1e6
+    value = mpix / (ms_per_step / 1e3)
+    alg_bytes = B * (H * W * C + oh * ow * C)  # per launch: u8 read once + u8 icon write
+    achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
+    workload_key = f"b{B}_{W}x{H}x{C}_d{D}"
+    pmc = read_pmc(args.pmc, workload_key)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+
+    out = {
+        "metric": BASELINE["metric"],
+        "value": round(value, 1),
+        "unit": "MP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (on-device splitmix64 images, HBM-resident before timing)",
+        "config": {
+            "workload": f"{B} x {W}x{H}x{C} uint8 images per GPU, Haar LL depth {D}, "
+                        f"{'REPLICATE' if args.border == 1 else 'CONSTANT'} border "
+                        "(BASELINE.json configs[2] at the metric's depth)",
+            "images_per_gpu": B, "height": H, "width": W, "channels": C, "depth": D,
+            "parallelism": f"image-parallel x{world} (no collectives)",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "kernel": f"haar_block_sum_kernel<L={D},C={C},u8>",
+            "kernel_ms": round(kernel_ms, 4),
+            "alg_bytes_per_launch": alg_bytes,
+            "pmc_source": os.path.relpath(args.pmc, REPO) if pmc else None,
+        },
+        "cpu_baseline": None,
+        "verified_vs_numpy_port": verified,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,155 @@
+/*
+ * wicca_haar.h — C ABI of the MI355X Haar LL ("icon") engine.
+ *
+ * This is the drop-in boundary for the one hot path of Todmount/wicca:
+ *
+ *   HaarCoder.get_small_copy(image, transform_depth,
+ *                            border_type=cv2.BORDER_REPLICATE, border_constant=0)
+ *     reference: wicca/wavelet_coder.py:50-67 (abstract form :31-38)
+ *     fused steps: validate_image      wicca/validation.py:80-101
+ *                  get_padded_copy     wicca/data_loader.py:66-117
+ *                  astype(np.float32)  wicca/wavelet_coder.py:59
+ *                  level loop          wicca/wavelet_coder.py:61-65
+ *                  clip + astype(u8)   wicca/wavelet_coder.py:67
+ *
+ * The reference is pure Python and binds no FFI of its own; the Python host
+ * layer (wicca_amd/_lib.py) binds these entry points with ctypes, exactly as
+ * INTEGRATION.md shows for a maintainer adding it to the reference.
+ *
+ * Conventions
+ *   - Images are HWC uint8, rows `row_pitch` bytes apart (pitch >= W*C).
+ *   - Output of depth D >= 1 is (ceil(H/2^D), ceil(W/2^D), C); depth <= 0
+ *     yields a copy of the input (reference behaviour).
+ *   - border_type uses OpenCV's numbering: 0 = BORDER_CONSTANT,
+ *     1 = BORDER_REPLICATE.  Any other value returns WICCA_ERR_BORDER; the
+ *     Python layer then materialises that padding on the host.
+ *   - Every entry point returns 0 on success or a negative WICCA_ERR_* code;
+ *     wicca_last_error() returns a thread-local message for the last failure.
+ *   - All entry points are re-entrant: each call leases a workspace (HIP
+ *     stream + scratch buffers) from a mutex-guarded per-device pool, the
+ *     last error is thread-local, device init is guarded by std::call_once.
+ *   - `stream` may be NULL (a per-thread stream is used and the call is
+ *     synchronous) or a hipStream_t (the call is asynchronous when both
+ *     buffers are device-resident).
+ */
+#ifndef WICCA_HAAR_H
+#define WICCA_HAAR_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes.  The first three map 1:1 onto the reference's ValueError
+ * messages (wicca/validation.py:94-99); the Python layer raises the same
+ * exception type with the same text. */
+#define WICCA_OK               0
+#define WICCA_ERR_NULL_IMAGE  -1 /* "Image didn't found. Please check your input." */
+#define WICCA_ERR_EMPTY       -2 /* "Image is empty" */
+#define WICCA_ERR_DTYPE       -3 /* "Image must be of type uint8" */
+#define WICCA_ERR_NDIM        -4 /* "Image must be 2D or 3D array" (data_loader.py:104-105) */
+#define WICCA_ERR_BORDER      -5 /* border type not implemented on device */
+#define WICCA_ERR_ARG         -6 /* invalid size / pitch / pointer combination */
+#define WICCA_ERR_HIP         -7 /* HIP runtime error (message in wicca_last_error) */
+#define WICCA_ERR_NOMEM       -8 /* device allocation failed */
+#define WICCA_ERR_NODEVICE    -9 /* no HIP device visible */
+
+/* One image of a ragged batch. */
+typedef struct wicca_image_desc {
+    const uint8_t* src;      /* HWC uint8 (host or device, see the call) */
+    uint8_t*       dst;      /* (oh, ow, C) uint8 (host or device) */
+    int64_t        height;   /* H */
+    int64_t        width;    /* W */
+    int64_t        src_pitch;/* bytes between input rows */
+    int64_t        dst_pitch;/* bytes between output rows */
+} wicca_image_desc;
+
+/* Number of visible HIP devices (0 when none). */
+int wicca_device_count(void);
+
+/* Thread-local description of the last error on this thread ("" if none). */
+const char* wicca_last_error(void);
+
+/* Library version string, e.g. "wicca_hip 0.1 gfx950". */
+const char* wicca_version(void);
+
+/* Output shape of get_small_copy for an (H, W) image at `depth`
+ * (wicca/wavelet_coder.py:58 ratio = 2**depth; data_loader.py:107-110). */
+int wicca_icon_shape(int64_t H, int64_t W, int depth, int64_t* out_h, int64_t* out_w);
+
+/*
+ * Single-image drop-in for HaarCoder.get_small_copy (wavelet_coder.py:50-67).
+ * src/dst may each be host or device memory (flags).  Host buffers are staged
+ * through per-thread device scratch; the call then synchronises.
+ */
+int wicca_haar_ll_u8(const uint8_t* src, int64_t H, int64_t W, int64_t C,
+                     int64_t src_pitch, int depth, int border_type,
+                     int border_constant, uint8_t* dst, int64_t dst_pitch,
+                     int src_is_device, int dst_is_device, int device,
+                     void* stream);
+
+/*
+ * The reference's pre-quantisation float32 LL plane (low_left after the
+ * level loop, wavelet_coder.py:61-65, before clip/astype at :67).
+ * Same arguments as wicca_haar_ll_u8, dst holds float32 (dst_pitch in bytes).
+ */
+int wicca_haar_ll_f32(const uint8_t* src, int64_t H, int64_t W, int64_t C,
+                      int64_t src_pitch, int depth, int border_type,
+                      int border_constant, float* dst, int64_t dst_pitch,
+                      int src_is_device, int dst_is_device, int device,
+                      void* stream);
+
+/*
+ * Uniform batch, device-resident: n images of identical (H, W, C), image i at
+ * src + i*src_image_stride, icon i at dst + i*dst_image_stride.  One launch.
+ * This is the batched form of the call ClassifierProcessor._get_img_batch
+ * makes per image (classifying_tools.py:297-323, call at :317).
+ */
+int wicca_haar_ll_u8_uniform(const uint8_t* src, int64_t n, int64_t H,
+                             int64_t W, int64_t C, int64_t src_pitch,
+                             int64_t src_image_stride, int depth,
+                             int border_type, int border_constant, uint8_t* dst,
+                             int64_t dst_pitch, int64_t dst_image_stride,
+                             int device, void* stream);
+
+/*
+ * Ragged batch: n images sharing C and depth, each with its own H, W and
+ * pitches (descs itself is a HOST array).  src/dst pointers are device or host
+ * memory per the flags; host images are packed into one aligned device
+ * staging buffer.  Depth 1..8 with C <= 4 runs as ONE launch.  This is the
+ * icon stage of ClassifierProcessor._get_img_batch (classifying_tools.py:
+ * 297-323) as a single call over the batch's (ragged) images.
+ */
+int wicca_haar_ll_u8_batch(const wicca_image_desc* descs, int64_t n, int64_t C,
+                           int depth, int border_type, int border_constant,
+                           int src_is_device, int dst_is_device, int device,
+                           void* stream);
+
+/*
+ * Multi-depth: the icon of every depth in depths[0..n_depths) from ONE upload
+ * of the image (the caller's depth loop,
+ * classifying_tools.py:546-551).  dsts[i] receives the icon of depths[i] with
+ * pitch dst_pitches[i].  Host or device buffers as in wicca_haar_ll_u8.
+ */
+int wicca_haar_ll_u8_multi(const uint8_t* src, int64_t H, int64_t W, int64_t C,
+                           int64_t src_pitch, const int* depths, int n_depths,
+                           int border_type, int border_constant,
+                           uint8_t* const* dsts, const int64_t* dst_pitches,
+                           int src_is_device, int dst_is_device, int device,
+                           void* stream);
+
+/*
+ * Deterministic synthetic images on device (no PCIe in timed regions):
+ * byte (i, y, x, c) = splitmix64-hash of (seed, i, y*W*C + x*C + c), see
+ * wicca_amd/synth.py for the host restatement.
+ */
+int wicca_synth_u8(uint8_t* dst, int64_t n, int64_t H, int64_t W, int64_t C,
+                   int64_t pitch, int64_t image_stride, uint64_t seed,
+                   int device, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* WICCA_HAAR_H */

@@ -1,0 +1,17 @@
+"""wicca_amd — MI355X-native Haar LL ("icon") engine for Todmount/wicca.
+
+Drop-in for the reference's one hot path, ``HaarCoder.get_small_copy``
+(``wicca/wavelet_coder.py:50-67``), computed by hand-written gfx950 HIP
+kernels behind the C ABI in ``include/wicca_haar.h``.
+
+    from wicca_amd import HaarCoder
+    coder = HaarCoder()
+    icon = coder.get_small_copy(image, transform_depth=5)
+"""
+from .coder import (BORDER_CONSTANT, BORDER_REFLECT, BORDER_REFLECT_101, BORDER_REPLICATE,
+                    BORDER_WRAP, HaarCoder, WaveletCoder)
+from .validation import validate_image
+
+__all__ = ["HaarCoder", "WaveletCoder", "validate_image", "BORDER_CONSTANT", "BORDER_REPLICATE",
+           "BORDER_REFLECT", "BORDER_WRAP", "BORDER_REFLECT_101"]
+__version__ = "0.1.0"

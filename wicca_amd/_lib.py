@@ -1,0 +1,108 @@
+"""ctypes binding of ``libwicca_hip.so`` (the C ABI in ``include/wicca_haar.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``make -C
+wicca_amd/csrc``).  There is no fallback: if the library is missing or no
+HIP device is visible, calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("WICCA_HIP_LIB", os.path.join(_HERE, "libwicca_hip.so"))
+
+WICCA_OK = 0
+WICCA_ERR_NULL_IMAGE = -1
+WICCA_ERR_EMPTY = -2
+WICCA_ERR_DTYPE = -3
+WICCA_ERR_NDIM = -4
+WICCA_ERR_BORDER = -5
+WICCA_ERR_ARG = -6
+WICCA_ERR_HIP = -7
+WICCA_ERR_NOMEM = -8
+WICCA_ERR_NODEVICE = -9
+
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_p = ctypes.c_void_p
+
+
+class ImageDesc(ctypes.Structure):
+    """``wicca_image_desc`` (include/wicca_haar.h)."""
+
+    _fields_ = [("src", _p), ("dst", _p), ("height", _i64), ("width", _i64),
+                ("src_pitch", _i64), ("dst_pitch", _i64)]
+
+
+# name -> (restype, argtypes); every symbol include/wicca_haar.h declares.
+SIGNATURES = {
+    "wicca_device_count": (_int, []),
+    "wicca_last_error": (ctypes.c_char_p, []),
+    "wicca_version": (ctypes.c_char_p, []),
+    "wicca_icon_shape": (_int, [_i64, _i64, _int, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
+    "wicca_haar_ll_u8": (_int, [_p, _i64, _i64, _i64, _i64, _int, _int, _int, _p, _i64,
+                                _int, _int, _int, _p]),
+    "wicca_haar_ll_f32": (_int, [_p, _i64, _i64, _i64, _i64, _int, _int, _int, _p, _i64,
+                                 _int, _int, _int, _p]),
+    "wicca_haar_ll_u8_uniform": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int,
+                                        _int, _p, _i64, _i64, _int, _p]),
+    "wicca_haar_ll_u8_batch": (_int, [ctypes.POINTER(ImageDesc), _i64, _i64, _int, _int, _int,
+                                      _int, _p]),
+    "wicca_haar_ll_u8_multi": (_int, [_p, _i64, _i64, _i64, _i64, ctypes.POINTER(_int), _int,
+                                      _int, _int, ctypes.POINTER(_p), ctypes.POINTER(_i64),
+                                      _int, _int, _int, _p]),
+    "wicca_synth_u8": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_uint64, _int,
+                              _p]),
+}
+
+_lock = threading.Lock()
+_lib: ctypes.CDLL | None = None
+
+
+class WiccaHipError(RuntimeError):
+    """A failure inside the HIP engine (device, allocation or launch)."""
+
+
+def load() -> ctypes.CDLL:
+    """Load the in-tree HIP library (once).  Raises if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"wicca HIP extension not built: {LIB_PATH} is missing "
+                    "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+            lib = ctypes.CDLL(LIB_PATH)  # CDLL: the GIL is released during calls
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def last_error() -> str:
+    msg = load().wicca_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int) -> None:
+    """Map a C-ABI status onto the reference's exception conventions."""
+    if rc == WICCA_OK:
+        return
+    msg = last_error()
+    if rc in (WICCA_ERR_NULL_IMAGE, WICCA_ERR_EMPTY, WICCA_ERR_DTYPE, WICCA_ERR_NDIM):
+        raise ValueError(msg)
+    if rc == WICCA_ERR_NOMEM:
+        raise MemoryError(msg)
+    if rc == WICCA_ERR_ARG:
+        raise ValueError(msg)
+    raise WiccaHipError(f"wicca_hip status {rc}: {msg}")
+
+
+def device_count() -> int:
+    return int(load().wicca_device_count())

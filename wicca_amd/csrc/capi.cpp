@@ -1,0 +1,569 @@
+// capi.cpp — C ABI of the Haar LL engine (declared in include/wicca_haar.h).
+//
+// Host side of the drop-in for HaarCoder.get_small_copy
+// (wicca/wavelet_coder.py:50-67).  Responsibilities:
+//   - argument checks mapped to the reference's error conventions
+//     (wicca/validation.py:80-101, wicca/data_loader.py:96-105),
+//   - the output-shape rule of get_padded_copy (data_loader.py:107-110),
+//   - staging of host buffers (H2D / D2H with 16-byte aligned device pitches),
+//   - the depth > 8 float32 tail (levels 9..D, reference rounding),
+//   - re-entrancy: ClassifierProcessor calls the coder from a
+//     ThreadPoolExecutor (classifying_tools.py:414-419), so every call takes a
+//     workspace (stream + scratch buffers) from a mutex-guarded pool and the
+//     last error is thread-local.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/wicca_haar.h"
+#include "haar_ll.h"
+
+namespace {
+
+thread_local std::string t_last_error;
+
+int fail(int code, const char* fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    t_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return fail(e_ == hipErrorOutOfMemory ? WICCA_ERR_NOMEM : WICCA_ERR_HIP,     \
+                        "HIP error %d (%s) in %s", (int)e_, hipGetErrorString(e_), #expr); \
+    } while (0)
+
+std::once_flag g_init_once;
+int g_device_count = 0;
+
+void init_once()
+{
+    std::call_once(g_init_once, [] {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        g_device_count = n;
+    });
+}
+
+// Growable device buffer.
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t n)
+    {
+        if (n <= cap) return hipSuccess;
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+        size_t want = std::max<size_t>(n, 1 << 20);
+        hipError_t e = hipMalloc(&ptr, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+};
+
+// One call's worth of resources; pooled per device, never shared concurrently.
+struct Workspace {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevBuf in, out, t0, t1, t2, meta;
+};
+
+std::mutex g_pool_mu;
+std::vector<std::unique_ptr<Workspace>> g_pool;  // idle workspaces
+
+struct WorkspaceLease {
+    Workspace* ws = nullptr;
+    ~WorkspaceLease()
+    {
+        if (!ws) return;
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        g_pool.emplace_back(ws);
+    }
+};
+
+int acquire(int device, WorkspaceLease& lease)
+{
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size(); ++i) {
+            if (g_pool[i]->device == device) {
+                lease.ws = g_pool[i].release();
+                g_pool.erase(g_pool.begin() + i);
+                return WICCA_OK;
+            }
+        }
+    }
+    auto* ws = new Workspace();
+    ws->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&ws->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ws;
+        return fail(WICCA_ERR_HIP, "hipStreamCreate failed: %s", hipGetErrorString(e));
+    }
+    lease.ws = ws;
+    return WICCA_OK;
+}
+
+int select_device(int device, int* out)
+{
+    init_once();
+    if (g_device_count <= 0) return fail(WICCA_ERR_NODEVICE, "no HIP device visible");
+    if (device < 0) {
+        int cur = 0;
+        HIP_TRY(hipGetDevice(&cur));
+        device = cur;
+    }
+    if (device >= g_device_count)
+        return fail(WICCA_ERR_ARG, "device %d out of range (%d visible)", device, g_device_count);
+    HIP_TRY(hipSetDevice(device));
+    *out = device;
+    return WICCA_OK;
+}
+
+inline int64_t round_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+void icon_dims(int64_t H, int64_t W, int depth, int64_t* oh, int64_t* ow)
+{
+    if (depth <= 0) {  // ratio 2**depth <= 1: no padding, loop runs zero times
+        *oh = H;
+        *ow = W;
+        return;
+    }
+    const int64_t r = (int64_t)1 << depth;
+    *oh = (H + r - 1) / r;
+    *ow = (W + r - 1) / r;
+}
+
+uint32_t saturate_k(int k) { return (uint32_t)std::min(255, std::max(0, k)); }
+
+int check_image(const void* src, int64_t H, int64_t W, int64_t C, int64_t pitch, int depth,
+                int border_type)
+{
+    if (!src) return fail(WICCA_ERR_NULL_IMAGE, "Image didn't found. Please check your input.");
+    if (H <= 0 || W <= 0 || C <= 0) return fail(WICCA_ERR_EMPTY, "Image is empty");
+    if (pitch < W * C) return fail(WICCA_ERR_ARG, "row pitch %lld < W*C %lld", (long long)pitch,
+                                   (long long)(W * C));
+    if (border_type != 0 && border_type != 1)
+        return fail(WICCA_ERR_BORDER, "border type %d is not implemented on device", border_type);
+    if (depth > 30) return fail(WICCA_ERR_ARG, "depth %d too large", depth);
+    return WICCA_OK;
+}
+
+// Device-resident uniform batch: n images -> n icons (OutT = uint8_t or float).
+template <typename OutT>
+int run_ll(const uint8_t* src, int64_t n, int64_t H, int64_t W, int64_t C, int64_t src_pitch,
+           int64_t src_stride, int depth, int border, int k, void* dst, int64_t dst_pitch,
+           int64_t dst_stride, Workspace* ws, hipStream_t stream, bool* used_scratch)
+{
+    wicca::LLParams p{};
+    p.src = src;
+    p.src_pitch = src_pitch;
+    p.src_image_stride = src_stride;
+    p.H = H;
+    p.W = W;
+    p.n_images = n;
+    p.border = border;
+    p.k = saturate_k(k);
+    if (depth <= 0) {
+        if constexpr (sizeof(OutT) == 1) {
+            for (int64_t i = 0; i < n; ++i)
+                HIP_TRY(hipMemcpy2DAsync((uint8_t*)dst + i * dst_stride, dst_pitch,
+                                         src + i * src_stride, src_pitch, W * C, H,
+                                         hipMemcpyDeviceToDevice, stream));
+            return WICCA_OK;
+        }
+        p.dst = (uint8_t*)dst;
+        p.dst_pitch = dst_pitch;
+        p.dst_image_stride = dst_stride;
+        p.out_h = H;
+        p.out_w = W;
+        HIP_TRY(wicca::launch_block_sum<OutT>(p, 0, (int)C, stream));
+        return WICCA_OK;
+    }
+    if (depth <= 8) {
+        int64_t oh, ow;
+        icon_dims(H, W, depth, &oh, &ow);
+        p.dst = (uint8_t*)dst;
+        p.dst_pitch = dst_pitch;
+        p.dst_image_stride = dst_stride;
+        p.out_h = oh;
+        p.out_w = ow;
+        HIP_TRY(wicca::launch_block_sum<OutT>(p, depth, (int)C, stream));
+        return WICCA_OK;
+    }
+    // depth > 8: exact level-8 sums over the 2^depth-padded image, then
+    // float32 levels 9..depth in the reference's order.
+    *used_scratch = true;
+    const int64_t r = (int64_t)1 << depth;
+    const int64_t Hp = (H + r - 1) / r * r, Wp = (W + r - 1) / r * r;
+    int64_t h = Hp >> 8, w = Wp >> 8;
+    const int64_t plane8 = h * w * C * 4;
+    if (plane8 * n > ((int64_t)8 << 30))
+        return fail(WICCA_ERR_NOMEM, "depth %d needs a %lld-byte intermediate plane", depth,
+                    (long long)(plane8 * n));
+    HIP_TRY(ws->t0.reserve((size_t)(plane8 * n)));
+    HIP_TRY(ws->t1.reserve((size_t)(plane8 * n / 4 + 16)));
+    HIP_TRY(ws->t2.reserve((size_t)(plane8 * n / 16 + 16)));
+    p.dst = (uint8_t*)ws->t0.ptr;
+    p.dst_pitch = w * C * 4;
+    p.dst_image_stride = plane8;
+    p.out_h = h;
+    p.out_w = w;
+    HIP_TRY(wicca::launch_block_sum<uint32_t>(p, 8, (int)C, stream));
+    const void* cur = ws->t0.ptr;
+    bool cur_is_sum = true;
+    DevBuf* ping[2] = {&ws->t1, &ws->t2};
+    for (int lvl = 9; lvl <= depth; ++lvl) {
+        const int64_t nh = h / 2, nw = w / 2;
+        const bool last = lvl == depth;
+        void* out;
+        int64_t opitch, ostride;
+        if (last) {
+            out = dst;
+            opitch = dst_pitch;
+            ostride = dst_stride;
+        } else {
+            out = ping[lvl & 1]->ptr;
+            opitch = nw * C * 4;
+            ostride = nh * nw * C * 4;
+        }
+        HIP_TRY(wicca::launch_level_f32(cur, w * C * 4, h * w * C * 4, cur_is_sum, out, opitch,
+                                        ostride, last && sizeof(OutT) == 1, n, nh, nw, (int)C,
+                                        stream));
+        cur = out;
+        cur_is_sum = false;
+        h = nh;
+        w = nw;
+    }
+    return WICCA_OK;
+}
+
+// Shared body of the single-image entry points.
+template <typename OutT>
+int single_image(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t src_pitch, int depth,
+                 int border_type, int border_constant, void* dst, int64_t dst_pitch,
+                 int src_is_device, int dst_is_device, int device, void* stream_in)
+{
+    int rc = check_image(src, H, W, C, src_pitch, depth, border_type);
+    if (rc) return rc;
+    if (!dst) return fail(WICCA_ERR_ARG, "dst is NULL");
+    int64_t oh, ow;
+    icon_dims(H, W, depth, &oh, &ow);
+    const int64_t out_row = ow * C * (int64_t)sizeof(OutT);
+    if (dst_pitch < out_row) return fail(WICCA_ERR_ARG, "dst pitch too small");
+    int dev;
+    if ((rc = select_device(device, &dev))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    Workspace* ws = lease.ws;
+    hipStream_t stream = stream_in ? (hipStream_t)stream_in : ws->stream;
+
+    const uint8_t* dsrc = src;
+    int64_t dpitch_in = src_pitch;
+    if (!src_is_device) {
+        dpitch_in = round_up(W * C, 64);
+        HIP_TRY(ws->in.reserve((size_t)(dpitch_in * H)));
+        HIP_TRY(hipMemcpy2DAsync(ws->in.ptr, dpitch_in, src, src_pitch, W * C, H,
+                                 hipMemcpyHostToDevice, stream));
+        dsrc = (const uint8_t*)ws->in.ptr;
+    }
+    void* ddst = dst;
+    int64_t dpitch_out = dst_pitch;
+    if (!dst_is_device) {
+        dpitch_out = round_up(out_row, 16);
+        HIP_TRY(ws->out.reserve((size_t)(dpitch_out * oh)));
+        ddst = ws->out.ptr;
+    }
+    bool used_scratch = false;
+    rc = run_ll<OutT>(dsrc, 1, H, W, C, dpitch_in, 0, depth, border_type, border_constant, ddst,
+                      dpitch_out, 0, ws, stream, &used_scratch);
+    if (rc) return rc;
+    if (!dst_is_device)
+        HIP_TRY(hipMemcpy2DAsync(dst, dst_pitch, ddst, dpitch_out, out_row, oh,
+                                 hipMemcpyDeviceToHost, stream));
+    if (!stream_in || !src_is_device || !dst_is_device || used_scratch)
+        HIP_TRY(hipStreamSynchronize(stream));
+    return WICCA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wicca_device_count(void)
+{
+    init_once();
+    return g_device_count;
+}
+
+const char* wicca_last_error(void) { return t_last_error.c_str(); }
+
+const char* wicca_version(void) { return "wicca_hip 0.1 gfx950"; }
+
+int wicca_icon_shape(int64_t H, int64_t W, int depth, int64_t* out_h, int64_t* out_w)
+{
+    if (!out_h || !out_w) return fail(WICCA_ERR_ARG, "null output pointer");
+    if (H <= 0 || W <= 0) return fail(WICCA_ERR_EMPTY, "Image is empty");
+    if (depth > 62) return fail(WICCA_ERR_ARG, "depth %d too large", depth);
+    icon_dims(H, W, depth, out_h, out_w);
+    return WICCA_OK;
+}
+
+int wicca_haar_ll_u8(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t src_pitch,
+                     int depth, int border_type, int border_constant, uint8_t* dst,
+                     int64_t dst_pitch, int src_is_device, int dst_is_device, int device,
+                     void* stream)
+{
+    return single_image<uint8_t>(src, H, W, C, src_pitch, depth, border_type, border_constant, dst,
+                                 dst_pitch, src_is_device, dst_is_device, device, stream);
+}
+
+int wicca_haar_ll_f32(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t src_pitch,
+                      int depth, int border_type, int border_constant, float* dst,
+                      int64_t dst_pitch, int src_is_device, int dst_is_device, int device,
+                      void* stream)
+{
+    return single_image<float>(src, H, W, C, src_pitch, depth, border_type, border_constant, dst,
+                               dst_pitch, src_is_device, dst_is_device, device, stream);
+}
+
+int wicca_haar_ll_u8_uniform(const uint8_t* src, int64_t n, int64_t H, int64_t W, int64_t C,
+                             int64_t src_pitch, int64_t src_image_stride, int depth,
+                             int border_type, int border_constant, uint8_t* dst, int64_t dst_pitch,
+                             int64_t dst_image_stride, int device, void* stream_in)
+{
+    if (n < 0) return fail(WICCA_ERR_ARG, "negative batch size");
+    if (n == 0) return WICCA_OK;
+    int rc = check_image(src, H, W, C, src_pitch, depth, border_type);
+    if (rc) return rc;
+    if (!dst) return fail(WICCA_ERR_ARG, "dst is NULL");
+    int64_t oh, ow;
+    icon_dims(H, W, depth, &oh, &ow);
+    if (dst_pitch < ow * C || (n > 1 && dst_image_stride < dst_pitch * oh) ||
+        (n > 1 && src_image_stride < src_pitch * H))
+        return fail(WICCA_ERR_ARG, "pitch/stride too small");
+    int dev;
+    if ((rc = select_device(device, &dev))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    hipStream_t stream = stream_in ? (hipStream_t)stream_in : lease.ws->stream;
+    bool used_scratch = false;
+    rc = run_ll<uint8_t>(src, n, H, W, C, src_pitch, src_image_stride, depth, border_type,
+                         border_constant, dst, dst_pitch, dst_image_stride, lease.ws, stream,
+                         &used_scratch);
+    if (rc) return rc;
+    if (!stream_in || used_scratch) HIP_TRY(hipStreamSynchronize(stream));
+    return WICCA_OK;
+}
+
+int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t C, int depth,
+                           int border_type, int border_constant, int src_is_device,
+                           int dst_is_device, int device, void* stream_in)
+{
+    if (n < 0 || (n > 0 && !descs_in)) return fail(WICCA_ERR_ARG, "bad descriptor array");
+    if (n == 0) return WICCA_OK;
+    if (C <= 0) return fail(WICCA_ERR_EMPTY, "Image is empty");
+    for (int64_t i = 0; i < n; ++i) {
+        int rc = check_image(descs_in[i].src, descs_in[i].height, descs_in[i].width, C,
+                             descs_in[i].src_pitch, depth, border_type);
+        if (rc) return rc;
+        if (!descs_in[i].dst) return fail(WICCA_ERR_ARG, "dst of image %lld is NULL", (long long)i);
+        int64_t oh, ow;
+        icon_dims(descs_in[i].height, descs_in[i].width, depth, &oh, &ow);
+        if (descs_in[i].dst_pitch < ow * C)
+            return fail(WICCA_ERR_ARG, "dst pitch of image %lld too small", (long long)i);
+    }
+    int dev, rc;
+    if ((rc = select_device(device, &dev))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    Workspace* ws = lease.ws;
+    hipStream_t stream = stream_in ? (hipStream_t)stream_in : ws->stream;
+
+    // Device-side view of every image: host images are packed into ws->in,
+    // host icons are produced in ws->out, all with 64/16-byte aligned pitches.
+    std::vector<wicca_image_desc> d(descs_in, descs_in + n);
+    std::vector<int64_t> oh((size_t)n), ow((size_t)n);
+    int64_t in_bytes = 0, out_bytes = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        icon_dims(d[i].height, d[i].width, depth, &oh[i], &ow[i]);
+        if (!src_is_device) in_bytes += round_up(d[i].width * C, 64) * d[i].height;
+        if (!dst_is_device) out_bytes += round_up(ow[i] * C, 16) * oh[i];
+    }
+    if (!src_is_device) {
+        HIP_TRY(ws->in.reserve((size_t)in_bytes));
+        int64_t off = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t pitch = round_up(d[i].width * C, 64);
+            uint8_t* p = (uint8_t*)ws->in.ptr + off;
+            HIP_TRY(hipMemcpy2DAsync(p, pitch, descs_in[i].src, descs_in[i].src_pitch,
+                                     d[i].width * C, d[i].height, hipMemcpyHostToDevice, stream));
+            d[i].src = p;
+            d[i].src_pitch = pitch;
+            off += pitch * d[i].height;
+        }
+    }
+    if (!dst_is_device) {
+        HIP_TRY(ws->out.reserve((size_t)out_bytes));
+        int64_t off = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t pitch = round_up(ow[i] * C, 16);
+            d[i].dst = (uint8_t*)ws->out.ptr + off;
+            d[i].dst_pitch = pitch;
+            off += pitch * oh[i];
+        }
+    }
+
+    bool one_launch = depth >= 1 && depth <= 8 && C <= 4;
+    for (int64_t i = 0; i < n && one_launch; ++i) {
+        one_launch = ((uintptr_t)d[i].src % 16 == 0) && d[i].src_pitch % 16 == 0 &&
+                     ((uintptr_t)d[i].dst % 16 == 0) && d[i].dst_pitch % 16 == 0 &&
+                     d[i].width * C < ((int64_t)1 << 30);
+    }
+    if (!one_launch) {  // per-image launches (generic kernel, copies, depth > 8 tail)
+        for (int64_t i = 0; i < n; ++i) {
+            bool used_scratch = false;
+            rc = run_ll<uint8_t>(d[i].src, 1, d[i].height, d[i].width, C, d[i].src_pitch, 0, depth,
+                                 border_type, border_constant, d[i].dst, d[i].dst_pitch, 0, ws,
+                                 stream, &used_scratch);
+            if (rc) return rc;
+            if (used_scratch) HIP_TRY(hipStreamSynchronize(stream));
+        }
+    } else {
+        std::vector<wicca::ImageDescDev> dd((size_t)n);
+        std::vector<int64_t> starts((size_t)n);
+        int64_t total = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            auto& e = dd[(size_t)i];
+            e.src = d[i].src;
+            e.dst = d[i].dst;
+            e.H = d[i].height;
+            e.W = d[i].width;
+            e.src_pitch = d[i].src_pitch;
+            e.dst_pitch = d[i].dst_pitch;
+            e.out_h = oh[i];
+            e.out_w = ow[i];
+            e.n_seg = (int32_t)wicca::segments_for(e.out_w, depth);
+            e.pad_ = 0;
+            starts[(size_t)i] = total;
+            total += e.out_h * e.n_seg;
+        }
+        if (total >= ((int64_t)1 << 32))
+            return fail(WICCA_ERR_ARG, "batch too large for one launch");
+        const size_t bytes_d = sizeof(wicca::ImageDescDev) * (size_t)n;
+        const size_t off_s = (size_t)round_up((int64_t)bytes_d, 16);
+        HIP_TRY(ws->meta.reserve(off_s + sizeof(int64_t) * (size_t)n));
+        uint8_t* meta = (uint8_t*)ws->meta.ptr;
+        HIP_TRY(hipMemcpyAsync(meta, dd.data(), bytes_d, hipMemcpyHostToDevice, stream));
+        HIP_TRY(hipMemcpyAsync(meta + off_s, starts.data(), sizeof(int64_t) * (size_t)n,
+                               hipMemcpyHostToDevice, stream));
+        wicca::LLParams p{};
+        p.n_images = n;
+        p.border = border_type;
+        p.k = saturate_k(border_constant);
+        p.dst = d[0].dst;  // alignment probe only; every descriptor is aligned
+        p.descs = (const wicca::ImageDescDev*)meta;
+        p.block_start = (const int64_t*)(meta + off_s);
+        p.total_blocks = total;
+        HIP_TRY(wicca::launch_block_sum<uint8_t>(p, depth, (int)C, stream));
+    }
+    if (!dst_is_device) {
+        for (int64_t i = 0; i < n; ++i)
+            HIP_TRY(hipMemcpy2DAsync(descs_in[i].dst, descs_in[i].dst_pitch, d[i].dst,
+                                     d[i].dst_pitch, ow[i] * C, oh[i], hipMemcpyDeviceToHost,
+                                     stream));
+    }
+    // descriptors and staging live in the workspace: finish before it returns
+    HIP_TRY(hipStreamSynchronize(stream));
+    return WICCA_OK;
+}
+
+int wicca_haar_ll_u8_multi(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t src_pitch,
+                           const int* depths, int n_depths, int border_type, int border_constant,
+                           uint8_t* const* dsts, const int64_t* dst_pitches, int src_is_device,
+                           int dst_is_device, int device, void* stream_in)
+{
+    int rc = check_image(src, H, W, C, src_pitch, 0, border_type);
+    if (rc) return rc;
+    if (n_depths < 0 || (n_depths > 0 && (!depths || !dsts || !dst_pitches)))
+        return fail(WICCA_ERR_ARG, "bad depth list");
+    if (n_depths == 0) return WICCA_OK;
+    int dev;
+    if ((rc = select_device(device, &dev))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    Workspace* ws = lease.ws;
+    hipStream_t stream = stream_in ? (hipStream_t)stream_in : ws->stream;
+    const uint8_t* dsrc = src;
+    int64_t dpitch_in = src_pitch;
+    if (!src_is_device) {  // one upload shared by every depth
+        dpitch_in = round_up(W * C, 64);
+        HIP_TRY(ws->in.reserve((size_t)(dpitch_in * H)));
+        HIP_TRY(hipMemcpy2DAsync(ws->in.ptr, dpitch_in, src, src_pitch, W * C, H,
+                                 hipMemcpyHostToDevice, stream));
+        dsrc = (const uint8_t*)ws->in.ptr;
+    }
+    for (int i = 0; i < n_depths; ++i) {
+        if (depths[i] > 30) return fail(WICCA_ERR_ARG, "depth %d too large", depths[i]);
+        if (!dsts[i]) return fail(WICCA_ERR_ARG, "dst %d is NULL", i);
+        int64_t oh, ow;
+        icon_dims(H, W, depths[i], &oh, &ow);
+        if (dst_pitches[i] < ow * C) return fail(WICCA_ERR_ARG, "dst pitch %d too small", i);
+        void* ddst = dsts[i];
+        int64_t dpo = dst_pitches[i];
+        if (!dst_is_device) {
+            dpo = round_up(ow * C, 16);
+            HIP_TRY(ws->out.reserve((size_t)(dpo * oh)));
+            ddst = ws->out.ptr;
+        }
+        bool used_scratch = false;
+        rc = run_ll<uint8_t>(dsrc, 1, H, W, C, dpitch_in, 0, depths[i], border_type,
+                             border_constant, ddst, dpo, 0, ws, stream, &used_scratch);
+        if (rc) return rc;
+        if (!dst_is_device) {
+            HIP_TRY(hipMemcpy2DAsync(dsts[i], dst_pitches[i], ddst, dpo, ow * C, oh,
+                                     hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipStreamSynchronize(stream));  // ws->out is reused by the next depth
+        } else if (used_scratch) {
+            HIP_TRY(hipStreamSynchronize(stream));
+        }
+    }
+    if (!stream_in || !src_is_device) HIP_TRY(hipStreamSynchronize(stream));
+    return WICCA_OK;
+}
+
+int wicca_synth_u8(uint8_t* dst, int64_t n, int64_t H, int64_t W, int64_t C, int64_t pitch,
+                   int64_t image_stride, uint64_t seed, int device, void* stream_in)
+{
+    if (!dst) return fail(WICCA_ERR_ARG, "dst is NULL");
+    if (n < 0 || H < 0 || W < 0 || C < 0) return fail(WICCA_ERR_ARG, "negative size");
+    if (pitch < W * C || pitch % 16 || (uintptr_t)dst % 16 ||
+        (n > 1 && (image_stride < pitch * H || image_stride % 16)))
+        return fail(WICCA_ERR_ARG, "synth needs 16-byte aligned rows and images");
+    int dev, rc;
+    if ((rc = select_device(device, &dev))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    hipStream_t stream = stream_in ? (hipStream_t)stream_in : lease.ws->stream;
+    HIP_TRY(wicca::launch_synth(dst, n, H, W * C, pitch, image_stride, seed, 0, stream));
+    if (!stream_in) HIP_TRY(hipStreamSynchronize(stream));
+    return WICCA_OK;
+}
+
+}  // extern "C"
