@@ -55,3 +55,16 @@ def test_null_image_maps_to_reference_message():
     assert rc == _lib.WICCA_ERR_NULL_IMAGE
     with pytest.raises(ValueError, match="Image didn't found"):
         _lib.check(rc)
+
+
+def test_single_hip_runtime_per_process():
+    """Our library and torch must share one libamdhip64 (see _lib._preload_hip_runtime)."""
+    _lib.load()
+    maps = open("/proc/self/maps").read()
+    runtimes = {ln.split()[-1] for ln in maps.splitlines() if "libamdhip64" in ln}
+    assert len(runtimes) == 1, runtimes
+    pytest.importorskip("torch")
+    import torch  # noqa: F401
+    maps = open("/proc/self/maps").read()
+    runtimes = {ln.split()[-1] for ln in maps.splitlines() if "libamdhip64" in ln}
+    assert len(runtimes) == 1, runtimes

@@ -65,13 +65,40 @@ class WiccaHipError(RuntimeError):
     """A failure inside the HIP engine (device, allocation or launch)."""
 
 
+def _preload_hip_runtime() -> str | None:
+    """Make this process use ONE HIP runtime.
+
+    PyTorch-ROCm wheels bundle their own ``libamdhip64.so`` (soname
+    ``libamdhip64.so.7``, like ``/opt/rocm/lib``'s).  If our library pulled in
+    ``/opt/rocm``'s copy first, a later ``import torch`` would load a second
+    runtime and find no GPU.  Loading torch's copy by path first (without
+    importing torch) makes our ``NEEDED libamdhip64.so.7`` resolve to it, and
+    torch later reuses the same file.  ``WICCA_HIP_RUNTIME`` overrides the path.
+    """
+    path = os.environ.get("WICCA_HIP_RUNTIME")
+    if not path:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+        if spec is None or not spec.origin:
+            return None
+        path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(path):
+        ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        return path
+    return None
+
+
+RUNTIME_PATH: str | None = None
+
+
 def load() -> ctypes.CDLL:
     """Load the in-tree HIP library (once).  Raises if it was not built."""
-    global _lib
+    global _lib, RUNTIME_PATH
     if _lib is not None:
         return _lib
     with _lock:
         if _lib is None:
+            RUNTIME_PATH = _preload_hip_runtime()
             if not os.path.exists(LIB_PATH):
                 raise ImportError(
                     f"wicca HIP extension not built: {LIB_PATH} is missing "
