@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""In-process A/B of libwicca_hip.so variants (interleaved rounds, same data, one device).
+
+    python tools/ab.py --libs tools/variants/lib_a.so tools/variants/lib_b.so \
+        --depths 1 3 5 --rounds 5
+
+Every variant is loaded with its own ctypes handle (RTLD_LOCAL), so each keeps
+its own kernels; all share one HIP runtime and one synthetic batch.  Reports the
+median and min over rounds of achieved GB/s (algorithmic bytes / kernel time).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", nargs="+", required=True)
+    ap.add_argument("--depths", nargs="+", type=int, default=[5])
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--images", type=int, default=128)
+    ap.add_argument("--height", type=int, default=4320)
+    ap.add_argument("--width", type=int, default=7680)
+    ap.add_argument("--channels", type=int, default=3)
+    ap.add_argument("--border", type=int, default=1)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    import torch
+    from wicca_amd import _lib as L
+    L.load()  # preload the shared runtime + bind the default library
+    libs = {}
+    for path in args.libs:
+        h = ctypes.CDLL(os.path.abspath(path))
+        for name, (res, argt) in L.SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.restype, fn.argtypes = res, argt
+        libs[os.path.basename(path)] = h
+
+    B, H, W, C = args.images, args.height, args.width, args.channels
+    pitch = (W * C + 15) // 16 * 16
+    src = torch.empty(B * H * pitch, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    first = next(iter(libs.values()))
+    assert first.wicca_synth_u8(ctypes.c_void_p(src.data_ptr()), B, H, W, C, pitch, H * pitch,
+                                0, -1, sh) == 0
+    results = []
+    for D in args.depths:
+        r = 1 << D
+        oh, ow = -(-H // r), -(-W // r)
+        opitch = (ow * C + 15) // 16 * 16
+        dst = torch.empty(B * oh * opitch, dtype=torch.uint8, device="cuda")
+        alg = B * (H * W * C + oh * ow * C)
+        ref = None
+        samples = {k: [] for k in libs}
+        for rnd in range(args.rounds):
+            for name, h in libs.items():
+                def step():
+                    rc = h.wicca_haar_ll_u8_uniform(
+                        ctypes.c_void_p(src.data_ptr()), B, H, W, C, pitch, H * pitch, D,
+                        args.border, 0, ctypes.c_void_p(dst.data_ptr()), opitch, oh * opitch,
+                        -1, sh)
+                    assert rc == 0, rc
+                for _ in range(2):
+                    step()
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(args.steps):
+                    step()
+                e1.record(stream)
+                e1.synchronize()
+                ms = e0.elapsed_time(e1) / args.steps
+                samples[name].append(alg / (ms / 1e3) / 1e9)
+                if rnd == 0:  # every variant must produce identical icons
+                    got = dst.clone()
+                    if ref is None:
+                        ref = got
+                    elif not torch.equal(ref, got):
+                        raise SystemExit(f"{name}: icons differ from {next(iter(libs))} at D={D}")
+        for name, v in samples.items():
+            row = {"lib": name, "depth": D, "median_gbs": round(statistics.median(v), 1),
+                   "min_gbs": round(min(v), 1), "max_gbs": round(max(v), 1), "rounds": len(v)}
+            results.append(row)
+            print(json.dumps(row), flush=True)
+        del dst
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(results, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

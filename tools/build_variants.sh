@@ -1,0 +1,22 @@
+#!/bin/bash
+# Build tuning variants of libwicca_hip.so into tools/variants/ (run here, not on the box).
+set -euo pipefail
+R=$(cd "$(dirname "$0")/.." && pwd)
+V=$R/tools/variants
+mkdir -p "$V"
+build() {  # name, extra flags
+  local name=$1; shift
+  local B=$V/build_$name
+  mkdir -p "$B"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off "$@" -c "$R/wicca_amd/csrc/haar_ll.hip" -o "$B/haar_ll.o"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off "$@" -x hip -c "$R/wicca_amd/csrc/capi.cpp" -o "$B/capi.o"
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/lib_$name.so" "$B/haar_ll.o" "$B/capi.o"
+  rm -rf "$B"
+}
+for spec in "$@"; do
+  name=${spec%%:*}; flags=${spec#*:}
+  [ "$name" = "$spec" ] && flags=""
+  build "$name" $flags &
+done
+wait
+ls -la "$V"

@@ -1,0 +1,129 @@
+// hbm_probe.hip — what read bandwidth can a streaming kernel reach on this MI355X?
+// Variants: grid-stride dwordx4 read-reduce with U loads in flight, plain vs
+// nontemporal loads, and a float4 copy for comparison with the guide's 6.29 TB/s.
+// Build: hipcc --offload-arch=gfx950 -O3 tools/hbm_probe.hip -o tools/hbm_probe
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s @%d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void read_reduce(const u32x4* __restrict__ p, size_t n, unsigned* out)
+{
+    u32x4 acc = {0, 0, 0, 0};
+    size_t stride = (size_t)gridDim.x * 256 * U;
+    for (size_t i = (size_t)blockIdx.x * 256 * U + threadIdx.x; i < n; i += stride) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            size_t j = i + (size_t)u * 256;
+            if (j < n) v[u] = NT ? __builtin_nontemporal_load(p + j) : p[j]; else v[u] = acc;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += v[u];
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[0] = 1;
+}
+
+// contiguous chunk per block (like the icon kernel's bands)
+template <int U>
+__global__ __launch_bounds__(256) void read_chunks(const u32x4* __restrict__ p, size_t per_block, unsigned* out)
+{
+    u32x4 acc = {0, 0, 0, 0};
+    const u32x4* b = p + (size_t)blockIdx.x * per_block;
+    for (size_t i = threadIdx.x; i < per_block; i += 256 * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = b[i + (size_t)u * 256];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += v[u];
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[0] = 1;
+}
+
+// the icon kernel's pattern: block = (image, 32-row band, 4096-px segment) of
+// 8K RGB rows (23,040 B pitch), 3 x dwordx4 per lane per row, buffer loads
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void read_bands(const unsigned char* __restrict__ p, int rows_per_band, unsigned* out)
+{
+    const int n_seg = 2, bands = 4320 / rows_per_band;
+    const int seg = blockIdx.x % n_seg, t = blockIdx.x / n_seg;
+    const int band = t % bands, img = t / bands;
+    const unsigned char* base = p + (size_t)img * 4320 * 23040 + (size_t)band * rows_per_band * 23040;
+    u32x4 acc = {0, 0, 0, 0};
+    unsigned off[3];
+    for (int k = 0; k < 3; ++k) off[k] = seg * 12288 + k * 4096 + 16 * threadIdx.x;
+    for (int r = 0; r < rows_per_band; r += U) {
+        u32x4 v[U][3];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(base + (size_t)(r + u) * 23040), (short)0, 23040, 0x00020000);
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                v[u][k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off[k], 0, NT ? 2 : 0));
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < 3; ++k) acc += v[u][k];
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[0] = 1;
+}
+
+__global__ __launch_bounds__(256) void copy4(const u32x4* __restrict__ a, u32x4* __restrict__ b, size_t n)
+{
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) b[i] = a[i];
+}
+
+template <typename F>
+float timeit(F f, int reps)
+{
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+    f(); CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i) f();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+int main()
+{
+    const size_t bytes = 12752640000ull;  // the bench batch: 128 x 8K RGB
+    const size_t n = bytes / 16;
+    u32x4* p; unsigned* out; u32x4* q;
+    CK(hipMalloc(&p, bytes)); CK(hipMalloc(&out, 64));
+    CK(hipMemset(p, 1, bytes));
+    const int reps = 10;
+    for (int blocks : {1024, 2048, 4096, 8192, 16384}) {
+#define RR(U, NT) { float ms = timeit([&] { hipLaunchKernelGGL((read_reduce<U, NT>), dim3(blocks), dim3(256), 0, 0, p, n, out); }, reps); \
+        printf("read_reduce U=%d nt=%d blocks=%6d  %.3f ms  %.1f GB/s\n", U, (int)NT, blocks, ms, bytes / ms / 1e6); }
+        RR(1, false) RR(2, false) RR(4, false) RR(8, false) RR(4, true) RR(8, true)
+    }
+    for (size_t per_block_bytes : {(size_t)393216, (size_t)786432, (size_t)3145728}) {
+        size_t pb = per_block_bytes / 16;
+        int blocks = (int)(n / pb);
+#define RC(U) { float ms = timeit([&] { hipLaunchKernelGGL((read_chunks<U>), dim3(blocks), dim3(256), 0, 0, p, pb, out); }, reps); \
+        printf("read_chunks U=%d chunk=%zu blocks=%d  %.3f ms  %.1f GB/s\n", U, per_block_bytes, blocks, ms, (double)blocks * per_block_bytes / ms / 1e6); }
+        RC(4) RC(8) RC(12)
+    }
+    for (int rpb : {2, 8, 32, 64}) {
+        int blocks = 128 * (4320 / rpb) * 2;
+#define RB(U, NT) if (U <= rpb) { float ms = timeit([&] { hipLaunchKernelGGL((read_bands<U, NT>), dim3(blocks), dim3(256), 0, 0, (const unsigned char*)p, rpb, out); }, reps); \
+        printf("read_bands rows=%d U=%d nt=%d blocks=%d  %.3f ms  %.1f GB/s\n", rpb, U, (int)NT, blocks, ms, (double)bytes / ms / 1e6); }
+        RB(2, true) RB(4, true) RB(8, true) RB(4, false) RB(8, false)
+    }
+    CK(hipFree(p));
+    const size_t cb = 4ull << 30;
+    CK(hipMalloc(&p, cb)); CK(hipMalloc(&q, cb)); CK(hipMemset(p, 1, cb));
+    for (int blocks : {2048, 8192, 32768}) {
+        float ms = timeit([&] { hipLaunchKernelGGL(copy4, dim3(blocks), dim3(256), 0, 0, p, q, cb / 16); }, reps);
+        printf("copy4 blocks=%d  %.3f ms  %.1f GB/s (read+write)\n", blocks, ms, 2.0 * cb / ms / 1e6);
+    }
+    return 0;
+}

@@ -459,7 +459,7 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
             e.dst_pitch = d[i].dst_pitch;
             e.out_h = oh[i];
             e.out_w = ow[i];
-            e.n_seg = (int32_t)wicca::segments_for(e.out_w, depth);
+            e.n_seg = (int32_t)wicca::segments_for(e.out_w, depth, (int)C);
             e.pad_ = 0;
             starts[(size_t)i] = total;
             total += e.out_h * e.n_seg;

@@ -4,7 +4,44 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Tuning knobs (defaults are the measured best; tools/build_variants.sh overrides).
+#ifndef WICCA_NT_LOADS
+#define WICCA_NT_LOADS 1      // non-temporal loads for the once-read image stream
+#endif
+#ifndef WICCA_BUFFER_LOADS
+#define WICCA_BUFFER_LOADS 1  // buffer_load with a per-row descriptor
+#endif
+#ifndef WICCA_CHUNK_ROWS
+#define WICCA_CHUNK_ROWS 0    // rows per load chunk (C dwordx4 per lane per row); 0 = table
+#endif
+
+#ifndef WICCA_STRIP
+#define WICCA_STRIP -1        // 1: wave-strip kernel, 0: LDS-segment kernel, -1: per-depth table
+#endif
+#ifndef WICCA_STRIP_CHUNK
+#define WICCA_STRIP_CHUNK 0   // rows per load chunk of the strip kernel; 0 = table
+#endif
+
 namespace wicca {
+
+// Which K1 variant serves depth L (in-process A/B, profiles/r01_ab_v7.json):
+// the wave-strip kernel wins at depths 2-3, the LDS-segment kernel elsewhere.
+constexpr bool use_strip_kernel(int L)
+{
+    return WICCA_STRIP >= 0 ? WICCA_STRIP == 1 : (L == 2 || L == 3);
+}
+
+constexpr int strip_chunk_rows(int L)
+{
+    return WICCA_STRIP_CHUNK > 0 ? WICCA_STRIP_CHUNK : 16;
+}
+
+// Rows of a band loaded back to back before they are reduced (measured,
+// profiles/r01_variants*.jsonl): deep chunks pay at large depth.
+constexpr int chunk_rows(int L)
+{
+    return WICCA_CHUNK_ROWS > 0 ? WICCA_CHUNK_ROWS : (L >= 4 ? 16 : 8);
+}
 
 // One image of a ragged batch, as the kernel reads it (device memory).
 struct ImageDescDev {
@@ -33,7 +70,7 @@ struct LLParams {
     int64_t total_blocks;
 };
 
-int64_t segments_for(int64_t out_w, int L);
+int64_t segments_for(int64_t out_w, int L, int C);  // column groups per icon row
 bool fast_path_ok(const LLParams& p, int L, int C);
 
 // Block sums of the padded 2^L x 2^L blocks, finished as OutT:

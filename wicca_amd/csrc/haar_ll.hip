@@ -37,6 +37,7 @@ namespace wicca {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+
 constexpr int kThreads = 256;
 constexpr int kSegPx = kThreads * 16;  // pixels per segment (16 per lane)
 
@@ -118,13 +119,33 @@ __device__ __forceinline__ uint32_t finish<uint32_t>(uint32_t s, int) { return s
 
 // ----------------------------------------------------------------------------
 // K1: fused padded block sum, 1 <= L <= 8, C in {1,2,3,4}.
+//
+// A workgroup owns one icon row (a band of 2^L input rows) of one 4,096-pixel
+// segment.  The band streams as chunks of U rows (U*C dwordx4 per lane in
+// flight).  Loads use a buffer descriptor per row (wave-uniform base in SGPRs,
+// per-lane 32-bit offset, `nt` for the once-read stream); the descriptor's
+// record count ends the row, so lanes past the row read zeros.
 // ----------------------------------------------------------------------------
+__device__ __forceinline__ u32x4 load_row16(const uint8_t* row, uint32_t nrec, uint32_t voff)
+{
+#if WICCA_BUFFER_LOADS
+    __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(row), (short)0, (int)nrec, 0x00020000);
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0,
+                                                                           WICCA_NT_LOADS ? 2 : 0));
+#else
+    (void)nrec;
+    return load16(row + voff);
+#endif
+}
+
 template <int L, int C, typename OutT, bool RAGGED>
 __global__ __launch_bounds__(kThreads) void haar_block_sum_kernel(LLParams p)
 {
     static_assert(L >= 1 && L <= 8, "integer path covers 1..8 levels");
     constexpr int R = 1 << L;
-    constexpr int U = R < 4 ? R : 4;                     // rows in flight per lane
+    constexpr int U = R < chunk_rows(L) ? R : chunk_rows(L);  // rows per load chunk
+    constexpr int CPB = R / U;                                       // chunks per band
     constexpr int kColBytes = kSegPx * C * 2;            // u16 column sums
     constexpr int kOutPerSeg = kSegPx >> L;              // icons per segment row
     constexpr int kStageBytes = kOutPerSeg * C * (int)sizeof(OutT);
@@ -142,179 +163,388 @@ __global__ __launch_bounds__(kThreads) void haar_block_sum_kernel(LLParams p)
     const int tid = threadIdx.x;
     const int64_t row_bytes = w.W * C;
     const int64_t px0 = (int64_t)w.seg * kSegPx;          // first pixel of segment
-    const int64_t y0 = (int64_t)w.oy << L;
+    const int oy = w.oy;                                  // icon row (band) of the block
+    const int64_t y0 = (int64_t)oy << L;                  // its first input row
     const int rows_real = (int)min<int64_t>(max<int64_t>(w.H - y0, 0), R);
     const bool replicate = p.border == 1;
-    const int nrows = replicate ? R : rows_real;
+    const int64_t last_row = w.H - 1;
+    const uint8_t* img = w.src;
 
-    // ---------------- phase V: vertical column sums ----------------
-    uint32_t lo[C][4], hi[C][4];
     uint32_t off[C];
     bool valid[C];
 #pragma unroll
     for (int k = 0; k < C; ++k) {
-        int64_t o = px0 * C + (int64_t)k * (kThreads * 16) + 16 * tid;  // byte in row
+        const int64_t o = px0 * C + (int64_t)k * (kThreads * 16) + 16 * tid;  // byte in row
         valid[k] = o < row_bytes;
+#if WICCA_BUFFER_LOADS
+        off[k] = (uint32_t)o;  // past the record count -> zeros
+#else
         off[k] = valid[k] ? (uint32_t)o : 0u;  // invalid lanes re-read byte 0
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { lo[k][j] = 0; hi[k][j] = 0; }
+#endif
     }
-    const uint8_t* img = w.src;
-    const int64_t last_row = w.H - 1;
-    int r = 0;
-    for (; r + U <= nrows; r += U) {
-        u32x4 v[U][C];
+    const uint32_t nrec = (uint32_t)((row_bytes + 15) & ~(int64_t)15);  // inside the pitch
+
+    auto issue = [&](u32x4 (&v)[U][C], int g) {
+        const int64_t ybase = y0 + g * U;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t y = min<int64_t>(y0 + r + u, last_row);
-            const uint8_t* row = img + y * w.src_pitch;
+            const uint8_t* row = img + min<int64_t>(ybase + u, last_row) * w.src_pitch;
 #pragma unroll
-            for (int k = 0; k < C; ++k) v[u][k] = load16(row + off[k]);
+            for (int k = 0; k < C; ++k) v[u][k] = load_row16(row, nrec, off[k]);
+        }
+    };
+
+    uint32_t lo[C][4], hi[C][4];
+    auto zero_acc = [&]() {
+#pragma unroll
+        for (int k = 0; k < C; ++k)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) { lo[k][j] = 0; hi[k][j] = 0; }
+    };
+
+    // Band epilogue: column sums -> LDS -> per-icon sums -> staged 16-B stores.
+    auto epilogue = [&]() {
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+            u32x4 a, b;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t l = valid[k] ? lo[k][j] : 0u;
+                const uint32_t h = valid[k] ? hi[k][j] : 0u;
+                const uint32_t w0 = __builtin_amdgcn_perm(h, l, 0x05040100u);  // cols 4j, 4j+1
+                const uint32_t w1 = __builtin_amdgcn_perm(h, l, 0x07060302u);  // cols 4j+2, 4j+3
+                if (j < 2) { a[2 * j] = w0; a[2 * j + 1] = w1; }
+                else       { b[2 * j - 4] = w0; b[2 * j - 3] = w1; }
+            }
+            u32x4* dstv = reinterpret_cast<u32x4*>(colsum + k * (kThreads * 16) + 16 * tid);
+            dstv[0] = a;
+            dstv[1] = b;
+        }
+        // REPLICATE pad columns whose source column W-1 lies in an earlier
+        // segment (only in the D > 8 pre-pass, where padding exceeds 2^L).
+        const bool tail = px0 + kSegPx > w.W;
+        bool last_elsewhere = false;
+        if constexpr (sizeof(OutT) == 4 && L == 8) last_elsewhere = replicate && tail && px0 > w.W - 1;
+        if (last_elsewhere && tid < C) {
+            uint32_t s = 0;
+            for (int rr = 0; rr < R; ++rr) {
+                const int64_t y = min<int64_t>(y0 + rr, last_row);
+                s += img[y * w.src_pitch + (w.W - 1) * C + tid];
+            }
+            lastcol[tid] = s;
+        }
+        __syncthreads();
+
+        constexpr int G = L <= 4 ? (1 << L) : 16;  // pixels per icon inside a lane
+        constexpr int NJ = 16 / G;                  // icons per lane
+        uint32_t words[8 * C];
+        {
+            const u32x4* srcv = reinterpret_cast<const u32x4*>(colsum + 16 * C * tid);
+#pragma unroll
+            for (int q = 0; q < 2 * C; ++q) {
+                const u32x4 t = srcv[q];
+                words[4 * q + 0] = t[0]; words[4 * q + 1] = t[1];
+                words[4 * q + 2] = t[2]; words[4 * q + 3] = t[3];
+            }
+        }
+        uint32_t s[NJ][C];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int c = 0; c < C; ++c) s[j][c] = 0;
+        const int64_t lane_px0 = px0 + 16 * tid;
+        if (!tail) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const int idx = i * C + c;
+                    const uint32_t wd = words[idx >> 1];
+                    s[i / G][c] += (idx & 1) ? (wd >> 16) : (wd & 0xFFFFu);
+                }
+        } else {
+            uint32_t last[C];
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                if (!replicate) last[c] = 0;
+                else if (last_elsewhere) last[c] = lastcol[c];
+                else last[c] = colsum[(w.W - 1 - px0) * C + c];
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const bool real = lane_px0 + i < w.W;
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const int idx = i * C + c;
+                    const uint32_t wd = words[idx >> 1];
+                    const uint32_t v = (idx & 1) ? (wd >> 16) : (wd & 0xFFFFu);
+                    s[i / G][c] += real ? v : last[c];
+                }
+            }
+        }
+        if constexpr (L > 4) {
+            constexpr int GL = 1 << (L - 4);  // lanes per icon (<= 16, inside a wave)
+#pragma unroll
+            for (int m = 1; m < GL; m <<= 1)
+#pragma unroll
+                for (int c = 0; c < C; ++c) s[0][c] += __shfl_xor(s[0][c], m, 64);
+        }
+        if constexpr (kReuse) __syncthreads();  // colsum reads done before staging
+
+        const int64_t seg_out0 = px0 >> L;
+        const int n_out = (int)min<int64_t>(kOutPerSeg, w.out_w - seg_out0);
+        OutT* stage_t = reinterpret_cast<OutT*>(stage);
+        const uint32_t k_const = p.k;
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            int o;  // icon index inside the segment
+            bool writer;
+            if constexpr (L > 4) {
+                o = tid >> (L - 4);
+                writer = (tid & ((1 << (L - 4)) - 1)) == 0;
+            } else {
+                o = tid * NJ + j;
+                writer = true;
+            }
+            if (writer && o < n_out) {
+                uint32_t pad_cells = 0;
+                if (!replicate) {
+                    const int64_t ox = seg_out0 + o;
+                    const int64_t cols_real = min<int64_t>(max<int64_t>(w.W - (ox << L), 0), R);
+                    pad_cells = (uint32_t)(R * R) - (uint32_t)(rows_real * cols_real);
+                }
+#pragma unroll
+                for (int c = 0; c < C; ++c)
+                    stage_t[o * C + c] = finish<OutT>(s[j][c] + k_const * pad_cells, L);
+            }
+        }
+        __syncthreads();
+
+        const int nbytes = n_out * C * (int)sizeof(OutT);
+        uint8_t* drow = w.dst + (int64_t)oy * w.dst_pitch + seg_out0 * C * (int64_t)sizeof(OutT);
+        // rows of the icon are 16-B aligned (launcher guarantees); the last
+        // partial chunk of a row is written with 4-B / 1-B stores
+        const int full = nbytes & ~15;
+        for (int i = tid * 16; i < full; i += kThreads * 16)
+            *reinterpret_cast<u32x4*>(drow + i) = *reinterpret_cast<const u32x4*>(stage + i);
+        if (tid < nbytes - full) drow[full + tid] = stage[full + tid];
+    };
+
+    // Reduce chunk g (its loads were issued earlier); CONSTANT rows below the
+    // image are masked out (their value enters as k * pad cells).
+    auto consume = [&](u32x4 (&v)[U][C], int g) {
+        const int c0 = g * U;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t m = (replicate || c0 + u < rows_real) ? 0x00FF00FFu : 0u;
+#pragma unroll
+            for (int k = 0; k < C; ++k)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    lo[k][j] += v[u][k][j] & m;
+                    hi[k][j] += (v[u][k][j] >> 8) & m;
+                }
+        }
+    };
+
+    zero_acc();
+    for (int g = 0; g < CPB; ++g) {
+        u32x4 v[U][C];
+        issue(v, g);
+        consume(v, g);
+    }
+    epilogue();
+}
+
+// ----------------------------------------------------------------------------
+// K1s: wave-strip block sum, 1 <= L <= 8, C in {1,2,3,4}.
+//
+// Each lane owns P whole pixels of a row (P*C bytes: 12 B = 4 RGB pixels,
+// 16 B for C = 1, 2, 4), so a wave owns a strip of 64*P pixels — a multiple
+// of 2^L for every L <= 8, i.e. icons never straddle waves.  A workgroup is 4
+// independent waves on adjacent strips of one band: no LDS transpose and no
+// workgroup barrier.  Per lane: one buffer_load_dwordx3/x4 (`nt`, per-row
+// descriptor) per row, packed-u16 column sums, then per-icon sums in
+// registers (2^L <= P) or across 2^L/P lanes with __shfl_xor (2^L > P).
+// Icons are staged per wave in LDS and leave as dword (or byte) stores.
+// ----------------------------------------------------------------------------
+template <int C>
+struct StripGeom {
+    static constexpr int P = (C == 3) ? 4 : 16 / C;  // pixels per lane
+    static constexpr int BYTES = P * C;              // 12 or 16
+    static constexpr int NDW = BYTES / 4;            // dwords per lane
+    static constexpr int STRIP = 64 * P;             // pixels per wave
+};
+
+template <int NDW>
+__device__ __forceinline__ void load_lane(uint32_t (&d)[NDW], const uint8_t* row, uint32_t nrec,
+                                          uint32_t voff)
+{
+    __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(row), (short)0, (int)nrec, 0x00020000);
+    if constexpr (NDW == 4) {
+        const u32x4 v = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, WICCA_NT_LOADS ? 2 : 0));
+        d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+    } else {
+        typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+        const u32x3 v = __builtin_bit_cast(
+            u32x3, __builtin_amdgcn_raw_buffer_load_b96(rs, voff, 0, WICCA_NT_LOADS ? 2 : 0));
+        d[0] = v[0]; d[1] = v[1]; d[2] = v[2];
+    }
+}
+
+template <int L, int C, typename OutT, bool RAGGED>
+__global__ __launch_bounds__(kThreads) void haar_strip_kernel(LLParams p)
+{
+    static_assert(L >= 1 && L <= 8, "integer path covers 1..8 levels");
+    using Geo = StripGeom<C>;
+    constexpr int P = Geo::P, NDW = Geo::NDW, STRIP = Geo::STRIP;
+    constexpr int R = 1 << L;
+    constexpr int G = 1 << L;                       // pixels per icon
+    constexpr int NJ = G <= P ? P / G : 1;           // icons per lane
+    constexpr int GL = G <= P ? 1 : G / P;           // lanes per icon
+    constexpr int U = R < strip_chunk_rows(L) ? R : strip_chunk_rows(L);
+    constexpr int ICONS = STRIP / G;                 // icons per wave strip
+    constexpr int STAGE = (ICONS * C * (int)sizeof(OutT) + 15) & ~15;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[4 * STAGE];
+
+    // ---- work: block -> (image, icon row, group of 4 strips); wave -> strip
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    BlockWork w = resolve_block<L, RAGGED>(p);
+    const int strip = w.seg * 4 + wave;
+    const int64_t spx0 = (int64_t)strip * STRIP;     // first pixel of the strip
+    const int64_t Wp = w.out_w << L;                 // padded width
+    if (spx0 >= Wp) return;                          // whole wave idle (no barriers below)
+    uint8_t* stage = smem + wave * STAGE;
+
+    const int64_t y0 = (int64_t)w.oy << L;
+    const int rows_real = (int)min<int64_t>(max<int64_t>(w.H - y0, 0), R);
+    const bool replicate = p.border == 1;
+    const int64_t last_row = w.H - 1;
+    const int64_t row_bytes = w.W * C;
+    const uint32_t nrec = (uint32_t)((row_bytes + 15) & ~(int64_t)15);
+    const int64_t lpx0 = spx0 + (int64_t)lane * P;    // first pixel of the lane
+    const uint32_t voff = (uint32_t)(lpx0 * C);       // past nrec -> zeros
+
+    // ---- vertical: packed u16 column sums (bytes 0,2 | 1,3 of each dword)
+    uint32_t lo[NDW], hi[NDW];
+#pragma unroll
+    for (int j = 0; j < NDW; ++j) { lo[j] = 0; hi[j] = 0; }
+    for (int r0 = 0; r0 < R; r0 += U) {
+        uint32_t d[U][NDW];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint8_t* row = w.src + min<int64_t>(y0 + r0 + u, last_row) * w.src_pitch;
+            load_lane<NDW>(d[u], row, nrec, voff);
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < U; ++u) {
+            const uint32_t m = (replicate || r0 + u < rows_real) ? 0x00FF00FFu : 0u;
 #pragma unroll
-            for (int k = 0; k < C; ++k) accumulate(lo[k], hi[k], v[u][k]);
-    }
-    for (; r < nrows; ++r) {  // CONSTANT border, partial last band only
-        const uint8_t* row = img + (y0 + r) * w.src_pitch;
-#pragma unroll
-        for (int k = 0; k < C; ++k) accumulate(lo[k], hi[k], load16(row + off[k]));
+            for (int j = 0; j < NDW; ++j) {
+                lo[j] += d[u][j] & m;
+                hi[j] += (d[u][j] >> 8) & m;
+            }
+        }
     }
 
-    // column sums -> LDS as linear u16 (byte order of the row)
+    // ---- per-pixel, per-channel column sums of this lane
+    auto colsum = [&](int byte) -> uint32_t {
+        const uint32_t r = (byte & 1) ? hi[byte >> 2] : lo[byte >> 2];
+        return ((byte >> 1) & 1) ? (r >> 16) : (r & 0xFFFFu);
+    };
+    uint32_t cs[P][C];
 #pragma unroll
-    for (int k = 0; k < C; ++k) {
-        u32x4 a, b;
+    for (int q = 0; q < P; ++q)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint32_t l = valid[k] ? lo[k][j] : 0u;
-            uint32_t h = valid[k] ? hi[k][j] : 0u;
-            uint32_t w0 = __builtin_amdgcn_perm(h, l, 0x05040100u);  // cols 4j, 4j+1
-            uint32_t w1 = __builtin_amdgcn_perm(h, l, 0x07060302u);  // cols 4j+2, 4j+3
-            if (j < 2) { a[2 * j] = w0; a[2 * j + 1] = w1; }
-            else       { b[2 * j - 4] = w0; b[2 * j - 3] = w1; }
+        for (int c = 0; c < C; ++c) cs[q][c] = colsum(q * C + c);
+
+    // ---- right padding: pixels >= W
+    if (spx0 + STRIP > w.W) {  // wave-uniform: this strip reaches the image edge
+        uint32_t last[C];
+        if (!replicate) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) last[c] = 0;
+        } else if (spx0 <= w.W - 1) {
+            // column W-1 lives in this wave: its lane broadcasts its sums
+            const int hl = (int)((w.W - 1 - spx0) / P);
+            const int hq = (int)((w.W - 1 - spx0) % P);
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                uint32_t mine = 0;
+#pragma unroll
+                for (int q = 0; q < P; ++q) mine = (q == hq) ? cs[q][c] : mine;
+                last[c] = __shfl(mine, hl, 64);
+            }
+        } else {
+            // only in the depth > 8 pre-pass: column W-1 is in an earlier strip
+            uint32_t mine = 0;
+            if (lane < C)
+                for (int rr = 0; rr < R; ++rr)
+                    mine += w.src[min<int64_t>(y0 + rr, last_row) * w.src_pitch + (w.W - 1) * C + lane];
+#pragma unroll
+            for (int c = 0; c < C; ++c) last[c] = __shfl(mine, c, 64);
         }
-        u32x4* dstv = reinterpret_cast<u32x4*>(colsum + k * (kThreads * 16) + 16 * tid);
-        dstv[0] = a;
-        dstv[1] = b;
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const bool real = lpx0 + q < w.W;
+#pragma unroll
+            for (int c = 0; c < C; ++c) cs[q][c] = real ? cs[q][c] : last[c];
+        }
     }
 
-    // REPLICATE pad columns whose source column W-1 lies in an earlier segment
-    // (only possible for the D > 8 pre-pass, where padding exceeds 2^L).
-    const bool tail = px0 + kSegPx > w.W;
-    const bool last_elsewhere = replicate && tail && px0 > w.W - 1;
-    if (last_elsewhere && tid < C) {
-        uint32_t s = 0;
-        for (int rr = 0; rr < R; ++rr) {
-            const int64_t y = min<int64_t>(y0 + rr, last_row);
-            s += img[y * w.src_pitch + (w.W - 1) * C + tid];
-        }
-        lastcol[tid] = s;
-    }
-    __syncthreads();
-
-    // ---------------- phase H: horizontal sums per icon ----------------
-    constexpr int G = L <= 4 ? (1 << L) : 16;   // pixels per icon inside a lane
-    constexpr int NJ = 16 / G;                   // icons per lane
-    uint32_t words[8 * C];
-    {
-        const u32x4* srcv = reinterpret_cast<const u32x4*>(colsum + 16 * C * tid);
-#pragma unroll
-        for (int q = 0; q < 2 * C; ++q) {
-            u32x4 t = srcv[q];
-            words[4 * q + 0] = t[0]; words[4 * q + 1] = t[1];
-            words[4 * q + 2] = t[2]; words[4 * q + 3] = t[3];
-        }
-    }
+    // ---- horizontal: icons inside the lane, then across GL lanes
     uint32_t s[NJ][C];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
-        for (int c = 0; c < C; ++c) s[j][c] = 0;
-
-    const int64_t lane_px0 = px0 + 16 * tid;
-    if (!tail) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const int idx = i * C + c;
-                const uint32_t wd = words[idx >> 1];
-                s[i / G][c] += (idx & 1) ? (wd >> 16) : (wd & 0xFFFFu);
-            }
-    } else {
-        uint32_t last[C];
-#pragma unroll
         for (int c = 0; c < C; ++c) {
-            if (!replicate) last[c] = 0;
-            else if (last_elsewhere) last[c] = lastcol[c];
-            else last[c] = colsum[(w.W - 1 - px0) * C + c];
-        }
+            uint32_t t = 0;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const bool real = lane_px0 + i < w.W;
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const int idx = i * C + c;
-                const uint32_t wd = words[idx >> 1];
-                const uint32_t v = (idx & 1) ? (wd >> 16) : (wd & 0xFFFFu);
-                s[i / G][c] += real ? v : last[c];
-            }
+            for (int q = 0; q < (G <= P ? G : P); ++q) t += cs[j * (G <= P ? G : P) + q][c];
+            s[j][c] = t;
         }
-    }
-    if constexpr (L > 4) {
-        constexpr int GL = 1 << (L - 4);  // lanes per icon (<= 16, inside a wave)
+    if constexpr (GL > 1) {
 #pragma unroll
         for (int m = 1; m < GL; m <<= 1)
 #pragma unroll
             for (int c = 0; c < C; ++c) s[0][c] += __shfl_xor(s[0][c], m, 64);
     }
 
-    if constexpr (kReuse) __syncthreads();  // colsum reads done before staging
-    // icons -> LDS staging
-    const int64_t seg_out0 = px0 >> L;
-    const int n_out = (int)min<int64_t>(kOutPerSeg, w.out_w - seg_out0);
-    OutT* stage_t = reinterpret_cast<OutT*>(stage);
+    // ---- finish + stage this wave's icons
+    const int64_t ox0 = spx0 >> L;                           // first icon of the strip
+    const int n_out = (int)min<int64_t>(ICONS, w.out_w - ox0);
+    OutT* st = reinterpret_cast<OutT*>(stage);
     const uint32_t k_const = p.k;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-        int o;  // icon index inside the segment
-        bool writer;
-        if constexpr (L > 4) {
-            o = tid >> (L - 4);
-            writer = (tid & ((1 << (L - 4)) - 1)) == 0;
-        } else {
-            o = tid * NJ + j;
-            writer = true;
-        }
+        const int o = (GL > 1) ? lane / GL : lane * NJ + j;
+        const bool writer = (GL > 1) ? (lane % GL) == 0 : true;
         if (writer && o < n_out) {
             uint32_t pad_cells = 0;
             if (!replicate) {
-                const int64_t ox = seg_out0 + o;
-                const int64_t cols_real = min<int64_t>(max<int64_t>(w.W - (ox << L), 0), R);
+                const int64_t cols_real = min<int64_t>(max<int64_t>(w.W - ((ox0 + o) << L), 0), R);
                 pad_cells = (uint32_t)(R * R) - (uint32_t)(rows_real * cols_real);
             }
 #pragma unroll
-            for (int c = 0; c < C; ++c)
-                stage_t[o * C + c] = finish<OutT>(s[j][c] + k_const * pad_cells, L);
+            for (int c = 0; c < C; ++c) st[o * C + c] = finish<OutT>(s[j][c] + k_const * pad_cells, L);
         }
     }
-    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    // ---------------- store: 16-byte chunks of the icon row ----------------
+    // ---- store the strip's icon bytes (contiguous in the icon row)
     const int nbytes = n_out * C * (int)sizeof(OutT);
-    uint8_t* drow = w.dst + (int64_t)w.oy * w.dst_pitch + seg_out0 * C * (int64_t)sizeof(OutT);
-    if (p.aligned_out) {
-        for (int i = tid * 16; i < nbytes; i += kThreads * 16) {
-            if (i + 16 <= nbytes) {
-                *reinterpret_cast<u32x4*>(drow + i) = *reinterpret_cast<const u32x4*>(stage + i);
-            } else {
-                for (int b = i; b < nbytes; ++b) drow[b] = stage[b];
-            }
-        }
+    uint8_t* drow = w.dst + (int64_t)w.oy * w.dst_pitch + ox0 * C * (int64_t)sizeof(OutT);
+    if ((((uintptr_t)drow | (uintptr_t)nbytes) & 3) == 0) {
+        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stage);
+        uint32_t* d32 = reinterpret_cast<uint32_t*>(drow);
+        for (int i = lane; i < (nbytes >> 2); i += 64) d32[i] = s32[i];
     } else {
-        for (int i = tid; i < nbytes; i += kThreads) drow[i] = stage[i];
+        for (int i = lane; i < nbytes; i += 64) drow[i] = stage[i];
     }
 }
 
@@ -476,6 +706,16 @@ static inline bool aligned16(const void* ptr, int64_t pitch, int64_t stride)
 template <int L, int C, typename OutT>
 static hipError_t launch_fast(const LLParams& p, int64_t blocks, hipStream_t stream)
 {
+    if constexpr (use_strip_kernel(L)) {
+        if (p.descs) {
+            hipLaunchKernelGGL((haar_strip_kernel<L, C, OutT, true>), dim3((uint32_t)blocks),
+                               dim3(kThreads), 0, stream, p);
+        } else {
+            hipLaunchKernelGGL((haar_strip_kernel<L, C, OutT, false>), dim3((uint32_t)blocks),
+                               dim3(kThreads), 0, stream, p);
+        }
+        return hipGetLastError();
+    }
     if (p.descs) {
         hipLaunchKernelGGL((haar_block_sum_kernel<L, C, OutT, true>), dim3((uint32_t)blocks),
                            dim3(kThreads), 0, stream, p);
@@ -514,7 +754,15 @@ static hipError_t dispatch_C(int L, int C, const LLParams& p, int64_t blocks, hi
     }
 }
 
-int64_t segments_for(int64_t out_w, int L) { return ((out_w << L) + kSegPx - 1) / kSegPx; }
+int64_t segments_for(int64_t out_w, int L, int C)
+{
+    if (use_strip_kernel(L)) {  // groups of 4 wave strips of 64*P pixels
+        const int64_t strip = 64 * ((C == 3) ? 4 : 16 / std::max(1, std::min(C, 4)));
+        const int64_t strips = ((out_w << L) + strip - 1) / strip;
+        return (strips + 3) / 4;
+    }
+    return ((out_w << L) + kSegPx - 1) / kSegPx;  // 4,096-pixel segments
+}
 
 bool fast_path_ok(const LLParams& p, int L, int C)
 {
@@ -528,8 +776,8 @@ hipError_t launch_block_sum(LLParams p, int L, int C, hipStream_t stream)
     const bool out_al = ((uintptr_t)p.dst % 16 == 0) && p.dst_pitch % 16 == 0 &&
                         p.dst_image_stride % 16 == 0;
     p.aligned_out = out_al ? 1 : 0;
-    if (p.descs == nullptr && fast_path_ok(p, L, C)) {
-        p.n_seg = (int32_t)segments_for(p.out_w, L);
+    if (p.descs == nullptr && out_al && fast_path_ok(p, L, C)) {
+        p.n_seg = (int32_t)segments_for(p.out_w, L, C);
         const int64_t blocks = p.n_images * p.out_h * p.n_seg;
         if (blocks <= 0) return hipSuccess;
         if (blocks >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
