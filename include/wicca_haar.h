@@ -148,6 +148,15 @@ int wicca_synth_u8(uint8_t* dst, int64_t n, int64_t H, int64_t W, int64_t C,
                    int64_t pitch, int64_t image_stride, uint64_t seed,
                    int device, void* stream);
 
+/*
+ * Rows [first_row, first_row + rows) of synthetic image `image_index` (the
+ * same bytes wicca_synth_u8 / wicca_amd.synth produce for the whole image):
+ * one rank's band of a row-sharded oversize image (BASELINE config 5).
+ */
+int wicca_synth_band_u8(uint8_t* dst, int64_t rows, int64_t W, int64_t C,
+                        int64_t pitch, uint64_t seed, int64_t image_index,
+                        int64_t first_row, int device, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -171,3 +171,44 @@ def test_device_synth_matches_host(coder):
     host = buf.cpu().numpy().reshape(n, H, pitch)[:, :, :W * C].reshape(n, H, W, C)
     for i in range(n):
         assert np.array_equal(host[i], synth_image(99, i, H, W, C))
+
+
+def test_device_band_synth_matches_host_rows(coder):
+    import ctypes
+    from wicca_amd import _lib
+    from wicca_amd.synth import synth_rows
+    torch = pytest.importorskip("torch")
+    W, C = 333, 3
+    pitch = (W * C + 15) // 16 * 16
+    for first, rows in ((0, 5), (17, 9)):
+        buf = torch.empty(rows * pitch, dtype=torch.uint8, device="cuda")
+        _lib.check(_lib.load().wicca_synth_band_u8(ctypes.c_void_p(buf.data_ptr()), rows, W, C,
+                                                   pitch, 42, 3, first, -1, None))
+        host = buf.cpu().numpy().reshape(rows, pitch)[:, :W * C].reshape(rows, W, C)
+        assert np.array_equal(host, synth_rows(42, 3, first, rows, W, C))
+
+
+def test_tiled_single_rank_on_device(coder):
+    """TiledHaar's HIP path (device tensors, RCCL group of one)."""
+    import os
+    import socket
+    torch = pytest.importorskip("torch")
+    import torch.distributed as dist
+    from wicca_amd.parallel import TiledHaar
+    if not dist.is_initialized():
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("nccl", rank=0, world_size=1,
+                                device_id=torch.device("cuda", 0))
+    rng = np.random.default_rng(12)
+    for (H, W, C, D, border, k) in [(1000, 640, 3, 5, 1, 0), (777, 512, 4, 3, 0, 9),
+                                    (300, 1024, 3, 8, 1, 0)]:
+        img = rng.integers(0, 256, (H, W, C), dtype=np.uint8)
+        band = torch.from_numpy(img).cuda()
+        icon = TiledHaar(D, border, k)(band, 0, H, [(0, H)])
+        assert np.array_equal(icon.cpu().numpy(), c_oracle.ll_int_block(img, D, border, k)[0])
+    dist.destroy_process_group()

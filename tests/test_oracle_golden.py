@@ -79,3 +79,10 @@ def test_synth_host_matches_c_oracle():
         a = synth_image(seed, idx, *shape)
         b = c_oracle.synth_u8(1, *shape, seed, idx)[0]
         assert np.array_equal(a, b)
+
+
+def test_synth_rows_is_a_slice_of_synth_image():
+    from wicca_amd.synth import synth_image, synth_rows
+    img = synth_image(3, 1, 11, 7, 3)
+    for a, b in ((0, 11), (1, 2), (3, 9), (10, 11)):
+        assert np.array_equal(synth_rows(3, 1, a, b - a, 7, 3), img[a:b])

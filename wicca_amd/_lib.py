@@ -55,6 +55,8 @@ SIGNATURES = {
                                       _int, _int, _int, _p]),
     "wicca_synth_u8": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_uint64, _int,
                               _p]),
+    "wicca_synth_band_u8": (_int, [_p, _i64, _i64, _i64, _i64, ctypes.c_uint64, _i64, _i64, _int,
+                                   _p]),
 }
 
 _lock = threading.Lock()

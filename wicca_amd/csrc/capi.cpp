@@ -111,7 +111,8 @@ int acquire(int device, WorkspaceLease& lease)
     }
     auto* ws = new Workspace();
     ws->device = device;
-    hipError_t e = hipStreamCreateWithFlags(&ws->stream, hipStreamNonBlocking);
+    // blocking stream: ordered after work on the legacy default stream (torch's null stream)
+    hipError_t e = hipStreamCreateWithFlags(&ws->stream, hipStreamDefault);
     if (e != hipSuccess) {
         delete ws;
         return fail(WICCA_ERR_HIP, "hipStreamCreate failed: %s", hipGetErrorString(e));
@@ -561,7 +562,26 @@ int wicca_synth_u8(uint8_t* dst, int64_t n, int64_t H, int64_t W, int64_t C, int
     WorkspaceLease lease;
     if ((rc = acquire(dev, lease))) return rc;
     hipStream_t stream = stream_in ? (hipStream_t)stream_in : lease.ws->stream;
-    HIP_TRY(wicca::launch_synth(dst, n, H, W * C, pitch, image_stride, seed, 0, stream));
+    HIP_TRY(wicca::launch_synth(dst, n, H, W * C, pitch, image_stride, seed, 0, 0, stream));
+    if (!stream_in) HIP_TRY(hipStreamSynchronize(stream));
+    return WICCA_OK;
+}
+
+int wicca_synth_band_u8(uint8_t* dst, int64_t rows, int64_t W, int64_t C, int64_t pitch,
+                        uint64_t seed, int64_t image_index, int64_t first_row, int device,
+                        void* stream_in)
+{
+    if (!dst) return fail(WICCA_ERR_ARG, "dst is NULL");
+    if (rows < 0 || W < 0 || C < 0 || first_row < 0) return fail(WICCA_ERR_ARG, "negative size");
+    if (pitch < W * C || pitch % 16 || (uintptr_t)dst % 16)
+        return fail(WICCA_ERR_ARG, "synth needs 16-byte aligned rows");
+    int dev, rc;
+    if ((rc = select_device(device, &dev))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    hipStream_t stream = stream_in ? (hipStream_t)stream_in : lease.ws->stream;
+    HIP_TRY(wicca::launch_synth(dst, 1, rows, W * C, pitch, 0, seed, image_index, first_row,
+                                stream));
     if (!stream_in) HIP_TRY(hipStreamSynchronize(stream));
     return WICCA_OK;
 }

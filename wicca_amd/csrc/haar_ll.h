@@ -86,6 +86,7 @@ hipError_t launch_level_f32(const void* in, int64_t in_pitch, int64_t in_img_str
                             int64_t n_img, int64_t out_h, int64_t out_w, int C, hipStream_t s);
 
 hipError_t launch_synth(uint8_t* dst, int64_t n, int64_t H, int64_t WC, int64_t pitch,
-                        int64_t image_stride, uint64_t seed, int64_t first_image, hipStream_t s);
+                        int64_t image_stride, uint64_t seed, int64_t first_image,
+                        int64_t first_row, hipStream_t s);
 
 }  // namespace wicca

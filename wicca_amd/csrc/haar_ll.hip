@@ -659,7 +659,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z)
 __global__ __launch_bounds__(kThreads) void synth_u8_kernel(uint8_t* dst, int64_t n, int64_t H,
                                                             int64_t WC, int64_t pitch,
                                                             int64_t image_stride, uint64_t seed,
-                                                            int64_t first_image)
+                                                            int64_t first_image, int64_t first_row)
 {
     const int64_t chunks_per_row = (WC + 15) / 16;
     const int64_t total = n * H * chunks_per_row;
@@ -671,7 +671,7 @@ __global__ __launch_bounds__(kThreads) void synth_u8_kernel(uint8_t* dst, int64_
         const int64_t y = row_id - img * H;
         const uint64_t key = mix64(seed * 0x100000001B3ull + (uint64_t)(first_image + img));
         const int64_t x0 = chunk * 16;
-        const int64_t b0 = y * WC + x0;  // row-major byte index inside the image
+        const int64_t b0 = (first_row + y) * WC + x0;  // row-major byte index inside the image
         uint8_t bytes[16];
         uint64_t q_cached = ~0ull, word = 0;
 #pragma unroll
@@ -819,13 +819,14 @@ hipError_t launch_level_f32(const void* in, int64_t in_pitch, int64_t in_img_str
 }
 
 hipError_t launch_synth(uint8_t* dst, int64_t n, int64_t H, int64_t WC, int64_t pitch,
-                        int64_t image_stride, uint64_t seed, int64_t first_image, hipStream_t s)
+                        int64_t image_stride, uint64_t seed, int64_t first_image,
+                        int64_t first_row, hipStream_t s)
 {
     const int64_t total = n * H * ((WC + 15) / 16);
     if (total <= 0) return hipSuccess;
     const uint32_t blocks = (uint32_t)std::min<int64_t>((total + kThreads - 1) / kThreads, 256 * 32);
     hipLaunchKernelGGL(synth_u8_kernel, dim3(blocks), dim3(kThreads), 0, s, dst, n, H, WC, pitch,
-                       image_stride, seed, first_image);
+                       image_stride, seed, first_image, first_row);
     return hipGetLastError();
 }
 

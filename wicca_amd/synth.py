@@ -31,6 +31,17 @@ def image_key(seed: int, index: int) -> np.uint64:
         return _mix64(np.array([z], np.uint64))[0]
 
 
+def synth_rows(seed: int, index: int, first_row: int, rows: int, W: int, C: int) -> np.ndarray:
+    """Rows ``[first_row, first_row + rows)`` of synthetic image ``index``."""
+    b0 = first_row * W * C
+    nbytes = rows * W * C
+    w0, w1 = b0 // 8, (b0 + nbytes + 7) // 8
+    with np.errstate(over="ignore"):
+        words = _mix64(image_key(seed, index) + np.arange(w0, w1, dtype=np.uint64))
+    raw = words.astype("<u8").view(np.uint8)[b0 - 8 * w0:b0 - 8 * w0 + nbytes]
+    return raw.reshape(rows, W, C).copy()
+
+
 def synth_image(seed: int, index: int, H: int, W: int, C: int) -> np.ndarray:
     """Image ``index`` of the synthetic stream ``seed`` as an (H, W, C) uint8 array."""
     nbytes = H * W * C
