@@ -103,6 +103,27 @@ __device__ __forceinline__ void accumulate(uint32_t (&lo)[4], uint32_t (&hi)[4],
     }
 }
 
+// Store NB bytes that sit at a multiple-of-NB offset, with the widest LDS
+// writes that alignment allows (one ds_write_b32/b16 instead of NB byte writes).
+template <int NB>
+__device__ __forceinline__ void stage_bytes(uint8_t* dst, const uint8_t (&b)[NB])
+{
+    if constexpr (NB % 4 == 0) {
+#pragma unroll
+        for (int q = 0; q < NB / 4; ++q)
+            reinterpret_cast<uint32_t*>(dst)[q] = (uint32_t)b[4 * q] | ((uint32_t)b[4 * q + 1] << 8) |
+                                                  ((uint32_t)b[4 * q + 2] << 16) |
+                                                  ((uint32_t)b[4 * q + 3] << 24);
+    } else if constexpr (NB % 2 == 0) {
+#pragma unroll
+        for (int q = 0; q < NB / 2; ++q)
+            reinterpret_cast<uint16_t*>(dst)[q] = (uint16_t)(b[2 * q] | (b[2 * q + 1] << 8));
+    } else {
+#pragma unroll
+        for (int q = 0; q < NB; ++q) dst[q] = b[q];
+    }
+}
+
 template <typename OutT>
 __device__ __forceinline__ OutT finish(uint32_t s, int L);
 
@@ -295,27 +316,43 @@ __global__ __launch_bounds__(kThreads) void haar_block_sum_kernel(LLParams p)
         const int n_out = (int)min<int64_t>(kOutPerSeg, w.out_w - seg_out0);
         OutT* stage_t = reinterpret_cast<OutT*>(stage);
         const uint32_t k_const = p.k;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            int o;  // icon index inside the segment
-            bool writer;
-            if constexpr (L > 4) {
-                o = tid >> (L - 4);
-                writer = (tid & ((1 << (L - 4)) - 1)) == 0;
-            } else {
-                o = tid * NJ + j;
-                writer = true;
+        auto icon_value = [&](int j, int o, int c) -> OutT {
+            uint32_t pad_cells = 0;
+            if (!replicate) {
+                const int64_t ox = seg_out0 + o;
+                const int64_t cols_real = min<int64_t>(max<int64_t>(w.W - (ox << L), 0), R);
+                pad_cells = (uint32_t)(R * R) - (uint32_t)(rows_real * cols_real);
             }
-            if (writer && o < n_out) {
-                uint32_t pad_cells = 0;
-                if (!replicate) {
-                    const int64_t ox = seg_out0 + o;
-                    const int64_t cols_real = min<int64_t>(max<int64_t>(w.W - (ox << L), 0), R);
-                    pad_cells = (uint32_t)(R * R) - (uint32_t)(rows_real * cols_real);
-                }
+            return finish<OutT>(s[j][c] + k_const * pad_cells, L);
+        };
+        bool packed = false;
+        if constexpr (sizeof(OutT) == 1 && L <= 4 && NJ * C > 1) {
+            if (tid * NJ + NJ <= n_out) {  // all NJ icons of this lane exist
+                uint8_t b[NJ * C];
 #pragma unroll
-                for (int c = 0; c < C; ++c)
-                    stage_t[o * C + c] = finish<OutT>(s[j][c] + k_const * pad_cells, L);
+                for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                    for (int c = 0; c < C; ++c) b[j * C + c] = (uint8_t)icon_value(j, tid * NJ + j, c);
+                stage_bytes<NJ * C>(stage + tid * NJ * C, b);
+                packed = true;
+            }
+        }
+        if (!packed) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                int o;  // icon index inside the segment
+                bool writer;
+                if constexpr (L > 4) {
+                    o = tid >> (L - 4);
+                    writer = (tid & ((1 << (L - 4)) - 1)) == 0;
+                } else {
+                    o = tid * NJ + j;
+                    writer = true;
+                }
+                if (writer && o < n_out) {
+#pragma unroll
+                    for (int c = 0; c < C; ++c) stage_t[o * C + c] = icon_value(j, o, c);
+                }
             }
         }
         __syncthreads();
@@ -348,11 +385,27 @@ __global__ __launch_bounds__(kThreads) void haar_block_sum_kernel(LLParams p)
     };
 
     zero_acc();
+#if WICCA_PIPE
+    {   // chunk g+1 is in flight while chunk g is reduced (CPB is a constant)
+        u32x4 va[U][C], vb[U][C];
+        issue(va, 0);
+#pragma unroll
+        for (int g = 0; g < CPB; g += 2) {
+            if (g + 1 < CPB) issue(vb, g + 1);
+            consume(va, g);
+            if (g + 1 < CPB) {
+                if (g + 2 < CPB) issue(va, g + 2);
+                consume(vb, g + 1);
+            }
+        }
+    }
+#else
     for (int g = 0; g < CPB; ++g) {
         u32x4 v[U][C];
         issue(v, g);
         consume(v, g);
     }
+#endif
     epilogue();
 }
 
@@ -432,13 +485,14 @@ __global__ __launch_bounds__(kThreads) void haar_strip_kernel(LLParams p)
     uint32_t lo[NDW], hi[NDW];
 #pragma unroll
     for (int j = 0; j < NDW; ++j) { lo[j] = 0; hi[j] = 0; }
-    for (int r0 = 0; r0 < R; r0 += U) {
-        uint32_t d[U][NDW];
+    auto sissue = [&](uint32_t (&d)[U][NDW], int r0) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint8_t* row = w.src + min<int64_t>(y0 + r0 + u, last_row) * w.src_pitch;
             load_lane<NDW>(d[u], row, nrec, voff);
         }
+    };
+    auto sconsume = [&](uint32_t (&d)[U][NDW], int r0) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t m = (replicate || r0 + u < rows_real) ? 0x00FF00FFu : 0u;
@@ -448,7 +502,28 @@ __global__ __launch_bounds__(kThreads) void haar_strip_kernel(LLParams p)
                 hi[j] += (d[u][j] >> 8) & m;
             }
         }
+    };
+#if WICCA_PIPE
+    {
+        uint32_t da[U][NDW], db[U][NDW];
+        sissue(da, 0);
+#pragma unroll
+        for (int r0 = 0; r0 < R; r0 += 2 * U) {
+            if (r0 + U < R) sissue(db, r0 + U);
+            sconsume(da, r0);
+            if (r0 + U < R) {
+                if (r0 + 2 * U < R) sissue(da, r0 + 2 * U);
+                sconsume(db, r0 + U);
+            }
+        }
     }
+#else
+    for (int r0 = 0; r0 < R; r0 += U) {
+        uint32_t d[U][NDW];
+        sissue(d, r0);
+        sconsume(d, r0);
+    }
+#endif
 
     // ---- per-pixel, per-channel column sums of this lane
     auto colsum = [&](int byte) -> uint32_t {
@@ -518,18 +593,35 @@ __global__ __launch_bounds__(kThreads) void haar_strip_kernel(LLParams p)
     const int n_out = (int)min<int64_t>(ICONS, w.out_w - ox0);
     OutT* st = reinterpret_cast<OutT*>(stage);
     const uint32_t k_const = p.k;
+    auto icon_value = [&](int j, int o, int c) -> OutT {
+        uint32_t pad_cells = 0;
+        if (!replicate) {
+            const int64_t cols_real = min<int64_t>(max<int64_t>(w.W - ((ox0 + o) << L), 0), R);
+            pad_cells = (uint32_t)(R * R) - (uint32_t)(rows_real * cols_real);
+        }
+        return finish<OutT>(s[j][c] + k_const * pad_cells, L);
+    };
+    bool packed = false;
+    if constexpr (sizeof(OutT) == 1 && GL == 1 && NJ * C > 1) {
+        if (lane * NJ + NJ <= n_out) {
+            uint8_t b[NJ * C];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        const int o = (GL > 1) ? lane / GL : lane * NJ + j;
-        const bool writer = (GL > 1) ? (lane % GL) == 0 : true;
-        if (writer && o < n_out) {
-            uint32_t pad_cells = 0;
-            if (!replicate) {
-                const int64_t cols_real = min<int64_t>(max<int64_t>(w.W - ((ox0 + o) << L), 0), R);
-                pad_cells = (uint32_t)(R * R) - (uint32_t)(rows_real * cols_real);
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int c = 0; c < C; ++c) b[j * C + c] = (uint8_t)icon_value(j, lane * NJ + j, c);
+            stage_bytes<NJ * C>(stage + lane * NJ * C, b);
+            packed = true;
+        }
+    }
+    if (!packed) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int o = (GL > 1) ? lane / GL : lane * NJ + j;
+            const bool writer = (GL > 1) ? (lane % GL) == 0 : true;
+            if (writer && o < n_out) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) st[o * C + c] = icon_value(j, o, c);
             }
-#pragma unroll
-            for (int c = 0; c < C; ++c) st[o * C + c] = finish<OutT>(s[j][c] + k_const * pad_cells, L);
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
