@@ -40,9 +40,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=["batch", "tiled"], default="batch",
+    ap.add_argument("--config", choices=["batch", "tiled", "multi"], default="batch",
                     help="batch: configs[2]/[3] image-parallel (default); "
-                         "tiled: configs[4], one 65536^2 RGB image row-sharded at depth 8")
+                         "tiled: configs[4], one 65536^2 RGB image row-sharded at depth 8; "
+                         "multi: configs[2]'s depth sweep 1..6 from one read (SURVEY 8f)")
+    ap.add_argument("--depths", default="1,2,3,4,5,6", help="depth list of --config multi")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--depth", type=int, default=5)
@@ -217,6 +219,85 @@ def run_tiled(args, torch, dist, world, rank, local_rank):
     }
 
 
+def run_multi(args, torch, rank):
+    """All depths of configs[2]'s sweep from ONE read of the batch
+    (wicca_haar_ll_u8_multi_uniform), against one launch per depth."""
+    from wicca_amd import _lib
+    lib = _lib.load()
+    B, H, W, C = args.images, args.height, args.width, args.channels
+    depths = [int(x) for x in args.depths.split(",")]
+    pitch = (W * C + 15) // 16 * 16
+    src = torch.empty(B * H * pitch, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    _lib.check(lib.wicca_synth_u8(ctypes.c_void_p(src.data_ptr()), B, H, W, C, pitch, H * pitch,
+                                  args.seed * 1000003 + rank, -1, sh))
+    outs, ptrs, pitches, strides, dims = [], [], [], [], []
+    for d in depths:
+        oh, ow = -(-H >> d), -(-W >> d)
+        op = (ow * C + 15) // 16 * 16
+        o = torch.empty(B * oh * op, dtype=torch.uint8, device="cuda")
+        outs.append(o)
+        ptrs.append(o.data_ptr())
+        pitches.append(op)
+        strides.append(oh * op)
+        dims.append((oh, ow))
+    nd = len(depths)
+    c_d = (ctypes.c_int * nd)(*depths)
+    c_p = (ctypes.c_void_p * nd)(*ptrs)
+    c_pi = (ctypes.c_int64 * nd)(*pitches)
+    c_s = (ctypes.c_int64 * nd)(*strides)
+
+    def multi():
+        _lib.check(lib.wicca_haar_ll_u8_multi_uniform(
+            ctypes.c_void_p(src.data_ptr()), B, H, W, C, pitch, H * pitch, c_d, nd, args.border,
+            0, c_p, c_pi, c_s, -1, sh))
+
+    def separate():
+        for i, d in enumerate(depths):
+            _lib.check(lib.wicca_haar_ll_u8_uniform(
+                ctypes.c_void_p(src.data_ptr()), B, H, W, C, pitch, H * pitch, d, args.border, 0,
+                ctypes.c_void_p(ptrs[i]), pitches[i], strides[i], -1, sh))
+
+    def timed(fn):
+        for _ in range(args.warmup):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(args.steps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / args.steps * 1e3, e0.elapsed_time(e1) / args.steps
+
+    sep_wall, sep_dev = timed(separate)
+    sep_icons = [o.clone() for o in outs]
+    multi_wall, multi_dev = timed(multi)
+    same = all(torch.equal(a, b) for a, b in zip(sep_icons, outs))
+    if not same:
+        raise SystemExit("multi-depth icons differ from per-depth icons")
+    mp = B * H * W / 1e6
+    in_bytes = B * H * W * C
+    return {
+        "metric": BASELINE["metric"],
+        "value": round(mp / (multi_wall / 1e3), 1), "unit": "MP/s (all depths per pixel)",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(multi_wall, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (on-device splitmix64 images, HBM-resident before timing)",
+        "config": {"workload": f"{B} x {W}x{H}x{C}, icons at depths {depths} per step "
+                               "(BASELINE configs[2] sweep) from one read",
+                   "depths": depths, "images_per_gpu": B},
+        "separate_depths_ms": round(sep_wall, 4),
+        "speedup_vs_separate": round(sep_wall / multi_wall, 3),
+        "input_read_GBps_equiv": round(in_bytes / (multi_dev / 1e3) / 1e9, 1),
+        "identical_to_separate": same,
+    }
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -234,6 +315,11 @@ def main():
     lib = _lib.load()
     if _lib.device_count() < 1:
         raise SystemExit("no HIP device visible")
+    if args.config == "multi":
+        out = run_multi(args, torch, rank)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        return
     if args.config == "tiled":
         out = run_tiled(args, torch, dist, world, rank, local_rank)
         if out is not None:

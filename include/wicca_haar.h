@@ -127,10 +127,12 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs, int64_t n, int64_t C,
                            void* stream);
 
 /*
- * Multi-depth: the icon of every depth in depths[0..n_depths) from ONE upload
- * of the image (the caller's depth loop,
- * classifying_tools.py:546-551).  dsts[i] receives the icon of depths[i] with
- * pitch dst_pitches[i].  Host or device buffers as in wicca_haar_ll_u8.
+ * Multi-depth: the icon of every depth in depths[0..n_depths) (SURVEY 8f item
+ * 1; the caller's depth loop, classifying_tools.py:546-551).  Depths 1..8 come
+ * from ONE upload and ONE read of the image (block sums + integer pyramid);
+ * depths <= 0 and > 8 are computed on their own.  dsts[i] receives the icon of
+ * depths[i] with pitch dst_pitches[i].  Host or device buffers as in
+ * wicca_haar_ll_u8.
  */
 int wicca_haar_ll_u8_multi(const uint8_t* src, int64_t H, int64_t W, int64_t C,
                            int64_t src_pitch, const int* depths, int n_depths,
@@ -138,6 +140,22 @@ int wicca_haar_ll_u8_multi(const uint8_t* src, int64_t H, int64_t W, int64_t C,
                            uint8_t* const* dsts, const int64_t* dst_pitches,
                            int src_is_device, int dst_is_device, int device,
                            void* stream);
+
+/*
+ * Multi-depth, device-resident uniform batch: icons of every depth in
+ * depths[0..n_depths) (distinct, each in 1..8) for n images of identical shape
+ * from ONE read of the batch — exact block sums at the smallest depth over the
+ * image padded to the largest depth, then an integer 2x2 pyramid.  Icon of
+ * depth depths[i] for image j at dsts[i] + j*dst_image_strides[i].
+ */
+int wicca_haar_ll_u8_multi_uniform(const uint8_t* src, int64_t n, int64_t H,
+                                   int64_t W, int64_t C, int64_t src_pitch,
+                                   int64_t src_image_stride, const int* depths,
+                                   int n_depths, int border_type,
+                                   int border_constant, uint8_t* const* dsts,
+                                   const int64_t* dst_pitches,
+                                   const int64_t* dst_image_strides, int device,
+                                   void* stream);
 
 /*
  * Deterministic synthetic images on device (no PCIe in timed regions):

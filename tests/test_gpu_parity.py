@@ -212,3 +212,80 @@ def test_tiled_single_rank_on_device(coder):
         icon = TiledHaar(D, border, k)(band, 0, H, [(0, H)])
         assert np.array_equal(icon.cpu().numpy(), c_oracle.ll_int_block(img, D, border, k)[0])
     dist.destroy_process_group()
+
+
+def test_multi_depth_goldens(coder):
+    """Every depth 1..8 of a golden image from one multi-depth call (one read)."""
+    by_name = {c["name"]: c for c in OK}
+    for tag in ("37x53x3", "64x64x3", "128x96x3", "45x130x2", "29x31x4"):
+        img = None
+        for border, k, suffix in ((1, 0, "rep"), (0, 7, "const7")):
+            depths = [d for d in range(1, 9) if f"rand_{tag}_d{d}_{suffix}" in by_name]
+            if len(depths) < 2:
+                continue
+            img = G.input_of(by_name[f"rand_{tag}_d{depths[0]}_{suffix}"])
+            res = coder.get_small_copy_multi(img, depths, border, k)
+            for d in depths:
+                assert G.sha(res[d]) == by_name[f"rand_{tag}_d{d}_{suffix}"]["out_sha256"], (tag, d)
+
+
+def test_multi_uniform_device_batch(coder):
+    import ctypes
+    from wicca_amd import _lib
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(31)
+    for (n, H, W, C, depths, border, k) in [(3, 270, 481, 3, [1, 2, 3, 4, 5, 6], 1, 0),
+                                            (2, 199, 333, 3, [2, 5, 8], 0, 200),
+                                            (4, 64, 640, 1, [1, 3, 6], 1, 0),
+                                            (2, 100, 130, 4, [3, 4], 0, 1)]:
+        imgs = rng.integers(0, 256, (n, H, W, C), dtype=np.uint8)
+        pitch = (W * C + 15) // 16 * 16
+        host = np.zeros((n, H, pitch), np.uint8)
+        host[:, :, :W * C] = imgs.reshape(n, H, W * C)
+        src = torch.from_numpy(host).cuda()
+        outs, ptrs, pitches, strides = [], [], [], []
+        for d in depths:
+            oh, ow = -(-H >> d), -(-W >> d)
+            op = (ow * C + 15) // 16 * 16
+            o = torch.zeros((n, oh, op), dtype=torch.uint8, device="cuda")
+            outs.append((o, oh, ow))
+            ptrs.append(o.data_ptr())
+            pitches.append(op)
+            strides.append(oh * op)
+        nd = len(depths)
+        _lib.check(_lib.load().wicca_haar_ll_u8_multi_uniform(
+            ctypes.c_void_p(src.data_ptr()), n, H, W, C, pitch, H * pitch,
+            (ctypes.c_int * nd)(*depths), nd, border, k, (ctypes.c_void_p * nd)(*ptrs),
+            (ctypes.c_int64 * nd)(*pitches), (ctypes.c_int64 * nd)(*strides), -1, None))
+        for d, (o, oh, ow) in zip(depths, outs):
+            got = o.cpu().numpy()[:, :, :ow * C].reshape(n, oh, ow, C)
+            for i in range(n):
+                ref = c_oracle.ll_int_block(imgs[i], d, border, k)[0]
+                assert np.array_equal(got[i], ref), (n, H, W, C, d, border, i)
+
+
+def test_multi_uniform_scratch_beyond_min_allocation(coder):
+    """Pyramid planes larger than the 1 MiB scratch minimum (regression: the
+    level-(dmin+1) plane was once written into the smaller ping-pong buffer)."""
+    import ctypes
+    from wicca_amd import _lib
+    torch = pytest.importorskip("torch")
+    n, H, W, C = 3, 1024, 2048, 3
+    depths = [1, 2, 4]
+    imgs = torch.randint(0, 256, (n, H, W * C), dtype=torch.uint8, device="cuda")
+    outs = []
+    for d in depths:
+        oh, ow = H >> d, W >> d
+        outs.append(torch.empty((n, oh, ow * C), dtype=torch.uint8, device="cuda"))
+    nd = len(depths)
+    _lib.check(_lib.load().wicca_haar_ll_u8_multi_uniform(
+        ctypes.c_void_p(imgs.data_ptr()), n, H, W, C, W * C, H * W * C,
+        (ctypes.c_int * nd)(*depths), nd, 1, 0,
+        (ctypes.c_void_p * nd)(*[o.data_ptr() for o in outs]),
+        (ctypes.c_int64 * nd)(*[o.shape[2] for o in outs]),
+        (ctypes.c_int64 * nd)(*[o.shape[1] * o.shape[2] for o in outs]), -1, None))
+    host = imgs.cpu().numpy().reshape(n, H, W, C)
+    for d, o in zip(depths, outs):
+        got = o.cpu().numpy().reshape(n, H >> d, W >> d, C)
+        for i in range(n):
+            assert np.array_equal(got[i], c_oracle.ll_int_block(host[i], d)[0])

@@ -53,6 +53,10 @@ SIGNATURES = {
     "wicca_haar_ll_u8_multi": (_int, [_p, _i64, _i64, _i64, _i64, ctypes.POINTER(_int), _int,
                                       _int, _int, ctypes.POINTER(_p), ctypes.POINTER(_i64),
                                       _int, _int, _int, _p]),
+    "wicca_haar_ll_u8_multi_uniform": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64,
+                                              ctypes.POINTER(_int), _int, _int, _int,
+                                              ctypes.POINTER(_p), ctypes.POINTER(_i64),
+                                              ctypes.POINTER(_i64), _int, _p]),
     "wicca_synth_u8": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_uint64, _int,
                               _p]),
     "wicca_synth_band_u8": (_int, [_p, _i64, _i64, _i64, _i64, ctypes.c_uint64, _i64, _i64, _int,

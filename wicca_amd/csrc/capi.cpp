@@ -219,8 +219,8 @@ int run_ll(const uint8_t* src, int64_t n, int64_t H, int64_t W, int64_t C, int64
         return fail(WICCA_ERR_NOMEM, "depth %d needs a %lld-byte intermediate plane", depth,
                     (long long)(plane8 * n));
     HIP_TRY(ws->t0.reserve((size_t)(plane8 * n)));
-    HIP_TRY(ws->t1.reserve((size_t)(plane8 * n / 4 + 16)));
-    HIP_TRY(ws->t2.reserve((size_t)(plane8 * n / 16 + 16)));
+    HIP_TRY(ws->t1.reserve((size_t)((h / 2) * (w / 2) * C * 4 * n + 16)));  // level 9
+    HIP_TRY(ws->t2.reserve((size_t)((h / 4) * (w / 4) * C * 4 * n + 16)));  // level 10
     p.dst = (uint8_t*)ws->t0.ptr;
     p.dst_pitch = w * C * 4;
     p.dst_image_stride = plane8;
@@ -240,7 +240,11 @@ int run_ll(const uint8_t* src, int64_t n, int64_t H, int64_t W, int64_t C, int64
             opitch = dst_pitch;
             ostride = dst_stride;
         } else {
-            out = ping[lvl & 1]->ptr;
+            // level 9 (the largest float plane) goes to t1, level 10 to t2, ...
+            DevBuf* nb = ping[(lvl - 9) & 1];
+            if ((size_t)(nh * nw * C * 4 * n) > nb->cap)
+                return fail(WICCA_ERR_ARG, "internal: float level scratch too small");
+            out = nb->ptr;
             opitch = nw * C * 4;
             ostride = nh * nw * C * 4;
         }
@@ -251,6 +255,108 @@ int run_ll(const uint8_t* src, int64_t n, int64_t H, int64_t W, int64_t C, int64
         cur_is_sum = false;
         h = nh;
         w = nw;
+    }
+    return WICCA_OK;
+}
+
+// Several depths (all in 1..8) of a device-resident uniform batch from ONE read
+// of the images: exact block sums at the smallest depth over the image padded
+// to the largest depth, then an integer 2x2 pyramid.  Padding to 2^dmax gives
+// every smaller depth's icon as the top-left crop of its level.
+int run_multi(const uint8_t* src, int64_t n, int64_t H, int64_t W, int64_t C, int64_t src_pitch,
+              int64_t src_stride, const int* depths, int n_depths, int border, int k,
+              uint8_t* const* dsts, const int64_t* dst_pitches, const int64_t* dst_strides,
+              Workspace* ws, hipStream_t stream)
+{
+    bool want[9] = {false};
+    int dmin = 9, dmax = 0;
+    for (int i = 0; i < n_depths; ++i) {
+        want[depths[i]] = true;
+        dmin = std::min(dmin, depths[i]);
+        dmax = std::max(dmax, depths[i]);
+    }
+    // Fast path: the single-pass multi-depth kernel (K5) for depths >= 2; a
+    // requested depth 1 gets its own K1 launch (a second read of the image).
+    const int kmin = std::max(dmin, 2);
+    if (dmax > kmin && wicca::multi_kernel_ok(src, src_pitch, src_stride, W, (int)C, kmin, dmax)) {
+        for (int i = 0; i < n_depths; ++i) {
+            if (depths[i] != 1) continue;
+            bool unused = false;
+            int rc = run_ll<uint8_t>(src, n, H, W, C, src_pitch, src_stride, 1, border, k, dsts[i],
+                                     dst_pitches[i], dst_strides[i], ws, stream, &unused);
+            if (rc) return rc;
+        }
+        wicca::MultiParams mp{};
+        mp.src = src;
+        mp.src_pitch = src_pitch;
+        mp.src_image_stride = src_stride;
+        mp.H = H;
+        mp.W = W;
+        mp.n_images = n;
+        mp.dmax = dmax;
+        mp.border = border;
+        mp.k = saturate_k(k);
+        for (int i = 0; i < n_depths; ++i) {
+            const int d = depths[i];
+            if (d < kmin) continue;
+            mp.want |= 1u << d;
+            mp.dst[d] = dsts[i];
+            mp.dst_pitch[d] = dst_pitches[i];
+            mp.dst_stride[d] = dst_strides[i];
+        }
+        HIP_TRY(wicca::launch_multi(mp, kmin, (int)C, stream));
+        return WICCA_OK;
+    }
+    const int64_t r = (int64_t)1 << dmax;
+    const int64_t Hp = (H + r - 1) / r * r, Wp = (W + r - 1) / r * r;
+    const int64_t h0 = Hp >> dmin, w0 = Wp >> dmin;
+    const int64_t pitch0 = round_up(w0 * C * 4, 16);  // bytes, 16-B aligned rows
+    const int64_t plane0 = pitch0 * h0;
+    HIP_TRY(ws->t0.reserve((size_t)(plane0 * n)));
+    HIP_TRY(ws->t1.reserve((size_t)((h0 / 2) * (w0 / 2) * C * 4 * n + 16)));  // level dmin+1
+    HIP_TRY(ws->t2.reserve((size_t)((h0 / 4) * (w0 / 4) * C * 4 * n + 16)));  // level dmin+2
+    wicca::LLParams p{};
+    p.src = src;
+    p.src_pitch = src_pitch;
+    p.src_image_stride = src_stride;
+    p.H = H;
+    p.W = W;
+    p.n_images = n;
+    p.border = border;
+    p.k = saturate_k(k);
+    p.dst = (uint8_t*)ws->t0.ptr;
+    p.dst_pitch = pitch0;
+    p.dst_image_stride = plane0;
+    p.out_h = h0;
+    p.out_w = w0;
+    HIP_TRY(wicca::launch_block_sum<uint32_t>(p, dmin, (int)C, stream));
+    const uint32_t* cur = (const uint32_t*)ws->t0.ptr;
+    int64_t cur_pitch = pitch0 / 4, cur_stride = plane0 / 4, h = h0, w = w0;
+    DevBuf* ping[2] = {&ws->t1, &ws->t2};
+    for (int t = dmin; t <= dmax; ++t) {
+        uint8_t* icon = nullptr;
+        int64_t ip = 0, is = 0, ih = 0, iw = 0;
+        if (want[t]) {
+            for (int i = 0; i < n_depths; ++i)
+                if (depths[i] == t) {
+                    icon = dsts[i];
+                    ip = dst_pitches[i];
+                    is = dst_strides[i];
+                }
+            icon_dims(H, W, t, &ih, &iw);
+        }
+        // level dmin+1 (the largest) goes to t1, dmin+2 to t2, then alternating
+        DevBuf* nb = ping[(t - dmin) & 1];
+        uint32_t* next = t < dmax ? (uint32_t*)nb->ptr : nullptr;
+        if (next && (size_t)((h / 2) * (w / 2) * C * 4 * n) > nb->cap)
+            return fail(WICCA_ERR_ARG, "internal: pyramid scratch too small");
+        HIP_TRY(wicca::launch_pyramid_step(cur, cur_pitch, cur_stride, h, w, (int)C, n, t, icon, ih,
+                                           iw, ip, is, next, stream));
+        cur = next;
+        h /= 2;
+        w /= 2;
+        cur_pitch = w * C;
+        cur_stride = h * w * C;
     }
     return WICCA_OK;
 }
@@ -505,6 +611,13 @@ int wicca_haar_ll_u8_multi(const uint8_t* src, int64_t H, int64_t W, int64_t C, 
     if (n_depths < 0 || (n_depths > 0 && (!depths || !dsts || !dst_pitches)))
         return fail(WICCA_ERR_ARG, "bad depth list");
     if (n_depths == 0) return WICCA_OK;
+    for (int i = 0; i < n_depths; ++i) {
+        if (depths[i] > 30) return fail(WICCA_ERR_ARG, "depth %d too large", depths[i]);
+        if (!dsts[i]) return fail(WICCA_ERR_ARG, "dst %d is NULL", i);
+        int64_t oh, ow;
+        icon_dims(H, W, depths[i], &oh, &ow);
+        if (dst_pitches[i] < ow * C) return fail(WICCA_ERR_ARG, "dst pitch %d too small", i);
+    }
     int dev;
     if ((rc = select_device(device, &dev))) return rc;
     WorkspaceLease lease;
@@ -520,32 +633,108 @@ int wicca_haar_ll_u8_multi(const uint8_t* src, int64_t H, int64_t W, int64_t C, 
                                  hipMemcpyHostToDevice, stream));
         dsrc = (const uint8_t*)ws->in.ptr;
     }
+    // device-side icon buffers (host destinations are staged in ws->out)
+    std::vector<uint8_t*> ddst((size_t)n_depths);
+    std::vector<int64_t> dpitch((size_t)n_depths), dstride((size_t)n_depths, 0);
+    std::vector<int64_t> oh((size_t)n_depths), ow((size_t)n_depths);
+    int64_t out_bytes = 0;
     for (int i = 0; i < n_depths; ++i) {
-        if (depths[i] > 30) return fail(WICCA_ERR_ARG, "depth %d too large", depths[i]);
-        if (!dsts[i]) return fail(WICCA_ERR_ARG, "dst %d is NULL", i);
-        int64_t oh, ow;
-        icon_dims(H, W, depths[i], &oh, &ow);
-        if (dst_pitches[i] < ow * C) return fail(WICCA_ERR_ARG, "dst pitch %d too small", i);
-        void* ddst = dsts[i];
-        int64_t dpo = dst_pitches[i];
-        if (!dst_is_device) {
-            dpo = round_up(ow * C, 16);
-            HIP_TRY(ws->out.reserve((size_t)(dpo * oh)));
-            ddst = ws->out.ptr;
-        }
-        bool used_scratch = false;
-        rc = run_ll<uint8_t>(dsrc, 1, H, W, C, dpitch_in, 0, depths[i], border_type,
-                             border_constant, ddst, dpo, 0, ws, stream, &used_scratch);
-        if (rc) return rc;
-        if (!dst_is_device) {
-            HIP_TRY(hipMemcpy2DAsync(dsts[i], dst_pitches[i], ddst, dpo, ow * C, oh,
-                                     hipMemcpyDeviceToHost, stream));
-            HIP_TRY(hipStreamSynchronize(stream));  // ws->out is reused by the next depth
-        } else if (used_scratch) {
-            HIP_TRY(hipStreamSynchronize(stream));
+        icon_dims(H, W, depths[i], &oh[i], &ow[i]);
+        if (!dst_is_device) out_bytes += round_up(ow[i] * C, 16) * oh[i];
+    }
+    if (!dst_is_device) HIP_TRY(ws->out.reserve((size_t)out_bytes));
+    int64_t off = 0;
+    for (int i = 0; i < n_depths; ++i) {
+        if (dst_is_device) {
+            ddst[i] = dsts[i];
+            dpitch[i] = dst_pitches[i];
+        } else {
+            ddst[i] = (uint8_t*)ws->out.ptr + off;
+            dpitch[i] = round_up(ow[i] * C, 16);
+            off += dpitch[i] * oh[i];
         }
     }
-    if (!stream_in || !src_is_device) HIP_TRY(hipStreamSynchronize(stream));
+    // depths 1..8 share one read; the rest (<= 0 copies, > 8 float tails) go alone
+    std::vector<int> shared;
+    std::vector<uint8_t*> sd;
+    std::vector<int64_t> sp, ss;
+    bool used_scratch = false;
+    for (int i = 0; i < n_depths; ++i) {
+        if (depths[i] >= 1 && depths[i] <= 8) {
+            if (std::find(shared.begin(), shared.end(), depths[i]) == shared.end()) {
+                shared.push_back(depths[i]);
+                sd.push_back(ddst[i]);
+                sp.push_back(dpitch[i]);
+                ss.push_back(0);
+            } else {  // repeated depth: copy after the shared pass
+                continue;
+            }
+        } else {
+            rc = run_ll<uint8_t>(dsrc, 1, H, W, C, dpitch_in, 0, depths[i], border_type,
+                                 border_constant, ddst[i], dpitch[i], 0, ws, stream, &used_scratch);
+            if (rc) return rc;
+            if (used_scratch) HIP_TRY(hipStreamSynchronize(stream));
+        }
+    }
+    if (shared.size() == 1) {
+        rc = run_ll<uint8_t>(dsrc, 1, H, W, C, dpitch_in, 0, shared[0], border_type,
+                             border_constant, sd[0], sp[0], 0, ws, stream, &used_scratch);
+        if (rc) return rc;
+    } else if (shared.size() > 1) {
+        rc = run_multi(dsrc, 1, H, W, C, dpitch_in, 0, shared.data(), (int)shared.size(),
+                       border_type, border_constant, sd.data(), sp.data(), ss.data(), ws, stream);
+        if (rc) return rc;
+        used_scratch = true;
+    }
+    for (int i = 0; i < n_depths; ++i) {  // repeated depths
+        if (depths[i] < 1 || depths[i] > 8) continue;
+        const size_t first = (size_t)(std::find(shared.begin(), shared.end(), depths[i]) -
+                                      shared.begin());
+        if (sd[first] != ddst[i])
+            HIP_TRY(hipMemcpy2DAsync(ddst[i], dpitch[i], sd[first], sp[first], ow[i] * C, oh[i],
+                                     hipMemcpyDeviceToDevice, stream));
+    }
+    if (!dst_is_device)
+        for (int i = 0; i < n_depths; ++i)
+            HIP_TRY(hipMemcpy2DAsync(dsts[i], dst_pitches[i], ddst[i], dpitch[i], ow[i] * C, oh[i],
+                                     hipMemcpyDeviceToHost, stream));
+    if (!stream_in || !src_is_device || !dst_is_device || used_scratch)
+        HIP_TRY(hipStreamSynchronize(stream));
+    return WICCA_OK;
+}
+
+int wicca_haar_ll_u8_multi_uniform(const uint8_t* src, int64_t n, int64_t H, int64_t W, int64_t C,
+                                   int64_t src_pitch, int64_t src_image_stride, const int* depths,
+                                   int n_depths, int border_type, int border_constant,
+                                   uint8_t* const* dsts, const int64_t* dst_pitches,
+                                   const int64_t* dst_image_strides, int device, void* stream_in)
+{
+    if (n < 0) return fail(WICCA_ERR_ARG, "negative batch size");
+    if (n == 0 || n_depths == 0) return WICCA_OK;
+    int rc = check_image(src, H, W, C, src_pitch, 0, border_type);
+    if (rc) return rc;
+    if (!depths || !dsts || !dst_pitches || !dst_image_strides)
+        return fail(WICCA_ERR_ARG, "bad depth list");
+    for (int i = 0; i < n_depths; ++i) {
+        if (depths[i] < 1 || depths[i] > 8)
+            return fail(WICCA_ERR_ARG, "multi-depth batches take depths 1..8 (got %d)", depths[i]);
+        for (int j = 0; j < i; ++j)
+            if (depths[j] == depths[i]) return fail(WICCA_ERR_ARG, "repeated depth %d", depths[i]);
+        int64_t oh, ow;
+        icon_dims(H, W, depths[i], &oh, &ow);
+        if (!dsts[i] || dst_pitches[i] < ow * C || (n > 1 && dst_image_strides[i] < dst_pitches[i] * oh))
+            return fail(WICCA_ERR_ARG, "bad icon buffer for depth %d", depths[i]);
+    }
+    int dev;
+    if ((rc = select_device(device, &dev))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    hipStream_t stream = stream_in ? (hipStream_t)stream_in : lease.ws->stream;
+    rc = run_multi(src, n, H, W, C, src_pitch, src_image_stride, depths, n_depths, border_type,
+                   border_constant, dsts, dst_pitches, dst_image_strides, lease.ws, stream);
+    if (rc) return rc;
+    // the block-sum planes live in the workspace: finish before it returns
+    HIP_TRY(hipStreamSynchronize(stream));
     return WICCA_OK;
 }
 

@@ -73,6 +73,24 @@ struct LLParams {
     int64_t total_blocks;
 };
 
+// Multi-depth kernel parameters (icons of every wanted depth from one read).
+struct MultiParams {
+    const uint8_t* src;
+    int64_t src_pitch, src_image_stride;
+    int64_t H, W, n_images;
+    int64_t n_bands;   // bands of 2^dmax rows per image (set by the launcher)
+    int32_t n_groups;  // groups of 4 wave strips per band (set by the launcher)
+    int32_t dmax;
+    uint32_t want;     // bit t set: write the icon of depth t
+    int32_t border;    // 0 constant, 1 replicate
+    uint32_t k;
+    uint8_t* dst[9];   // per depth t: icon base, row pitch, image stride
+    int64_t dst_pitch[9], dst_stride[9];
+};
+bool multi_kernel_ok(const uint8_t* src, int64_t src_pitch, int64_t src_stride, int64_t W, int C,
+                     int dmin, int dmax);
+hipError_t launch_multi(MultiParams p, int dmin, int C, hipStream_t s);
+
 int64_t segments_for(int64_t out_w, int L, int C);  // column groups per icon row
 bool fast_path_ok(const LLParams& p, int L, int C);
 
@@ -87,6 +105,13 @@ hipError_t launch_block_sum(LLParams p, int L, int C, hipStream_t stream);
 hipError_t launch_level_f32(const void* in, int64_t in_pitch, int64_t in_img_stride, bool in_sum,
                             void* out, int64_t out_pitch, int64_t out_img_stride, bool out_u8,
                             int64_t n_img, int64_t out_h, int64_t out_w, int C, hipStream_t s);
+
+// One level of the exact integer pyramid (multi-depth icons from one read).
+//   in_pitch / in_stride in uint32 elements; `next` is written dense.
+hipError_t launch_pyramid_step(const uint32_t* in, int64_t in_pitch, int64_t in_stride, int64_t h,
+                               int64_t w, int C, int64_t n_img, int t, uint8_t* icon,
+                               int64_t icon_h, int64_t icon_w, int64_t icon_pitch,
+                               int64_t icon_stride, uint32_t* next, hipStream_t s);
 
 hipError_t launch_synth(uint8_t* dst, int64_t n, int64_t H, int64_t WC, int64_t pitch,
                         int64_t image_stride, uint64_t seed, int64_t first_image,

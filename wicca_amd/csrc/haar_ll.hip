@@ -37,6 +37,8 @@ namespace wicca {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+static inline bool aligned16(const void* ptr, int64_t pitch, int64_t stride);
+
 
 constexpr int kThreads = 256;
 constexpr int kSegPx = kThreads * 16;  // pixels per segment (16 per lane)
@@ -735,6 +737,335 @@ __global__ __launch_bounds__(kThreads) void haar_level_f32_kernel(
             reinterpret_cast<float*>(orow)[j * C + c] = v;
         }
     }
+}
+
+// ----------------------------------------------------------------------------
+// K5: multi-depth wave-strip kernel — icons of every wanted depth in
+// [DMIN, dmax] from ONE read of the image (the caller's
+// depth loop, classifying_tools.py:546-551).
+//
+// Geometry as K1s (a lane owns P whole pixels, a wave a 64*P-pixel strip, a
+// workgroup 4 strips of one band of 2^dmax rows of the image padded to
+// 2^dmax; padding to 2^dmax yields every smaller depth's icon as the top-left
+// crop of its level).  Rows stream in chunks of CH rows, the next
+// chunk in flight while the current one is reduced.  Each completed block of
+// 2^DMIN rows feeds a per-lane binary counter of packed-u16 column sums, one
+// register set per level: two completed level-t row blocks add into one
+// level-(t+1) block (u16 holds 2^t * 255 for t <= 8).  Every completed level
+// emits its icon-row segment at once, so no intermediate plane reaches HBM:
+// traffic = image + icons.
+// ----------------------------------------------------------------------------
+struct MultiCtx {
+    int64_t spx0, lpx0, y_band;
+    int lane, band, img;
+    bool replicate, tail;
+};
+
+template <int LV, int C>
+__device__ __forceinline__ void emit_level(const MultiParams& p, const MultiCtx& x, int idx,
+                                           const uint32_t (&lo)[StripGeom<C>::NDW],
+                                           const uint32_t (&hi)[StripGeom<C>::NDW])
+{
+    using Geo = StripGeom<C>;
+    constexpr int P = Geo::P, STRIP = Geo::STRIP;
+    constexpr int G = 1 << LV;
+    constexpr int NJ = G <= P ? P / G : 1;
+    constexpr int GL = G <= P ? 1 : G / P;
+    constexpr int GI = G <= P ? G : P;  // pixels of one icon inside a lane
+    const int64_t oy = ((int64_t)x.band << (p.dmax - LV)) + idx;
+    if (oy >= ((p.H + G - 1) >> LV)) return;  // wave-uniform: a row that exists only as padding
+    const int64_t ox0 = x.spx0 >> LV;
+    const int n_out = (int)min<int64_t>(STRIP / G, ((p.W + G - 1) >> LV) - ox0);
+    if (n_out <= 0) return;  // wave-uniform
+
+    uint32_t cs[P][C];
+#pragma unroll
+    for (int q = 0; q < P; ++q)
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const int byte = q * C + c;
+            const uint32_t r = (byte & 1) ? hi[byte >> 2] : lo[byte >> 2];
+            cs[q][c] = ((byte >> 1) & 1) ? (r >> 16) : (r & 0xFFFFu);
+        }
+    if (x.tail) {  // right padding: the strip holding column W-1 holds every pad column
+        uint32_t last[C];
+        if (!x.replicate) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) last[c] = 0;
+        } else {
+            const int hl = (int)((p.W - 1 - x.spx0) / P);
+            const int hq = (int)((p.W - 1 - x.spx0) % P);
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                uint32_t mine = 0;
+#pragma unroll
+                for (int q = 0; q < P; ++q) mine = (q == hq) ? cs[q][c] : mine;
+                last[c] = __shfl(mine, hl, 64);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < P; ++q) {
+            const bool real = x.lpx0 + q < p.W;
+#pragma unroll
+            for (int c = 0; c < C; ++c) cs[q][c] = real ? cs[q][c] : last[c];
+        }
+    }
+    uint32_t s[NJ][C];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            uint32_t t = 0;
+#pragma unroll
+            for (int q = 0; q < GI; ++q) t += cs[j * GI + q][c];
+            s[j][c] = t;
+        }
+    if constexpr (GL > 1) {
+#pragma unroll
+        for (int m = 1; m < GL; m <<= 1)
+#pragma unroll
+            for (int c = 0; c < C; ++c) s[0][c] += __shfl_xor(s[0][c], m, 64);
+    }
+    const int64_t yb = x.y_band + (int64_t)idx * G;
+    const int rows_real = (int)min<int64_t>(max<int64_t>(p.H - yb, 0), G);
+    uint8_t* drow = p.dst[LV] + (int64_t)x.img * p.dst_stride[LV] + oy * p.dst_pitch[LV] + ox0 * C;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int o = (GL > 1) ? x.lane / GL : x.lane * NJ + j;
+        const bool writer = (GL > 1) ? (x.lane % GL) == 0 : true;
+        if (writer && o < n_out) {
+            uint32_t pad_cells = 0;
+            if (!x.replicate) {
+                const int64_t cols_real = min<int64_t>(max<int64_t>(p.W - ((ox0 + o) << LV), 0), G);
+                pad_cells = (uint32_t)(G * G) - (uint32_t)(rows_real * cols_real);
+            }
+#pragma unroll
+            for (int c = 0; c < C; ++c)
+                drow[o * C + c] = (uint8_t)((s[j][c] + p.k * pad_cells) >> (2 * LV));
+        }
+    }
+}
+
+// Binary-counter carry from level L upward (compile-time L keeps the pending
+// registers in VGPRs).
+template <int L, int DMIN, int DMAX, int C>
+struct Cascade {
+    static constexpr int NDW = StripGeom<C>::NDW;
+    static __device__ __forceinline__ void run(const MultiParams& p, const MultiCtx& x, int count,
+                                               uint32_t (&lo)[NDW], uint32_t (&hi)[NDW],
+                                               uint32_t (&plo)[DMAX - DMIN][NDW],
+                                               uint32_t (&phi)[DMAX - DMIN][NDW])
+    {
+        if constexpr (L < DMAX) {
+            const int idx = (count >> (L - DMIN)) - 1;  // index of the completed level-L block
+            if ((idx & 1) == 0) {                      // first half of a level-(L+1) block
+#pragma unroll
+                for (int j = 0; j < NDW; ++j) { plo[L - DMIN][j] = lo[j]; phi[L - DMIN][j] = hi[j]; }
+                return;
+            }
+#pragma unroll
+            for (int j = 0; j < NDW; ++j) { lo[j] += plo[L - DMIN][j]; hi[j] += phi[L - DMIN][j]; }
+            if ((p.want >> (L + 1)) & 1) emit_level<L + 1, C>(p, x, idx >> 1, lo, hi);
+            Cascade<L + 1, DMIN, DMAX, C>::run(p, x, count, lo, hi, plo, phi);
+        }
+    }
+};
+
+template <int DMIN, int DMAX, int C>
+__global__ __launch_bounds__(kThreads) void haar_multi_kernel(MultiParams p)
+{
+    using Geo = StripGeom<C>;
+    constexpr int NDW = Geo::NDW, STRIP = Geo::STRIP;
+    constexpr int SB = 1 << DMIN;              // rows per level-DMIN block
+    constexpr int CH = SB < 8 ? SB : 8;        // rows per load chunk (divides SB)
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    uint32_t b = blockIdx.x;
+    const int g = (int)(b % (uint32_t)p.n_groups);
+    b /= (uint32_t)p.n_groups;
+    const int band = (int)(b % (uint32_t)p.n_bands);
+    const int img = (int)(b / (uint32_t)p.n_bands);
+    constexpr int R = 1 << DMAX;
+    const int64_t Wp = ((p.W + R - 1) >> DMAX) << DMAX;
+    MultiCtx x;
+    x.spx0 = (int64_t)(g * 4 + wave) * STRIP;
+    if (x.spx0 >= Wp) return;  // whole wave idle (no workgroup barriers in this kernel)
+    x.lane = lane;
+    x.band = band;
+    x.img = img;
+    x.lpx0 = x.spx0 + (int64_t)lane * Geo::P;
+    x.y_band = (int64_t)band << DMAX;
+    x.replicate = p.border == 1;
+    x.tail = x.spx0 + STRIP > p.W;
+
+    const uint8_t* src = p.src + (int64_t)img * p.src_image_stride;
+    const int64_t last_row = p.H - 1;
+    const uint32_t nrec = (uint32_t)((p.W * C + 15) & ~(int64_t)15);
+    const uint32_t voff = (uint32_t)(x.lpx0 * C);
+    auto issue = [&](uint32_t (&d)[CH][NDW], int ci) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const uint8_t* row = src + min<int64_t>(x.y_band + ci * CH + u, last_row) * p.src_pitch;
+            load_lane<NDW>(d[u], row, nrec, voff);
+        }
+    };
+    uint32_t lo[NDW], hi[NDW], plo[DMAX - DMIN][NDW], phi[DMAX - DMIN][NDW];
+#pragma unroll
+    for (int j = 0; j < NDW; ++j) { lo[j] = 0; hi[j] = 0; }
+    constexpr int nchunks = R / CH;
+    uint32_t da[CH][NDW];
+    issue(da, 0);
+#pragma unroll 1
+    for (int ci = 0; ci < nchunks; ++ci) {
+        uint32_t db[CH][NDW];
+        if (ci + 1 < nchunks) issue(db, ci + 1);
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int64_t y = x.y_band + ci * CH + u;
+            const uint32_t m = (x.replicate || y < p.H) ? 0x00FF00FFu : 0u;
+#pragma unroll
+            for (int j = 0; j < NDW; ++j) {
+                lo[j] += da[u][j] & m;
+                hi[j] += (da[u][j] >> 8) & m;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < CH; ++u)
+#pragma unroll
+            for (int j = 0; j < NDW; ++j) da[u][j] = db[u][j];
+        if ((((ci + 1) * CH) & (SB - 1)) == 0) {  // a level-DMIN block is complete
+            const int count = ((ci + 1) * CH) >> DMIN;
+            if ((p.want >> DMIN) & 1) emit_level<DMIN, C>(p, x, count - 1, lo, hi);
+            Cascade<DMIN, DMIN, DMAX, C>::run(p, x, count, lo, hi, plo, phi);
+#pragma unroll
+            for (int j = 0; j < NDW; ++j) { lo[j] = 0; hi[j] = 0; }
+        }
+    }
+}
+
+template <int DMIN, int DMAX, int C>
+static hipError_t launch_multi_k(const MultiParams& p, int64_t blocks, hipStream_t s)
+{
+    if constexpr (DMIN < DMAX) {
+        hipLaunchKernelGGL((haar_multi_kernel<DMIN, DMAX, C>), dim3((uint32_t)blocks), dim3(kThreads),
+                           0, s, p);
+        return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int DMIN, int C>
+static hipError_t launch_multi_dc(int dmax, const MultiParams& p, int64_t blocks, hipStream_t s)
+{
+    switch (dmax) {
+    case 2: return launch_multi_k<DMIN, 2, C>(p, blocks, s);
+    case 3: return launch_multi_k<DMIN, 3, C>(p, blocks, s);
+    case 4: return launch_multi_k<DMIN, 4, C>(p, blocks, s);
+    case 5: return launch_multi_k<DMIN, 5, C>(p, blocks, s);
+    case 6: return launch_multi_k<DMIN, 6, C>(p, blocks, s);
+    case 7: return launch_multi_k<DMIN, 7, C>(p, blocks, s);
+    case 8: return launch_multi_k<DMIN, 8, C>(p, blocks, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <int C>
+static hipError_t launch_multi_c(int dmin, const MultiParams& p, int64_t blocks, hipStream_t s)
+{
+    switch (dmin) {  // depth 1 is served by K1 (a 2-row block per step starves the stream)
+    case 2: return launch_multi_dc<2, C>(p.dmax, p, blocks, s);
+    case 3: return launch_multi_dc<3, C>(p.dmax, p, blocks, s);
+    case 4: return launch_multi_dc<4, C>(p.dmax, p, blocks, s);
+    case 5: return launch_multi_dc<5, C>(p.dmax, p, blocks, s);
+    case 6: return launch_multi_dc<6, C>(p.dmax, p, blocks, s);
+    case 7: return launch_multi_dc<7, C>(p.dmax, p, blocks, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+bool multi_kernel_ok(const uint8_t* src, int64_t src_pitch, int64_t src_stride, int64_t W, int C,
+                     int dmin, int dmax)
+{
+    return C >= 1 && C <= 4 && dmin >= 2 && dmin < dmax && dmax <= 8 &&
+           W * C < ((int64_t)1 << 30) && aligned16(src, src_pitch, src_stride);
+}
+
+hipError_t launch_multi(MultiParams p, int dmin, int C, hipStream_t s)
+{
+    const int64_t R = (int64_t)1 << p.dmax;
+    const int64_t Hp = (p.H + R - 1) / R * R, Wp = (p.W + R - 1) / R * R;
+    const int64_t strip = 64 * ((C == 3) ? 4 : 16 / C);
+    p.n_bands = Hp / R;
+    p.n_groups = (int32_t)(((Wp + strip - 1) / strip + 3) / 4);
+    const int64_t blocks = p.n_images * p.n_bands * p.n_groups;
+    if (blocks <= 0) return hipSuccess;
+    if (blocks >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
+    switch (C) {
+    case 1: return launch_multi_c<1>(dmin, p, blocks, s);
+    case 2: return launch_multi_c<2>(dmin, p, blocks, s);
+    case 3: return launch_multi_c<3>(dmin, p, blocks, s);
+    case 4: return launch_multi_c<4>(dmin, p, blocks, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// ----------------------------------------------------------------------------
+// K4: integer pyramid step for multi-depth icons.
+// Input: exact block sums S_t (uint32, h x w x C) of the 2^dmax-padded image.
+// Writes icon_t = S_t >> 2t for the cropped (icon_h, icon_w) window when
+// `icon` is set, and S_{t+1} (2x2 sums, exact) when `next` is set.  One lane
+// per S_{t+1} element (or per S_t element on the last level).
+// ----------------------------------------------------------------------------
+__global__ __launch_bounds__(kThreads) void pyramid_step_kernel(
+    const uint32_t* in, int64_t in_pitch, int64_t in_stride, int64_t h, int64_t w, int C,
+    int64_t n_img, int t, uint8_t* icon, int64_t icon_h, int64_t icon_w, int64_t icon_pitch,
+    int64_t icon_stride, uint32_t* next)
+{
+    const int64_t nh = next ? h / 2 : h, nw = next ? w / 2 : w;
+    const int64_t per = nh * nw * C;
+    const int64_t total = per * n_img;
+    for (int64_t e = blockIdx.x * (int64_t)kThreads + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * kThreads) {
+        const int64_t img = e / per;
+        int64_t rem = e - img * per;
+        const int64_t i = rem / (nw * C);
+        rem -= i * nw * C;
+        const int64_t j = rem / C;
+        const int c = (int)(rem - j * C);
+        const uint32_t* base = in + img * in_stride;
+        uint8_t* ibase = icon ? icon + img * icon_stride : nullptr;
+        if (!next) {
+            const uint32_t v = base[i * in_pitch + j * C + c];
+            if (icon && i < icon_h && j < icon_w) ibase[i * icon_pitch + j * C + c] = (uint8_t)(v >> (2 * t));
+            continue;
+        }
+        uint32_t acc = 0;
+#pragma unroll
+        for (int di = 0; di < 2; ++di)
+#pragma unroll
+            for (int dj = 0; dj < 2; ++dj) {
+                const int64_t ii = 2 * i + di, jj = 2 * j + dj;
+                const uint32_t v = base[ii * in_pitch + jj * C + c];
+                acc += v;
+                if (icon && ii < icon_h && jj < icon_w)
+                    ibase[ii * icon_pitch + jj * C + c] = (uint8_t)(v >> (2 * t));
+            }
+        next[img * nh * nw * C + (i * nw + j) * C + c] = acc;
+    }
+}
+
+hipError_t launch_pyramid_step(const uint32_t* in, int64_t in_pitch, int64_t in_stride, int64_t h,
+                               int64_t w, int C, int64_t n_img, int t, uint8_t* icon,
+                               int64_t icon_h, int64_t icon_w, int64_t icon_pitch,
+                               int64_t icon_stride, uint32_t* next, hipStream_t s)
+{
+    const int64_t total = (next ? (h / 2) * (w / 2) : h * w) * C * n_img;
+    if (total <= 0) return hipSuccess;
+    const uint32_t blocks = (uint32_t)std::min<int64_t>((total + kThreads - 1) / kThreads, 256 * 64);
+    hipLaunchKernelGGL(pyramid_step_kernel, dim3(blocks), dim3(kThreads), 0, s, in, in_pitch,
+                       in_stride, h, w, C, n_img, t, icon, icon_h, icon_w, icon_pitch, icon_stride,
+                       next);
+    return hipGetLastError();
 }
 
 // ----------------------------------------------------------------------------
