@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -138,6 +139,21 @@ int select_device(int device, int* out)
 }
 
 inline int64_t round_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+// Upload `height` rows of `width` bytes from host memory (row pitch spitch)
+// to device memory (row pitch dpitch) on `stream`.  One hipMemcpy2DAsync from
+// pageable memory: the runtime's own staging measured 49 GB/s single-threaded
+// and 55 GB/s from 4-16 threads on MI355X (PCIe Gen5 x16, 63 GB/s spec),
+// ahead of a 2-slot pinned ring with CPU copies (32 / 51 GB/s) and of pinning
+// the caller's buffer in place (no faster, and unsafe when two threads pass
+// the same array) — tools/host_path_bench.py, profiles/r01_host_path.jsonl.
+int upload_rows(Workspace*, void* dst, int64_t dpitch, const uint8_t* src, int64_t spitch,
+                int64_t width, int64_t height, hipStream_t stream)
+{
+    HIP_TRY(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyHostToDevice,
+                             stream));
+    return WICCA_OK;
+}
 
 void icon_dims(int64_t H, int64_t W, int depth, int64_t* oh, int64_t* ow)
 {
@@ -386,8 +402,8 @@ int single_image(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t sr
     if (!src_is_device) {
         dpitch_in = round_up(W * C, 64);
         HIP_TRY(ws->in.reserve((size_t)(dpitch_in * H)));
-        HIP_TRY(hipMemcpy2DAsync(ws->in.ptr, dpitch_in, src, src_pitch, W * C, H,
-                                 hipMemcpyHostToDevice, stream));
+        rc = upload_rows(ws, ws->in.ptr, dpitch_in, src, src_pitch, W * C, H, stream);
+        if (rc) return rc;
         dsrc = (const uint8_t*)ws->in.ptr;
     }
     void* ddst = dst;
@@ -519,8 +535,9 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
         for (int64_t i = 0; i < n; ++i) {
             const int64_t pitch = round_up(d[i].width * C, 64);
             uint8_t* p = (uint8_t*)ws->in.ptr + off;
-            HIP_TRY(hipMemcpy2DAsync(p, pitch, descs_in[i].src, descs_in[i].src_pitch,
-                                     d[i].width * C, d[i].height, hipMemcpyHostToDevice, stream));
+            rc = upload_rows(ws, p, pitch, descs_in[i].src, descs_in[i].src_pitch, d[i].width * C,
+                             d[i].height, stream);
+            if (rc) return rc;
             d[i].src = p;
             d[i].src_pitch = pitch;
             off += pitch * d[i].height;
@@ -629,8 +646,8 @@ int wicca_haar_ll_u8_multi(const uint8_t* src, int64_t H, int64_t W, int64_t C, 
     if (!src_is_device) {  // one upload shared by every depth
         dpitch_in = round_up(W * C, 64);
         HIP_TRY(ws->in.reserve((size_t)(dpitch_in * H)));
-        HIP_TRY(hipMemcpy2DAsync(ws->in.ptr, dpitch_in, src, src_pitch, W * C, H,
-                                 hipMemcpyHostToDevice, stream));
+        rc = upload_rows(ws, ws->in.ptr, dpitch_in, src, src_pitch, W * C, H, stream);
+        if (rc) return rc;
         dsrc = (const uint8_t*)ws->in.ptr;
     }
     // device-side icon buffers (host destinations are staged in ws->out)
