@@ -177,7 +177,8 @@ def run_tiled(args, torch, dist, world, rank, local_rank):
         dist.barrier()
     wall = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([wall, kernel_ms], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, kernel_ms = float(t[0]), float(t[1])
     verified = None
@@ -305,11 +306,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
-    torch.cuda.set_device(local_rank)
+    # one rank per GPU; the modulo only matters for a rehearsal with more ranks
+    # than GPUs (WICCA_BENCH_BACKEND=gloo), never for the driver's runs
+    device = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        backend = os.environ.get("WICCA_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     from wicca_amd import _lib
     lib = _lib.load()
@@ -372,7 +380,8 @@ def main():
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one kernel launch per step
 
     if dist is not None:
-        t = torch.tensor([wall, kernel_ms], dtype=torch.float64, device="cuda")
+        t = torch.tensor([wall, kernel_ms], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall, kernel_ms = float(t[0]), float(t[1])
 

@@ -73,6 +73,36 @@ __global__ __launch_bounds__(256) void read_bands(const unsigned char* __restric
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[0] = 1;
 }
 
+// D=1 / D=2 traffic shape: read a (rows x 12 KiB) band segment, write rows*12KiB/(4^D)
+// bytes of icons with 16-B stores (the icon kernel's bytes, not its arithmetic)
+template <int ROWS, int D>
+__global__ __launch_bounds__(256) void rw_bands(const unsigned char* __restrict__ p, unsigned char* __restrict__ q)
+{
+    const int n_seg = 2, bands = 4320 / ROWS;
+    const int seg = blockIdx.x % n_seg, t = blockIdx.x / n_seg;
+    const int band = t % bands, img = t / bands;
+    const unsigned char* base = p + (size_t)img * 4320 * 23040 + (size_t)band * ROWS * 23040;
+    u32x4 acc = {0, 0, 0, 0};
+    unsigned off[3];
+    for (int k = 0; k < 3; ++k) off[k] = seg * 12288 + k * 4096 + 16 * threadIdx.x;
+    u32x4 v[ROWS][3];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(base + (size_t)r * 23040), (short)0, 23040, 0x00020000);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) v[r][k] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off[k], 0, 2));
+    }
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) acc += v[r][k];
+    // icon bytes of this block: ROWS*12288 / 4^D ; one 16-B store per lane while in range
+    const int out_bytes = ROWS * 12288 >> (2 * D);
+    const int out_row = 23040 >> D;  // icon row pitch (bytes) for this D
+    unsigned char* o = q + (size_t)img * (4320 >> D) * out_row + (size_t)band * (ROWS >> D) * out_row + seg * (12288 >> D);
+    for (int i = threadIdx.x * 16; i < out_bytes; i += 256 * 16) *reinterpret_cast<u32x4*>(o + i) = acc;
+}
+
 __global__ __launch_bounds__(256) void copy4(const u32x4* __restrict__ a, u32x4* __restrict__ b, size_t n)
 {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) b[i] = a[i];
@@ -117,6 +147,14 @@ int main()
 #define RB(U, NT) if (U <= rpb) { float ms = timeit([&] { hipLaunchKernelGGL((read_bands<U, NT>), dim3(blocks), dim3(256), 0, 0, (const unsigned char*)p, rpb, out); }, reps); \
         printf("read_bands rows=%d U=%d nt=%d blocks=%d  %.3f ms  %.1f GB/s\n", rpb, U, (int)NT, blocks, ms, (double)bytes / ms / 1e6); }
         RB(2, true) RB(4, true) RB(8, true) RB(4, false) RB(8, false)
+    }
+    {
+        unsigned char* q;
+        CK(hipMalloc(&q, bytes / 4 + (1 << 20)));
+#define RW(ROWS, D) { int blocks = 128 * (4320 / ROWS) * 2; float ms = timeit([&] { hipLaunchKernelGGL((rw_bands<ROWS, D>), dim3(blocks), dim3(256), 0, 0, (const unsigned char*)p, q); }, reps); \
+        double tot = (double)bytes * (1.0 + 1.0 / (1 << (2 * D))); printf("rw_bands rows=%d D=%d  %.3f ms  %.1f GB/s (read+write)\n", ROWS, D, ms, tot / ms / 1e6); }
+        RW(2, 1) RW(4, 1) RW(8, 1) RW(4, 2) RW(8, 2) RW(8, 3)
+        CK(hipFree(q));
     }
     CK(hipFree(p));
     const size_t cb = 4ull << 30;
