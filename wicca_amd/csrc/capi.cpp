@@ -291,17 +291,20 @@ int run_multi(const uint8_t* src, int64_t n, int64_t H, int64_t W, int64_t C, in
         dmin = std::min(dmin, depths[i]);
         dmax = std::max(dmax, depths[i]);
     }
-    // Fast path: the single-pass multi-depth kernel (K5) for depths >= 2; a
-    // requested depth 1 gets its own K1 launch (a second read of the image).
+    // Fast path (aligned rows, C <= 4): depth 1 and a lone depth >= 2 get their
+    // own K1 launch; two or more depths >= 2 share ONE read in K5.
     const int kmin = std::max(dmin, 2);
-    if (dmax > kmin && wicca::multi_kernel_ok(src, src_pitch, src_stride, W, (int)C, kmin, dmax)) {
+    if (wicca::multi_kernel_ok(src, src_pitch, src_stride, W, (int)C, 2, 3)) {
+        int n_k5 = 0;
+        for (int d = 2; d <= 8; ++d) n_k5 += want[d] ? 1 : 0;
         for (int i = 0; i < n_depths; ++i) {
-            if (depths[i] != 1) continue;
+            if (depths[i] != 1 && n_k5 >= 2) continue;
             bool unused = false;
-            int rc = run_ll<uint8_t>(src, n, H, W, C, src_pitch, src_stride, 1, border, k, dsts[i],
-                                     dst_pitches[i], dst_strides[i], ws, stream, &unused);
+            int rc = run_ll<uint8_t>(src, n, H, W, C, src_pitch, src_stride, depths[i], border, k,
+                                     dsts[i], dst_pitches[i], dst_strides[i], ws, stream, &unused);
             if (rc) return rc;
         }
+        if (n_k5 < 2) return WICCA_OK;
         wicca::MultiParams mp{};
         mp.src = src;
         mp.src_pitch = src_pitch;
@@ -323,6 +326,8 @@ int run_multi(const uint8_t* src, int64_t n, int64_t H, int64_t W, int64_t C, in
         HIP_TRY(wicca::launch_multi(mp, kmin, (int)C, stream));
         return WICCA_OK;
     }
+    // Generic layouts: exact uint32 block sums at dmin over the image padded to
+    // 2^dmax, then an integer 2x2 pyramid (one read of the image, planes in HBM).
     const int64_t r = (int64_t)1 << dmax;
     const int64_t Hp = (H + r - 1) / r * r, Wp = (W + r - 1) / r * r;
     const int64_t h0 = Hp >> dmin, w0 = Wp >> dmin;

@@ -8,16 +8,10 @@
 #ifndef WICCA_NT_LOADS
 #define WICCA_NT_LOADS 1      // non-temporal loads for the once-read image stream
 #endif
-#ifndef WICCA_BUFFER_LOADS
-#define WICCA_BUFFER_LOADS 1  // buffer_load with a per-row descriptor
-#endif
 #ifndef WICCA_CHUNK_ROWS
 #define WICCA_CHUNK_ROWS 0    // rows per load chunk (C dwordx4 per lane per row); 0 = table
 #endif
 
-#ifndef WICCA_PIPE
-#define WICCA_PIPE 0          // software-pipeline the row chunks inside a band
-#endif
 #ifndef WICCA_STRIP
 #define WICCA_STRIP -1        // 1: wave-strip kernel, 0: LDS-segment kernel, -1: per-depth table
 #endif

@@ -86,15 +86,6 @@ __device__ __forceinline__ BlockWork resolve_block(const LLParams& p)
     return w;
 }
 
-__device__ __forceinline__ u32x4 load16(const uint8_t* p)
-{
-#if WICCA_NT_LOADS
-    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-#else
-    return *reinterpret_cast<const u32x4*>(p);
-#endif
-}
-
 // Packed column sums: lo holds bytes 0,2 of each dword, hi bytes 1,3.
 __device__ __forceinline__ void accumulate(uint32_t (&lo)[4], uint32_t (&hi)[4], u32x4 v)
 {
@@ -151,15 +142,10 @@ __device__ __forceinline__ uint32_t finish<uint32_t>(uint32_t s, int) { return s
 // ----------------------------------------------------------------------------
 __device__ __forceinline__ u32x4 load_row16(const uint8_t* row, uint32_t nrec, uint32_t voff)
 {
-#if WICCA_BUFFER_LOADS
     __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(row), (short)0, (int)nrec, 0x00020000);
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0,
                                                                            WICCA_NT_LOADS ? 2 : 0));
-#else
-    (void)nrec;
-    return load16(row + voff);
-#endif
 }
 
 template <int L, int C, typename OutT, bool RAGGED>
@@ -199,11 +185,7 @@ __global__ __launch_bounds__(kThreads) void haar_block_sum_kernel(LLParams p)
     for (int k = 0; k < C; ++k) {
         const int64_t o = px0 * C + (int64_t)k * (kThreads * 16) + 16 * tid;  // byte in row
         valid[k] = o < row_bytes;
-#if WICCA_BUFFER_LOADS
         off[k] = (uint32_t)o;  // past the record count -> zeros
-#else
-        off[k] = valid[k] ? (uint32_t)o : 0u;  // invalid lanes re-read byte 0
-#endif
     }
     const uint32_t nrec = (uint32_t)((row_bytes + 15) & ~(int64_t)15);  // inside the pitch
 
@@ -387,27 +369,12 @@ __global__ __launch_bounds__(kThreads) void haar_block_sum_kernel(LLParams p)
     };
 
     zero_acc();
-#if WICCA_PIPE
-    {   // chunk g+1 is in flight while chunk g is reduced (CPB is a constant)
-        u32x4 va[U][C], vb[U][C];
-        issue(va, 0);
-#pragma unroll
-        for (int g = 0; g < CPB; g += 2) {
-            if (g + 1 < CPB) issue(vb, g + 1);
-            consume(va, g);
-            if (g + 1 < CPB) {
-                if (g + 2 < CPB) issue(va, g + 2);
-                consume(vb, g + 1);
-            }
-        }
-    }
-#else
     for (int g = 0; g < CPB; ++g) {
         u32x4 v[U][C];
         issue(v, g);
         consume(v, g);
     }
-#endif
+
     epilogue();
 }
 
@@ -505,27 +472,12 @@ __global__ __launch_bounds__(kThreads) void haar_strip_kernel(LLParams p)
             }
         }
     };
-#if WICCA_PIPE
-    {
-        uint32_t da[U][NDW], db[U][NDW];
-        sissue(da, 0);
-#pragma unroll
-        for (int r0 = 0; r0 < R; r0 += 2 * U) {
-            if (r0 + U < R) sissue(db, r0 + U);
-            sconsume(da, r0);
-            if (r0 + U < R) {
-                if (r0 + 2 * U < R) sissue(da, r0 + 2 * U);
-                sconsume(db, r0 + U);
-            }
-        }
-    }
-#else
     for (int r0 = 0; r0 < R; r0 += U) {
         uint32_t d[U][NDW];
         sissue(d, r0);
         sconsume(d, r0);
     }
-#endif
+
 
     // ---- per-pixel, per-channel column sums of this lane
     auto colsum = [&](int byte) -> uint32_t {
