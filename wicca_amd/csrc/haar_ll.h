@@ -28,6 +28,12 @@ constexpr bool use_strip_kernel(int L)
     return WICCA_STRIP >= 0 ? WICCA_STRIP == 1 : (L == 2 || L == 3);
 }
 
+// Pixels a strip-kernel lane owns: whole pixels in 12 or 16 contiguous bytes,
+// so every wave load instruction is one contiguous 768 B / 1 KiB.  (Lanes of
+// 16 whole RGB pixels — C dwordx4 at a 48-B lane stride — measured 4.3-4.6
+// TB/s against 6.6: strided wave loads cost far more than an LDS transpose.)
+constexpr int strip_lane_pixels(int C) { return C == 3 ? 4 : 16 / C; }
+
 constexpr int strip_chunk_rows(int L)
 {
     return WICCA_STRIP_CHUNK > 0 ? WICCA_STRIP_CHUNK : 16;

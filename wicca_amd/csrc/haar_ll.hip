@@ -374,7 +374,13 @@ __global__ __launch_bounds__(kThreads) void haar_block_sum_kernel(LLParams p)
         issue(v, g);
         consume(v, g);
     }
-
+#ifdef WICCA_ABLATE_EPILOGUE  // timing-only build: stream + reduce, no LDS/store phase
+#pragma unroll
+    for (int k = 0; k < C; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(lo[k][j]), "v"(hi[k][j]));
+    return;
+#endif
     epilogue();
 }
 
@@ -392,8 +398,8 @@ __global__ __launch_bounds__(kThreads) void haar_block_sum_kernel(LLParams p)
 // ----------------------------------------------------------------------------
 template <int C>
 struct StripGeom {
-    static constexpr int P = (C == 3) ? 4 : 16 / C;  // pixels per lane
-    static constexpr int BYTES = P * C;              // 12 or 16
+    static constexpr int P = strip_lane_pixels(C);  // pixels per lane
+    static constexpr int BYTES = P * C;              // 12 or 16 (narrow), 16*C (wide)
     static constexpr int NDW = BYTES / 4;            // dwords per lane
     static constexpr int STRIP = 64 * P;             // pixels per wave
 };
@@ -404,10 +410,13 @@ __device__ __forceinline__ void load_lane(uint32_t (&d)[NDW], const uint8_t* row
 {
     __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(row), (short)0, (int)nrec, 0x00020000);
-    if constexpr (NDW == 4) {
-        const u32x4 v = __builtin_bit_cast(
-            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0, WICCA_NT_LOADS ? 2 : 0));
-        d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+    if constexpr (NDW % 4 == 0) {  // NDW/4 dwordx4 pieces (a wide lane: 16 whole pixels)
+#pragma unroll
+        for (int q = 0; q < NDW / 4; ++q) {
+            const u32x4 v = __builtin_bit_cast(
+                u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16 * q, 0, WICCA_NT_LOADS ? 2 : 0));
+            d[4 * q] = v[0]; d[4 * q + 1] = v[1]; d[4 * q + 2] = v[2]; d[4 * q + 3] = v[3];
+        }
     } else {
         typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
         const u32x3 v = __builtin_bit_cast(
@@ -946,7 +955,7 @@ hipError_t launch_multi(MultiParams p, int dmin, int C, hipStream_t s)
 {
     const int64_t R = (int64_t)1 << p.dmax;
     const int64_t Hp = (p.H + R - 1) / R * R, Wp = (p.W + R - 1) / R * R;
-    const int64_t strip = 64 * ((C == 3) ? 4 : 16 / C);
+    const int64_t strip = 64 * strip_lane_pixels(C);
     p.n_bands = Hp / R;
     p.n_groups = (int32_t)(((Wp + strip - 1) / strip + 3) / 4);
     const int64_t blocks = p.n_images * p.n_bands * p.n_groups;
@@ -1132,7 +1141,7 @@ static hipError_t dispatch_C(int L, int C, const LLParams& p, int64_t blocks, hi
 int64_t segments_for(int64_t out_w, int L, int C)
 {
     if (use_strip_kernel(L)) {  // groups of 4 wave strips of 64*P pixels
-        const int64_t strip = 64 * ((C == 3) ? 4 : 16 / std::max(1, std::min(C, 4)));
+        const int64_t strip = 64 * strip_lane_pixels(std::max(1, std::min(C, 4)));
         const int64_t strips = ((out_w << L) + strip - 1) / strip;
         return (strips + 3) / 4;
     }
