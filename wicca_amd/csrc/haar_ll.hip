@@ -131,6 +131,166 @@ __device__ __forceinline__ float finish<float>(uint32_t s, int L)
 template <>
 __device__ __forceinline__ uint32_t finish<uint32_t>(uint32_t s, int) { return s; }
 
+// Band epilogue of the segment kernel K1: column sums -> LDS -> per-icon sums
+// -> staged 16-B stores of one icon row of one segment.
+template <int L, int C, typename OutT>
+__device__ __forceinline__ void band_epilogue(const LLParams& p, const BlockWork& w, int tid,
+                                              int64_t px0, int oy, int64_t y0, int rows_real,
+                                              const bool (&valid)[C], const uint32_t (&lo)[C][4],
+                                              const uint32_t (&hi)[C][4], uint16_t* colsum,
+                                              uint8_t* stage, uint32_t* lastcol)
+{
+    constexpr int R = 1 << L;
+    constexpr int kColBytes = kSegPx * C * 2;
+    constexpr int kOutPerSeg = kSegPx >> L;
+    constexpr int kStageAligned = (kOutPerSeg * C * (int)sizeof(OutT) + 15) & ~15;
+    constexpr bool kReuse = kColBytes + kStageAligned > 40 * 1024;
+    const bool replicate = p.border == 1;
+    const int64_t last_row = w.H - 1;
+    const uint8_t* img = w.src;
+
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+        u32x4 a, b;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t l = valid[k] ? lo[k][j] : 0u;
+            const uint32_t h = valid[k] ? hi[k][j] : 0u;
+            const uint32_t w0 = __builtin_amdgcn_perm(h, l, 0x05040100u);  // cols 4j, 4j+1
+            const uint32_t w1 = __builtin_amdgcn_perm(h, l, 0x07060302u);  // cols 4j+2, 4j+3
+            if (j < 2) { a[2 * j] = w0; a[2 * j + 1] = w1; }
+            else       { b[2 * j - 4] = w0; b[2 * j - 3] = w1; }
+        }
+        u32x4* dstv = reinterpret_cast<u32x4*>(colsum + k * (kThreads * 16) + 16 * tid);
+        dstv[0] = a;
+        dstv[1] = b;
+    }
+    // REPLICATE pad columns whose source column W-1 lies in an earlier
+    // segment (only in the D > 8 pre-pass, where padding exceeds 2^L).
+    const bool tail = px0 + kSegPx > w.W;
+    bool last_elsewhere = false;
+    if constexpr (sizeof(OutT) == 4 && L == 8) last_elsewhere = replicate && tail && px0 > w.W - 1;
+    if (last_elsewhere && tid < C) {
+        uint32_t s = 0;
+        for (int rr = 0; rr < R; ++rr) {
+            const int64_t y = min<int64_t>(y0 + rr, last_row);
+            s += img[y * w.src_pitch + (w.W - 1) * C + tid];
+        }
+        lastcol[tid] = s;
+    }
+    __syncthreads();
+
+    constexpr int G = L <= 4 ? (1 << L) : 16;  // pixels per icon inside a lane
+    constexpr int NJ = 16 / G;                  // icons per lane
+    uint32_t words[8 * C];
+    {
+        const u32x4* srcv = reinterpret_cast<const u32x4*>(colsum + 16 * C * tid);
+#pragma unroll
+        for (int q = 0; q < 2 * C; ++q) {
+            const u32x4 t = srcv[q];
+            words[4 * q + 0] = t[0]; words[4 * q + 1] = t[1];
+            words[4 * q + 2] = t[2]; words[4 * q + 3] = t[3];
+        }
+    }
+    uint32_t s[NJ][C];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int c = 0; c < C; ++c) s[j][c] = 0;
+    const int64_t lane_px0 = px0 + 16 * tid;
+    if (!tail) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int idx = i * C + c;
+                const uint32_t wd = words[idx >> 1];
+                s[i / G][c] += (idx & 1) ? (wd >> 16) : (wd & 0xFFFFu);
+            }
+    } else {
+        uint32_t last[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            if (!replicate) last[c] = 0;
+            else if (last_elsewhere) last[c] = lastcol[c];
+            else last[c] = colsum[(w.W - 1 - px0) * C + c];
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const bool real = lane_px0 + i < w.W;
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const int idx = i * C + c;
+                const uint32_t wd = words[idx >> 1];
+                const uint32_t v = (idx & 1) ? (wd >> 16) : (wd & 0xFFFFu);
+                s[i / G][c] += real ? v : last[c];
+            }
+        }
+    }
+    if constexpr (L > 4) {
+        constexpr int GL = 1 << (L - 4);  // lanes per icon (<= 16, inside a wave)
+#pragma unroll
+        for (int m = 1; m < GL; m <<= 1)
+#pragma unroll
+            for (int c = 0; c < C; ++c) s[0][c] += __shfl_xor(s[0][c], m, 64);
+    }
+    if constexpr (kReuse) __syncthreads();  // colsum reads done before staging
+
+    const int64_t seg_out0 = px0 >> L;
+    const int n_out = (int)min<int64_t>(kOutPerSeg, w.out_w - seg_out0);
+    OutT* stage_t = reinterpret_cast<OutT*>(stage);
+    const uint32_t k_const = p.k;
+    auto icon_value = [&](int j, int o, int c) -> OutT {
+        uint32_t pad_cells = 0;
+        if (!replicate) {
+            const int64_t ox = seg_out0 + o;
+            const int64_t cols_real = min<int64_t>(max<int64_t>(w.W - (ox << L), 0), R);
+            pad_cells = (uint32_t)(R * R) - (uint32_t)(rows_real * cols_real);
+        }
+        return finish<OutT>(s[j][c] + k_const * pad_cells, L);
+    };
+    bool packed = false;
+    if constexpr (sizeof(OutT) == 1 && L <= 4 && NJ * C > 1) {
+        if (tid * NJ + NJ <= n_out) {  // all NJ icons of this lane exist
+            uint8_t b[NJ * C];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int c = 0; c < C; ++c) b[j * C + c] = (uint8_t)icon_value(j, tid * NJ + j, c);
+            stage_bytes<NJ * C>(stage + tid * NJ * C, b);
+            packed = true;
+        }
+    }
+    if (!packed) {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            int o;  // icon index inside the segment
+            bool writer;
+            if constexpr (L > 4) {
+                o = tid >> (L - 4);
+                writer = (tid & ((1 << (L - 4)) - 1)) == 0;
+            } else {
+                o = tid * NJ + j;
+                writer = true;
+            }
+            if (writer && o < n_out) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) stage_t[o * C + c] = icon_value(j, o, c);
+            }
+        }
+    }
+    __syncthreads();
+
+    const int nbytes = n_out * C * (int)sizeof(OutT);
+    uint8_t* drow = w.dst + (int64_t)oy * w.dst_pitch + seg_out0 * C * (int64_t)sizeof(OutT);
+    // rows of the icon are 16-B aligned (launcher guarantees); the last
+    // partial chunk of a row is written with 4-B / 1-B stores
+    const int full = nbytes & ~15;
+    for (int i = tid * 16; i < full; i += kThreads * 16)
+        *reinterpret_cast<u32x4*>(drow + i) = *reinterpret_cast<const u32x4*>(stage + i);
+    if (tid < nbytes - full) drow[full + tid] = stage[full + tid];
+}
+
 // ----------------------------------------------------------------------------
 // K1: fused padded block sum, 1 <= L <= 8, C in {1,2,3,4}.
 //
@@ -207,148 +367,9 @@ __global__ __launch_bounds__(kThreads) void haar_block_sum_kernel(LLParams p)
             for (int j = 0; j < 4; ++j) { lo[k][j] = 0; hi[k][j] = 0; }
     };
 
-    // Band epilogue: column sums -> LDS -> per-icon sums -> staged 16-B stores.
     auto epilogue = [&]() {
-#pragma unroll
-        for (int k = 0; k < C; ++k) {
-            u32x4 a, b;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t l = valid[k] ? lo[k][j] : 0u;
-                const uint32_t h = valid[k] ? hi[k][j] : 0u;
-                const uint32_t w0 = __builtin_amdgcn_perm(h, l, 0x05040100u);  // cols 4j, 4j+1
-                const uint32_t w1 = __builtin_amdgcn_perm(h, l, 0x07060302u);  // cols 4j+2, 4j+3
-                if (j < 2) { a[2 * j] = w0; a[2 * j + 1] = w1; }
-                else       { b[2 * j - 4] = w0; b[2 * j - 3] = w1; }
-            }
-            u32x4* dstv = reinterpret_cast<u32x4*>(colsum + k * (kThreads * 16) + 16 * tid);
-            dstv[0] = a;
-            dstv[1] = b;
-        }
-        // REPLICATE pad columns whose source column W-1 lies in an earlier
-        // segment (only in the D > 8 pre-pass, where padding exceeds 2^L).
-        const bool tail = px0 + kSegPx > w.W;
-        bool last_elsewhere = false;
-        if constexpr (sizeof(OutT) == 4 && L == 8) last_elsewhere = replicate && tail && px0 > w.W - 1;
-        if (last_elsewhere && tid < C) {
-            uint32_t s = 0;
-            for (int rr = 0; rr < R; ++rr) {
-                const int64_t y = min<int64_t>(y0 + rr, last_row);
-                s += img[y * w.src_pitch + (w.W - 1) * C + tid];
-            }
-            lastcol[tid] = s;
-        }
-        __syncthreads();
-
-        constexpr int G = L <= 4 ? (1 << L) : 16;  // pixels per icon inside a lane
-        constexpr int NJ = 16 / G;                  // icons per lane
-        uint32_t words[8 * C];
-        {
-            const u32x4* srcv = reinterpret_cast<const u32x4*>(colsum + 16 * C * tid);
-#pragma unroll
-            for (int q = 0; q < 2 * C; ++q) {
-                const u32x4 t = srcv[q];
-                words[4 * q + 0] = t[0]; words[4 * q + 1] = t[1];
-                words[4 * q + 2] = t[2]; words[4 * q + 3] = t[3];
-            }
-        }
-        uint32_t s[NJ][C];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int c = 0; c < C; ++c) s[j][c] = 0;
-        const int64_t lane_px0 = px0 + 16 * tid;
-        if (!tail) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-#pragma unroll
-                for (int c = 0; c < C; ++c) {
-                    const int idx = i * C + c;
-                    const uint32_t wd = words[idx >> 1];
-                    s[i / G][c] += (idx & 1) ? (wd >> 16) : (wd & 0xFFFFu);
-                }
-        } else {
-            uint32_t last[C];
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                if (!replicate) last[c] = 0;
-                else if (last_elsewhere) last[c] = lastcol[c];
-                else last[c] = colsum[(w.W - 1 - px0) * C + c];
-            }
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const bool real = lane_px0 + i < w.W;
-#pragma unroll
-                for (int c = 0; c < C; ++c) {
-                    const int idx = i * C + c;
-                    const uint32_t wd = words[idx >> 1];
-                    const uint32_t v = (idx & 1) ? (wd >> 16) : (wd & 0xFFFFu);
-                    s[i / G][c] += real ? v : last[c];
-                }
-            }
-        }
-        if constexpr (L > 4) {
-            constexpr int GL = 1 << (L - 4);  // lanes per icon (<= 16, inside a wave)
-#pragma unroll
-            for (int m = 1; m < GL; m <<= 1)
-#pragma unroll
-                for (int c = 0; c < C; ++c) s[0][c] += __shfl_xor(s[0][c], m, 64);
-        }
-        if constexpr (kReuse) __syncthreads();  // colsum reads done before staging
-
-        const int64_t seg_out0 = px0 >> L;
-        const int n_out = (int)min<int64_t>(kOutPerSeg, w.out_w - seg_out0);
-        OutT* stage_t = reinterpret_cast<OutT*>(stage);
-        const uint32_t k_const = p.k;
-        auto icon_value = [&](int j, int o, int c) -> OutT {
-            uint32_t pad_cells = 0;
-            if (!replicate) {
-                const int64_t ox = seg_out0 + o;
-                const int64_t cols_real = min<int64_t>(max<int64_t>(w.W - (ox << L), 0), R);
-                pad_cells = (uint32_t)(R * R) - (uint32_t)(rows_real * cols_real);
-            }
-            return finish<OutT>(s[j][c] + k_const * pad_cells, L);
-        };
-        bool packed = false;
-        if constexpr (sizeof(OutT) == 1 && L <= 4 && NJ * C > 1) {
-            if (tid * NJ + NJ <= n_out) {  // all NJ icons of this lane exist
-                uint8_t b[NJ * C];
-#pragma unroll
-                for (int j = 0; j < NJ; ++j)
-#pragma unroll
-                    for (int c = 0; c < C; ++c) b[j * C + c] = (uint8_t)icon_value(j, tid * NJ + j, c);
-                stage_bytes<NJ * C>(stage + tid * NJ * C, b);
-                packed = true;
-            }
-        }
-        if (!packed) {
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                int o;  // icon index inside the segment
-                bool writer;
-                if constexpr (L > 4) {
-                    o = tid >> (L - 4);
-                    writer = (tid & ((1 << (L - 4)) - 1)) == 0;
-                } else {
-                    o = tid * NJ + j;
-                    writer = true;
-                }
-                if (writer && o < n_out) {
-#pragma unroll
-                    for (int c = 0; c < C; ++c) stage_t[o * C + c] = icon_value(j, o, c);
-                }
-            }
-        }
-        __syncthreads();
-
-        const int nbytes = n_out * C * (int)sizeof(OutT);
-        uint8_t* drow = w.dst + (int64_t)oy * w.dst_pitch + seg_out0 * C * (int64_t)sizeof(OutT);
-        // rows of the icon are 16-B aligned (launcher guarantees); the last
-        // partial chunk of a row is written with 4-B / 1-B stores
-        const int full = nbytes & ~15;
-        for (int i = tid * 16; i < full; i += kThreads * 16)
-            *reinterpret_cast<u32x4*>(drow + i) = *reinterpret_cast<const u32x4*>(stage + i);
-        if (tid < nbytes - full) drow[full + tid] = stage[full + tid];
+        band_epilogue<L, C, OutT>(p, w, tid, px0, oy, y0, rows_real, valid, lo, hi, colsum, stage,
+                                  lastcol);
     };
 
     // Reduce chunk g (its loads were issued earlier); CONSTANT rows below the
