@@ -12,6 +12,10 @@
 #define WICCA_CHUNK_ROWS 0    // rows per load chunk (C dwordx4 per lane per row); 0 = table
 #endif
 
+#ifndef WICCA_K1_WAVES
+#define WICCA_K1_WAVES 0      // K1 register budget: minimum waves per SIMD (0 = compiler's choice)
+#endif
+
 #ifndef WICCA_STRIP
 #define WICCA_STRIP -1        // 1: wave-strip kernel, 0: LDS-segment kernel, -1: per-depth table
 #endif

@@ -309,12 +309,17 @@ __device__ __forceinline__ u32x4 load_row16(const uint8_t* row, uint32_t nrec, u
 }
 
 template <int L, int C, typename OutT, bool RAGGED>
-__global__ __launch_bounds__(kThreads) void haar_block_sum_kernel(LLParams p)
+__global__ __launch_bounds__(kThreads)
+#if WICCA_K1_WAVES > 0
+__attribute__((amdgpu_waves_per_eu(WICCA_K1_WAVES)))
+#endif
+void haar_block_sum_kernel(LLParams p)
 {
     static_assert(L >= 1 && L <= 8, "integer path covers 1..8 levels");
     constexpr int R = 1 << L;
     constexpr int U = R < chunk_rows(L) ? R : chunk_rows(L);  // rows per load chunk
     constexpr int CPB = R / U;                                       // chunks per band
+    static_assert(R % U == 0, "chunk rows must divide the band");
     constexpr int kColBytes = kSegPx * C * 2;            // u16 column sums
     constexpr int kOutPerSeg = kSegPx >> L;              // icons per segment row
     constexpr int kStageBytes = kOutPerSeg * C * (int)sizeof(OutT);
