@@ -289,3 +289,22 @@ def test_multi_uniform_scratch_beyond_min_allocation(coder):
         got = o.cpu().numpy().reshape(n, H >> d, W >> d, C)
         for i in range(n):
             assert np.array_equal(got[i], c_oracle.ll_int_block(host[i], d)[0])
+
+
+def test_tall_strip_partial_band_groups(coder):
+    """Small depths walk several bands per wave: icon heights that are not a
+    multiple of the bands per wave, images shorter than one band group, and a
+    ragged batch mixing them, against the integer oracle (both borders)."""
+    rng = np.random.default_rng(31)
+    for d in (1, 2, 3, 4):
+        for H in (1, 2, 3, 5, 17, 31, 33, 63, 65, 97, 129, 255):
+            W = int(rng.integers(1, 1400))
+            img = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+            for border, k in ((1, 0), (0, 131)):
+                out = coder.get_small_copy(img, d, border, k)
+                ref, _ = c_oracle.ll_int_block(img, d, border, k)
+                assert np.array_equal(out, ref), (H, W, d, border)
+        batch = [rng.integers(0, 256, (int(h), int(rng.integers(1, 2100)), 3), dtype=np.uint8)
+                 for h in rng.integers(1, 200, 7)]
+        for o, im in zip(coder.get_small_copies(batch, d), batch):
+            assert np.array_equal(o, c_oracle.ll_int_block(im, d, 1, 0)[0])
