@@ -8,6 +8,10 @@
 #ifndef WICCA_NT_LOADS
 #define WICCA_NT_LOADS 1      // non-temporal loads for the once-read image stream
 #endif
+#ifndef WICCA_NT_STORES
+#define WICCA_NT_STORES 1     // non-temporal icon stores (K1, K1s, K5): +2-9 % at D = 1-5
+                              // (profiles/r01_ab_nt_stores.json)
+#endif
 #ifndef WICCA_CHUNK_ROWS
 #define WICCA_CHUNK_ROWS 0    // rows per load chunk (C dwordx4 per lane per row); 0 = table
 #endif

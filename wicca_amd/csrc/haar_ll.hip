@@ -286,8 +286,11 @@ __device__ __forceinline__ void band_epilogue(const LLParams& p, const BlockWork
     // rows of the icon are 16-B aligned (launcher guarantees); the last
     // partial chunk of a row is written with 4-B / 1-B stores
     const int full = nbytes & ~15;
-    for (int i = tid * 16; i < full; i += kThreads * 16)
-        *reinterpret_cast<u32x4*>(drow + i) = *reinterpret_cast<const u32x4*>(stage + i);
+    for (int i = tid * 16; i < full; i += kThreads * 16) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(stage + i);
+        if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(drow + i));
+        else *reinterpret_cast<u32x4*>(drow + i) = v;
+    }
     if (tid < nbytes - full) drow[full + tid] = stage[full + tid];
 }
 
@@ -623,7 +626,10 @@ __global__ __launch_bounds__(kThreads) void haar_strip_kernel(LLParams p)
     if ((((uintptr_t)drow | (uintptr_t)nbytes) & 3) == 0) {
         const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stage);
         uint32_t* d32 = reinterpret_cast<uint32_t*>(drow);
-        for (int i = lane; i < (nbytes >> 2); i += 64) d32[i] = s32[i];
+        for (int i = lane; i < (nbytes >> 2); i += 64) {
+            if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s32[i], d32 + i);
+            else d32[i] = s32[i];
+        }
     } else {
         for (int i = lane; i < nbytes; i += 64) drow[i] = stage[i];
     }
@@ -827,8 +833,11 @@ __device__ __forceinline__ void emit_level(const MultiParams& p, const MultiCtx&
                 pad_cells = (uint32_t)(G * G) - (uint32_t)(rows_real * cols_real);
             }
 #pragma unroll
-            for (int c = 0; c < C; ++c)
-                drow[o * C + c] = (uint8_t)((s[j][c] + p.k * pad_cells) >> (2 * LV));
+            for (int c = 0; c < C; ++c) {
+                const uint8_t v = (uint8_t)((s[j][c] + p.k * pad_cells) >> (2 * LV));
+                if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(v, drow + o * C + c);
+                else drow[o * C + c] = v;
+            }
         }
     }
 }
