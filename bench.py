@@ -278,7 +278,7 @@ def run_multi(args, torch, rank):
     sep_icons = [o.clone() for o in outs]
     multi_wall, multi_dev = timed(multi)
     same = all(torch.equal(a, b) for a, b in zip(sep_icons, outs))
-    if not same:
+    if not same and not args.no_verify:  # --no-verify: timing-only experiment builds
         raise SystemExit("multi-depth icons differ from per-depth icons")
     mp = B * H * W / 1e6
     in_bytes = B * H * W * C

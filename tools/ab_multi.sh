@@ -4,7 +4,7 @@ set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 DEPTHS=${DEPTHS:-"2,3,4,5,6"}
 ROUNDS=${ROUNDS:-2}
-OUT=$R/gpurun_out/ab_multi.jsonl
+OUT=$R/gpurun_out/ab_multi${TAG:+_$TAG}.jsonl
 : > "$OUT"
 for round in $(seq $ROUNDS); do
   for lib in "$@"; do

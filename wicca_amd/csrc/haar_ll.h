@@ -26,6 +26,18 @@
 #ifndef WICCA_STRIP_CHUNK
 #define WICCA_STRIP_CHUNK 0   // rows per load chunk of the strip kernel; 0 = table
 #endif
+#ifndef WICCA_MULTI_DOT
+#define WICCA_MULTI_DOT 1     // K5: v_dot4 per-(icon, channel) sums on interior strips
+#endif
+#ifndef WICCA_MULTI_WAVES
+#define WICCA_MULTI_WAVES 4   // K5: wave strips per workgroup
+#endif
+#ifndef WICCA_MULTI_CHUNK
+#define WICCA_MULTI_CHUNK 8   // K5 interior strips: rows per load chunk (double-buffered)
+#endif
+#ifndef WICCA_STRIP_DOT
+#define WICCA_STRIP_DOT 1     // strip kernel: v_dot4 per-(icon, channel) sums on non-edge strips
+#endif
 
 namespace wicca {
 

@@ -42,6 +42,7 @@ static inline bool aligned16(const void* ptr, int64_t pitch, int64_t stride);
 
 constexpr int kThreads = 256;
 constexpr int kSegPx = kThreads * 16;  // pixels per segment (16 per lane)
+constexpr int kMultiWaves = WICCA_MULTI_WAVES;  // K5: wave strips per workgroup
 
 // ----------------------------------------------------------------------------
 // Work decomposition: block -> (image, output row, segment).
@@ -454,6 +455,23 @@ __device__ __forceinline__ void load_lane(uint32_t (&d)[NDW], const uint8_t* row
     }
 }
 
+// Byte mask (0x01 per selected byte) of dword dw of a strip lane: the bytes
+// that belong to target t = j * C + c, i.e. channel c of the lane's j-th icon.
+template <int C>
+__host__ __device__ constexpr uint32_t strip_dot_mask(int L, int dw, int t)
+{
+    constexpr int P = strip_lane_pixels(C);
+    const int GI = (1 << L) <= P ? (1 << L) : P;  // pixels of one icon inside a lane
+    uint32_t m = 0;
+    for (int i = 0; i < 4; ++i) {
+        const int b = 4 * dw + i;
+        if ((b / C / GI) * C + b % C == t) m |= 1u << (8 * i);
+    }
+    return m;
+}
+static_assert(strip_dot_mask<3>(2, 0, 0) == 0x01000001u && strip_dot_mask<3>(2, 1, 2) == 0x00000100u,
+              "RGB dword masks");
+
 template <int L, int C, typename OutT, bool RAGGED>
 __global__ __launch_bounds__(kThreads) void haar_strip_kernel(LLParams p)
 {
@@ -488,91 +506,126 @@ __global__ __launch_bounds__(kThreads) void haar_strip_kernel(LLParams p)
     const int64_t lpx0 = spx0 + (int64_t)lane * P;    // first pixel of the lane
     const uint32_t voff = (uint32_t)(lpx0 * C);       // past nrec -> zeros
 
-    // ---- vertical: packed u16 column sums (bytes 0,2 | 1,3 of each dword)
-    uint32_t lo[NDW], hi[NDW];
-#pragma unroll
-    for (int j = 0; j < NDW; ++j) { lo[j] = 0; hi[j] = 0; }
-    auto sissue = [&](uint32_t (&d)[U][NDW], int r0) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint8_t* row = w.src + min<int64_t>(y0 + r0 + u, last_row) * w.src_pitch;
-            load_lane<NDW>(d[u], row, nrec, voff);
-        }
-    };
-    auto sconsume = [&](uint32_t (&d)[U][NDW], int r0) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t m = (replicate || r0 + u < rows_real) ? 0x00FF00FFu : 0u;
-#pragma unroll
-            for (int j = 0; j < NDW; ++j) {
-                lo[j] += d[u][j] & m;
-                hi[j] += (d[u][j] >> 8) & m;
-            }
-        }
-    };
-    for (int r0 = 0; r0 < R; r0 += U) {
-        uint32_t d[U][NDW];
-        sissue(d, r0);
-        sconsume(d, r0);
-    }
-
-
-    // ---- per-pixel, per-channel column sums of this lane
-    auto colsum = [&](int byte) -> uint32_t {
-        const uint32_t r = (byte & 1) ? hi[byte >> 2] : lo[byte >> 2];
-        return ((byte >> 1) & 1) ? (r >> 16) : (r & 0xFFFFu);
-    };
-    uint32_t cs[P][C];
-#pragma unroll
-    for (int q = 0; q < P; ++q)
-#pragma unroll
-        for (int c = 0; c < C; ++c) cs[q][c] = colsum(q * C + c);
-
-    // ---- right padding: pixels >= W
-    if (spx0 + STRIP > w.W) {  // wave-uniform: this strip reaches the image edge
-        uint32_t last[C];
-        if (!replicate) {
-#pragma unroll
-            for (int c = 0; c < C; ++c) last[c] = 0;
-        } else if (spx0 <= w.W - 1) {
-            // column W-1 lives in this wave: its lane broadcasts its sums
-            const int hl = (int)((w.W - 1 - spx0) / P);
-            const int hq = (int)((w.W - 1 - spx0) % P);
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                uint32_t mine = 0;
-#pragma unroll
-                for (int q = 0; q < P; ++q) mine = (q == hq) ? cs[q][c] : mine;
-                last[c] = __shfl(mine, hl, 64);
-            }
-        } else {
-            // only in the depth > 8 pre-pass: column W-1 is in an earlier strip
-            uint32_t mine = 0;
-            if (lane < C)
-                for (int rr = 0; rr < R; ++rr)
-                    mine += w.src[min<int64_t>(y0 + rr, last_row) * w.src_pitch + (w.W - 1) * C + lane];
-#pragma unroll
-            for (int c = 0; c < C; ++c) last[c] = __shfl(mine, c, 64);
-        }
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-            const bool real = lpx0 + q < w.W;
-#pragma unroll
-            for (int c = 0; c < C; ++c) cs[q][c] = real ? cs[q][c] : last[c];
-        }
-    }
-
-    // ---- horizontal: icons inside the lane, then across GL lanes
     uint32_t s[NJ][C];
+    const bool tail = spx0 + STRIP > w.W;  // wave-uniform: this strip reaches the image edge
+    if (WICCA_STRIP_DOT && !tail) {
+        // ---- every pixel of the strip is real: per-(icon, channel) block sums
+        // straight from the loaded bytes, one v_dot4_u32_u8 per distinct
+        // (icon, channel) of a dword (9 per RGB row against 15 packed-u16
+        // ops, and no per-pixel unpacking afterwards).  CONSTANT rows below
+        // the image load from past the record count, i.e. zeros.
+        uint32_t acc[NJ * C];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+        for (int t = 0; t < NJ * C; ++t) acc[t] = 0;
+        for (int r0 = 0; r0 < R; r0 += U) {
+            uint32_t d[U][NDW];
 #pragma unroll
-        for (int c = 0; c < C; ++c) {
-            uint32_t t = 0;
+            for (int u = 0; u < U; ++u) {
+                const uint8_t* row = w.src + min<int64_t>(y0 + r0 + u, last_row) * w.src_pitch;
+                const uint32_t vo = (replicate || r0 + u < rows_real) ? voff : 0xFFFFFFF0u;
+                load_lane<NDW>(d[u], row, nrec, vo);
+            }
 #pragma unroll
-            for (int q = 0; q < (G <= P ? G : P); ++q) t += cs[j * (G <= P ? G : P) + q][c];
-            s[j][c] = t;
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int dw = 0; dw < NDW; ++dw)
+#pragma unroll
+                    for (int t = 0; t < NJ * C; ++t) {
+                        const uint32_t m = strip_dot_mask<C>(L, dw, t);
+                        if (m != 0) acc[t] = __builtin_amdgcn_udot4(d[u][dw], m, acc[t], false);
+                    }
         }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int c = 0; c < C; ++c) s[j][c] = acc[j * C + c];
+    } else {
+        // ---- vertical: packed u16 column sums (bytes 0,2 | 1,3 of each dword)
+        uint32_t lo[NDW], hi[NDW];
+    #pragma unroll
+        for (int j = 0; j < NDW; ++j) { lo[j] = 0; hi[j] = 0; }
+        auto sissue = [&](uint32_t (&d)[U][NDW], int r0) {
+    #pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint8_t* row = w.src + min<int64_t>(y0 + r0 + u, last_row) * w.src_pitch;
+                load_lane<NDW>(d[u], row, nrec, voff);
+            }
+        };
+        auto sconsume = [&](uint32_t (&d)[U][NDW], int r0) {
+    #pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t m = (replicate || r0 + u < rows_real) ? 0x00FF00FFu : 0u;
+    #pragma unroll
+                for (int j = 0; j < NDW; ++j) {
+                    lo[j] += d[u][j] & m;
+                    hi[j] += (d[u][j] >> 8) & m;
+                }
+            }
+        };
+        for (int r0 = 0; r0 < R; r0 += U) {
+            uint32_t d[U][NDW];
+            sissue(d, r0);
+            sconsume(d, r0);
+        }
+
+
+        // ---- per-pixel, per-channel column sums of this lane
+        auto colsum = [&](int byte) -> uint32_t {
+            const uint32_t r = (byte & 1) ? hi[byte >> 2] : lo[byte >> 2];
+            return ((byte >> 1) & 1) ? (r >> 16) : (r & 0xFFFFu);
+        };
+        uint32_t cs[P][C];
+    #pragma unroll
+        for (int q = 0; q < P; ++q)
+    #pragma unroll
+            for (int c = 0; c < C; ++c) cs[q][c] = colsum(q * C + c);
+
+        // ---- right padding: pixels >= W
+        if (tail) {
+            uint32_t last[C];
+            if (!replicate) {
+    #pragma unroll
+                for (int c = 0; c < C; ++c) last[c] = 0;
+            } else if (spx0 <= w.W - 1) {
+                // column W-1 lives in this wave: its lane broadcasts its sums
+                const int hl = (int)((w.W - 1 - spx0) / P);
+                const int hq = (int)((w.W - 1 - spx0) % P);
+    #pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    uint32_t mine = 0;
+    #pragma unroll
+                    for (int q = 0; q < P; ++q) mine = (q == hq) ? cs[q][c] : mine;
+                    last[c] = __shfl(mine, hl, 64);
+                }
+            } else {
+                // only in the depth > 8 pre-pass: column W-1 is in an earlier strip
+                uint32_t mine = 0;
+                if (lane < C)
+                    for (int rr = 0; rr < R; ++rr)
+                        mine += w.src[min<int64_t>(y0 + rr, last_row) * w.src_pitch + (w.W - 1) * C + lane];
+    #pragma unroll
+                for (int c = 0; c < C; ++c) last[c] = __shfl(mine, c, 64);
+            }
+    #pragma unroll
+            for (int q = 0; q < P; ++q) {
+                const bool real = lpx0 + q < w.W;
+    #pragma unroll
+                for (int c = 0; c < C; ++c) cs[q][c] = real ? cs[q][c] : last[c];
+            }
+        }
+
+        // ---- horizontal: icons inside the lane
+    #pragma unroll
+        for (int j = 0; j < NJ; ++j)
+    #pragma unroll
+            for (int c = 0; c < C; ++c) {
+                uint32_t t = 0;
+    #pragma unroll
+                for (int q = 0; q < (G <= P ? G : P); ++q) t += cs[j * (G <= P ? G : P) + q][c];
+                s[j][c] = t;
+            }
+    }
+    // ---- across the GL lanes of an icon
     if constexpr (GL > 1) {
 #pragma unroll
         for (int m = 1; m < GL; m <<= 1)
@@ -752,6 +805,9 @@ struct MultiCtx {
     int64_t spx0, lpx0, y_band;
     int lane, band, img;
     bool replicate, tail;
+    uint8_t* stage;  // the workgroup's icon staging area (interior strips, MultiStage)
+    int wave, n_int;  // wave in the workgroup; interior (dot-path) strips of the group
+    int64_t gpx0;     // first pixel of the workgroup's 4 strips
 };
 
 template <int LV, int C>
@@ -867,8 +923,241 @@ struct Cascade {
     }
 };
 
+// ---- K5 interior strips (every pixel real): per-(icon, channel) sums with
+// v_dot4_u32_u8, as in K1s.  A level-t lane partial holds NJ_t icons x C
+// channels (NJ_t = P / 2^t icons inside the lane, or 1 partial of an icon
+// spread over 2^t / P lanes); the binary counter carries those partials, so a
+// level costs C (not 2 * NDW) pending registers and no per-pixel unpacking.
+template <int C, int T>
+constexpr int lane_icons()
+{
+    return (1 << T) <= strip_lane_pixels(C) ? strip_lane_pixels(C) >> T : 1;
+}
+
+// Icon rows of interior strips are staged in LDS and leave in bursts, once per
+// flush window of FW level-DMIN blocks (once per band when 2^(DMAX-DMIN) <= 16).
+// CDNA's vmcnt counts stores too, so a store issued between two load chunks
+// makes the next load wait also wait for the store to complete; stores at
+// every block (16 per 64-row band) cost K5 ~30 % of its time.
 template <int DMIN, int DMAX, int C>
-__global__ __launch_bounds__(kThreads) void haar_multi_kernel(MultiParams p)
+struct MultiStage {
+    static constexpr int FW = (DMAX - DMIN) < 4 ? (1 << (DMAX - DMIN)) : 16;
+    static constexpr int WINDOWS = (1 << (DMAX - DMIN)) / FW;  // flush windows per band
+    static constexpr int NBUF = WINDOWS > 1 ? 2 : 1;
+    static constexpr int per(int t) { return 1 << (t - DMIN); }  // level-DMIN blocks per level-t row
+    static constexpr int slots(int t) { return per(t) < FW ? FW / per(t) : 1; }
+    static constexpr int row_bytes(int t) { return (StripGeom<C>::STRIP >> t) * C; }  // one wave
+    static constexpr int row_pitch(int t) { return (kMultiWaves * row_bytes(t) + 15) & ~15; }
+    static constexpr int off(int t)
+    {
+        int o = 0;
+        for (int u = DMIN; u < t; ++u) o += slots(u) * row_pitch(u);
+        return o;
+    }
+    static constexpr int BUF = off(DMAX + 1);
+    static constexpr int BYTES = NBUF * BUF;  // per workgroup
+};
+
+template <int LV, int DMIN, int DMAX, int C, int NT>
+__device__ __forceinline__ void emit_level_dot(const MultiParams& p, const MultiCtx& x, int idx,
+                                               const uint32_t (&sv)[NT])
+{
+    using Geo = StripGeom<C>;
+    using S = MultiStage<DMIN, DMAX, C>;
+    constexpr int P = Geo::P;
+    constexpr int G = 1 << LV;
+    constexpr int NJ = lane_icons<C, LV>();
+    constexpr int GL = G <= P ? 1 : G / P;
+    uint32_t s[NJ][C];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int c = 0; c < C; ++c) s[j][c] = sv[j * C + c];
+    if constexpr (GL > 1) {
+#pragma unroll
+        for (int m = 1; m < GL; m <<= 1)
+#pragma unroll
+            for (int c = 0; c < C; ++c) s[0][c] += __shfl_xor(s[0][c], m, 64);
+    }
+    // interior strip: every column is real, only rows below the image pad
+    uint32_t pad = 0;
+    if (!x.replicate) {
+        const int64_t yb = x.y_band + (int64_t)idx * G;
+        const int rows_real = (int)min<int64_t>(max<int64_t>(p.H - yb, 0), G);
+        pad = p.k * (uint32_t)((G - rows_real) * G);
+    }
+    const int buf = S::NBUF > 1 ? ((((idx + 1) << (LV - DMIN)) - 1) / S::FW) & 1 : 0;  // window parity
+    uint8_t* st = x.stage + buf * S::BUF + S::off(LV) + (idx % S::slots(LV)) * S::row_pitch(LV) +
+                  x.wave * S::row_bytes(LV);
+    if constexpr (GL == 1) {
+        uint8_t b[NJ * C];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int c = 0; c < C; ++c) b[j * C + c] = (uint8_t)((s[j][c] + pad) >> (2 * LV));
+        stage_bytes<NJ * C>(st + x.lane * NJ * C, b);
+    } else if (x.lane % GL == 0) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) st[(x.lane / GL) * C + c] = (uint8_t)((s[0][c] + pad) >> (2 * LV));
+    }
+}
+
+// Store the level rows completed in the flush window that ends with
+// level-DMIN block `count` (1-based within the band), after a workgroup
+// barrier: each staged row holds the interior strips' segments side by side
+// (768 B of RGB icons at depth 2), stored with 16-B stores where aligned; the
+// rows of the window are dealt round-robin to the 4 waves.  Every wave of the
+// workgroup (interior, tail or idle) calls this once per window.
+template <int DMIN, int DMAX, int C>
+__device__ __forceinline__ void store_window(const MultiParams& p, const MultiCtx& x, int count)
+{
+    using S = MultiStage<DMIN, DMAX, C>;
+    // LDS-only barrier: __syncthreads()'s release fence would also wait for the
+    // wave's outstanding global stores/loads (vmcnt), which this does not need
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    const int buf = S::NBUF > 1 ? ((count - 1) / S::FW) & 1 : 0;
+    int k = 0;  // running (level, row) index, dealt to the waves
+#pragma unroll
+    for (int t = DMIN; t <= DMAX; ++t) {
+        if (!((p.want >> t) & 1) || (count % S::per(t)) != 0) continue;
+        const int nrows = S::per(t) < S::FW ? S::FW / S::per(t) : 1;
+        const int first = count / S::per(t) - nrows;  // first level-t row of the window
+        const int64_t out_h = (p.H + (1 << t) - 1) >> t;
+        const int nbytes = x.n_int * S::row_bytes(t);
+#pragma unroll 1
+        for (int r = 0; r < nrows; ++r, ++k) {
+            if (k % kMultiWaves != x.wave) continue;
+            const int idx = first + r;
+            const int64_t oy = ((int64_t)x.band << (p.dmax - t)) + idx;
+            if (oy >= out_h || nbytes == 0) continue;  // rows that exist only as padding
+            const uint8_t* st = x.stage + buf * S::BUF + S::off(t) + (idx % S::slots(t)) * S::row_pitch(t);
+            uint8_t* drow = p.dst[t] + (int64_t)x.img * p.dst_stride[t] + oy * p.dst_pitch[t] +
+                            (x.gpx0 >> t) * C;
+#ifdef WICCA_MULTI_ONE_ROW  // experiment: every row of the band lands on its first row
+            drow -= (int64_t)idx * p.dst_pitch[t];
+#endif
+#ifdef WICCA_MULTI_ABLATE_STORE  // timing-only build: icons computed and staged, not stored
+            if (x.lane == 0x7FFF) drow[0] = st[0];
+#else
+            if ((((uintptr_t)drow | (uintptr_t)nbytes) & 15) == 0) {
+                const u32x4* s16 = reinterpret_cast<const u32x4*>(st);
+                u32x4* d16 = reinterpret_cast<u32x4*>(drow);
+                for (int i = x.lane; i < (nbytes >> 4); i += 64) {
+                    if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s16[i], d16 + i);
+                    else d16[i] = s16[i];
+                }
+            } else if ((((uintptr_t)drow | (uintptr_t)nbytes) & 3) == 0) {
+                const uint32_t* s32 = reinterpret_cast<const uint32_t*>(st);
+                uint32_t* d32 = reinterpret_cast<uint32_t*>(drow);
+                for (int i = x.lane; i < (nbytes >> 2); i += 64) {
+                    if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s32[i], d32 + i);
+                    else d32[i] = s32[i];
+                }
+            } else {
+                for (int i = x.lane; i < nbytes; i += 64) drow[i] = st[i];
+            }
+#endif
+        }
+    }
+}
+
+template <int L, int DMIN, int DMAX, int C, int NT>
+struct CascadeDot {
+    static __device__ __forceinline__ void run(const MultiParams& p, const MultiCtx& x, int count,
+                                               const uint32_t (&cur)[NT],
+                                               uint32_t (&pend)[DMAX - DMIN][NT])
+    {
+        if constexpr (L < DMAX) {
+            const int idx = (count >> (L - DMIN)) - 1;  // index of the completed level-L block
+            if ((idx & 1) == 0) {                      // first half of a level-(L+1) block
+#pragma unroll
+                for (int t = 0; t < NT; ++t) pend[L - DMIN][t] = cur[t];
+                return;
+            }
+            constexpr int nj0 = lane_icons<C, L>(), nj1 = lane_icons<C, L + 1>();
+            uint32_t nxt[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) nxt[t] = 0;
+#pragma unroll
+            for (int j = 0; j < nj1; ++j)
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    if constexpr (nj0 > nj1)
+                        nxt[j * C + c] = cur[2 * j * C + c] + cur[(2 * j + 1) * C + c] +
+                                         pend[L - DMIN][2 * j * C + c] +
+                                         pend[L - DMIN][(2 * j + 1) * C + c];
+                    else
+                        nxt[j * C + c] = cur[j * C + c] + pend[L - DMIN][j * C + c];
+                }
+            if ((p.want >> (L + 1)) & 1) emit_level_dot<L + 1, DMIN, DMAX, C, NT>(p, x, idx >> 1, nxt);
+            CascadeDot<L + 1, DMIN, DMAX, C, NT>::run(p, x, count, nxt, pend);
+        }
+    }
+};
+
+template <int DMIN, int DMAX, int C>
+__device__ __forceinline__ void multi_wave_dot(const MultiParams& p, const MultiCtx& x,
+                                               const uint8_t* src, uint32_t nrec, uint32_t voff)
+{
+    using Geo = StripGeom<C>;
+    using S = MultiStage<DMIN, DMAX, C>;
+    constexpr int NDW = Geo::NDW;
+    constexpr int NT = lane_icons<C, DMIN>() * C;  // level-DMIN targets per lane
+    constexpr int SB = 1 << DMIN;                   // rows per level-DMIN block
+    constexpr int R = 1 << DMAX;
+    constexpr int CH = R < WICCA_MULTI_CHUNK ? R : WICCA_MULTI_CHUNK;  // rows per load chunk
+    constexpr int nchunks = R / CH;
+    const int64_t last_row = p.H - 1;
+    auto issue = [&](uint32_t (&d)[CH][NDW], int ci) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int64_t y = x.y_band + ci * CH + u;
+            const uint32_t vo = (x.replicate || y <= last_row) ? voff : 0xFFFFFFF0u;  // CONSTANT: zeros
+            load_lane<NDW>(d[u], src + min<int64_t>(y, last_row) * p.src_pitch, nrec, vo);
+        }
+    };
+    uint32_t acc[NT], pend[DMAX - DMIN][NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = 0;
+    auto consume = [&](const uint32_t (&d)[CH][NDW], int ci) {
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+#pragma unroll
+            for (int dw = 0; dw < NDW; ++dw)
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    const uint32_t m = strip_dot_mask<C>(DMIN, dw, t);
+                    if (m != 0) acc[t] = __builtin_amdgcn_udot4(d[u][dw], m, acc[t], false);
+                }
+            if (((ci * CH + u + 1) & (SB - 1)) == 0) {  // a level-DMIN block is complete
+                const int count = (ci * CH + u + 1) >> DMIN;
+                if ((p.want >> DMIN) & 1) emit_level_dot<DMIN, DMIN, DMAX, C, NT>(p, x, count - 1, acc);
+                CascadeDot<DMIN, DMIN, DMAX, C, NT>::run(p, x, count, acc, pend);
+#pragma unroll
+                for (int t = 0; t < NT; ++t) acc[t] = 0;
+            }
+        }
+        // windows end on chunk boundaries (FW * 2^DMIN >= CH)
+        const int count = ((ci + 1) * CH) >> DMIN;
+        if ((((ci + 1) * CH) & (SB - 1)) == 0 && count % S::FW == 0)
+            store_window<DMIN, DMAX, C>(p, x, count);
+    };
+    // ping-pong chunk buffers: the next chunk is in flight while one is reduced
+    uint32_t da[CH][NDW], db[CH][NDW];
+    issue(da, 0);
+#pragma unroll 1
+    for (int ci = 0; ci < nchunks; ci += 2) {
+        if (ci + 1 < nchunks) issue(db, ci + 1);
+        consume(da, ci);
+        if (ci + 1 < nchunks) {
+            if (ci + 2 < nchunks) issue(da, ci + 2);
+            consume(db, ci + 1);
+        }
+    }
+}
+
+template <int DMIN, int DMAX, int C>
+__global__ __launch_bounds__(64 * kMultiWaves) void haar_multi_kernel(MultiParams p)
 {
     using Geo = StripGeom<C>;
     constexpr int NDW = Geo::NDW, STRIP = Geo::STRIP;
@@ -883,9 +1172,12 @@ __global__ __launch_bounds__(kThreads) void haar_multi_kernel(MultiParams p)
     const int img = (int)(b / (uint32_t)p.n_bands);
     constexpr int R = 1 << DMAX;
     const int64_t Wp = ((p.W + R - 1) >> DMAX) << DMAX;
+    using MS = MultiStage<DMIN, DMAX, C>;
     MultiCtx x;
-    x.spx0 = (int64_t)(g * 4 + wave) * STRIP;
-    if (x.spx0 >= Wp) return;  // whole wave idle (no workgroup barriers in this kernel)
+    x.spx0 = (int64_t)(g * kMultiWaves + wave) * STRIP;
+    x.gpx0 = (int64_t)g * kMultiWaves * STRIP;
+    x.wave = wave;
+    x.n_int = WICCA_MULTI_DOT ? (int)min<int64_t>(max<int64_t>((p.W - x.gpx0) / STRIP, 0), kMultiWaves) : 0;
     x.lane = lane;
     x.band = band;
     x.img = img;
@@ -893,11 +1185,21 @@ __global__ __launch_bounds__(kThreads) void haar_multi_kernel(MultiParams p)
     x.y_band = (int64_t)band << DMAX;
     x.replicate = p.border == 1;
     x.tail = x.spx0 + STRIP > p.W;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[MS::BYTES];
+    x.stage = smem;
+    if (x.spx0 >= Wp) {  // idle wave: only its share of the workgroup's stores
+        for (int w = 1; w <= MS::WINDOWS; ++w) store_window<DMIN, DMAX, C>(p, x, w * MS::FW);
+        return;
+    }
 
     const uint8_t* src = p.src + (int64_t)img * p.src_image_stride;
     const int64_t last_row = p.H - 1;
     const uint32_t nrec = (uint32_t)((p.W * C + 15) & ~(int64_t)15);
     const uint32_t voff = (uint32_t)(x.lpx0 * C);
+    if (WICCA_MULTI_DOT && !x.tail) {  // wave-uniform
+        multi_wave_dot<DMIN, DMAX, C>(p, x, src, nrec, voff);
+        return;
+    }
     auto issue = [&](uint32_t (&d)[CH][NDW], int ci) {
 #pragma unroll
         for (int u = 0; u < CH; ++u) {
@@ -937,13 +1239,17 @@ __global__ __launch_bounds__(kThreads) void haar_multi_kernel(MultiParams p)
             for (int j = 0; j < NDW; ++j) { lo[j] = 0; hi[j] = 0; }
         }
     }
+    // this wave stored its own icons; it still takes its share of the interior
+    // strips' staged rows (the workgroup's barriers must match)
+    for (int w = 1; w <= MultiStage<DMIN, DMAX, C>::WINDOWS; ++w)
+        store_window<DMIN, DMAX, C>(p, x, w * MultiStage<DMIN, DMAX, C>::FW);
 }
 
 template <int DMIN, int DMAX, int C>
 static hipError_t launch_multi_k(const MultiParams& p, int64_t blocks, hipStream_t s)
 {
     if constexpr (DMIN < DMAX) {
-        hipLaunchKernelGGL((haar_multi_kernel<DMIN, DMAX, C>), dim3((uint32_t)blocks), dim3(kThreads),
+        hipLaunchKernelGGL((haar_multi_kernel<DMIN, DMAX, C>), dim3((uint32_t)blocks), dim3(64 * kMultiWaves),
                            0, s, p);
         return hipGetLastError();
     }
@@ -992,7 +1298,7 @@ hipError_t launch_multi(MultiParams p, int dmin, int C, hipStream_t s)
     const int64_t Hp = (p.H + R - 1) / R * R, Wp = (p.W + R - 1) / R * R;
     const int64_t strip = 64 * strip_lane_pixels(C);
     p.n_bands = Hp / R;
-    p.n_groups = (int32_t)(((Wp + strip - 1) / strip + 3) / 4);
+    p.n_groups = (int32_t)(((Wp + strip - 1) / strip + kMultiWaves - 1) / kMultiWaves);
     const int64_t blocks = p.n_images * p.n_bands * p.n_groups;
     if (blocks <= 0) return hipSuccess;
     if (blocks >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
