@@ -8,9 +8,12 @@ build() {  # name, extra flags
   local name=$1; shift
   local B=$V/build_$name
   mkdir -p "$B"
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off "$@" -c "$R/wicca_amd/csrc/haar_ll.hip" -o "$B/haar_ll.o"
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off "$@" -x hip -c "$R/wicca_amd/csrc/capi.cpp" -o "$B/capi.o"
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/lib_$name.so" "$B/haar_ll.o" "$B/capi.o"
+  local F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off"
+  /opt/rocm/bin/hipcc $F "$@" -c "$R/wicca_amd/csrc/haar_ll.hip" -o "$B/haar_ll.o" &
+  /opt/rocm/bin/hipcc $F "$@" -c "$R/wicca_amd/csrc/haar_multi.hip" -o "$B/haar_multi.o" &
+  /opt/rocm/bin/hipcc $F "$@" -x hip -c "$R/wicca_amd/csrc/capi.cpp" -o "$B/capi.o" &
+  wait
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/lib_$name.so" "$B/haar_ll.o" "$B/haar_multi.o" "$B/capi.o"
   rm -rf "$B"
 }
 for spec in "$@"; do

@@ -1,0 +1,170 @@
+// haar_device.h — device-side helpers shared by the gfx950 kernels
+// (haar_ll.hip: K1, K1s, K2-K4; haar_multi.hip: K5).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "haar_ll.h"
+
+namespace wicca {
+
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+inline bool aligned16(const void* ptr, int64_t pitch, int64_t stride)
+{
+    return ((uintptr_t)ptr % 16 == 0) && (pitch % 16 == 0) && (stride % 16 == 0);
+}
+
+
+constexpr int kThreads = 256;
+constexpr int kSegPx = kThreads * 16;  // pixels per segment (16 per lane)
+constexpr int kMultiWaves = WICCA_MULTI_WAVES;  // K5: wave strips per workgroup
+constexpr int kStripWaves = WICCA_STRIP_WAVES;  // K1s: wave strips per workgroup
+
+// ----------------------------------------------------------------------------
+// Work decomposition: block -> (image, output row, segment).
+// ----------------------------------------------------------------------------
+struct BlockWork {
+    const uint8_t* src;
+    uint8_t* dst;
+    int64_t H, W, src_pitch, dst_pitch, out_h, out_w;
+    int32_t oy, seg, n_seg;
+};
+
+template <int L, bool RAGGED>
+__device__ __forceinline__ BlockWork resolve_block(const LLParams& p)
+{
+    BlockWork w;
+    uint32_t b = blockIdx.x;
+    if constexpr (RAGGED) {
+        // binary search the per-image block prefix (n_images is small)
+        int lo = 0, hi = p.n_images - 1;
+        while (lo < hi) {
+            int mid = (lo + hi + 1) >> 1;
+            if (p.block_start[mid] <= (int64_t)b) lo = mid; else hi = mid - 1;
+        }
+        const ImageDescDev d = p.descs[lo];
+        b -= (uint32_t)p.block_start[lo];
+        w.src = d.src; w.dst = d.dst; w.H = d.H; w.W = d.W;
+        w.src_pitch = d.src_pitch; w.dst_pitch = d.dst_pitch;
+        w.out_h = d.out_h; w.out_w = d.out_w; w.n_seg = d.n_seg;
+        w.seg = (int32_t)(b % (uint32_t)w.n_seg);
+        w.oy = (int32_t)(b / (uint32_t)w.n_seg);
+    } else {
+        uint32_t seg = b % (uint32_t)p.n_seg;
+        uint32_t t = b / (uint32_t)p.n_seg;
+        uint32_t oy = t % (uint32_t)p.out_h;
+        uint32_t img = t / (uint32_t)p.out_h;
+        w.src = p.src + (int64_t)img * p.src_image_stride;
+        w.dst = p.dst + (int64_t)img * p.dst_image_stride;
+        w.H = p.H; w.W = p.W; w.src_pitch = p.src_pitch; w.dst_pitch = p.dst_pitch;
+        w.out_h = p.out_h; w.out_w = p.out_w; w.n_seg = p.n_seg;
+        w.seg = (int32_t)seg; w.oy = (int32_t)oy;
+    }
+    return w;
+}
+
+// Packed column sums: lo holds bytes 0,2 of each dword, hi bytes 1,3.
+__device__ __forceinline__ void accumulate(uint32_t (&lo)[4], uint32_t (&hi)[4], u32x4 v)
+{
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        lo[j] += v[j] & 0x00FF00FFu;
+        hi[j] += (v[j] >> 8) & 0x00FF00FFu;
+    }
+}
+
+// Store NB bytes that sit at a multiple-of-NB offset, with the widest LDS
+// writes that alignment allows (one ds_write_b32/b16 instead of NB byte writes).
+template <int NB>
+__device__ __forceinline__ void stage_bytes(uint8_t* dst, const uint8_t (&b)[NB])
+{
+    if constexpr (NB % 4 == 0) {
+#pragma unroll
+        for (int q = 0; q < NB / 4; ++q)
+            reinterpret_cast<uint32_t*>(dst)[q] = (uint32_t)b[4 * q] | ((uint32_t)b[4 * q + 1] << 8) |
+                                                  ((uint32_t)b[4 * q + 2] << 16) |
+                                                  ((uint32_t)b[4 * q + 3] << 24);
+    } else if constexpr (NB % 2 == 0) {
+#pragma unroll
+        for (int q = 0; q < NB / 2; ++q)
+            reinterpret_cast<uint16_t*>(dst)[q] = (uint16_t)(b[2 * q] | (b[2 * q + 1] << 8));
+    } else {
+#pragma unroll
+        for (int q = 0; q < NB; ++q) dst[q] = b[q];
+    }
+}
+
+template <typename OutT>
+__device__ __forceinline__ OutT finish(uint32_t s, int L);
+
+template <>
+__device__ __forceinline__ uint8_t finish<uint8_t>(uint32_t s, int L) { return (uint8_t)(s >> (2 * L)); }
+template <>
+__device__ __forceinline__ float finish<float>(uint32_t s, int L)
+{
+    // exact: s < 2^24 and the scale is a power of two
+    return (float)s * (1.0f / (float)(1u << (2 * L)));
+}
+template <>
+__device__ __forceinline__ uint32_t finish<uint32_t>(uint32_t s, int) { return s; }
+
+__device__ __forceinline__ u32x4 load_row16(const uint8_t* row, uint32_t nrec, uint32_t voff)
+{
+    __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(row), (short)0, (int)nrec, 0x00020000);
+    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0,
+                                                                           WICCA_NT_LOADS ? 2 : 0));
+}
+
+template <int C>
+struct StripGeom {
+    static constexpr int P = strip_lane_pixels(C);  // pixels per lane
+    static constexpr int BYTES = P * C;              // 12 or 16 (narrow), 16*C (wide)
+    static constexpr int NDW = BYTES / 4;            // dwords per lane
+    static constexpr int STRIP = 64 * P;             // pixels per wave
+};
+
+template <int NDW>
+__device__ __forceinline__ void load_lane(uint32_t (&d)[NDW], const uint8_t* row, uint32_t nrec,
+                                          uint32_t voff)
+{
+    __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(row), (short)0, (int)nrec, 0x00020000);
+    if constexpr (NDW % 4 == 0) {  // NDW/4 dwordx4 pieces (a wide lane: 16 whole pixels)
+#pragma unroll
+        for (int q = 0; q < NDW / 4; ++q) {
+            const u32x4 v = __builtin_bit_cast(
+                u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16 * q, 0, WICCA_NT_LOADS ? 2 : 0));
+            d[4 * q] = v[0]; d[4 * q + 1] = v[1]; d[4 * q + 2] = v[2]; d[4 * q + 3] = v[3];
+        }
+    } else {
+        typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+        const u32x3 v = __builtin_bit_cast(
+            u32x3, __builtin_amdgcn_raw_buffer_load_b96(rs, voff, 0, WICCA_NT_LOADS ? 2 : 0));
+        d[0] = v[0]; d[1] = v[1]; d[2] = v[2];
+    }
+}
+
+// Byte mask (0x01 per selected byte) of dword dw of a strip lane: the bytes
+// that belong to target t = j * C + c, i.e. channel c of the lane's j-th icon.
+template <int C>
+__host__ __device__ constexpr uint32_t strip_dot_mask(int L, int dw, int t)
+{
+    constexpr int P = strip_lane_pixels(C);
+    const int GI = (1 << L) <= P ? (1 << L) : P;  // pixels of one icon inside a lane
+    uint32_t m = 0;
+    for (int i = 0; i < 4; ++i) {
+        const int b = 4 * dw + i;
+        if ((b / C / GI) * C + b % C == t) m |= 1u << (8 * i);
+    }
+    return m;
+}
+static_assert(strip_dot_mask<3>(2, 0, 0) == 0x01000001u && strip_dot_mask<3>(2, 1, 2) == 0x00000100u,
+              "RGB dword masks");
+
+}  // namespace wicca

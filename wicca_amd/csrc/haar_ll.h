@@ -35,6 +35,12 @@
 #ifndef WICCA_MULTI_CHUNK
 #define WICCA_MULTI_CHUNK 8   // K5 interior strips: rows per load chunk (double-buffered)
 #endif
+#ifndef WICCA_STRIP_WAVES
+#define WICCA_STRIP_WAVES 4   // K1s: wave strips per workgroup
+#endif
+#ifndef WICCA_STRIP_COOP
+#define WICCA_STRIP_COOP 0    // K1s: workgroup-cooperative icon-row stores
+#endif
 #ifndef WICCA_STRIP_DOT
 #define WICCA_STRIP_DOT 1     // strip kernel: v_dot4 per-(icon, channel) sums on non-edge strips
 #endif

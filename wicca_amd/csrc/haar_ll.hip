@@ -31,106 +31,11 @@
 
 #include <algorithm>
 
-#include "haar_ll.h"
+#include "haar_device.h"
 
 namespace wicca {
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-static inline bool aligned16(const void* ptr, int64_t pitch, int64_t stride);
-
-
-constexpr int kThreads = 256;
-constexpr int kSegPx = kThreads * 16;  // pixels per segment (16 per lane)
-constexpr int kMultiWaves = WICCA_MULTI_WAVES;  // K5: wave strips per workgroup
-
-// ----------------------------------------------------------------------------
-// Work decomposition: block -> (image, output row, segment).
-// ----------------------------------------------------------------------------
-struct BlockWork {
-    const uint8_t* src;
-    uint8_t* dst;
-    int64_t H, W, src_pitch, dst_pitch, out_h, out_w;
-    int32_t oy, seg, n_seg;
-};
-
-template <int L, bool RAGGED>
-__device__ __forceinline__ BlockWork resolve_block(const LLParams& p)
-{
-    BlockWork w;
-    uint32_t b = blockIdx.x;
-    if constexpr (RAGGED) {
-        // binary search the per-image block prefix (n_images is small)
-        int lo = 0, hi = p.n_images - 1;
-        while (lo < hi) {
-            int mid = (lo + hi + 1) >> 1;
-            if (p.block_start[mid] <= (int64_t)b) lo = mid; else hi = mid - 1;
-        }
-        const ImageDescDev d = p.descs[lo];
-        b -= (uint32_t)p.block_start[lo];
-        w.src = d.src; w.dst = d.dst; w.H = d.H; w.W = d.W;
-        w.src_pitch = d.src_pitch; w.dst_pitch = d.dst_pitch;
-        w.out_h = d.out_h; w.out_w = d.out_w; w.n_seg = d.n_seg;
-        w.seg = (int32_t)(b % (uint32_t)w.n_seg);
-        w.oy = (int32_t)(b / (uint32_t)w.n_seg);
-    } else {
-        uint32_t seg = b % (uint32_t)p.n_seg;
-        uint32_t t = b / (uint32_t)p.n_seg;
-        uint32_t oy = t % (uint32_t)p.out_h;
-        uint32_t img = t / (uint32_t)p.out_h;
-        w.src = p.src + (int64_t)img * p.src_image_stride;
-        w.dst = p.dst + (int64_t)img * p.dst_image_stride;
-        w.H = p.H; w.W = p.W; w.src_pitch = p.src_pitch; w.dst_pitch = p.dst_pitch;
-        w.out_h = p.out_h; w.out_w = p.out_w; w.n_seg = p.n_seg;
-        w.seg = (int32_t)seg; w.oy = (int32_t)oy;
-    }
-    return w;
-}
-
-// Packed column sums: lo holds bytes 0,2 of each dword, hi bytes 1,3.
-__device__ __forceinline__ void accumulate(uint32_t (&lo)[4], uint32_t (&hi)[4], u32x4 v)
-{
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        lo[j] += v[j] & 0x00FF00FFu;
-        hi[j] += (v[j] >> 8) & 0x00FF00FFu;
-    }
-}
-
-// Store NB bytes that sit at a multiple-of-NB offset, with the widest LDS
-// writes that alignment allows (one ds_write_b32/b16 instead of NB byte writes).
-template <int NB>
-__device__ __forceinline__ void stage_bytes(uint8_t* dst, const uint8_t (&b)[NB])
-{
-    if constexpr (NB % 4 == 0) {
-#pragma unroll
-        for (int q = 0; q < NB / 4; ++q)
-            reinterpret_cast<uint32_t*>(dst)[q] = (uint32_t)b[4 * q] | ((uint32_t)b[4 * q + 1] << 8) |
-                                                  ((uint32_t)b[4 * q + 2] << 16) |
-                                                  ((uint32_t)b[4 * q + 3] << 24);
-    } else if constexpr (NB % 2 == 0) {
-#pragma unroll
-        for (int q = 0; q < NB / 2; ++q)
-            reinterpret_cast<uint16_t*>(dst)[q] = (uint16_t)(b[2 * q] | (b[2 * q + 1] << 8));
-    } else {
-#pragma unroll
-        for (int q = 0; q < NB; ++q) dst[q] = b[q];
-    }
-}
-
-template <typename OutT>
-__device__ __forceinline__ OutT finish(uint32_t s, int L);
-
-template <>
-__device__ __forceinline__ uint8_t finish<uint8_t>(uint32_t s, int L) { return (uint8_t)(s >> (2 * L)); }
-template <>
-__device__ __forceinline__ float finish<float>(uint32_t s, int L)
-{
-    // exact: s < 2^24 and the scale is a power of two
-    return (float)s * (1.0f / (float)(1u << (2 * L)));
-}
-template <>
-__device__ __forceinline__ uint32_t finish<uint32_t>(uint32_t s, int) { return s; }
+// shared device helpers: haar_device.h
 
 // Band epilogue of the segment kernel K1: column sums -> LDS -> per-icon sums
 // -> staged 16-B stores of one icon row of one segment.
@@ -304,13 +209,6 @@ __device__ __forceinline__ void band_epilogue(const LLParams& p, const BlockWork
 // per-lane 32-bit offset, `nt` for the once-read stream); the descriptor's
 // record count ends the row, so lanes past the row read zeros.
 // ----------------------------------------------------------------------------
-__device__ __forceinline__ u32x4 load_row16(const uint8_t* row, uint32_t nrec, uint32_t voff)
-{
-    __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(row), (short)0, (int)nrec, 0x00020000);
-    return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0,
-                                                                           WICCA_NT_LOADS ? 2 : 0));
-}
 
 template <int L, int C, typename OutT, bool RAGGED>
 __global__ __launch_bounds__(kThreads)
@@ -426,54 +324,8 @@ void haar_block_sum_kernel(LLParams p)
 // registers (2^L <= P) or across 2^L/P lanes with __shfl_xor (2^L > P).
 // Icons are staged per wave in LDS and leave as dword (or byte) stores.
 // ----------------------------------------------------------------------------
-template <int C>
-struct StripGeom {
-    static constexpr int P = strip_lane_pixels(C);  // pixels per lane
-    static constexpr int BYTES = P * C;              // 12 or 16 (narrow), 16*C (wide)
-    static constexpr int NDW = BYTES / 4;            // dwords per lane
-    static constexpr int STRIP = 64 * P;             // pixels per wave
-};
-
-template <int NDW>
-__device__ __forceinline__ void load_lane(uint32_t (&d)[NDW], const uint8_t* row, uint32_t nrec,
-                                          uint32_t voff)
-{
-    __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(row), (short)0, (int)nrec, 0x00020000);
-    if constexpr (NDW % 4 == 0) {  // NDW/4 dwordx4 pieces (a wide lane: 16 whole pixels)
-#pragma unroll
-        for (int q = 0; q < NDW / 4; ++q) {
-            const u32x4 v = __builtin_bit_cast(
-                u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16 * q, 0, WICCA_NT_LOADS ? 2 : 0));
-            d[4 * q] = v[0]; d[4 * q + 1] = v[1]; d[4 * q + 2] = v[2]; d[4 * q + 3] = v[3];
-        }
-    } else {
-        typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
-        const u32x3 v = __builtin_bit_cast(
-            u32x3, __builtin_amdgcn_raw_buffer_load_b96(rs, voff, 0, WICCA_NT_LOADS ? 2 : 0));
-        d[0] = v[0]; d[1] = v[1]; d[2] = v[2];
-    }
-}
-
-// Byte mask (0x01 per selected byte) of dword dw of a strip lane: the bytes
-// that belong to target t = j * C + c, i.e. channel c of the lane's j-th icon.
-template <int C>
-__host__ __device__ constexpr uint32_t strip_dot_mask(int L, int dw, int t)
-{
-    constexpr int P = strip_lane_pixels(C);
-    const int GI = (1 << L) <= P ? (1 << L) : P;  // pixels of one icon inside a lane
-    uint32_t m = 0;
-    for (int i = 0; i < 4; ++i) {
-        const int b = 4 * dw + i;
-        if ((b / C / GI) * C + b % C == t) m |= 1u << (8 * i);
-    }
-    return m;
-}
-static_assert(strip_dot_mask<3>(2, 0, 0) == 0x01000001u && strip_dot_mask<3>(2, 1, 2) == 0x00000100u,
-              "RGB dword masks");
-
 template <int L, int C, typename OutT, bool RAGGED>
-__global__ __launch_bounds__(kThreads) void haar_strip_kernel(LLParams p)
+__global__ __launch_bounds__(64 * kStripWaves) void haar_strip_kernel(LLParams p)
 {
     static_assert(L >= 1 && L <= 8, "integer path covers 1..8 levels");
     using Geo = StripGeom<C>;
@@ -484,207 +336,234 @@ __global__ __launch_bounds__(kThreads) void haar_strip_kernel(LLParams p)
     constexpr int GL = G <= P ? 1 : G / P;           // lanes per icon
     constexpr int U = R < strip_chunk_rows(L) ? R : strip_chunk_rows(L);
     constexpr int ICONS = STRIP / G;                 // icons per wave strip
-    constexpr int STAGE = (ICONS * C * (int)sizeof(OutT) + 15) & ~15;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[4 * STAGE];
+    constexpr int ROWB = ICONS * C * (int)sizeof(OutT);  // icon bytes of a full strip
+    // Cooperative stores: the workgroup's strips are staged side by side and
+    // leave together as one contiguous icon-row piece of kStripWaves * ROWB
+    // bytes (16-B stores) after an LDS-only barrier; else each wave stores its own.
+    constexpr bool kCoop = WICCA_STRIP_COOP && ROWB % 16 == 0;
+    constexpr int STAGE = kCoop ? ROWB : (ROWB + 15) & ~15;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kStripWaves * STAGE];
 
-    // ---- work: block -> (image, icon row, group of 4 strips); wave -> strip
+    // ---- work: block -> (image, icon row, group of kStripWaves strips); wave -> strip
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     BlockWork w = resolve_block<L, RAGGED>(p);
-    const int strip = w.seg * 4 + wave;
+    const int strip = w.seg * kStripWaves + wave;
     const int64_t spx0 = (int64_t)strip * STRIP;     // first pixel of the strip
     const int64_t Wp = w.out_w << L;                 // padded width
-    if (spx0 >= Wp) return;                          // whole wave idle (no barriers below)
     uint8_t* stage = smem + wave * STAGE;
+    if (spx0 < Wp) {  // else the whole wave is idle (it only joins the cooperative store)
 
-    const int64_t y0 = (int64_t)w.oy << L;
-    const int rows_real = (int)min<int64_t>(max<int64_t>(w.H - y0, 0), R);
-    const bool replicate = p.border == 1;
-    const int64_t last_row = w.H - 1;
-    const int64_t row_bytes = w.W * C;
-    const uint32_t nrec = (uint32_t)((row_bytes + 15) & ~(int64_t)15);
-    const int64_t lpx0 = spx0 + (int64_t)lane * P;    // first pixel of the lane
-    const uint32_t voff = (uint32_t)(lpx0 * C);       // past nrec -> zeros
+        const int64_t y0 = (int64_t)w.oy << L;
+        const int rows_real = (int)min<int64_t>(max<int64_t>(w.H - y0, 0), R);
+        const bool replicate = p.border == 1;
+        const int64_t last_row = w.H - 1;
+        const int64_t row_bytes = w.W * C;
+        const uint32_t nrec = (uint32_t)((row_bytes + 15) & ~(int64_t)15);
+        const int64_t lpx0 = spx0 + (int64_t)lane * P;    // first pixel of the lane
+        const uint32_t voff = (uint32_t)(lpx0 * C);       // past nrec -> zeros
 
-    uint32_t s[NJ][C];
-    const bool tail = spx0 + STRIP > w.W;  // wave-uniform: this strip reaches the image edge
-    if (WICCA_STRIP_DOT && !tail) {
-        // ---- every pixel of the strip is real: per-(icon, channel) block sums
-        // straight from the loaded bytes, one v_dot4_u32_u8 per distinct
-        // (icon, channel) of a dword (9 per RGB row against 15 packed-u16
-        // ops, and no per-pixel unpacking afterwards).  CONSTANT rows below
-        // the image load from past the record count, i.e. zeros.
-        uint32_t acc[NJ * C];
+        uint32_t s[NJ][C];
+        const bool tail = spx0 + STRIP > w.W;  // wave-uniform: this strip reaches the image edge
+        if (WICCA_STRIP_DOT && !tail) {
+            // ---- every pixel of the strip is real: per-(icon, channel) block sums
+            // straight from the loaded bytes, one v_dot4_u32_u8 per distinct
+            // (icon, channel) of a dword (9 per RGB row against 15 packed-u16
+            // ops, and no per-pixel unpacking afterwards).  CONSTANT rows below
+            // the image load from past the record count, i.e. zeros.
+            uint32_t acc[NJ * C];
 #pragma unroll
-        for (int t = 0; t < NJ * C; ++t) acc[t] = 0;
-        for (int r0 = 0; r0 < R; r0 += U) {
-            uint32_t d[U][NDW];
+            for (int t = 0; t < NJ * C; ++t) acc[t] = 0;
+            for (int r0 = 0; r0 < R; r0 += U) {
+                uint32_t d[U][NDW];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint8_t* row = w.src + min<int64_t>(y0 + r0 + u, last_row) * w.src_pitch;
-                const uint32_t vo = (replicate || r0 + u < rows_real) ? voff : 0xFFFFFFF0u;
-                load_lane<NDW>(d[u], row, nrec, vo);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int dw = 0; dw < NDW; ++dw)
-#pragma unroll
-                    for (int t = 0; t < NJ * C; ++t) {
-                        const uint32_t m = strip_dot_mask<C>(L, dw, t);
-                        if (m != 0) acc[t] = __builtin_amdgcn_udot4(d[u][dw], m, acc[t], false);
-                    }
-        }
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int c = 0; c < C; ++c) s[j][c] = acc[j * C + c];
-    } else {
-        // ---- vertical: packed u16 column sums (bytes 0,2 | 1,3 of each dword)
-        uint32_t lo[NDW], hi[NDW];
-    #pragma unroll
-        for (int j = 0; j < NDW; ++j) { lo[j] = 0; hi[j] = 0; }
-        auto sissue = [&](uint32_t (&d)[U][NDW], int r0) {
-    #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint8_t* row = w.src + min<int64_t>(y0 + r0 + u, last_row) * w.src_pitch;
-                load_lane<NDW>(d[u], row, nrec, voff);
-            }
-        };
-        auto sconsume = [&](uint32_t (&d)[U][NDW], int r0) {
-    #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t m = (replicate || r0 + u < rows_real) ? 0x00FF00FFu : 0u;
-    #pragma unroll
-                for (int j = 0; j < NDW; ++j) {
-                    lo[j] += d[u][j] & m;
-                    hi[j] += (d[u][j] >> 8) & m;
+                for (int u = 0; u < U; ++u) {
+                    const uint8_t* row = w.src + min<int64_t>(y0 + r0 + u, last_row) * w.src_pitch;
+                    const uint32_t vo = (replicate || r0 + u < rows_real) ? voff : 0xFFFFFFF0u;
+                    load_lane<NDW>(d[u], row, nrec, vo);
                 }
-            }
-        };
-        for (int r0 = 0; r0 < R; r0 += U) {
-            uint32_t d[U][NDW];
-            sissue(d, r0);
-            sconsume(d, r0);
-        }
-
-
-        // ---- per-pixel, per-channel column sums of this lane
-        auto colsum = [&](int byte) -> uint32_t {
-            const uint32_t r = (byte & 1) ? hi[byte >> 2] : lo[byte >> 2];
-            return ((byte >> 1) & 1) ? (r >> 16) : (r & 0xFFFFu);
-        };
-        uint32_t cs[P][C];
-    #pragma unroll
-        for (int q = 0; q < P; ++q)
-    #pragma unroll
-            for (int c = 0; c < C; ++c) cs[q][c] = colsum(q * C + c);
-
-        // ---- right padding: pixels >= W
-        if (tail) {
-            uint32_t last[C];
-            if (!replicate) {
-    #pragma unroll
-                for (int c = 0; c < C; ++c) last[c] = 0;
-            } else if (spx0 <= w.W - 1) {
-                // column W-1 lives in this wave: its lane broadcasts its sums
-                const int hl = (int)((w.W - 1 - spx0) / P);
-                const int hq = (int)((w.W - 1 - spx0) % P);
-    #pragma unroll
-                for (int c = 0; c < C; ++c) {
-                    uint32_t mine = 0;
-    #pragma unroll
-                    for (int q = 0; q < P; ++q) mine = (q == hq) ? cs[q][c] : mine;
-                    last[c] = __shfl(mine, hl, 64);
-                }
-            } else {
-                // only in the depth > 8 pre-pass: column W-1 is in an earlier strip
-                uint32_t mine = 0;
-                if (lane < C)
-                    for (int rr = 0; rr < R; ++rr)
-                        mine += w.src[min<int64_t>(y0 + rr, last_row) * w.src_pitch + (w.W - 1) * C + lane];
-    #pragma unroll
-                for (int c = 0; c < C; ++c) last[c] = __shfl(mine, c, 64);
-            }
-    #pragma unroll
-            for (int q = 0; q < P; ++q) {
-                const bool real = lpx0 + q < w.W;
-    #pragma unroll
-                for (int c = 0; c < C; ++c) cs[q][c] = real ? cs[q][c] : last[c];
-            }
-        }
-
-        // ---- horizontal: icons inside the lane
-    #pragma unroll
-        for (int j = 0; j < NJ; ++j)
-    #pragma unroll
-            for (int c = 0; c < C; ++c) {
-                uint32_t t = 0;
-    #pragma unroll
-                for (int q = 0; q < (G <= P ? G : P); ++q) t += cs[j * (G <= P ? G : P) + q][c];
-                s[j][c] = t;
-            }
-    }
-    // ---- across the GL lanes of an icon
-    if constexpr (GL > 1) {
 #pragma unroll
-        for (int m = 1; m < GL; m <<= 1)
+                for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int c = 0; c < C; ++c) s[0][c] += __shfl_xor(s[0][c], m, 64);
-    }
-
-    // ---- finish + stage this wave's icons
-    const int64_t ox0 = spx0 >> L;                           // first icon of the strip
-    const int n_out = (int)min<int64_t>(ICONS, w.out_w - ox0);
-    OutT* st = reinterpret_cast<OutT*>(stage);
-    const uint32_t k_const = p.k;
-    auto icon_value = [&](int j, int o, int c) -> OutT {
-        uint32_t pad_cells = 0;
-        if (!replicate) {
-            const int64_t cols_real = min<int64_t>(max<int64_t>(w.W - ((ox0 + o) << L), 0), R);
-            pad_cells = (uint32_t)(R * R) - (uint32_t)(rows_real * cols_real);
-        }
-        return finish<OutT>(s[j][c] + k_const * pad_cells, L);
-    };
-    bool packed = false;
-    if constexpr (sizeof(OutT) == 1 && GL == 1 && NJ * C > 1) {
-        if (lane * NJ + NJ <= n_out) {
-            uint8_t b[NJ * C];
+                    for (int dw = 0; dw < NDW; ++dw)
+#pragma unroll
+                        for (int t = 0; t < NJ * C; ++t) {
+                            const uint32_t m = strip_dot_mask<C>(L, dw, t);
+                            if (m != 0) acc[t] = __builtin_amdgcn_udot4(d[u][dw], m, acc[t], false);
+                        }
+            }
 #pragma unroll
             for (int j = 0; j < NJ; ++j)
 #pragma unroll
-                for (int c = 0; c < C; ++c) b[j * C + c] = (uint8_t)icon_value(j, lane * NJ + j, c);
-            stage_bytes<NJ * C>(stage + lane * NJ * C, b);
-            packed = true;
+                for (int c = 0; c < C; ++c) s[j][c] = acc[j * C + c];
+        } else {
+            // ---- vertical: packed u16 column sums (bytes 0,2 | 1,3 of each dword)
+            uint32_t lo[NDW], hi[NDW];
+#pragma unroll
+            for (int j = 0; j < NDW; ++j) { lo[j] = 0; hi[j] = 0; }
+            auto sissue = [&](uint32_t (&d)[U][NDW], int r0) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint8_t* row = w.src + min<int64_t>(y0 + r0 + u, last_row) * w.src_pitch;
+                    load_lane<NDW>(d[u], row, nrec, voff);
+                }
+            };
+            auto sconsume = [&](uint32_t (&d)[U][NDW], int r0) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t m = (replicate || r0 + u < rows_real) ? 0x00FF00FFu : 0u;
+#pragma unroll
+                    for (int j = 0; j < NDW; ++j) {
+                        lo[j] += d[u][j] & m;
+                        hi[j] += (d[u][j] >> 8) & m;
+                    }
+                }
+            };
+            for (int r0 = 0; r0 < R; r0 += U) {
+                uint32_t d[U][NDW];
+                sissue(d, r0);
+                sconsume(d, r0);
+            }
+
+
+            // ---- per-pixel, per-channel column sums of this lane
+            auto colsum = [&](int byte) -> uint32_t {
+                const uint32_t r = (byte & 1) ? hi[byte >> 2] : lo[byte >> 2];
+                return ((byte >> 1) & 1) ? (r >> 16) : (r & 0xFFFFu);
+            };
+            uint32_t cs[P][C];
+#pragma unroll
+            for (int q = 0; q < P; ++q)
+#pragma unroll
+                for (int c = 0; c < C; ++c) cs[q][c] = colsum(q * C + c);
+
+            // ---- right padding: pixels >= W
+            if (tail) {
+                uint32_t last[C];
+                if (!replicate) {
+#pragma unroll
+                    for (int c = 0; c < C; ++c) last[c] = 0;
+                } else if (spx0 <= w.W - 1) {
+                    // column W-1 lives in this wave: its lane broadcasts its sums
+                    const int hl = (int)((w.W - 1 - spx0) / P);
+                    const int hq = (int)((w.W - 1 - spx0) % P);
+#pragma unroll
+                    for (int c = 0; c < C; ++c) {
+                        uint32_t mine = 0;
+#pragma unroll
+                        for (int q = 0; q < P; ++q) mine = (q == hq) ? cs[q][c] : mine;
+                        last[c] = __shfl(mine, hl, 64);
+                    }
+                } else {
+                    // only in the depth > 8 pre-pass: column W-1 is in an earlier strip
+                    uint32_t mine = 0;
+                    if (lane < C)
+                        for (int rr = 0; rr < R; ++rr)
+                            mine += w.src[min<int64_t>(y0 + rr, last_row) * w.src_pitch + (w.W - 1) * C + lane];
+#pragma unroll
+                    for (int c = 0; c < C; ++c) last[c] = __shfl(mine, c, 64);
+                }
+#pragma unroll
+                for (int q = 0; q < P; ++q) {
+                    const bool real = lpx0 + q < w.W;
+#pragma unroll
+                    for (int c = 0; c < C; ++c) cs[q][c] = real ? cs[q][c] : last[c];
+                }
+            }
+
+            // ---- horizontal: icons inside the lane
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    uint32_t t = 0;
+#pragma unroll
+                    for (int q = 0; q < (G <= P ? G : P); ++q) t += cs[j * (G <= P ? G : P) + q][c];
+                    s[j][c] = t;
+                }
         }
-    }
-    if (!packed) {
+        // ---- across the GL lanes of an icon
+        if constexpr (GL > 1) {
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-            const int o = (GL > 1) ? lane / GL : lane * NJ + j;
-            const bool writer = (GL > 1) ? (lane % GL) == 0 : true;
-            if (writer && o < n_out) {
+            for (int m = 1; m < GL; m <<= 1)
 #pragma unroll
-                for (int c = 0; c < C; ++c) st[o * C + c] = icon_value(j, o, c);
+                for (int c = 0; c < C; ++c) s[0][c] += __shfl_xor(s[0][c], m, 64);
+        }
+
+        // ---- finish + stage this wave's icons
+        const int64_t ox0 = spx0 >> L;                           // first icon of the strip
+        const int n_out = (int)min<int64_t>(ICONS, w.out_w - ox0);
+        OutT* st = reinterpret_cast<OutT*>(stage);
+        const uint32_t k_const = p.k;
+        auto icon_value = [&](int j, int o, int c) -> OutT {
+            uint32_t pad_cells = 0;
+            if (!replicate) {
+                const int64_t cols_real = min<int64_t>(max<int64_t>(w.W - ((ox0 + o) << L), 0), R);
+                pad_cells = (uint32_t)(R * R) - (uint32_t)(rows_real * cols_real);
+            }
+            return finish<OutT>(s[j][c] + k_const * pad_cells, L);
+        };
+        bool packed = false;
+        if constexpr (sizeof(OutT) == 1 && GL == 1 && NJ * C > 1) {
+            if (lane * NJ + NJ <= n_out) {
+                uint8_t b[NJ * C];
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                    for (int c = 0; c < C; ++c) b[j * C + c] = (uint8_t)icon_value(j, lane * NJ + j, c);
+                stage_bytes<NJ * C>(stage + lane * NJ * C, b);
+                packed = true;
+            }
+        }
+        if (!packed) {
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int o = (GL > 1) ? lane / GL : lane * NJ + j;
+                const bool writer = (GL > 1) ? (lane % GL) == 0 : true;
+                if (writer && o < n_out) {
+#pragma unroll
+                    for (int c = 0; c < C; ++c) st[o * C + c] = icon_value(j, o, c);
+                }
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+        if constexpr (!kCoop) {
+            // ---- store the strip's icon bytes (contiguous in the icon row)
+            const int nbytes = n_out * C * (int)sizeof(OutT);
+            uint8_t* drow = w.dst + (int64_t)w.oy * w.dst_pitch + ox0 * C * (int64_t)sizeof(OutT);
+            if ((((uintptr_t)drow | (uintptr_t)nbytes) & 3) == 0) {
+                const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stage);
+                uint32_t* d32 = reinterpret_cast<uint32_t*>(drow);
+                for (int i = lane; i < (nbytes >> 2); i += 64) {
+                    if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s32[i], d32 + i);
+                    else d32[i] = s32[i];
+                }
+            } else {
+                for (int i = lane; i < nbytes; i += 64) drow[i] = stage[i];
             }
         }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    // ---- store the strip's icon bytes (contiguous in the icon row)
-    const int nbytes = n_out * C * (int)sizeof(OutT);
-    uint8_t* drow = w.dst + (int64_t)w.oy * w.dst_pitch + ox0 * C * (int64_t)sizeof(OutT);
-    if ((((uintptr_t)drow | (uintptr_t)nbytes) & 3) == 0) {
-        const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stage);
-        uint32_t* d32 = reinterpret_cast<uint32_t*>(drow);
-        for (int i = lane; i < (nbytes >> 2); i += 64) {
-            if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s32[i], d32 + i);
-            else d32[i] = s32[i];
+    if constexpr (kCoop) {
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS-only barrier
+        const int64_t gox0 = ((int64_t)w.seg * kStripWaves * STRIP) >> L;  // first icon of the group
+        const int nbytes =
+            (int)max<int64_t>(min<int64_t>((int64_t)kStripWaves * ICONS, w.out_w - gox0), 0) * C *
+            (int)sizeof(OutT);
+        uint8_t* drow = w.dst + (int64_t)w.oy * w.dst_pitch + gox0 * C * (int64_t)sizeof(OutT);
+        const int tid = threadIdx.x;
+        if ((((uintptr_t)drow | (uintptr_t)nbytes) & 15) == 0) {
+            const u32x4* s16 = reinterpret_cast<const u32x4*>(smem);
+            u32x4* d16 = reinterpret_cast<u32x4*>(drow);
+            for (int i = tid; i < (nbytes >> 4); i += 64 * kStripWaves) {
+                if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s16[i], d16 + i);
+                else d16[i] = s16[i];
+            }
+        } else {
+            for (int i = tid; i < nbytes; i += 64 * kStripWaves) drow[i] = smem[i];
         }
-    } else {
-        for (int i = lane; i < nbytes; i += 64) drow[i] = stage[i];
     }
 }
 
@@ -782,532 +661,6 @@ __global__ __launch_bounds__(kThreads) void haar_level_f32_kernel(
         } else {
             reinterpret_cast<float*>(orow)[j * C + c] = v;
         }
-    }
-}
-
-// ----------------------------------------------------------------------------
-// K5: multi-depth wave-strip kernel — icons of every wanted depth in
-// [DMIN, dmax] from ONE read of the image (the caller's
-// depth loop, classifying_tools.py:546-551).
-//
-// Geometry as K1s (a lane owns P whole pixels, a wave a 64*P-pixel strip, a
-// workgroup 4 strips of one band of 2^dmax rows of the image padded to
-// 2^dmax; padding to 2^dmax yields every smaller depth's icon as the top-left
-// crop of its level).  Rows stream in chunks of CH rows, the next
-// chunk in flight while the current one is reduced.  Each completed block of
-// 2^DMIN rows feeds a per-lane binary counter of packed-u16 column sums, one
-// register set per level: two completed level-t row blocks add into one
-// level-(t+1) block (u16 holds 2^t * 255 for t <= 8).  Every completed level
-// emits its icon-row segment at once, so no intermediate plane reaches HBM:
-// traffic = image + icons.
-// ----------------------------------------------------------------------------
-struct MultiCtx {
-    int64_t spx0, lpx0, y_band;
-    int lane, band, img;
-    bool replicate, tail;
-    uint8_t* stage;  // the workgroup's icon staging area (interior strips, MultiStage)
-    int wave, n_int;  // wave in the workgroup; interior (dot-path) strips of the group
-    int64_t gpx0;     // first pixel of the workgroup's 4 strips
-};
-
-template <int LV, int C>
-__device__ __forceinline__ void emit_level(const MultiParams& p, const MultiCtx& x, int idx,
-                                           const uint32_t (&lo)[StripGeom<C>::NDW],
-                                           const uint32_t (&hi)[StripGeom<C>::NDW])
-{
-    using Geo = StripGeom<C>;
-    constexpr int P = Geo::P, STRIP = Geo::STRIP;
-    constexpr int G = 1 << LV;
-    constexpr int NJ = G <= P ? P / G : 1;
-    constexpr int GL = G <= P ? 1 : G / P;
-    constexpr int GI = G <= P ? G : P;  // pixels of one icon inside a lane
-    const int64_t oy = ((int64_t)x.band << (p.dmax - LV)) + idx;
-    if (oy >= ((p.H + G - 1) >> LV)) return;  // wave-uniform: a row that exists only as padding
-    const int64_t ox0 = x.spx0 >> LV;
-    const int n_out = (int)min<int64_t>(STRIP / G, ((p.W + G - 1) >> LV) - ox0);
-    if (n_out <= 0) return;  // wave-uniform
-
-    uint32_t cs[P][C];
-#pragma unroll
-    for (int q = 0; q < P; ++q)
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            const int byte = q * C + c;
-            const uint32_t r = (byte & 1) ? hi[byte >> 2] : lo[byte >> 2];
-            cs[q][c] = ((byte >> 1) & 1) ? (r >> 16) : (r & 0xFFFFu);
-        }
-    if (x.tail) {  // right padding: the strip holding column W-1 holds every pad column
-        uint32_t last[C];
-        if (!x.replicate) {
-#pragma unroll
-            for (int c = 0; c < C; ++c) last[c] = 0;
-        } else {
-            const int hl = (int)((p.W - 1 - x.spx0) / P);
-            const int hq = (int)((p.W - 1 - x.spx0) % P);
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                uint32_t mine = 0;
-#pragma unroll
-                for (int q = 0; q < P; ++q) mine = (q == hq) ? cs[q][c] : mine;
-                last[c] = __shfl(mine, hl, 64);
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < P; ++q) {
-            const bool real = x.lpx0 + q < p.W;
-#pragma unroll
-            for (int c = 0; c < C; ++c) cs[q][c] = real ? cs[q][c] : last[c];
-        }
-    }
-    uint32_t s[NJ][C];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int c = 0; c < C; ++c) {
-            uint32_t t = 0;
-#pragma unroll
-            for (int q = 0; q < GI; ++q) t += cs[j * GI + q][c];
-            s[j][c] = t;
-        }
-    if constexpr (GL > 1) {
-#pragma unroll
-        for (int m = 1; m < GL; m <<= 1)
-#pragma unroll
-            for (int c = 0; c < C; ++c) s[0][c] += __shfl_xor(s[0][c], m, 64);
-    }
-    const int64_t yb = x.y_band + (int64_t)idx * G;
-    const int rows_real = (int)min<int64_t>(max<int64_t>(p.H - yb, 0), G);
-    uint8_t* drow = p.dst[LV] + (int64_t)x.img * p.dst_stride[LV] + oy * p.dst_pitch[LV] + ox0 * C;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-        const int o = (GL > 1) ? x.lane / GL : x.lane * NJ + j;
-        const bool writer = (GL > 1) ? (x.lane % GL) == 0 : true;
-        if (writer && o < n_out) {
-            uint32_t pad_cells = 0;
-            if (!x.replicate) {
-                const int64_t cols_real = min<int64_t>(max<int64_t>(p.W - ((ox0 + o) << LV), 0), G);
-                pad_cells = (uint32_t)(G * G) - (uint32_t)(rows_real * cols_real);
-            }
-#pragma unroll
-            for (int c = 0; c < C; ++c) {
-                const uint8_t v = (uint8_t)((s[j][c] + p.k * pad_cells) >> (2 * LV));
-                if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(v, drow + o * C + c);
-                else drow[o * C + c] = v;
-            }
-        }
-    }
-}
-
-// Binary-counter carry from level L upward (compile-time L keeps the pending
-// registers in VGPRs).
-template <int L, int DMIN, int DMAX, int C>
-struct Cascade {
-    static constexpr int NDW = StripGeom<C>::NDW;
-    static __device__ __forceinline__ void run(const MultiParams& p, const MultiCtx& x, int count,
-                                               uint32_t (&lo)[NDW], uint32_t (&hi)[NDW],
-                                               uint32_t (&plo)[DMAX - DMIN][NDW],
-                                               uint32_t (&phi)[DMAX - DMIN][NDW])
-    {
-        if constexpr (L < DMAX) {
-            const int idx = (count >> (L - DMIN)) - 1;  // index of the completed level-L block
-            if ((idx & 1) == 0) {                      // first half of a level-(L+1) block
-#pragma unroll
-                for (int j = 0; j < NDW; ++j) { plo[L - DMIN][j] = lo[j]; phi[L - DMIN][j] = hi[j]; }
-                return;
-            }
-#pragma unroll
-            for (int j = 0; j < NDW; ++j) { lo[j] += plo[L - DMIN][j]; hi[j] += phi[L - DMIN][j]; }
-            if ((p.want >> (L + 1)) & 1) emit_level<L + 1, C>(p, x, idx >> 1, lo, hi);
-            Cascade<L + 1, DMIN, DMAX, C>::run(p, x, count, lo, hi, plo, phi);
-        }
-    }
-};
-
-// ---- K5 interior strips (every pixel real): per-(icon, channel) sums with
-// v_dot4_u32_u8, as in K1s.  A level-t lane partial holds NJ_t icons x C
-// channels (NJ_t = P / 2^t icons inside the lane, or 1 partial of an icon
-// spread over 2^t / P lanes); the binary counter carries those partials, so a
-// level costs C (not 2 * NDW) pending registers and no per-pixel unpacking.
-template <int C, int T>
-constexpr int lane_icons()
-{
-    return (1 << T) <= strip_lane_pixels(C) ? strip_lane_pixels(C) >> T : 1;
-}
-
-// Icon rows of interior strips are staged in LDS and leave in bursts, once per
-// flush window of FW level-DMIN blocks (once per band when 2^(DMAX-DMIN) <= 16).
-// CDNA's vmcnt counts stores too, so a store issued between two load chunks
-// makes the next load wait also wait for the store to complete; stores at
-// every block (16 per 64-row band) cost K5 ~30 % of its time.
-template <int DMIN, int DMAX, int C>
-struct MultiStage {
-    static constexpr int FW = (DMAX - DMIN) < 4 ? (1 << (DMAX - DMIN)) : 16;
-    static constexpr int WINDOWS = (1 << (DMAX - DMIN)) / FW;  // flush windows per band
-    static constexpr int NBUF = WINDOWS > 1 ? 2 : 1;
-    static constexpr int per(int t) { return 1 << (t - DMIN); }  // level-DMIN blocks per level-t row
-    static constexpr int slots(int t) { return per(t) < FW ? FW / per(t) : 1; }
-    static constexpr int row_bytes(int t) { return (StripGeom<C>::STRIP >> t) * C; }  // one wave
-    static constexpr int row_pitch(int t) { return (kMultiWaves * row_bytes(t) + 15) & ~15; }
-    static constexpr int off(int t)
-    {
-        int o = 0;
-        for (int u = DMIN; u < t; ++u) o += slots(u) * row_pitch(u);
-        return o;
-    }
-    static constexpr int BUF = off(DMAX + 1);
-    static constexpr int BYTES = NBUF * BUF;  // per workgroup
-};
-
-template <int LV, int DMIN, int DMAX, int C, int NT>
-__device__ __forceinline__ void emit_level_dot(const MultiParams& p, const MultiCtx& x, int idx,
-                                               const uint32_t (&sv)[NT])
-{
-    using Geo = StripGeom<C>;
-    using S = MultiStage<DMIN, DMAX, C>;
-    constexpr int P = Geo::P;
-    constexpr int G = 1 << LV;
-    constexpr int NJ = lane_icons<C, LV>();
-    constexpr int GL = G <= P ? 1 : G / P;
-    uint32_t s[NJ][C];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int c = 0; c < C; ++c) s[j][c] = sv[j * C + c];
-    if constexpr (GL > 1) {
-#pragma unroll
-        for (int m = 1; m < GL; m <<= 1)
-#pragma unroll
-            for (int c = 0; c < C; ++c) s[0][c] += __shfl_xor(s[0][c], m, 64);
-    }
-    // interior strip: every column is real, only rows below the image pad
-    uint32_t pad = 0;
-    if (!x.replicate) {
-        const int64_t yb = x.y_band + (int64_t)idx * G;
-        const int rows_real = (int)min<int64_t>(max<int64_t>(p.H - yb, 0), G);
-        pad = p.k * (uint32_t)((G - rows_real) * G);
-    }
-    const int buf = S::NBUF > 1 ? ((((idx + 1) << (LV - DMIN)) - 1) / S::FW) & 1 : 0;  // window parity
-    uint8_t* st = x.stage + buf * S::BUF + S::off(LV) + (idx % S::slots(LV)) * S::row_pitch(LV) +
-                  x.wave * S::row_bytes(LV);
-    if constexpr (GL == 1) {
-        uint8_t b[NJ * C];
-#pragma unroll
-        for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int c = 0; c < C; ++c) b[j * C + c] = (uint8_t)((s[j][c] + pad) >> (2 * LV));
-        stage_bytes<NJ * C>(st + x.lane * NJ * C, b);
-    } else if (x.lane % GL == 0) {
-#pragma unroll
-        for (int c = 0; c < C; ++c) st[(x.lane / GL) * C + c] = (uint8_t)((s[0][c] + pad) >> (2 * LV));
-    }
-}
-
-// Store the level rows completed in the flush window that ends with
-// level-DMIN block `count` (1-based within the band), after a workgroup
-// barrier: each staged row holds the interior strips' segments side by side
-// (768 B of RGB icons at depth 2), stored with 16-B stores where aligned; the
-// rows of the window are dealt round-robin to the 4 waves.  Every wave of the
-// workgroup (interior, tail or idle) calls this once per window.
-template <int DMIN, int DMAX, int C>
-__device__ __forceinline__ void store_window(const MultiParams& p, const MultiCtx& x, int count)
-{
-    using S = MultiStage<DMIN, DMAX, C>;
-    // LDS-only barrier: __syncthreads()'s release fence would also wait for the
-    // wave's outstanding global stores/loads (vmcnt), which this does not need
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    const int buf = S::NBUF > 1 ? ((count - 1) / S::FW) & 1 : 0;
-    int k = 0;  // running (level, row) index, dealt to the waves
-#pragma unroll
-    for (int t = DMIN; t <= DMAX; ++t) {
-        if (!((p.want >> t) & 1) || (count % S::per(t)) != 0) continue;
-        const int nrows = S::per(t) < S::FW ? S::FW / S::per(t) : 1;
-        const int first = count / S::per(t) - nrows;  // first level-t row of the window
-        const int64_t out_h = (p.H + (1 << t) - 1) >> t;
-        const int nbytes = x.n_int * S::row_bytes(t);
-#pragma unroll 1
-        for (int r = 0; r < nrows; ++r, ++k) {
-            if (k % kMultiWaves != x.wave) continue;
-            const int idx = first + r;
-            const int64_t oy = ((int64_t)x.band << (p.dmax - t)) + idx;
-            if (oy >= out_h || nbytes == 0) continue;  // rows that exist only as padding
-            const uint8_t* st = x.stage + buf * S::BUF + S::off(t) + (idx % S::slots(t)) * S::row_pitch(t);
-            uint8_t* drow = p.dst[t] + (int64_t)x.img * p.dst_stride[t] + oy * p.dst_pitch[t] +
-                            (x.gpx0 >> t) * C;
-#ifdef WICCA_MULTI_ONE_ROW  // experiment: every row of the band lands on its first row
-            drow -= (int64_t)idx * p.dst_pitch[t];
-#endif
-#ifdef WICCA_MULTI_ABLATE_STORE  // timing-only build: icons computed and staged, not stored
-            if (x.lane == 0x7FFF) drow[0] = st[0];
-#else
-            if ((((uintptr_t)drow | (uintptr_t)nbytes) & 15) == 0) {
-                const u32x4* s16 = reinterpret_cast<const u32x4*>(st);
-                u32x4* d16 = reinterpret_cast<u32x4*>(drow);
-                for (int i = x.lane; i < (nbytes >> 4); i += 64) {
-                    if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s16[i], d16 + i);
-                    else d16[i] = s16[i];
-                }
-            } else if ((((uintptr_t)drow | (uintptr_t)nbytes) & 3) == 0) {
-                const uint32_t* s32 = reinterpret_cast<const uint32_t*>(st);
-                uint32_t* d32 = reinterpret_cast<uint32_t*>(drow);
-                for (int i = x.lane; i < (nbytes >> 2); i += 64) {
-                    if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s32[i], d32 + i);
-                    else d32[i] = s32[i];
-                }
-            } else {
-                for (int i = x.lane; i < nbytes; i += 64) drow[i] = st[i];
-            }
-#endif
-        }
-    }
-}
-
-template <int L, int DMIN, int DMAX, int C, int NT>
-struct CascadeDot {
-    static __device__ __forceinline__ void run(const MultiParams& p, const MultiCtx& x, int count,
-                                               const uint32_t (&cur)[NT],
-                                               uint32_t (&pend)[DMAX - DMIN][NT])
-    {
-        if constexpr (L < DMAX) {
-            const int idx = (count >> (L - DMIN)) - 1;  // index of the completed level-L block
-            if ((idx & 1) == 0) {                      // first half of a level-(L+1) block
-#pragma unroll
-                for (int t = 0; t < NT; ++t) pend[L - DMIN][t] = cur[t];
-                return;
-            }
-            constexpr int nj0 = lane_icons<C, L>(), nj1 = lane_icons<C, L + 1>();
-            uint32_t nxt[NT];
-#pragma unroll
-            for (int t = 0; t < NT; ++t) nxt[t] = 0;
-#pragma unroll
-            for (int j = 0; j < nj1; ++j)
-#pragma unroll
-                for (int c = 0; c < C; ++c) {
-                    if constexpr (nj0 > nj1)
-                        nxt[j * C + c] = cur[2 * j * C + c] + cur[(2 * j + 1) * C + c] +
-                                         pend[L - DMIN][2 * j * C + c] +
-                                         pend[L - DMIN][(2 * j + 1) * C + c];
-                    else
-                        nxt[j * C + c] = cur[j * C + c] + pend[L - DMIN][j * C + c];
-                }
-            if ((p.want >> (L + 1)) & 1) emit_level_dot<L + 1, DMIN, DMAX, C, NT>(p, x, idx >> 1, nxt);
-            CascadeDot<L + 1, DMIN, DMAX, C, NT>::run(p, x, count, nxt, pend);
-        }
-    }
-};
-
-template <int DMIN, int DMAX, int C>
-__device__ __forceinline__ void multi_wave_dot(const MultiParams& p, const MultiCtx& x,
-                                               const uint8_t* src, uint32_t nrec, uint32_t voff)
-{
-    using Geo = StripGeom<C>;
-    using S = MultiStage<DMIN, DMAX, C>;
-    constexpr int NDW = Geo::NDW;
-    constexpr int NT = lane_icons<C, DMIN>() * C;  // level-DMIN targets per lane
-    constexpr int SB = 1 << DMIN;                   // rows per level-DMIN block
-    constexpr int R = 1 << DMAX;
-    constexpr int CH = R < WICCA_MULTI_CHUNK ? R : WICCA_MULTI_CHUNK;  // rows per load chunk
-    constexpr int nchunks = R / CH;
-    const int64_t last_row = p.H - 1;
-    auto issue = [&](uint32_t (&d)[CH][NDW], int ci) {
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const int64_t y = x.y_band + ci * CH + u;
-            const uint32_t vo = (x.replicate || y <= last_row) ? voff : 0xFFFFFFF0u;  // CONSTANT: zeros
-            load_lane<NDW>(d[u], src + min<int64_t>(y, last_row) * p.src_pitch, nrec, vo);
-        }
-    };
-    uint32_t acc[NT], pend[DMAX - DMIN][NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = 0;
-    auto consume = [&](const uint32_t (&d)[CH][NDW], int ci) {
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-#pragma unroll
-            for (int dw = 0; dw < NDW; ++dw)
-#pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    const uint32_t m = strip_dot_mask<C>(DMIN, dw, t);
-                    if (m != 0) acc[t] = __builtin_amdgcn_udot4(d[u][dw], m, acc[t], false);
-                }
-            if (((ci * CH + u + 1) & (SB - 1)) == 0) {  // a level-DMIN block is complete
-                const int count = (ci * CH + u + 1) >> DMIN;
-                if ((p.want >> DMIN) & 1) emit_level_dot<DMIN, DMIN, DMAX, C, NT>(p, x, count - 1, acc);
-                CascadeDot<DMIN, DMIN, DMAX, C, NT>::run(p, x, count, acc, pend);
-#pragma unroll
-                for (int t = 0; t < NT; ++t) acc[t] = 0;
-            }
-        }
-        // windows end on chunk boundaries (FW * 2^DMIN >= CH)
-        const int count = ((ci + 1) * CH) >> DMIN;
-        if ((((ci + 1) * CH) & (SB - 1)) == 0 && count % S::FW == 0)
-            store_window<DMIN, DMAX, C>(p, x, count);
-    };
-    // ping-pong chunk buffers: the next chunk is in flight while one is reduced
-    uint32_t da[CH][NDW], db[CH][NDW];
-    issue(da, 0);
-#pragma unroll 1
-    for (int ci = 0; ci < nchunks; ci += 2) {
-        if (ci + 1 < nchunks) issue(db, ci + 1);
-        consume(da, ci);
-        if (ci + 1 < nchunks) {
-            if (ci + 2 < nchunks) issue(da, ci + 2);
-            consume(db, ci + 1);
-        }
-    }
-}
-
-template <int DMIN, int DMAX, int C>
-__global__ __launch_bounds__(64 * kMultiWaves) void haar_multi_kernel(MultiParams p)
-{
-    using Geo = StripGeom<C>;
-    constexpr int NDW = Geo::NDW, STRIP = Geo::STRIP;
-    constexpr int SB = 1 << DMIN;              // rows per level-DMIN block
-    constexpr int CH = SB < 8 ? SB : 8;        // rows per load chunk (divides SB)
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    uint32_t b = blockIdx.x;
-    const int g = (int)(b % (uint32_t)p.n_groups);
-    b /= (uint32_t)p.n_groups;
-    const int band = (int)(b % (uint32_t)p.n_bands);
-    const int img = (int)(b / (uint32_t)p.n_bands);
-    constexpr int R = 1 << DMAX;
-    const int64_t Wp = ((p.W + R - 1) >> DMAX) << DMAX;
-    using MS = MultiStage<DMIN, DMAX, C>;
-    MultiCtx x;
-    x.spx0 = (int64_t)(g * kMultiWaves + wave) * STRIP;
-    x.gpx0 = (int64_t)g * kMultiWaves * STRIP;
-    x.wave = wave;
-    x.n_int = WICCA_MULTI_DOT ? (int)min<int64_t>(max<int64_t>((p.W - x.gpx0) / STRIP, 0), kMultiWaves) : 0;
-    x.lane = lane;
-    x.band = band;
-    x.img = img;
-    x.lpx0 = x.spx0 + (int64_t)lane * Geo::P;
-    x.y_band = (int64_t)band << DMAX;
-    x.replicate = p.border == 1;
-    x.tail = x.spx0 + STRIP > p.W;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[MS::BYTES];
-    x.stage = smem;
-    if (x.spx0 >= Wp) {  // idle wave: only its share of the workgroup's stores
-        for (int w = 1; w <= MS::WINDOWS; ++w) store_window<DMIN, DMAX, C>(p, x, w * MS::FW);
-        return;
-    }
-
-    const uint8_t* src = p.src + (int64_t)img * p.src_image_stride;
-    const int64_t last_row = p.H - 1;
-    const uint32_t nrec = (uint32_t)((p.W * C + 15) & ~(int64_t)15);
-    const uint32_t voff = (uint32_t)(x.lpx0 * C);
-    if (WICCA_MULTI_DOT && !x.tail) {  // wave-uniform
-        multi_wave_dot<DMIN, DMAX, C>(p, x, src, nrec, voff);
-        return;
-    }
-    auto issue = [&](uint32_t (&d)[CH][NDW], int ci) {
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const uint8_t* row = src + min<int64_t>(x.y_band + ci * CH + u, last_row) * p.src_pitch;
-            load_lane<NDW>(d[u], row, nrec, voff);
-        }
-    };
-    uint32_t lo[NDW], hi[NDW], plo[DMAX - DMIN][NDW], phi[DMAX - DMIN][NDW];
-#pragma unroll
-    for (int j = 0; j < NDW; ++j) { lo[j] = 0; hi[j] = 0; }
-    constexpr int nchunks = R / CH;
-    uint32_t da[CH][NDW];
-    issue(da, 0);
-#pragma unroll 1
-    for (int ci = 0; ci < nchunks; ++ci) {
-        uint32_t db[CH][NDW];
-        if (ci + 1 < nchunks) issue(db, ci + 1);
-#pragma unroll
-        for (int u = 0; u < CH; ++u) {
-            const int64_t y = x.y_band + ci * CH + u;
-            const uint32_t m = (x.replicate || y < p.H) ? 0x00FF00FFu : 0u;
-#pragma unroll
-            for (int j = 0; j < NDW; ++j) {
-                lo[j] += da[u][j] & m;
-                hi[j] += (da[u][j] >> 8) & m;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < CH; ++u)
-#pragma unroll
-            for (int j = 0; j < NDW; ++j) da[u][j] = db[u][j];
-        if ((((ci + 1) * CH) & (SB - 1)) == 0) {  // a level-DMIN block is complete
-            const int count = ((ci + 1) * CH) >> DMIN;
-            if ((p.want >> DMIN) & 1) emit_level<DMIN, C>(p, x, count - 1, lo, hi);
-            Cascade<DMIN, DMIN, DMAX, C>::run(p, x, count, lo, hi, plo, phi);
-#pragma unroll
-            for (int j = 0; j < NDW; ++j) { lo[j] = 0; hi[j] = 0; }
-        }
-    }
-    // this wave stored its own icons; it still takes its share of the interior
-    // strips' staged rows (the workgroup's barriers must match)
-    for (int w = 1; w <= MultiStage<DMIN, DMAX, C>::WINDOWS; ++w)
-        store_window<DMIN, DMAX, C>(p, x, w * MultiStage<DMIN, DMAX, C>::FW);
-}
-
-template <int DMIN, int DMAX, int C>
-static hipError_t launch_multi_k(const MultiParams& p, int64_t blocks, hipStream_t s)
-{
-    if constexpr (DMIN < DMAX) {
-        hipLaunchKernelGGL((haar_multi_kernel<DMIN, DMAX, C>), dim3((uint32_t)blocks), dim3(64 * kMultiWaves),
-                           0, s, p);
-        return hipGetLastError();
-    }
-    return hipErrorInvalidValue;
-}
-
-template <int DMIN, int C>
-static hipError_t launch_multi_dc(int dmax, const MultiParams& p, int64_t blocks, hipStream_t s)
-{
-    switch (dmax) {
-    case 2: return launch_multi_k<DMIN, 2, C>(p, blocks, s);
-    case 3: return launch_multi_k<DMIN, 3, C>(p, blocks, s);
-    case 4: return launch_multi_k<DMIN, 4, C>(p, blocks, s);
-    case 5: return launch_multi_k<DMIN, 5, C>(p, blocks, s);
-    case 6: return launch_multi_k<DMIN, 6, C>(p, blocks, s);
-    case 7: return launch_multi_k<DMIN, 7, C>(p, blocks, s);
-    case 8: return launch_multi_k<DMIN, 8, C>(p, blocks, s);
-    default: return hipErrorInvalidValue;
-    }
-}
-
-template <int C>
-static hipError_t launch_multi_c(int dmin, const MultiParams& p, int64_t blocks, hipStream_t s)
-{
-    switch (dmin) {  // depth 1 is served by K1 (a 2-row block per step starves the stream)
-    case 2: return launch_multi_dc<2, C>(p.dmax, p, blocks, s);
-    case 3: return launch_multi_dc<3, C>(p.dmax, p, blocks, s);
-    case 4: return launch_multi_dc<4, C>(p.dmax, p, blocks, s);
-    case 5: return launch_multi_dc<5, C>(p.dmax, p, blocks, s);
-    case 6: return launch_multi_dc<6, C>(p.dmax, p, blocks, s);
-    case 7: return launch_multi_dc<7, C>(p.dmax, p, blocks, s);
-    default: return hipErrorInvalidValue;
-    }
-}
-
-bool multi_kernel_ok(const uint8_t* src, int64_t src_pitch, int64_t src_stride, int64_t W, int C,
-                     int dmin, int dmax)
-{
-    return C >= 1 && C <= 4 && dmin >= 2 && dmin < dmax && dmax <= 8 &&
-           W * C < ((int64_t)1 << 30) && aligned16(src, src_pitch, src_stride);
-}
-
-hipError_t launch_multi(MultiParams p, int dmin, int C, hipStream_t s)
-{
-    const int64_t R = (int64_t)1 << p.dmax;
-    const int64_t Hp = (p.H + R - 1) / R * R, Wp = (p.W + R - 1) / R * R;
-    const int64_t strip = 64 * strip_lane_pixels(C);
-    p.n_bands = Hp / R;
-    p.n_groups = (int32_t)(((Wp + strip - 1) / strip + kMultiWaves - 1) / kMultiWaves);
-    const int64_t blocks = p.n_images * p.n_bands * p.n_groups;
-    if (blocks <= 0) return hipSuccess;
-    if (blocks >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
-    switch (C) {
-    case 1: return launch_multi_c<1>(dmin, p, blocks, s);
-    case 2: return launch_multi_c<2>(dmin, p, blocks, s);
-    case 3: return launch_multi_c<3>(dmin, p, blocks, s);
-    case 4: return launch_multi_c<4>(dmin, p, blocks, s);
-    default: return hipErrorInvalidValue;
     }
 }
 
@@ -1423,10 +776,6 @@ __global__ __launch_bounds__(kThreads) void synth_u8_kernel(uint8_t* dst, int64_
 // ----------------------------------------------------------------------------
 // Launchers
 // ----------------------------------------------------------------------------
-static inline bool aligned16(const void* ptr, int64_t pitch, int64_t stride)
-{
-    return ((uintptr_t)ptr % 16 == 0) && (pitch % 16 == 0) && (stride % 16 == 0);
-}
 
 template <int L, int C, typename OutT>
 static hipError_t launch_fast(const LLParams& p, int64_t blocks, hipStream_t stream)
@@ -1434,10 +783,10 @@ static hipError_t launch_fast(const LLParams& p, int64_t blocks, hipStream_t str
     if constexpr (use_strip_kernel(L)) {
         if (p.descs) {
             hipLaunchKernelGGL((haar_strip_kernel<L, C, OutT, true>), dim3((uint32_t)blocks),
-                               dim3(kThreads), 0, stream, p);
+                               dim3(64 * kStripWaves), 0, stream, p);
         } else {
             hipLaunchKernelGGL((haar_strip_kernel<L, C, OutT, false>), dim3((uint32_t)blocks),
-                               dim3(kThreads), 0, stream, p);
+                               dim3(64 * kStripWaves), 0, stream, p);
         }
         return hipGetLastError();
     }
@@ -1481,10 +830,10 @@ static hipError_t dispatch_C(int L, int C, const LLParams& p, int64_t blocks, hi
 
 int64_t segments_for(int64_t out_w, int L, int C)
 {
-    if (use_strip_kernel(L)) {  // groups of 4 wave strips of 64*P pixels
+    if (use_strip_kernel(L)) {  // groups of kStripWaves wave strips of 64*P pixels
         const int64_t strip = 64 * strip_lane_pixels(std::max(1, std::min(C, 4)));
         const int64_t strips = ((out_w << L) + strip - 1) / strip;
-        return (strips + 3) / 4;
+        return (strips + kStripWaves - 1) / kStripWaves;
     }
     return ((out_w << L) + kSegPx - 1) / kSegPx;  // 4,096-pixel segments
 }
