@@ -58,7 +58,7 @@ def parse():
                     help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01.json"),
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01b.json"),
                     help="PMC summary (rocprofv3 FETCH_SIZE/WRITE_SIZE) for roofline.traffic")
     return ap.parse_args()
 
@@ -438,7 +438,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": f"haar_block_sum_kernel<L={D},C={C},u8>",
+            "kernel": (f"haar_strip_kernel<L={D},C={C},u8>" if D in (2, 3)
+                       else f"haar_block_sum_kernel<L={D},C={C},u8>"),
             "kernel_ms": round(kernel_ms, 4),
             "alg_bytes_per_launch": alg_bytes,
             "pmc_source": os.path.relpath(args.pmc, REPO) if pmc else None,
