@@ -308,3 +308,44 @@ def test_tall_strip_partial_band_groups(coder):
                  for h in rng.integers(1, 200, 7)]
         for o, im in zip(coder.get_small_copies(batch, d), batch):
             assert np.array_equal(o, c_oracle.ll_int_block(im, d, 1, 0)[0])
+
+
+def test_multi_depth1_windows_tails(coder):
+    """K5 with depth 1 in the set: several flush windows per band (up to 8 at
+    depths {1, 8}), interior / edge / idle wave strips of a workgroup, both
+    borders, C = 1..4, against the integer oracle per depth."""
+    import ctypes
+    from wicca_amd import _lib
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(77)
+    cases = [(2, 77, 300, 3, [1, 2], 1, 0), (1, 300, 1030, 3, [1, 8], 0, 255),
+             (2, 129, 257, 3, [1, 4, 7], 1, 0), (1, 64, 2049, 1, [1, 5], 0, 3),
+             (2, 33, 515, 2, [1, 3, 6], 1, 0), (1, 260, 700, 4, [1, 2, 8], 0, 90),
+             (3, 18, 769, 3, [1, 2, 3, 4, 5, 6], 0, 17)]
+    for (n, H, W, C, depths, border, k) in cases:
+        imgs = rng.integers(0, 256, (n, H, W, C), dtype=np.uint8)
+        pitch = (W * C + 15) // 16 * 16
+        host = np.zeros((n, H, pitch), np.uint8)
+        host[:, :, :W * C] = imgs.reshape(n, H, W * C)
+        src = torch.from_numpy(host).cuda()
+        outs, ptrs, pitches, strides = [], [], [], []
+        for d in depths:
+            oh, ow = -(-H >> d), -(-W >> d)
+            op = (ow * C + 15) // 16 * 16
+            o = torch.full((n, oh, op), 7, dtype=torch.uint8, device="cuda")
+            outs.append((o, oh, ow))
+            ptrs.append(o.data_ptr())
+            pitches.append(op)
+            strides.append(oh * op)
+        nd = len(depths)
+        _lib.check(_lib.load().wicca_haar_ll_u8_multi_uniform(
+            ctypes.c_void_p(src.data_ptr()), n, H, W, C, pitch, H * pitch,
+            (ctypes.c_int * nd)(*depths), nd, border, k, (ctypes.c_void_p * nd)(*ptrs),
+            (ctypes.c_int64 * nd)(*pitches), (ctypes.c_int64 * nd)(*strides), -1, None))
+        for d, (o, oh, ow) in zip(depths, outs):
+            full = o.cpu().numpy()
+            got = full[:, :, :ow * C].reshape(n, oh, ow, C)
+            assert (full[:, :, ow * C:] == 7).all(), ("row padding written", H, W, C, d)
+            for i in range(n):
+                ref = c_oracle.ll_int_block(imgs[i], d, border, k)[0]
+                assert np.array_equal(got[i], ref), (n, H, W, C, d, border, i)

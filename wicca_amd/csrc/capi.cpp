@@ -291,14 +291,16 @@ int run_multi(const uint8_t* src, int64_t n, int64_t H, int64_t W, int64_t C, in
         dmin = std::min(dmin, depths[i]);
         dmax = std::max(dmax, depths[i]);
     }
-    // Fast path (aligned rows, C <= 4): depth 1 and a lone depth >= 2 get their
-    // own K1 launch; two or more depths >= 2 share ONE read in K5.
-    const int kmin = std::max(dmin, 2);
-    if (wicca::multi_kernel_ok(src, src_pitch, src_stride, W, (int)C, 2, 3)) {
+    // Fast path (aligned rows, C <= 4): two or more depths >= k5_lo share ONE
+    // read in K5; a lone depth (and depth 1 when K5 does not serve it) gets
+    // its own K1 launch.
+    const int k5_lo = WICCA_MULTI_D1 ? 1 : 2;
+    const int kmin = std::max(dmin, k5_lo);
+    if (wicca::multi_kernel_ok(src, src_pitch, src_stride, W, (int)C, k5_lo, k5_lo + 1)) {
         int n_k5 = 0;
-        for (int d = 2; d <= 8; ++d) n_k5 += want[d] ? 1 : 0;
+        for (int d = k5_lo; d <= 8; ++d) n_k5 += want[d] ? 1 : 0;
         for (int i = 0; i < n_depths; ++i) {
-            if (depths[i] != 1 && n_k5 >= 2) continue;
+            if (depths[i] >= k5_lo && n_k5 >= 2) continue;
             bool unused = false;
             int rc = run_ll<uint8_t>(src, n, H, W, C, src_pitch, src_stride, depths[i], border, k,
                                      dsts[i], dst_pitches[i], dst_strides[i], ws, stream, &unused);

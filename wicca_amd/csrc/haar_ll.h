@@ -32,6 +32,13 @@
 #ifndef WICCA_MULTI_WAVES
 #define WICCA_MULTI_WAVES 4   // K5: wave strips per workgroup
 #endif
+#ifndef WICCA_MULTI_D1
+#define WICCA_MULTI_D1 1      // K5 also serves depth 1: depths 1-6 in 3.3 ms vs 5.1-5.3 with a
+                              // separate K1 launch for depth 1 (profiles/r01_ab_k5_depth1.json)
+#endif
+#ifndef WICCA_MULTI_FW
+#define WICCA_MULTI_FW 16     // K5: level-DMIN blocks per flush window (power of 2)
+#endif
 #ifndef WICCA_MULTI_CHUNK
 #define WICCA_MULTI_CHUNK 8   // K5 interior strips: rows per load chunk (double-buffered)
 #endif

@@ -160,7 +160,7 @@ constexpr int lane_icons()
 // every block (16 per 64-row band) cost K5 ~30 % of its time.
 template <int DMIN, int DMAX, int C>
 struct MultiStage {
-    static constexpr int FW = (DMAX - DMIN) < 4 ? (1 << (DMAX - DMIN)) : 16;
+    static constexpr int FW = (1 << (DMAX - DMIN)) < WICCA_MULTI_FW ? (1 << (DMAX - DMIN)) : WICCA_MULTI_FW;
     static constexpr int WINDOWS = (1 << (DMAX - DMIN)) / FW;  // flush windows per band
     static constexpr int NBUF = WINDOWS > 1 ? 2 : 1;
     static constexpr int per(int t) { return 1 << (t - DMIN); }  // level-DMIN blocks per level-t row
@@ -493,7 +493,10 @@ static hipError_t launch_multi_dc(int dmax, const MultiParams& p, int64_t blocks
 template <int C>
 static hipError_t launch_multi_c(int dmin, const MultiParams& p, int64_t blocks, hipStream_t s)
 {
-    switch (dmin) {  // depth 1 is served by K1 (a 2-row block per step starves the stream)
+    switch (dmin) {
+#if WICCA_MULTI_D1
+    case 1: return launch_multi_dc<1, C>(p.dmax, p, blocks, s);
+#endif
     case 2: return launch_multi_dc<2, C>(p.dmax, p, blocks, s);
     case 3: return launch_multi_dc<3, C>(p.dmax, p, blocks, s);
     case 4: return launch_multi_dc<4, C>(p.dmax, p, blocks, s);
@@ -507,7 +510,7 @@ static hipError_t launch_multi_c(int dmin, const MultiParams& p, int64_t blocks,
 bool multi_kernel_ok(const uint8_t* src, int64_t src_pitch, int64_t src_stride, int64_t W, int C,
                      int dmin, int dmax)
 {
-    return C >= 1 && C <= 4 && dmin >= 2 && dmin < dmax && dmax <= 8 &&
+    return C >= 1 && C <= 4 && dmin >= (WICCA_MULTI_D1 ? 1 : 2) && dmin < dmax && dmax <= 8 &&
            W * C < ((int64_t)1 << 30) && aligned16(src, src_pitch, src_stride);
 }
 
