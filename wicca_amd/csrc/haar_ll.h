@@ -45,9 +45,6 @@
 #ifndef WICCA_STRIP_WAVES
 #define WICCA_STRIP_WAVES 4   // K1s: wave strips per workgroup
 #endif
-#ifndef WICCA_STRIP_COOP
-#define WICCA_STRIP_COOP 0    // K1s: workgroup-cooperative icon-row stores
-#endif
 #ifndef WICCA_STRIP_DOT
 #define WICCA_STRIP_DOT 1     // strip kernel: v_dot4 per-(icon, channel) sums on non-edge strips
 #endif

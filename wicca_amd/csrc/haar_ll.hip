@@ -336,12 +336,7 @@ __global__ __launch_bounds__(64 * kStripWaves) void haar_strip_kernel(LLParams p
     constexpr int GL = G <= P ? 1 : G / P;           // lanes per icon
     constexpr int U = R < strip_chunk_rows(L) ? R : strip_chunk_rows(L);
     constexpr int ICONS = STRIP / G;                 // icons per wave strip
-    constexpr int ROWB = ICONS * C * (int)sizeof(OutT);  // icon bytes of a full strip
-    // Cooperative stores: the workgroup's strips are staged side by side and
-    // leave together as one contiguous icon-row piece of kStripWaves * ROWB
-    // bytes (16-B stores) after an LDS-only barrier; else each wave stores its own.
-    constexpr bool kCoop = WICCA_STRIP_COOP && ROWB % 16 == 0;
-    constexpr int STAGE = kCoop ? ROWB : (ROWB + 15) & ~15;
+    constexpr int STAGE = (ICONS * C * (int)sizeof(OutT) + 15) & ~15;
     __shared__ __attribute__((aligned(16))) uint8_t smem[kStripWaves * STAGE];
 
     // ---- work: block -> (image, icon row, group of kStripWaves strips); wave -> strip
@@ -352,7 +347,7 @@ __global__ __launch_bounds__(64 * kStripWaves) void haar_strip_kernel(LLParams p
     const int64_t spx0 = (int64_t)strip * STRIP;     // first pixel of the strip
     const int64_t Wp = w.out_w << L;                 // padded width
     uint8_t* stage = smem + wave * STAGE;
-    if (spx0 < Wp) {  // else the whole wave is idle (it only joins the cooperative store)
+    if (spx0 < Wp) {  // else the whole wave is idle (no workgroup barriers in this kernel)
 
         const int64_t y0 = (int64_t)w.oy << L;
         const int rows_real = (int)min<int64_t>(max<int64_t>(w.H - y0, 0), R);
@@ -530,39 +525,18 @@ __global__ __launch_bounds__(64 * kStripWaves) void haar_strip_kernel(LLParams p
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-        if constexpr (!kCoop) {
-            // ---- store the strip's icon bytes (contiguous in the icon row)
-            const int nbytes = n_out * C * (int)sizeof(OutT);
-            uint8_t* drow = w.dst + (int64_t)w.oy * w.dst_pitch + ox0 * C * (int64_t)sizeof(OutT);
-            if ((((uintptr_t)drow | (uintptr_t)nbytes) & 3) == 0) {
-                const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stage);
-                uint32_t* d32 = reinterpret_cast<uint32_t*>(drow);
-                for (int i = lane; i < (nbytes >> 2); i += 64) {
-                    if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s32[i], d32 + i);
-                    else d32[i] = s32[i];
-                }
-            } else {
-                for (int i = lane; i < nbytes; i += 64) drow[i] = stage[i];
-            }
-        }
-    }
-    if constexpr (kCoop) {
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS-only barrier
-        const int64_t gox0 = ((int64_t)w.seg * kStripWaves * STRIP) >> L;  // first icon of the group
-        const int nbytes =
-            (int)max<int64_t>(min<int64_t>((int64_t)kStripWaves * ICONS, w.out_w - gox0), 0) * C *
-            (int)sizeof(OutT);
-        uint8_t* drow = w.dst + (int64_t)w.oy * w.dst_pitch + gox0 * C * (int64_t)sizeof(OutT);
-        const int tid = threadIdx.x;
-        if ((((uintptr_t)drow | (uintptr_t)nbytes) & 15) == 0) {
-            const u32x4* s16 = reinterpret_cast<const u32x4*>(smem);
-            u32x4* d16 = reinterpret_cast<u32x4*>(drow);
-            for (int i = tid; i < (nbytes >> 4); i += 64 * kStripWaves) {
-                if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s16[i], d16 + i);
-                else d16[i] = s16[i];
+        // ---- store the strip's icon bytes (contiguous in the icon row)
+        const int nbytes = n_out * C * (int)sizeof(OutT);
+        uint8_t* drow = w.dst + (int64_t)w.oy * w.dst_pitch + ox0 * C * (int64_t)sizeof(OutT);
+        if ((((uintptr_t)drow | (uintptr_t)nbytes) & 3) == 0) {
+            const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stage);
+            uint32_t* d32 = reinterpret_cast<uint32_t*>(drow);
+            for (int i = lane; i < (nbytes >> 2); i += 64) {
+                if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s32[i], d32 + i);
+                else d32[i] = s32[i];
             }
         } else {
-            for (int i = tid; i < nbytes; i += 64 * kStripWaves) drow[i] = smem[i];
+            for (int i = lane; i < nbytes; i += 64) drow[i] = stage[i];
         }
     }
 }

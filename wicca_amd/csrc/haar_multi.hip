@@ -252,9 +252,6 @@ __device__ __forceinline__ void store_window(const MultiParams& p, const MultiCt
             const uint8_t* st = x.stage + buf * S::BUF + S::off(t) + (idx % S::slots(t)) * S::row_pitch(t);
             uint8_t* drow = p.dst[t] + (int64_t)x.img * p.dst_stride[t] + oy * p.dst_pitch[t] +
                             (x.gpx0 >> t) * C;
-#ifdef WICCA_MULTI_ONE_ROW  // experiment: every row of the band lands on its first row
-            drow -= (int64_t)idx * p.dst_pitch[t];
-#endif
 #ifdef WICCA_MULTI_ABLATE_STORE  // timing-only build: icons computed and staged, not stored
             if (x.lane == 0x7FFF) drow[0] = st[0];
 #else
