@@ -113,6 +113,32 @@ __device__ __forceinline__ float finish<float>(uint32_t s, int L)
 template <>
 __device__ __forceinline__ uint32_t finish<uint32_t>(uint32_t s, int) { return s; }
 
+// Icon stores into a wave-uniform row base.  WICCA_STORE_AUX < 0: flat
+// stores, non-temporal when WICCA_NT_STORES; otherwise a raw buffer store with
+// that cache-policy immediate (gfx950: sc0 = 1, nt = 2, sc1 = 16).
+__device__ __forceinline__ void store_row_b32(uint8_t* row, uint32_t byte_off, uint32_t v)
+{
+    if constexpr (WICCA_STORE_AUX >= 0) {
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b32(v, rs, byte_off, 0, WICCA_STORE_AUX);
+    } else if constexpr (WICCA_NT_STORES) {
+        __builtin_nontemporal_store(v, reinterpret_cast<uint32_t*>(row + byte_off));
+    } else {
+        *reinterpret_cast<uint32_t*>(row + byte_off) = v;
+    }
+}
+__device__ __forceinline__ void store_row_b128(uint8_t* row, uint32_t byte_off, u32x4 v)
+{
+    if constexpr (WICCA_STORE_AUX >= 0) {
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row, (short)0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, byte_off, 0, WICCA_STORE_AUX);
+    } else if constexpr (WICCA_NT_STORES) {
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(row + byte_off));
+    } else {
+        *reinterpret_cast<u32x4*>(row + byte_off) = v;
+    }
+}
+
 __device__ __forceinline__ u32x4 load_row16(const uint8_t* row, uint32_t nrec, uint32_t voff)
 {
     __amdgpu_buffer_rsrc_t rs =

@@ -12,6 +12,9 @@
 #define WICCA_NT_STORES 1     // non-temporal icon stores (K1, K1s, K5): +2-9 % at D = 1-5
                               // (profiles/r01_ab_nt_stores.json)
 #endif
+#ifndef WICCA_STORE_AUX
+#define WICCA_STORE_AUX -1    // icon stores: < 0 flat (nt per WICCA_NT_STORES), else buffer-store cache policy
+#endif
 #ifndef WICCA_CHUNK_ROWS
 #define WICCA_CHUNK_ROWS 0    // rows per load chunk (C dwordx4 per lane per row); 0 = table
 #endif

@@ -193,9 +193,7 @@ __device__ __forceinline__ void band_epilogue(const LLParams& p, const BlockWork
     // partial chunk of a row is written with 4-B / 1-B stores
     const int full = nbytes & ~15;
     for (int i = tid * 16; i < full; i += kThreads * 16) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(stage + i);
-        if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(drow + i));
-        else *reinterpret_cast<u32x4*>(drow + i) = v;
+        store_row_b128(drow, (uint32_t)i, *reinterpret_cast<const u32x4*>(stage + i));
     }
     if (tid < nbytes - full) drow[full + tid] = stage[full + tid];
 }
@@ -530,10 +528,8 @@ __global__ __launch_bounds__(64 * kStripWaves) void haar_strip_kernel(LLParams p
         uint8_t* drow = w.dst + (int64_t)w.oy * w.dst_pitch + ox0 * C * (int64_t)sizeof(OutT);
         if ((((uintptr_t)drow | (uintptr_t)nbytes) & 3) == 0) {
             const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stage);
-            uint32_t* d32 = reinterpret_cast<uint32_t*>(drow);
             for (int i = lane; i < (nbytes >> 2); i += 64) {
-                if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s32[i], d32 + i);
-                else d32[i] = s32[i];
+                store_row_b32(drow, 4u * (uint32_t)i, s32[i]);
             }
         } else {
             for (int i = lane; i < nbytes; i += 64) drow[i] = stage[i];

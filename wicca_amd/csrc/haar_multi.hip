@@ -257,17 +257,13 @@ __device__ __forceinline__ void store_window(const MultiParams& p, const MultiCt
 #else
             if ((((uintptr_t)drow | (uintptr_t)nbytes) & 15) == 0) {
                 const u32x4* s16 = reinterpret_cast<const u32x4*>(st);
-                u32x4* d16 = reinterpret_cast<u32x4*>(drow);
                 for (int i = x.lane; i < (nbytes >> 4); i += 64) {
-                    if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s16[i], d16 + i);
-                    else d16[i] = s16[i];
+                    store_row_b128(drow, 16u * (uint32_t)i, s16[i]);
                 }
             } else if ((((uintptr_t)drow | (uintptr_t)nbytes) & 3) == 0) {
                 const uint32_t* s32 = reinterpret_cast<const uint32_t*>(st);
-                uint32_t* d32 = reinterpret_cast<uint32_t*>(drow);
                 for (int i = x.lane; i < (nbytes >> 2); i += 64) {
-                    if constexpr (WICCA_NT_STORES) __builtin_nontemporal_store(s32[i], d32 + i);
-                    else d32[i] = s32[i];
+                    store_row_b32(drow, 4u * (uint32_t)i, s32[i]);
                 }
             } else {
                 for (int i = x.lane; i < nbytes; i += 64) drow[i] = st[i];
