@@ -127,6 +127,21 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs, int64_t n, int64_t C,
                            void* stream);
 
 /*
+ * Multi-GPU driver for host arrays: the ragged batch of HOST images `descs`
+ * (as in wicca_haar_ll_u8_batch with src/dst on the host) is split into
+ * contiguous image ranges balanced by pixel count, one per device of
+ * devices[0..n_devices) (NULL / 0: every visible device); one host thread per
+ * device uploads, runs the batch launch on its own stream and downloads.
+ * Image-parallel, no inter-device traffic.  Serves one process that owns
+ * several GPUs, e.g. the ClassifierProcessor icon stage
+ * (classifying_tools.py:297-323) fed from a thread pool; the benchmark's
+ * one-process-per-GPU form is bench.py over torch.distributed.
+ */
+int wicca_haar_ll_u8_batch_multi_gpu(const wicca_image_desc* descs, int64_t n, int64_t C,
+                                     int depth, int border_type, int border_constant,
+                                     const int* devices, int n_devices);
+
+/*
  * Multi-depth: the icon of every depth in depths[0..n_depths) (SURVEY 8f item
  * 1; the caller's depth loop, classifying_tools.py:546-551).  Depths 1..8 come
  * from ONE upload and ONE read of the image (block sums + integer pyramid);

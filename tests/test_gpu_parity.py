@@ -349,3 +349,23 @@ def test_multi_depth1_windows_tails(coder):
             for i in range(n):
                 ref = c_oracle.ll_int_block(imgs[i], d, border, k)[0]
                 assert np.array_equal(got[i], ref), (n, H, W, C, d, border, i)
+
+
+def test_batch_multi_gpu_entry(coder):
+    """wicca_haar_ll_u8_batch_multi_gpu: the ragged host batch split over
+    device lists (the same device listed several times on a one-GPU box runs
+    concurrent host threads on it) matches the per-image oracle; uneven image
+    sizes, fewer images than devices, C = 1 and 3, both borders."""
+    rng = np.random.default_rng(5)
+    batches = [[rng.integers(0, 256, (int(h), int(w), 3), dtype=np.uint8)
+                for h, w in zip(rng.integers(1, 700, 9), rng.integers(1, 900, 9))],
+               [rng.integers(0, 256, (320, 224, 1), dtype=np.uint8)],  # no padding: (H, W, 1) + padding raises like the reference
+               [rng.integers(0, 256, (2000, 64, 3), dtype=np.uint8),
+                rng.integers(0, 256, (5, 5, 3), dtype=np.uint8)]]
+    for devices in ([0], [0, 0], [0, 0, 0, 0, 0]):
+        for imgs in batches:
+            for d, border, k in ((3, 1, 0), (5, 0, 77)):
+                outs = coder.get_small_copies(imgs, d, border, k, devices=devices)
+                for o, im in zip(outs, imgs):
+                    ref = c_oracle.ll_int_block(im, d, border, k)[0]
+                    assert np.array_equal(o, ref), (devices, im.shape, d, border)

@@ -49,7 +49,9 @@ SIGNATURES = {
     "wicca_haar_ll_u8_uniform": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, _int, _int,
                                         _int, _p, _i64, _i64, _int, _p]),
     "wicca_haar_ll_u8_batch": (_int, [ctypes.POINTER(ImageDesc), _i64, _i64, _int, _int, _int,
-                                      _int, _p]),
+                                      _int, _int, _int, _p]),
+    "wicca_haar_ll_u8_batch_multi_gpu": (_int, [ctypes.POINTER(ImageDesc), _i64, _i64, _int, _int,
+                                                _int, ctypes.POINTER(_int), _int]),
     "wicca_haar_ll_u8_multi": (_int, [_p, _i64, _i64, _i64, _i64, ctypes.POINTER(_int), _int,
                                       _int, _int, ctypes.POINTER(_p), ctypes.POINTER(_i64),
                                       _int, _int, _int, _p]),

@@ -156,11 +156,15 @@ class HaarCoder(WaveletCoder):
 
     def get_small_copies(self, images: Sequence[np.ndarray], transform_depth: int,
                          border_type: int = BORDER_REPLICATE,
-                         border_constant: int = 0) -> list[np.ndarray]:
+                         border_constant: int = 0,
+                         devices: Sequence[int] | None = None) -> list[np.ndarray]:
         """Icons of a ragged batch of images, one kernel launch per channel count.
 
         Equivalent to ``[self.get_small_copy(im, d, ...) for im in images]``
-        (each image validated exactly like the single-image call).
+        (each image validated exactly like the single-image call).  With
+        ``devices`` (several device ids), the batch is split image-parallel
+        over those GPUs, one host thread each
+        (``wicca_haar_ll_u8_batch_multi_gpu``).
         """
         prepared = [self._prepare(im, transform_depth, border_type, border_constant)
                     for im in images]
@@ -187,8 +191,14 @@ class HaarCoder(WaveletCoder):
             border = prepared[idx[0]][2]
             k = prepared[idx[0]][3]
             depth = prepared[idx[0]][1]
-            _lib.check(self._lib.wicca_haar_ll_u8_batch(descs, len(idx), C, depth, border, k,
-                                                        0, 0, self.device, None))
+            if devices is not None and len(devices) > 1:
+                devs = (ctypes.c_int * len(devices))(*devices)
+                _lib.check(self._lib.wicca_haar_ll_u8_batch_multi_gpu(
+                    descs, len(idx), C, depth, border, k, devs, len(devices)))
+            else:
+                dev = devices[0] if devices else self.device
+                _lib.check(self._lib.wicca_haar_ll_u8_batch(descs, len(idx), C, depth, border, k,
+                                                            0, 0, dev, None))
             del keep
         return outs  # type: ignore[return-value]
 

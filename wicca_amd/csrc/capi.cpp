@@ -21,6 +21,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/wicca_haar.h"
@@ -622,6 +623,59 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
     }
     // descriptors and staging live in the workspace: finish before it returns
     HIP_TRY(hipStreamSynchronize(stream));
+    return WICCA_OK;
+}
+
+int wicca_haar_ll_u8_batch_multi_gpu(const wicca_image_desc* descs, int64_t n, int64_t C,
+                                     int depth, int border_type, int border_constant,
+                                     const int* devices, int n_devices)
+{
+    if (n < 0 || (n > 0 && !descs)) return fail(WICCA_ERR_ARG, "bad descriptor array");
+    if (n == 0) return WICCA_OK;
+    init_once();
+    if (g_device_count <= 0) return fail(WICCA_ERR_NODEVICE, "no HIP device visible");
+    std::vector<int> devs;
+    if (devices && n_devices > 0) {
+        devs.assign(devices, devices + n_devices);
+    } else {
+        for (int d = 0; d < g_device_count; ++d) devs.push_back(d);
+    }
+    for (int d : devs)
+        if (d < 0 || d >= g_device_count) return fail(WICCA_ERR_ARG, "device %d out of range", d);
+    // contiguous image ranges balanced by pixel count, at most one per device
+    const int nd = (int)std::min<int64_t>((int64_t)devs.size(), n);
+    int64_t total = 0;
+    for (int64_t i = 0; i < n; ++i) total += std::max<int64_t>(descs[i].height, 0) * std::max<int64_t>(descs[i].width, 0);
+    std::vector<int64_t> first((size_t)nd + 1, n);  // range r = images [first[r], first[r+1])
+    first[0] = 0;
+    {
+        int64_t acc = 0;
+        int r = 0;
+        for (int64_t i = 0; i < n && r < nd - 1; ++i) {
+            acc += std::max<int64_t>(descs[i].height, 0) * std::max<int64_t>(descs[i].width, 0);
+            // close range r after image i once it holds its share, leaving an
+            // image for each later range
+            if (acc >= total * (r + 1) / nd && n - (i + 1) >= nd - 1 - r) first[(size_t)++r] = i + 1;
+        }
+    }
+    std::vector<int> rcs((size_t)nd, WICCA_OK);
+    std::vector<std::string> msgs((size_t)nd);
+    auto work = [&](int r) {
+        const int64_t a = first[(size_t)r], b = first[(size_t)r + 1];
+        if (b <= a) return;
+        rcs[(size_t)r] = wicca_haar_ll_u8_batch(descs + a, b - a, C, depth, border_type,
+                                                border_constant, 0, 0, devs[(size_t)r], nullptr);
+        if (rcs[(size_t)r]) msgs[(size_t)r] = t_last_error;
+    };
+    std::vector<std::thread> pool;
+    for (int r = 1; r < nd; ++r) pool.emplace_back(work, r);
+    work(0);
+    for (auto& t : pool) t.join();
+    for (int r = 0; r < nd; ++r)
+        if (rcs[(size_t)r]) {
+            t_last_error = msgs[(size_t)r];
+            return rcs[(size_t)r];
+        }
     return WICCA_OK;
 }
 
