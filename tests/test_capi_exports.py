@@ -68,3 +68,19 @@ def test_single_hip_runtime_per_process():
     maps = open("/proc/self/maps").read()
     runtimes = {ln.split()[-1] for ln in maps.splitlines() if "libamdhip64" in ln}
     assert len(runtimes) == 1, runtimes
+
+
+def test_multi_gpu_batch_host_checks():
+    """The multi-GPU host-batch entry: an empty batch is a no-op and a bad
+    descriptor array is an argument error, before any device is touched; on
+    a box without a GPU a real batch reports 'no device' (never a CPU path)."""
+    lib = _lib.load()
+    assert lib.wicca_haar_ll_u8_batch_multi_gpu(None, 0, 3, 2, 1, 0, None, 0) == 0
+    assert lib.wicca_haar_ll_u8_batch_multi_gpu(None, 2, 3, 2, 1, 0, None, 0) == _lib.WICCA_ERR_ARG
+    if _lib.device_count() == 0:
+        img = (ctypes.c_uint8 * 48)()
+        out = (ctypes.c_uint8 * 12)()
+        desc = (_lib.ImageDesc * 1)(_lib.ImageDesc(ctypes.addressof(img), ctypes.addressof(out),
+                                                   4, 4, 12, 6))
+        rc = lib.wicca_haar_ll_u8_batch_multi_gpu(desc, 1, 3, 1, 1, 0, None, 0)
+        assert rc == _lib.WICCA_ERR_NODEVICE
