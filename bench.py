@@ -40,10 +40,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=["batch", "tiled", "multi"], default="batch",
+    ap.add_argument("--config", choices=["batch", "tiled", "multi", "ragged"], default="batch",
                     help="batch: configs[2]/[3] image-parallel (default); "
                          "tiled: configs[4], one 65536^2 RGB image row-sharded at depth 8; "
-                         "multi: configs[2]'s depth sweep 1..6 from one read (SURVEY 8f)")
+                         "multi: configs[2]'s depth sweep 1..6 from one read (SURVEY 8f); "
+                         "ragged: a batch of random-size images in one launch (A7 caller)")
     ap.add_argument("--depths", default="1,2,3,4,5,6", help="depth list of --config multi")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
@@ -220,6 +221,83 @@ def run_tiled(args, torch, dist, world, rank, local_rank):
     }
 
 
+def run_ragged(args, torch, rank):
+    """A ragged batch (the caller's real shape: files of different sizes) in
+    ONE launch through wicca_haar_ll_u8_batch with device descriptors."""
+    from wicca_amd import _lib
+    lib = _lib.load()
+    B, C, D = args.images, args.channels, args.depth
+    rng = np.random.default_rng(args.seed)
+    Hs = rng.integers(args.height // 2, args.height + 1, B)
+    Ws = rng.integers(args.width // 2, args.width + 1, B)
+    r = 1 << D
+    pitches = [(int(w) * C + 15) // 16 * 16 for w in Ws]
+    ohs = [-(-int(h) // r) for h in Hs]
+    ows = [-(-int(w) // r) for w in Ws]
+    opitches = [(ow * C + 15) // 16 * 16 for ow in ows]
+    in_off = np.concatenate([[0], np.cumsum([p * int(h) for p, h in zip(pitches, Hs)])])
+    out_off = np.concatenate([[0], np.cumsum([p * oh for p, oh in zip(opitches, ohs)])])
+    src = torch.empty(int(in_off[-1]), dtype=torch.uint8, device="cuda")
+    dst = torch.empty(int(out_off[-1]), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    descs = (_lib.ImageDesc * B)()
+    for i in range(B):
+        h, w = int(Hs[i]), int(Ws[i])
+        _lib.check(lib.wicca_synth_u8(ctypes.c_void_p(src.data_ptr() + int(in_off[i])), 1, h, w, C,
+                                      pitches[i], h * pitches[i], args.seed * 1000003 + i, -1, sh))
+        descs[i] = _lib.ImageDesc(src.data_ptr() + int(in_off[i]), dst.data_ptr() + int(out_off[i]),
+                                  h, w, pitches[i], opitches[i])
+
+    def step():
+        _lib.check(lib.wicca_haar_ll_u8_batch(descs, B, C, D, args.border, 0, 1, 1, -1, sh))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall_ms = (time.perf_counter() - t0) / args.steps * 1e3
+    dev_ms = e0.elapsed_time(e1) / args.steps
+    verified = None
+    if not args.no_verify:
+        from oracle import haar_numpy
+        from wicca_amd.synth import synth_image
+        i = B - 1
+        h, w = int(Hs[i]), int(Ws[i])
+        ref = haar_numpy.get_small_copy(synth_image(args.seed * 1000003 + i, 0, h, w, C), D,
+                                        args.border)
+        raw = dst[int(out_off[i]):int(out_off[i]) + opitches[i] * ohs[i]].view(ohs[i], opitches[i])
+        got = raw[:, :ows[i] * C].cpu().numpy().reshape(ohs[i], ows[i], C)
+        verified = bool(np.array_equal(got, ref))
+        if not verified:
+            raise SystemExit("ragged bench verification FAILED")
+    alg = int(sum(int(h) * int(w) * C for h, w in zip(Hs, Ws)) + sum(oh * ow * C for oh, ow in zip(ohs, ows)))
+    mpix = float(sum(int(h) * int(w) for h, w in zip(Hs, Ws))) / 1e6
+    return {
+        "metric": BASELINE["metric"], "value": round(mpix / (wall_ms / 1e3), 1), "unit": "MP/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall_ms, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (on-device splitmix64 images of random sizes, HBM-resident before timing)",
+        "config": {"workload": f"ragged batch of {B} RGB images, H in [{args.height // 2}, "
+                               f"{args.height}], W in [{args.width // 2}, {args.width}], depth {D}, "
+                               "one launch (device descriptors)",
+                   "images": B, "megapixels": round(mpix, 2), "depth": D},
+        "roofline": {"bound": "hbm", "achieved": round(alg / (dev_ms / 1e3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(alg / (dev_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "descriptor upload + ragged block-sum launch (stream time per call)",
+                     "kernel_ms": round(dev_ms, 4), "alg_bytes_per_launch": alg},
+        "cpu_baseline": None, "verified_vs_numpy_port": verified,
+    }
+
+
 def run_multi(args, torch, rank):
     """All depths of configs[2]'s sweep from ONE read of the batch
     (wicca_haar_ll_u8_multi_uniform), against one launch per depth."""
@@ -325,6 +403,11 @@ def main():
         raise SystemExit("no HIP device visible")
     if args.config == "multi":
         out = run_multi(args, torch, rank)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        return
+    if args.config == "ragged":
+        out = run_ragged(args, torch, rank)
         if rank == 0:
             print(json.dumps(out), flush=True)
         return
