@@ -144,7 +144,7 @@ __device__ __forceinline__ u32x4 load_row16(const uint8_t* row, uint32_t nrec, u
     __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(row), (short)0, (int)nrec, 0x00020000);
     return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, 0,
-                                                                           WICCA_NT_LOADS ? 2 : 0));
+                                                                           WICCA_LOAD_AUX));
 }
 
 template <int C>
@@ -165,13 +165,13 @@ __device__ __forceinline__ void load_lane(uint32_t (&d)[NDW], const uint8_t* row
 #pragma unroll
         for (int q = 0; q < NDW / 4; ++q) {
             const u32x4 v = __builtin_bit_cast(
-                u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16 * q, 0, WICCA_NT_LOADS ? 2 : 0));
+                u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16 * q, 0, WICCA_LOAD_AUX));
             d[4 * q] = v[0]; d[4 * q + 1] = v[1]; d[4 * q + 2] = v[2]; d[4 * q + 3] = v[3];
         }
     } else {
         typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
         const u32x3 v = __builtin_bit_cast(
-            u32x3, __builtin_amdgcn_raw_buffer_load_b96(rs, voff, 0, WICCA_NT_LOADS ? 2 : 0));
+            u32x3, __builtin_amdgcn_raw_buffer_load_b96(rs, voff, 0, WICCA_LOAD_AUX));
         d[0] = v[0]; d[1] = v[1]; d[2] = v[2];
     }
 }

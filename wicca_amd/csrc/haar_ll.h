@@ -8,6 +8,9 @@
 #ifndef WICCA_NT_LOADS
 #define WICCA_NT_LOADS 1      // non-temporal loads for the once-read image stream
 #endif
+#ifndef WICCA_LOAD_AUX        // image-stream buffer-load cache policy (gfx950: sc0 = 1, nt = 2, sc1 = 16)
+#define WICCA_LOAD_AUX (WICCA_NT_LOADS ? 2 : 0)
+#endif
 #ifndef WICCA_NT_STORES
 #define WICCA_NT_STORES 1     // non-temporal icon stores (K1, K1s, K5): +2-9 % at D = 1-5
                               // (profiles/r01_ab_nt_stores.json)
