@@ -123,18 +123,33 @@ int acquire(int device, WorkspaceLease& lease)
     return WICCA_OK;
 }
 
-int select_device(int device, int* out)
+// Restores the calling thread's current HIP device when an entry point
+// returns: entries switch to the requested device, the caller's selection
+// (e.g. torch's) is left as it was.
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard() = default;
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+int select_device(int device, int* out, DeviceGuard& guard)
 {
     init_once();
     if (g_device_count <= 0) return fail(WICCA_ERR_NODEVICE, "no HIP device visible");
-    if (device < 0) {
-        int cur = 0;
-        HIP_TRY(hipGetDevice(&cur));
-        device = cur;
-    }
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    if (device < 0) device = cur;
     if (device >= g_device_count)
         return fail(WICCA_ERR_ARG, "device %d out of range (%d visible)", device, g_device_count);
-    HIP_TRY(hipSetDevice(device));
+    if (device != cur) {
+        HIP_TRY(hipSetDevice(device));
+        guard.prev = cur;
+    }
     *out = device;
     return WICCA_OK;
 }
@@ -398,8 +413,9 @@ int single_image(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t sr
     icon_dims(H, W, depth, &oh, &ow);
     const int64_t out_row = ow * C * (int64_t)sizeof(OutT);
     if (dst_pitch < out_row) return fail(WICCA_ERR_ARG, "dst pitch too small");
+    DeviceGuard dg;
     int dev;
-    if ((rc = select_device(device, &dev))) return rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
     WorkspaceLease lease;
     if ((rc = acquire(dev, lease))) return rc;
     Workspace* ws = lease.ws;
@@ -489,8 +505,9 @@ int wicca_haar_ll_u8_uniform(const uint8_t* src, int64_t n, int64_t H, int64_t W
     if (dst_pitch < ow * C || (n > 1 && dst_image_stride < dst_pitch * oh) ||
         (n > 1 && src_image_stride < src_pitch * H))
         return fail(WICCA_ERR_ARG, "pitch/stride too small");
+    DeviceGuard dg;
     int dev;
-    if ((rc = select_device(device, &dev))) return rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
     WorkspaceLease lease;
     if ((rc = acquire(dev, lease))) return rc;
     hipStream_t stream = stream_in ? (hipStream_t)stream_in : lease.ws->stream;
@@ -520,8 +537,9 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
         if (descs_in[i].dst_pitch < ow * C)
             return fail(WICCA_ERR_ARG, "dst pitch of image %lld too small", (long long)i);
     }
+    DeviceGuard dg;
     int dev, rc;
-    if ((rc = select_device(device, &dev))) return rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
     WorkspaceLease lease;
     if ((rc = acquire(dev, lease))) return rc;
     Workspace* ws = lease.ws;
@@ -696,8 +714,9 @@ int wicca_haar_ll_u8_multi(const uint8_t* src, int64_t H, int64_t W, int64_t C, 
         icon_dims(H, W, depths[i], &oh, &ow);
         if (dst_pitches[i] < ow * C) return fail(WICCA_ERR_ARG, "dst pitch %d too small", i);
     }
+    DeviceGuard dg;
     int dev;
-    if ((rc = select_device(device, &dev))) return rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
     WorkspaceLease lease;
     if ((rc = acquire(dev, lease))) return rc;
     Workspace* ws = lease.ws;
@@ -803,8 +822,9 @@ int wicca_haar_ll_u8_multi_uniform(const uint8_t* src, int64_t n, int64_t H, int
         if (!dsts[i] || dst_pitches[i] < ow * C || (n > 1 && dst_image_strides[i] < dst_pitches[i] * oh))
             return fail(WICCA_ERR_ARG, "bad icon buffer for depth %d", depths[i]);
     }
+    DeviceGuard dg;
     int dev;
-    if ((rc = select_device(device, &dev))) return rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
     WorkspaceLease lease;
     if ((rc = acquire(dev, lease))) return rc;
     hipStream_t stream = stream_in ? (hipStream_t)stream_in : lease.ws->stream;
@@ -824,8 +844,9 @@ int wicca_synth_u8(uint8_t* dst, int64_t n, int64_t H, int64_t W, int64_t C, int
     if (pitch < W * C || pitch % 16 || (uintptr_t)dst % 16 ||
         (n > 1 && (image_stride < pitch * H || image_stride % 16)))
         return fail(WICCA_ERR_ARG, "synth needs 16-byte aligned rows and images");
+    DeviceGuard dg;
     int dev, rc;
-    if ((rc = select_device(device, &dev))) return rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
     WorkspaceLease lease;
     if ((rc = acquire(dev, lease))) return rc;
     hipStream_t stream = stream_in ? (hipStream_t)stream_in : lease.ws->stream;
@@ -842,8 +863,9 @@ int wicca_synth_band_u8(uint8_t* dst, int64_t rows, int64_t W, int64_t C, int64_
     if (rows < 0 || W < 0 || C < 0 || first_row < 0) return fail(WICCA_ERR_ARG, "negative size");
     if (pitch < W * C || pitch % 16 || (uintptr_t)dst % 16)
         return fail(WICCA_ERR_ARG, "synth needs 16-byte aligned rows");
+    DeviceGuard dg;
     int dev, rc;
-    if ((rc = select_device(device, &dev))) return rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
     WorkspaceLease lease;
     if ((rc = acquire(dev, lease))) return rc;
     hipStream_t stream = stream_in ? (hipStream_t)stream_in : lease.ws->stream;
