@@ -51,6 +51,12 @@
 #ifndef WICCA_STRIP_WAVES
 #define WICCA_STRIP_WAVES 4   // K1s: wave strips per workgroup
 #endif
+#ifndef WICCA_STRIP_WG_CAP3
+#define WICCA_STRIP_WG_CAP3 4   // K1s at D=3: at most this many workgroups (= waves/SIMD) per CU
+#endif
+#ifndef WICCA_K1_WG_CAP1
+#define WICCA_K1_WG_CAP1 0      // K1 at D=1: at most this many workgroups per CU (0 = no cap)
+#endif
 #ifndef WICCA_STRIP_DOT
 #define WICCA_STRIP_DOT 1     // strip kernel: v_dot4 per-(icon, channel) sums on non-edge strips
 #endif
@@ -69,6 +75,14 @@ constexpr bool use_strip_kernel(int L)
 // 16 whole RGB pixels — C dwordx4 at a 48-B lane stride — measured 4.3-4.6
 // TB/s against 6.6: strided wave loads cost far more than an LDS transpose.)
 constexpr int strip_lane_pixels(int C) { return C == 3 ? 4 : 16 / C; }
+
+// Occupancy caps, enforced through the workgroup's LDS footprint (a CU holds
+// 160 KiB): fewer concurrent row streams read faster at D = 3
+// (profiles/r01_ab_occupancy_caps.json).
+constexpr int kLdsPerCU = 160 * 1024;
+constexpr int lds_for_cap(int cap) { return cap > 0 ? kLdsPerCU / (cap + 1) + 16 : 0; }
+constexpr int strip_min_lds(int L) { return L == 3 ? lds_for_cap(WICCA_STRIP_WG_CAP3) : 0; }
+constexpr int k1_min_lds(int L) { return L == 1 ? lds_for_cap(WICCA_K1_WG_CAP1) : 0; }
 
 constexpr int strip_chunk_rows(int L)
 {

@@ -227,7 +227,7 @@ void haar_block_sum_kernel(LLParams p)
 
     // Wide outputs (f32/u32 at small L) reuse the column-sum area for staging.
     constexpr bool kReuse = kColBytes + kStageAligned > 40 * 1024;
-    constexpr int kSmem = (kReuse ? kColBytes : kColBytes + kStageAligned) + 16;
+    constexpr int kSmem = std::max((kReuse ? kColBytes : kColBytes + kStageAligned) + 16, k1_min_lds(L));
     __shared__ __attribute__((aligned(16))) uint8_t smem[kSmem];
     uint16_t* colsum = reinterpret_cast<uint16_t*>(smem);
     uint8_t* stage = kReuse ? smem : smem + kColBytes;
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(64 * kStripWaves) void haar_strip_kernel(LLParams p
     constexpr int U = R < strip_chunk_rows(L) ? R : strip_chunk_rows(L);
     constexpr int ICONS = STRIP / G;                 // icons per wave strip
     constexpr int STAGE = (ICONS * C * (int)sizeof(OutT) + 15) & ~15;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kStripWaves * STAGE];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[std::max(kStripWaves * STAGE, strip_min_lds(L))];
 
     // ---- work: block -> (image, icon row, group of kStripWaves strips); wave -> strip
     const int lane = threadIdx.x & 63;
