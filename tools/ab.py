@@ -61,7 +61,8 @@ def main():
     for D in args.depths:
         r = 1 << D
         oh, ow = -(-H // r), -(-W // r)
-        opitch = (ow * C + 15) // 16 * 16
+        align = int(os.environ.get("WICCA_AB_OPITCH_ALIGN", "16"))  # icon row pitch alignment
+        opitch = (ow * C + align - 1) // align * align
         dst = torch.empty(B * oh * opitch, dtype=torch.uint8, device="cuda")
         alg = B * (H * W * C + oh * ow * C)
         ref = None
