@@ -8,7 +8,7 @@
 #ifndef WICCA_NT_LOADS
 #define WICCA_NT_LOADS 1      // non-temporal loads for the once-read image stream
 #endif
-#ifndef WICCA_LOAD_AUX        // image-stream buffer-load cache policy (gfx950: sc0 = 1, nt = 2, sc1 = 16)
+#ifndef WICCA_LOAD_AUX  // image-stream load cache policy (sc0 = 1, nt = 2, sc1 = 16; profiles/r01_ab_load_policy.json)
 #define WICCA_LOAD_AUX (WICCA_NT_LOADS ? 2 : 0)
 #endif
 #ifndef WICCA_NT_STORES
@@ -16,7 +16,8 @@
                               // (profiles/r01_ab_nt_stores.json)
 #endif
 #ifndef WICCA_STORE_AUX
-#define WICCA_STORE_AUX -1    // icon stores: < 0 flat (nt per WICCA_NT_STORES), else buffer-store cache policy
+#define WICCA_STORE_AUX -1    // icon stores: < 0 flat (nt per WICCA_NT_STORES), else buffer-store
+                              // cache policy (profiles/r01_ab_store_policy.json)
 #endif
 #ifndef WICCA_CHUNK_ROWS
 #define WICCA_CHUNK_ROWS 0    // rows per load chunk (C dwordx4 per lane per row); 0 = table
@@ -36,7 +37,7 @@
 #define WICCA_MULTI_DOT 1     // K5: v_dot4 per-(icon, channel) sums on interior strips
 #endif
 #ifndef WICCA_MULTI_WAVES
-#define WICCA_MULTI_WAVES 4   // K5: wave strips per workgroup
+#define WICCA_MULTI_WAVES 4   // K5: wave strips per workgroup (8: slower, profiles/r01_ab_k5_stores.json)
 #endif
 #ifndef WICCA_MULTI_D1
 #define WICCA_MULTI_D1 1      // K5 also serves depth 1: depths 1-6 in 3.3 ms vs 5.1-5.3 with a
@@ -58,7 +59,7 @@
 #define WICCA_K1_WG_CAP1 0      // K1 at D=1: at most this many workgroups per CU (0 = no cap)
 #endif
 #ifndef WICCA_STRIP_DOT
-#define WICCA_STRIP_DOT 1     // strip kernel: v_dot4 per-(icon, channel) sums on non-edge strips
+#define WICCA_STRIP_DOT 1     // strip kernel: v_dot4 per-(icon, channel) sums on non-edge strips (neutral, fewer VGPRs)
 #endif
 
 namespace wicca {
@@ -77,8 +78,9 @@ constexpr bool use_strip_kernel(int L)
 constexpr int strip_lane_pixels(int C) { return C == 3 ? 4 : 16 / C; }
 
 // Occupancy caps, enforced through the workgroup's LDS footprint (a CU holds
-// 160 KiB): fewer concurrent row streams read faster at D = 3
-// (profiles/r01_ab_occupancy_caps.json).
+// 160 KiB).  At D = 3 the cap of 4 waves/SIMD also lifts the compiler's VGPR
+// target (107 instead of 63 VGPRs, more rows in flight per wave): +3.2-3.5 %;
+// caps measured slower at D = 1, 2 and 4-6 (profiles/r01_ab_occupancy_caps.json).
 constexpr int kLdsPerCU = 160 * 1024;
 constexpr int lds_for_cap(int cap) { return cap > 0 ? kLdsPerCU / (cap + 1) + 16 : 0; }
 constexpr int strip_min_lds(int L) { return L == 3 ? lds_for_cap(WICCA_STRIP_WG_CAP3) : 0; }
