@@ -369,3 +369,38 @@ def test_batch_multi_gpu_entry(coder):
                 for o, im in zip(outs, imgs):
                     ref = c_oracle.ll_int_block(im, d, border, k)[0]
                     assert np.array_equal(o, ref), (devices, im.shape, d, border)
+
+
+def test_batch_ragged_device_descriptors(coder):
+    """wicca_haar_ll_u8_batch with device-resident images and icons (the
+    bench's --config ragged path): one launch over random sizes, the strip
+    kernel (D = 2, 3) and the segment kernel (D = 1, 4-6), both borders."""
+    import ctypes
+    from wicca_amd import _lib
+    torch = pytest.importorskip("torch")
+    lib = _lib.load()
+    rng = np.random.default_rng(44)
+    for C in (1, 3, 4):
+        shapes = [(int(rng.integers(1, 600)), int(rng.integers(1, 5200))) for _ in range(11)]
+        imgs = [rng.integers(0, 256, (h, w, C), dtype=np.uint8) for h, w in shapes]
+        pitches = [(w * C + 15) // 16 * 16 for _, w in shapes]
+        srcs = []
+        for im, p in zip(imgs, pitches):
+            host = np.zeros((im.shape[0], p), np.uint8)
+            host[:, :im.shape[1] * C] = im.reshape(im.shape[0], -1)
+            srcs.append(torch.from_numpy(host).cuda())
+        for d, border, k in ((1, 1, 0), (2, 0, 9), (3, 1, 0), (4, 0, 250), (5, 1, 0), (6, 0, 3)):
+            r = 1 << d
+            descs = (_lib.ImageDesc * len(imgs))()
+            outs = []
+            for i, ((h, w), p) in enumerate(zip(shapes, pitches)):
+                oh, ow = -(-h // r), -(-w // r)
+                op = (ow * C + 15) // 16 * 16
+                o = torch.full((oh, op), 5, dtype=torch.uint8, device="cuda")
+                outs.append((o, oh, ow))
+                descs[i] = _lib.ImageDesc(srcs[i].data_ptr(), o.data_ptr(), h, w, p, op)
+            _lib.check(lib.wicca_haar_ll_u8_batch(descs, len(imgs), C, d, border, k, 1, 1, -1, None))
+            torch.cuda.synchronize()
+            for im, (o, oh, ow) in zip(imgs, outs):
+                got = o.cpu().numpy()[:, :ow * C].reshape(oh, ow, C)
+                assert np.array_equal(got, c_oracle.ll_int_block(im, d, border, k)[0]), (C, d, im.shape)
