@@ -92,7 +92,8 @@ constexpr int strip_chunk_rows(int L)
 }
 
 // Rows of a band loaded back to back before they are reduced (measured,
-// profiles/r01_variants*.jsonl): deep chunks pay at large depth.
+// profiles/r01_ab_epilogue_ablation.json, r01_ab_occupancy.json): 16-row chunks
+// beat 8 at D >= 4.
 constexpr int chunk_rows(int L)
 {
     return WICCA_CHUNK_ROWS > 0 ? WICCA_CHUNK_ROWS : (L >= 4 ? 16 : 8);
