@@ -521,7 +521,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": (f"haar_strip_kernel<L={D},C={C},u8>" if D in (2, 3)
+            "kernel": (f"haar_strip_kernel<L={D},C={C},u8>" if D in (2, 3, 5, 6)
                        else f"haar_block_sum_kernel<L={D},C={C},u8>"),
             "kernel_ms": round(kernel_ms, 4),
             "alg_bytes_per_launch": alg_bytes,

@@ -55,6 +55,9 @@
 #ifndef WICCA_STRIP_WG_CAP3
 #define WICCA_STRIP_WG_CAP3 4   // K1s at D=3: at most this many workgroups (= waves/SIMD) per CU
 #endif
+#ifndef WICCA_STRIP_WG_CAP_HI
+#define WICCA_STRIP_WG_CAP_HI 2 // K1s at D>=4 (when selected): at most this many workgroups per CU
+#endif
 #ifndef WICCA_K1_WG_CAP1
 #define WICCA_K1_WG_CAP1 0      // K1 at D=1: at most this many workgroups per CU (0 = no cap)
 #endif
@@ -64,11 +67,13 @@
 
 namespace wicca {
 
-// Which K1 variant serves depth L (in-process A/B, profiles/r01_ab_v7.json):
-// the wave-strip kernel wins at depths 2-3, the LDS-segment kernel elsewhere.
+// Which K1 variant serves depth L (in-process A/B, profiles/r01_ab_v7.json,
+// r01_ab_strip_caps.json): the wave-strip kernel at depths 2-3, and at 5-6 when
+// capped at 2 waves/SIMD (+0.4-1.1 % over the LDS-segment kernel); the
+// LDS-segment kernel at depths 1, 4, 7, 8.
 constexpr bool use_strip_kernel(int L)
 {
-    return WICCA_STRIP >= 0 ? WICCA_STRIP == 1 : (L == 2 || L == 3);
+    return WICCA_STRIP >= 0 ? WICCA_STRIP == 1 : (L == 2 || L == 3 || L == 5 || L == 6);
 }
 
 // Pixels a strip-kernel lane owns: whole pixels in 12 or 16 contiguous bytes,
@@ -78,12 +83,16 @@ constexpr bool use_strip_kernel(int L)
 constexpr int strip_lane_pixels(int C) { return C == 3 ? 4 : 16 / C; }
 
 // Occupancy caps, enforced through the workgroup's LDS footprint (a CU holds
-// 160 KiB).  At D = 3 the cap of 4 waves/SIMD also lifts the compiler's VGPR
-// target (107 instead of 63 VGPRs, more rows in flight per wave): +3.2-3.5 %;
-// caps measured slower at D = 1, 2 and 4-6 (profiles/r01_ab_occupancy_caps.json).
+// 160 KiB).  A cap also lifts the compiler's VGPR target (more rows in flight
+// per wave): K1s at D = 3 capped at 4 waves/SIMD +3.2-3.5 %, K1s at D = 5-6
+// capped at 2; caps measured slower for K1 at D = 1 and 4-6 and K1s at D = 2
+// (profiles/r01_ab_occupancy_caps.json, r01_ab_strip_caps.json).
 constexpr int kLdsPerCU = 160 * 1024;
 constexpr int lds_for_cap(int cap) { return cap > 0 ? kLdsPerCU / (cap + 1) + 16 : 0; }
-constexpr int strip_min_lds(int L) { return L == 3 ? lds_for_cap(WICCA_STRIP_WG_CAP3) : 0; }
+constexpr int strip_min_lds(int L)
+{
+    return L == 3 ? lds_for_cap(WICCA_STRIP_WG_CAP3) : L >= 4 ? lds_for_cap(WICCA_STRIP_WG_CAP_HI) : 0;
+}
 constexpr int k1_min_lds(int L) { return L == 1 ? lds_for_cap(WICCA_K1_WG_CAP1) : 0; }
 
 constexpr int strip_chunk_rows(int L)
