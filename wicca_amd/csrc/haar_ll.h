@@ -89,9 +89,12 @@ constexpr int strip_lane_pixels(int C) { return C == 3 ? 4 : 16 / C; }
 // (profiles/r01_ab_occupancy_caps.json, r01_ab_strip_caps.json).
 constexpr int kLdsPerCU = 160 * 1024;
 constexpr int lds_for_cap(int cap) { return cap > 0 ? kLdsPerCU / (cap + 1) + 16 : 0; }
-constexpr int strip_min_lds(int L)
+constexpr int strip_min_lds(int L, bool ragged)
 {
-    return L == 3 ? lds_for_cap(WICCA_STRIP_WG_CAP3) : L >= 4 ? lds_for_cap(WICCA_STRIP_WG_CAP_HI) : 0;
+    // a ragged batch at D = 3 (smaller images, descriptor search per block)
+    // runs faster uncapped
+    return L == 3 ? (ragged ? 0 : lds_for_cap(WICCA_STRIP_WG_CAP3))
+                  : L >= 4 ? lds_for_cap(WICCA_STRIP_WG_CAP_HI) : 0;
 }
 constexpr int k1_min_lds(int L) { return L == 1 ? lds_for_cap(WICCA_K1_WG_CAP1) : 0; }
 

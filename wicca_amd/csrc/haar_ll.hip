@@ -335,7 +335,7 @@ __global__ __launch_bounds__(64 * kStripWaves) void haar_strip_kernel(LLParams p
     constexpr int U = R < strip_chunk_rows(L) ? R : strip_chunk_rows(L);
     constexpr int ICONS = STRIP / G;                 // icons per wave strip
     constexpr int STAGE = (ICONS * C * (int)sizeof(OutT) + 15) & ~15;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[std::max(kStripWaves * STAGE, strip_min_lds(L))];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[std::max(kStripWaves * STAGE, strip_min_lds(L, RAGGED))];
 
     // ---- work: block -> (image, icon row, group of kStripWaves strips); wave -> strip
     const int lane = threadIdx.x & 63;
