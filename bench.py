@@ -59,13 +59,45 @@ def parse():
                     help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print each rank's (rank, world) and exit before touching the GPU")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01b.json"),
                     help="PMC summary (rocprofv3 FETCH_SIZE/WRITE_SIZE) for roofline.traffic")
     return ap.parse_args()
 
 
+def _cpu_share():
+    """CPUs this process may run on (affinity), the cgroup CPU quota (cpus, or
+    None) and the memory the host reports available (bytes)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    avail = None
+    try:
+        with open("/proc/meminfo") as f:
+            for ln in f:
+                if ln.startswith("MemAvailable:"):
+                    avail = int(ln.split()[1]) * 1024
+    except (OSError, ValueError):
+        pass
+    return aff, quota, avail
+
+
 def cpu_baseline(args, budget_s: float):
-    """NumPy port of the reference on this host (oracle/haar_numpy.py)."""
+    """NumPy port of the reference on this host (oracle/haar_numpy.py).
+
+    BASELINE.md §3(b): image-parallel ``ThreadPoolExecutor`` over every CPU
+    this process may run on (``os.sched_getaffinity``), bounded only by host
+    memory (the port widens an 8K RGB image to a 398 MB float32 plane, ~0.8 GB
+    of working set per thread); the single-thread rate (one
+    ClassifierProcessor worker) and a 16-thread pool are reported beside it.
+    """
     from concurrent.futures import ThreadPoolExecutor
 
     from oracle import haar_numpy
@@ -73,28 +105,39 @@ def cpu_baseline(args, budget_s: float):
 
     H, W, C, d = args.height, args.width, args.channels, args.depth
     mp = H * W / 1e6
+    per_thread_bytes = 8 * H * W * C  # u8 image + f32 plane + level-1 sums, with slack
     pool_imgs = [synth_image(1234, i, H, W, C) for i in range(4)]
+
+    def one(i):
+        haar_numpy.get_small_copy(pool_imgs[i % 4], d, args.border)
+
     # single thread, as ClassifierProcessor runs it in one worker
     t0 = time.perf_counter()
     n1 = 0
     while True:
-        haar_numpy.get_small_copy(pool_imgs[n1 % 4], d, args.border)
+        one(n1)
         n1 += 1
-        if time.perf_counter() - t0 > budget_s / 3 or n1 >= 64:
+        if time.perf_counter() - t0 > budget_s / 4 or n1 >= 64:
             break
     single = n1 * mp / (time.perf_counter() - t0)
-    # image-parallel thread pool on this process's CPU share
-    threads = max(1, min(16, os.cpu_count() or 1))
-    n_par = max(threads, int(single * budget_s * 0.66 * min(threads, 8) / mp / 4) // threads
-                * threads)
-    n_par = min(n_par, 4 * threads)
-    with ThreadPoolExecutor(threads) as ex:
-        list(ex.map(lambda i: haar_numpy.get_small_copy(pool_imgs[i % 4], d, args.border),
-                    range(threads)))  # warm
-        t0 = time.perf_counter()
-        list(ex.map(lambda i: haar_numpy.get_small_copy(pool_imgs[i % 4], d, args.border),
-                    range(n_par)))
-        par = n_par * mp / (time.perf_counter() - t0)
+
+    def pool_rate(threads: int, n: int) -> float:
+        with ThreadPoolExecutor(threads) as ex:
+            list(ex.map(one, range(min(threads, 8))))  # warm the pool
+            t = time.perf_counter()
+            list(ex.map(one, range(n)))
+            return n * mp / (time.perf_counter() - t)
+
+    aff, quota, avail = _cpu_share()
+    mem_cap = max(1, int(0.5 * avail / per_thread_bytes)) if avail else 64
+    threads = max(1, min(aff, mem_cap))
+    # enough images for ~budget/2 of wall time at the expected parallel rate
+    eff = min(threads, quota or threads)
+    n_all = max(threads, int(single * eff * budget_s / 2 / mp) // threads * threads)
+    n_all = min(n_all, 4 * threads)
+    par = pool_rate(threads, n_all)
+    t16 = min(16, aff)
+    par16 = pool_rate(t16, 2 * t16) if t16 != threads else par
     model = ""
     try:
         with open("/proc/cpuinfo") as f:
@@ -103,9 +146,12 @@ def cpu_baseline(args, budget_s: float):
         pass
     return {
         "value": round(par, 2), "unit": "MP/s", "cores": threads, "kind": "port",
-        "sample": f"{n_par} synthetic {W}x{H}x{C} images (seed 1234) at depth {d}, "
-                  f"ThreadPoolExecutor({threads}); single-thread {n1} images",
+        "sample": f"{n_all} synthetic {W}x{H}x{C} images (seed 1234) at depth {d}, "
+                  f"ThreadPoolExecutor({threads}) over the process's CPU affinity; "
+                  f"single-thread {n1} images; 16 threads {2 * t16} images",
         "single_thread_value": round(single, 2),
+        "threads16_value": round(par16, 2),
+        "affinity_cpus": aff, "cgroup_cpu_quota": quota, "memory_thread_cap": mem_cap,
         "host_cpus": os.cpu_count(), "cpu_model": model,
     }
 
@@ -377,11 +423,37 @@ def run_multi(args, torch, rank):
     }
 
 
+def spawn_ranks(n: int) -> int:
+    """``bench.py --gpus N`` without a launcher: start N ranks (one per GPU)
+    through ``torch.distributed.run`` as a CHILD process and return its exit
+    code.  This parent never touches the GPU (no torch import, no HIP call)
+    and never execs, so the children initialise the devices themselves."""
+    import socket
+    import subprocess
+    with socket.socket() as s:  # a free rendezvous port on the loopback
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch "
+                         "one rank per GPU (or pass --gpus N alone and bench.py starts them)")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:  # launcher check only (tests/test_bench_launch.py): no GPU, no torch
+        print(json.dumps({"rank": rank, "local_rank": local_rank, "world": world}), flush=True)
+        return
 
     import torch
     # one rank per GPU; the modulo only matters for a rehearsal with more ranks
@@ -396,6 +468,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group(backend)
+        world = dist.get_world_size()
 
     from wicca_amd import _lib
     lib = _lib.load()

@@ -213,6 +213,27 @@ def main() -> None:
         run(f"cfg3_8k_d{d}", img, d, store_input=False, synth={"seed": 0, "index": 1},
             store_f32=False)
 
+    # 9. batch / depth-list groups whose members differ in alignment: the
+    #    reference pads each image (and each depth) on its own, so a CONSTANT
+    #    border must reach every unaligned member even when the first member
+    #    needs no padding.  "group" names the batch / depth list a case belongs
+    #    to; its members are listed in order.
+    for k, d in ((77, 3), (0, 3), (200, 5)):
+        members = [(64, 64, 3), (61, 59, 3), (32, 40, 3), (45, 130, 3), (64, 63, 3)]
+        if d == 5:
+            members = [(64, 96, 3), (70, 33, 3), (128, 32, 3), (97, 100, 3)]
+        for j, sh in enumerate(members):
+            img = rng.integers(0, 256, sh, dtype=np.uint8)
+            run(f"group_batch_const{k}_d{d}_m{j}", img, d, border=0, k=k)
+            cases[-1]["group"] = f"batch_const{k}_d{d}"
+    for sh, k, depths in (((62, 62, 3), 77, (1, 3)), ((48, 40, 3), 5, (2, 3, 4, 5)),
+                          ((64, 72, 4), 250, (3, 4, 6)), ((62, 62, 3), 77, (3, 1))):
+        img = rng.integers(0, 256, sh, dtype=np.uint8)
+        tag = "x".join(map(str, sh)) + "_" + "".join(map(str, depths))
+        for d in depths:
+            run(f"group_multi_{tag}_const{k}_d{d}", img, d, border=0, k=k)
+            cases[-1]["group"] = f"multi_{tag}_const{k}"
+
     with open(os.path.join(HERE, "cases.json"), "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py",
                    "reference": "Todmount/wicca @ 2025-09-19 (wicca/wavelet_coder.py:50-67)",

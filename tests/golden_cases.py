@@ -73,3 +73,14 @@ def f32_of(case):
 
 def sha(a) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def groups(prefix: str):
+    """{group name: [cases in order]} for batch ("batch_") or depth-list
+    ("multi_") groups (make_golden.py section 9)."""
+    out: dict = {}
+    for c in cases("ok"):
+        g = c.get("group")
+        if g and g.startswith(prefix):
+            out.setdefault(g, []).append(c)
+    return out

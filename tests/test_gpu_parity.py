@@ -404,3 +404,54 @@ def test_batch_ragged_device_descriptors(coder):
             for im, (o, oh, ow) in zip(imgs, outs):
                 got = o.cpu().numpy()[:, :ow * C].reshape(oh, ow, C)
                 assert np.array_equal(got, c_oracle.ll_int_block(im, d, border, k)[0]), (C, d, im.shape)
+
+
+BATCH_GROUPS = G.groups("batch_")
+MULTI_GROUPS = G.groups("multi_")
+
+
+@pytest.mark.parametrize("group", sorted(BATCH_GROUPS))
+def test_group_batch_goldens(coder, group):
+    """A CONSTANT batch whose first member needs no padding and later members
+    do (reference: each image padded with the constant on its own,
+    data_loader.py:107-117) — one ragged launch, one host thread per
+    listed device, and the per-image call all match the reference."""
+    members = BATCH_GROUPS[group]
+    imgs = [G.input_of(c) for c in members]
+    d, k = members[0]["depth"], members[0]["border_constant"]
+    assert all(c["border_type"] == 0 for c in members)
+    for devices in (None, [0, 0]):
+        outs = coder.get_small_copies(imgs, d, 0, k, devices=devices)
+        for c, o in zip(members, outs):
+            assert G.sha(o) == c["out_sha256"], (group, c["name"], devices)
+    for im, c in zip(imgs, members):
+        assert G.sha(coder.get_small_copy(im, d, 0, k)) == c["out_sha256"]
+        assert np.array_equal(coder.get_small_copy(im, d, 0, k), c_oracle.ll_int_block(im, d, 0, k)[0])
+
+
+@pytest.mark.parametrize("group", sorted(MULTI_GROUPS))
+def test_group_multi_depth_goldens(coder, group):
+    """get_small_copy_multi with CONSTANT k where the smallest depth is
+    aligned and a larger one is not (e.g. 62x62 at depths [1, 3], k = 77)."""
+    members = MULTI_GROUPS[group]
+    img = G.input_of(members[0])
+    k = members[0]["border_constant"]
+    res = coder.get_small_copy_multi(img, [c["depth"] for c in members], 0, k)
+    for c in members:
+        assert G.sha(res[c["depth"]]) == c["out_sha256"], (group, c["depth"])
+
+
+def test_batch_constant_first_aligned_vs_oracle(coder):
+    """CONSTANT k=77 on [64x64x3, 61x59x3] at depth 3, first image
+    aligned — icons equal the per-image oracle (not REPLICATE-padded)."""
+    rng = np.random.default_rng(77)
+    imgs = [rng.integers(0, 256, (64, 64, 3), dtype=np.uint8),
+            rng.integers(0, 256, (61, 59, 3), dtype=np.uint8)]
+    for devices in (None, [0, 0]):
+        outs = coder.get_small_copies(imgs, 3, 0, 77, devices=devices)
+        for im, o in zip(imgs, outs):
+            assert np.array_equal(o, c_oracle.ll_int_block(im, 3, 0, 77)[0]), devices
+    img = rng.integers(0, 256, (62, 62, 3), dtype=np.uint8)
+    res = coder.get_small_copy_multi(img, [1, 3], 0, 77)
+    for d in (1, 3):
+        assert np.array_equal(res[d], c_oracle.ll_int_block(img, d, 0, 77)[0]), d

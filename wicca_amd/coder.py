@@ -187,10 +187,10 @@ class HaarCoder(WaveletCoder):
                 keep.append(img)
                 descs[j] = _lib.ImageDesc(img.ctypes.data, out.ctypes.data, H, W,
                                           img.strides[0], ow * C)
-            # host-padded images (exotic borders) already carry their padding
-            border = prepared[idx[0]][2]
-            k = prepared[idx[0]][3]
-            depth = prepared[idx[0]][1]
+            # _prepare gives every member the caller's border and constant
+            # (host-padded exotic borders come back as REPLICATE, needing none)
+            _, depth, border, k = prepared[idx[0]]
+            assert all(prepared[i][2:] == (border, k) for i in idx)
             if devices is not None and len(devices) > 1:
                 devs = (ctypes.c_int * len(devices))(*devices)
                 _lib.check(self._lib.wicca_haar_ll_u8_batch_multi_gpu(
@@ -219,7 +219,9 @@ class HaarCoder(WaveletCoder):
             if d <= 0:
                 result[d] = self._copy(img, image.ndim)
         if dev_depths:
-            img, _, border, k = prepared[[p[1] for p in prepared].index(dev_depths[0])]
+            # one image, the caller's border and constant for every depth (the
+            # C side pads each depth on its own)
+            img, _, border, k = prepared[0]
             H, W, C = img.shape
             outs = []
             for d in dev_depths:
@@ -265,11 +267,17 @@ class HaarCoder(WaveletCoder):
             raise IndexError(MSG_2D_INDEX)
         k = _border_value(border_constant) if border == BORDER_CONSTANT else 0
         img = _as_hwc(image)
-        if padded and border in _HOST_PAD_MODES:
-            img = np.pad(img, [(0, add_r), (0, add_c), (0, 0)], mode=_HOST_PAD_MODES[border])
-            border = BORDER_REPLICATE  # padding already materialised
-        elif not padded:
-            border, k = BORDER_REPLICATE, 0  # no padding: the border is irrelevant
+        # The caller's CONSTANT / REPLICATE border and constant are carried
+        # through whether or not THIS image needs padding (the kernels add
+        # nothing when it does not), so every member of a batch or depth list
+        # launches with the same border as the reference's per-image call.
+        # Other border types are materialised on the host; the launch then sees
+        # an image that needs no padding, under REPLICATE.
+        if border not in (BORDER_CONSTANT, BORDER_REPLICATE):
+            if padded:
+                img = np.pad(img, [(0, add_r), (0, add_c), (0, 0)],
+                             mode=_HOST_PAD_MODES[border])
+            border, k = BORDER_REPLICATE, 0
         return img, depth, border, k
 
     def _copy(self, img: np.ndarray, ndim: int) -> np.ndarray:
