@@ -74,6 +74,32 @@ const char* wicca_last_error(void);
 /* Library version string, e.g. "wicca_hip 0.1 gfx950". */
 const char* wicca_version(void);
 
+/* Name of the kernel a depth-`depth`, C-channel aligned batch dispatches
+ * (uniform, or ragged when `ragged` != 0) as rocprofv3 prints it without the
+ * namespace and argument list, e.g. "haar_strip_kernel<5, 3, unsigned char,
+ * false>": what bench.py reports as the roofline kernel, cross-checked
+ * against the profiler's trace. */
+const char* wicca_kernel_name(int depth, int64_t C, int ragged);
+
+/* Split n items with the given weights into n_ranges contiguous, non-empty
+ * ranges of near-equal total weight (1 <= n_ranges <= n): range r is
+ * [first[r], first[r+1]), first has n_ranges + 1 entries.  The split the
+ * multi-GPU batch entry uses (pixel counts as weights). */
+int wicca_balance_ranges(const int64_t* weights, int64_t n, int n_ranges, int64_t* first);
+
+/* Device memory held by idle pooled workspaces of `device` (-1: all devices).
+ * The pool keeps at most WICCA_WORKSPACE_CAP_MB (default 4096) idle per
+ * device; a workspace returned above the cap frees its buffers first. */
+int64_t wicca_workspace_bytes(int device);
+
+/* Set the idle-pool cap in bytes (bytes < 0: leave it); returns the previous
+ * cap.  Overrides WICCA_WORKSPACE_CAP_MB. */
+int64_t wicca_set_workspace_cap(int64_t bytes);
+
+/* Free every idle pooled workspace (streams, events, buffers) of `device`
+ * (-1: all devices).  Workspaces leased by running calls are unaffected. */
+int wicca_release_workspaces(int device);
+
 /* Output shape of get_small_copy for an (H, W) image at `depth`
  * (wicca/wavelet_coder.py:58 ratio = 2**depth; data_loader.py:107-110). */
 int wicca_icon_shape(int64_t H, int64_t W, int depth, int64_t* out_h, int64_t* out_w);

@@ -1,0 +1,87 @@
+"""Host-only helpers of the C ABI (no GPU needed): the multi-GPU range split,
+the kernel-name report bench.py uses for its roofline line, and the
+workspace-pool controls."""
+import ctypes
+
+import numpy as np
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from wicca_amd import _lib
+
+
+def _split(weights, nr):
+    lib = _lib.load()
+    n = len(weights)
+    w = (ctypes.c_int64 * max(n, 1))(*weights)
+    first = (ctypes.c_int64 * (nr + 1))()
+    rc = lib.wicca_balance_ranges(w, n, nr, first)
+    return rc, list(first)
+
+
+def test_split_small_then_large_uses_both_devices():
+    # [small, large] on 2 devices used to run everything on device 0
+    rc, first = _split([10, 10_000], 2)
+    assert rc == 0 and first == [0, 1, 2]
+
+
+def test_split_equal_weights():
+    assert _split([5] * 8, 4) == (0, [0, 2, 4, 6, 8])
+    assert _split([1, 1, 1], 3) == (0, [0, 1, 2, 3])
+
+
+def test_split_large_first():
+    rc, first = _split([100, 1, 1, 1], 2)
+    assert rc == 0 and first == [0, 1, 4]
+
+
+def test_split_rejects_bad_arguments():
+    lib = _lib.load()
+    first = (ctypes.c_int64 * 4)()
+    w = (ctypes.c_int64 * 2)(1, 2)
+    assert lib.wicca_balance_ranges(w, 2, 3, first) == _lib.WICCA_ERR_ARG
+    assert lib.wicca_balance_ranges(w, 2, 0, first) == _lib.WICCA_ERR_ARG
+    assert lib.wicca_balance_ranges(None, 2, 1, first) == _lib.WICCA_ERR_ARG
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.integers(0, 10_000_000), min_size=1, max_size=60), st.integers(1, 8))
+def test_split_properties(weights, nr):
+    nr = min(nr, len(weights))
+    rc, first = _split(weights, nr)
+    assert rc == 0
+    assert first[0] == 0 and first[-1] == len(weights)
+    assert all(a < b for a, b in zip(first, first[1:])), first  # contiguous, non-empty
+    # no range is heavier than its fair share plus its largest item
+    total = sum(weights)
+    for a, b in zip(first, first[1:]):
+        part = sum(weights[a:b])
+        assert part <= total / nr + max(weights[a:b]) + 1
+
+
+@pytest.mark.parametrize("depth", range(1, 9))
+def test_kernel_name_matches_dispatch_table(depth):
+    lib = _lib.load()
+    name = lib.wicca_kernel_name(depth, 3, 0).decode()
+    strip = depth in (2, 3, 5, 6)  # use_strip_kernel (haar_ll.h)
+    assert name == ("haar_strip_kernel" if strip else "haar_block_sum_kernel") + \
+        f"<{depth}, 3, unsigned char, false>"
+    assert lib.wicca_kernel_name(depth, 1, 1).decode().endswith(f"<{depth}, 1, unsigned char, true>")
+
+
+def test_kernel_name_other_paths():
+    lib = _lib.load()
+    assert "haar_level_f32_kernel" in lib.wicca_kernel_name(9, 3, 0).decode()
+    assert lib.wicca_kernel_name(3, 5, 0).decode().startswith("haar_block_sum_generic_kernel")
+    assert lib.wicca_kernel_name(0, 3, 0).decode() == "hipMemcpy2DAsync"
+
+
+def test_workspace_controls_without_device():
+    lib = _lib.load()
+    assert lib.wicca_workspace_bytes(-1) >= 0
+    prev = lib.wicca_set_workspace_cap(123 << 20)
+    assert prev >= 0
+    assert lib.wicca_set_workspace_cap(-1) == 123 << 20  # query leaves it
+    lib.wicca_set_workspace_cap(prev)
+    assert lib.wicca_release_workspaces(-1) == 0

@@ -33,6 +33,10 @@ def main():
     ap.add_argument("--channels", type=int, default=3)
     ap.add_argument("--border", type=int, default=1)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--ragged", type=float, default=0.0,
+                    help="> 0: a ragged batch, H, W drawn from [ragged * size, size], one "
+                         "wicca_haar_ll_u8_batch call with device descriptors")
+    ap.add_argument("--ragged-align", type=int, default=16, help="row pitch alignment (bytes)")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the identical-icons check (ablation builds compute garbage)")
     args = ap.parse_args()
@@ -49,14 +53,28 @@ def main():
         libs[os.path.basename(path)] = h
 
     B, H, W, C = args.images, args.height, args.width, args.channels
-    pitch = (W * C + 15) // 16 * 16
-    src = torch.empty(B * H * pitch, dtype=torch.uint8, device="cuda")
+    import numpy as np
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     sh = ctypes.c_void_p(stream.cuda_stream)
     first = next(iter(libs.values()))
-    assert first.wicca_synth_u8(ctypes.c_void_p(src.data_ptr()), B, H, W, C, pitch, H * pitch,
-                                0, -1, sh) == 0
+    if args.ragged > 0:
+        rng = np.random.default_rng(0)
+        Hs = [int(x) for x in rng.integers(int(H * args.ragged), H + 1, B)]
+        Ws = [int(x) for x in rng.integers(int(W * args.ragged), W + 1, B)]
+        al = args.ragged_align
+        pitches = [(w * C + al - 1) // al * al for w in Ws]
+    else:
+        Hs, Ws = [H] * B, [W] * B
+        pitches = [(W * C + 15) // 16 * 16] * B
+    offs = np.concatenate([[0], np.cumsum([p * h for p, h in zip(pitches, Hs)])]).astype(np.int64)
+    src = torch.empty(int(offs[-1]), dtype=torch.uint8, device="cuda")
+    for i in range(B):
+        if args.ragged > 0 or i == 0:
+            n_i = 1 if args.ragged > 0 else B
+            assert first.wicca_synth_u8(ctypes.c_void_p(src.data_ptr() + int(offs[i])), n_i, Hs[i],
+                                        Ws[i], C, pitches[i], Hs[i] * pitches[i], i, -1, sh) == 0
+    pitch = pitches[0]
     results = []
     for D in args.depths:
         r = 1 << D
@@ -64,12 +82,20 @@ def main():
         align = int(os.environ.get("WICCA_AB_OPITCH_ALIGN", "16"))  # icon row pitch alignment
         opitch = (ow * C + align - 1) // align * align
         dst = torch.empty(B * oh * opitch, dtype=torch.uint8, device="cuda")
-        alg = B * (H * W * C + oh * ow * C)
+        alg = sum(h * w * C + (-(-h // r)) * (-(-w // r)) * C for h, w in zip(Hs, Ws))
+        descs = (L.ImageDesc * B)()
+        for i in range(B):
+            descs[i] = L.ImageDesc(src.data_ptr() + int(offs[i]), dst.data_ptr() + i * oh * opitch,
+                                   Hs[i], Ws[i], pitches[i], opitch)
         ref = None
         samples = {k: [] for k in libs}
         for rnd in range(args.rounds):
             for name, h in libs.items():
                 def step():
+                    if args.ragged > 0:
+                        rc = h.wicca_haar_ll_u8_batch(descs, B, C, D, args.border, 0, 1, 1, -1, sh)
+                        assert rc == 0, rc
+                        return
                     rc = h.wicca_haar_ll_u8_uniform(
                         ctypes.c_void_p(src.data_ptr()), B, H, W, C, pitch, H * pitch, D,
                         args.border, 0, ctypes.c_void_p(dst.data_ptr()), opitch, oh * opitch,

@@ -41,6 +41,11 @@ SIGNATURES = {
     "wicca_device_count": (_int, []),
     "wicca_last_error": (ctypes.c_char_p, []),
     "wicca_version": (ctypes.c_char_p, []),
+    "wicca_kernel_name": (ctypes.c_char_p, [_int, _i64, _int]),
+    "wicca_balance_ranges": (_int, [ctypes.POINTER(_i64), _i64, _int, ctypes.POINTER(_i64)]),
+    "wicca_workspace_bytes": (_i64, [_int]),
+    "wicca_release_workspaces": (_int, [_int]),
+    "wicca_set_workspace_cap": (_i64, [_i64]),
     "wicca_icon_shape": (_int, [_i64, _i64, _int, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     "wicca_haar_ll_u8": (_int, [_p, _i64, _i64, _i64, _i64, _int, _int, _int, _p, _i64,
                                 _int, _int, _int, _p]),

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -69,32 +70,111 @@ struct DevBuf {
     hipError_t reserve(size_t n)
     {
         if (n <= cap) return hipSuccess;
-        if (ptr) (void)hipFree(ptr);
-        ptr = nullptr;
-        cap = 0;
+        release();
         size_t want = std::max<size_t>(n, 1 << 20);
         hipError_t e = hipMalloc(&ptr, want);
         if (e == hipSuccess) cap = want;
+        else ptr = nullptr;
         return e;
+    }
+    void release()
+    {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
     }
 };
 
 // One call's worth of resources; pooled per device, never shared concurrently.
+//   in / out      staging of host images and icons
+//   t0..t2        scratch planes (depth > 8 tail, generic multi-depth pyramid)
+//   meta[2]       ragged-batch descriptors, two slots used alternately: a slot
+//                 is rewritten only after the launch that read it has finished
+//                 (meta_done[slot]), so a ragged call on a caller's stream does
+//                 not have to wait for its own kernel; meta_host[slot] keeps the
+//                 bytes the slot holds, and an identical descriptor set (the same
+//                 batch again: the reference runs every batch once per
+//                 classifier and depth, classifying_tools.py:339-352, 546-551)
+//                 skips the upload.
 struct Workspace {
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf in, out, t0, t1, t2, meta;
+    DevBuf in, out, t0, t1, t2;
+    DevBuf meta[2];
+    hipEvent_t meta_done[2] = {nullptr, nullptr};
+    std::vector<uint8_t> meta_host[2];
+    int meta_slot = 0;
+    size_t bytes() const
+    {
+        return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap;
+    }
+    void release_buffers()
+    {
+        for (int i = 0; i < 2; ++i) {
+            if (meta_done[i]) (void)hipEventSynchronize(meta_done[i]);
+            meta[i].release();
+            meta_host[i].clear();
+        }
+        in.release();
+        out.release();
+        t0.release();
+        t1.release();
+        t2.release();
+    }
+    void destroy()
+    {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != device) (void)hipSetDevice(device);
+        release_buffers();
+        for (int i = 0; i < 2; ++i)
+            if (meta_done[i]) (void)hipEventDestroy(meta_done[i]);
+        if (stream) (void)hipStreamDestroy(stream);
+        if (cur >= 0 && cur != device) (void)hipSetDevice(cur);
+    }
 };
 
 std::mutex g_pool_mu;
 std::vector<std::unique_ptr<Workspace>> g_pool;  // idle workspaces
+
+// Idle device memory the pool may keep per device (WICCA_WORKSPACE_CAP_MB,
+// default 4096 MiB): a workspace returned while its device's idle pool already
+// holds that much gives its buffers back first.  Thirty-two threads on 8K
+// inputs otherwise pin ~3 GB per device for the life of the process.
+std::atomic<int64_t> g_pool_cap{-1};  // bytes; -1 = not read from the environment yet
+
+size_t pool_cap_bytes()
+{
+    int64_t cap = g_pool_cap.load();
+    if (cap < 0) {
+        const char* e = getenv("WICCA_WORKSPACE_CAP_MB");
+        const long long mb = e ? atoll(e) : 4096;
+        int64_t want = (int64_t)std::max<long long>(mb, 0) << 20;
+        g_pool_cap.compare_exchange_strong(cap, want);
+        cap = g_pool_cap.load();
+    }
+    return (size_t)cap;
+}
+
+size_t idle_bytes_locked(int device)
+{
+    size_t b = 0;
+    for (auto& w : g_pool)
+        if (device < 0 || w->device == device) b += w->bytes();
+    return b;
+}
 
 struct WorkspaceLease {
     Workspace* ws = nullptr;
     ~WorkspaceLease()
     {
         if (!ws) return;
-        std::lock_guard<std::mutex> g(g_pool_mu);
+        std::unique_lock<std::mutex> g(g_pool_mu);
+        if (idle_bytes_locked(ws->device) + ws->bytes() > pool_cap_bytes()) {
+            g.unlock();
+            ws->release_buffers();  // its stream and events stay pooled
+            g.lock();
+        }
         g_pool.emplace_back(ws);
     }
 };
@@ -115,9 +195,12 @@ int acquire(int device, WorkspaceLease& lease)
     ws->device = device;
     // blocking stream: ordered after work on the legacy default stream (torch's null stream)
     hipError_t e = hipStreamCreateWithFlags(&ws->stream, hipStreamDefault);
+    for (int i = 0; i < 2 && e == hipSuccess; ++i)
+        e = hipEventCreateWithFlags(&ws->meta_done[i], hipEventDisableTiming);
     if (e != hipSuccess) {
+        ws->destroy();
         delete ws;
-        return fail(WICCA_ERR_HIP, "hipStreamCreate failed: %s", hipGetErrorString(e));
+        return fail(WICCA_ERR_HIP, "workspace creation failed: %s", hipGetErrorString(e));
     }
     lease.ws = ws;
     return WICCA_OK;
@@ -449,6 +532,27 @@ int single_image(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t sr
     return WICCA_OK;
 }
 
+// Split n weighted items into nr contiguous ranges (nr <= n, every range
+// non-empty) whose weights approach total/nr: range r closes after item i once
+// it holds its cumulative share, or when exactly one item per remaining range
+// is left.  first[r] .. first[r+1] is range r; first[nr] = n.
+void balance_ranges(const int64_t* w, int64_t n, int nr, int64_t* first)
+{
+    int64_t total = 0;
+    for (int64_t i = 0; i < n; ++i) total += std::max<int64_t>(w[i], 0);
+    first[0] = 0;
+    int r = 0;
+    int64_t acc = 0;
+    for (int64_t i = 0; i < n && r < nr - 1; ++i) {
+        acc += std::max<int64_t>(w[i], 0);
+        const int64_t left = n - (i + 1);   // items after i
+        const int later = nr - 1 - r;       // ranges after r
+        const bool share = (double)acc * nr >= (double)total * (r + 1);
+        if ((share && left >= later) || left == later) first[++r] = i + 1;
+    }
+    for (int k = r + 1; k <= nr; ++k) first[k] = n;
+}
+
 }  // namespace
 
 extern "C" {
@@ -461,7 +565,58 @@ int wicca_device_count(void)
 
 const char* wicca_last_error(void) { return t_last_error.c_str(); }
 
-const char* wicca_version(void) { return "wicca_hip 0.1 gfx950"; }
+const char* wicca_version(void) { return "wicca_hip 0.2 gfx950"; }
+
+const char* wicca_kernel_name(int depth, int64_t C, int ragged)
+{
+    if (depth > 8 && C >= 1 && C <= 4) return "haar_block_sum_kernel<8, C, unsigned int, false> + haar_level_f32_kernel";
+    if (depth < 1) return "hipMemcpy2DAsync";
+    const char* n = wicca::block_sum_kernel_name(depth, (int)C, ragged != 0);
+    return n[0] ? n : "haar_block_sum_generic_kernel<unsigned char>";
+}
+
+int wicca_balance_ranges(const int64_t* weights, int64_t n, int n_ranges, int64_t* first)
+{
+    if (n < 0 || n_ranges < 1 || n_ranges > std::max<int64_t>(n, 1) || (n > 0 && !weights) || !first)
+        return fail(WICCA_ERR_ARG, "balance_ranges: need 1 <= n_ranges <= n and valid arrays");
+    if (n == 0) {
+        first[0] = first[1] = 0;
+        return WICCA_OK;
+    }
+    balance_ranges(weights, n, n_ranges, first);
+    return WICCA_OK;
+}
+
+int64_t wicca_workspace_bytes(int device)
+{
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    return (int64_t)idle_bytes_locked(device);
+}
+
+int64_t wicca_set_workspace_cap(int64_t bytes)
+{
+    const int64_t prev = (int64_t)pool_cap_bytes();
+    if (bytes >= 0) g_pool_cap.store(bytes);
+    return prev;
+}
+
+int wicca_release_workspaces(int device)
+{
+    std::vector<std::unique_ptr<Workspace>> drop;
+    {
+        std::lock_guard<std::mutex> g(g_pool_mu);
+        for (size_t i = 0; i < g_pool.size();) {
+            if (device < 0 || g_pool[i]->device == device) {
+                drop.push_back(std::move(g_pool[i]));
+                g_pool.erase(g_pool.begin() + i);
+            } else {
+                ++i;
+            }
+        }
+    }
+    for (auto& w : drop) w->destroy();
+    return WICCA_OK;
+}
 
 int wicca_icon_shape(int64_t H, int64_t W, int depth, int64_t* out_h, int64_t* out_w)
 {
@@ -616,13 +771,32 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
         }
         if (total >= ((int64_t)1 << 32))
             return fail(WICCA_ERR_ARG, "batch too large for one launch");
+        // descriptors + block prefix, packed; uploaded into the workspace's
+        // next meta slot unless that slot already holds these exact bytes
         const size_t bytes_d = sizeof(wicca::ImageDescDev) * (size_t)n;
         const size_t off_s = (size_t)round_up((int64_t)bytes_d, 16);
-        HIP_TRY(ws->meta.reserve(off_s + sizeof(int64_t) * (size_t)n));
-        uint8_t* meta = (uint8_t*)ws->meta.ptr;
-        HIP_TRY(hipMemcpyAsync(meta, dd.data(), bytes_d, hipMemcpyHostToDevice, stream));
-        HIP_TRY(hipMemcpyAsync(meta + off_s, starts.data(), sizeof(int64_t) * (size_t)n,
-                               hipMemcpyHostToDevice, stream));
+        const size_t meta_bytes = off_s + sizeof(int64_t) * (size_t)n;
+        std::vector<uint8_t> packed(meta_bytes, 0);
+        memcpy(packed.data(), dd.data(), bytes_d);
+        memcpy(packed.data() + off_s, starts.data(), sizeof(int64_t) * (size_t)n);
+        int slot = -1;
+        for (int k = 0; k < 2 && slot < 0; ++k)
+            if (ws->meta_host[k] == packed) slot = k;  // same batch again: no upload
+        if (slot < 0) {
+            slot = ws->meta_slot;
+            ws->meta_slot ^= 1;
+            // the launch that last read this slot must be done before it is rewritten
+            HIP_TRY(hipEventSynchronize(ws->meta_done[slot]));
+            ws->meta_host[slot].clear();
+            HIP_TRY(ws->meta[slot].reserve(meta_bytes));
+            HIP_TRY(hipMemcpyAsync(ws->meta[slot].ptr, packed.data(), meta_bytes,
+                                   hipMemcpyHostToDevice, stream));
+            ws->meta_host[slot] = std::move(packed);
+        } else {
+            // uploaded by an earlier call, possibly on another stream
+            HIP_TRY(hipStreamWaitEvent(stream, ws->meta_done[slot], 0));
+        }
+        uint8_t* meta = (uint8_t*)ws->meta[slot].ptr;
         wicca::LLParams p{};
         p.n_images = n;
         p.border = border_type;
@@ -632,6 +806,7 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
         p.block_start = (const int64_t*)(meta + off_s);
         p.total_blocks = total;
         HIP_TRY(wicca::launch_block_sum<uint8_t>(p, depth, (int)C, stream));
+        HIP_TRY(hipEventRecord(ws->meta_done[slot], stream));
     }
     if (!dst_is_device) {
         for (int64_t i = 0; i < n; ++i)
@@ -639,8 +814,11 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
                                      d[i].dst_pitch, ow[i] * C, oh[i], hipMemcpyDeviceToHost,
                                      stream));
     }
-    // descriptors and staging live in the workspace: finish before it returns
-    HIP_TRY(hipStreamSynchronize(stream));
+    // staging lives in the workspace: finish before it returns, unless every
+    // buffer is the caller's device memory on the caller's stream (descriptors
+    // are guarded by meta_done)
+    if (!stream_in || !src_is_device || !dst_is_device || !one_launch)
+        HIP_TRY(hipStreamSynchronize(stream));
     return WICCA_OK;
 }
 
@@ -662,20 +840,11 @@ int wicca_haar_ll_u8_batch_multi_gpu(const wicca_image_desc* descs, int64_t n, i
         if (d < 0 || d >= g_device_count) return fail(WICCA_ERR_ARG, "device %d out of range", d);
     // contiguous image ranges balanced by pixel count, at most one per device
     const int nd = (int)std::min<int64_t>((int64_t)devs.size(), n);
-    int64_t total = 0;
-    for (int64_t i = 0; i < n; ++i) total += std::max<int64_t>(descs[i].height, 0) * std::max<int64_t>(descs[i].width, 0);
-    std::vector<int64_t> first((size_t)nd + 1, n);  // range r = images [first[r], first[r+1])
-    first[0] = 0;
-    {
-        int64_t acc = 0;
-        int r = 0;
-        for (int64_t i = 0; i < n && r < nd - 1; ++i) {
-            acc += std::max<int64_t>(descs[i].height, 0) * std::max<int64_t>(descs[i].width, 0);
-            // close range r after image i once it holds its share, leaving an
-            // image for each later range
-            if (acc >= total * (r + 1) / nd && n - (i + 1) >= nd - 1 - r) first[(size_t)++r] = i + 1;
-        }
-    }
+    std::vector<int64_t> px((size_t)n);
+    for (int64_t i = 0; i < n; ++i)
+        px[(size_t)i] = std::max<int64_t>(descs[i].height, 0) * std::max<int64_t>(descs[i].width, 0);
+    std::vector<int64_t> first((size_t)nd + 1);  // range r = images [first[r], first[r+1])
+    balance_ranges(px.data(), n, nd, first.data());
     std::vector<int> rcs((size_t)nd, WICCA_OK);
     std::vector<std::string> msgs((size_t)nd);
     auto work = [&](int r) {

@@ -25,6 +25,27 @@ constexpr int kSegPx = kThreads * 16;  // pixels per segment (16 per lane)
 constexpr int kMultiWaves = WICCA_MULTI_WAVES;  // K5: wave strips per workgroup
 constexpr int kStripWaves = WICCA_STRIP_WAVES;  // K1s: wave strips per workgroup
 
+// Workgroups are dealt to the 8 XCDs round-robin (block b runs on XCD b % 8),
+// and each XCD has its own L2.  WICCA_XCD_REMAP re-deals the logical block
+// order so that XCD x runs runs of K consecutive logical blocks (K = -1: one
+// contiguous 1/8 of the grid per XCD).
+constexpr uint32_t kXcds = 8;
+__device__ __forceinline__ uint32_t logical_block(uint32_t b, uint32_t n)
+{
+    if constexpr (WICCA_XCD_REMAP == 0) {
+        return b;
+    } else if constexpr (WICCA_XCD_REMAP < 0) {
+        const uint32_t x = b % kXcds, i = b / kXcds, q = n / kXcds, r = n % kXcds;
+        return x * q + min(x, r) + i;
+    } else {
+        constexpr uint32_t K = WICCA_XCD_REMAP;
+        const uint32_t full = n / (kXcds * K) * (kXcds * K);
+        if (b >= full) return b;  // the ragged tail keeps hardware order
+        const uint32_t x = b % kXcds, i = b / kXcds;
+        return (i / K) * (kXcds * K) + x * K + i % K;
+    }
+}
+
 // ----------------------------------------------------------------------------
 // Work decomposition: block -> (image, output row, segment).
 // ----------------------------------------------------------------------------
@@ -39,14 +60,35 @@ template <int L, bool RAGGED>
 __device__ __forceinline__ BlockWork resolve_block(const LLParams& p)
 {
     BlockWork w;
-    uint32_t b = blockIdx.x;
+    uint32_t b = logical_block(blockIdx.x, gridDim.x);
     if constexpr (RAGGED) {
-        // binary search the per-image block prefix (n_images is small)
-        int lo = 0, hi = p.n_images - 1;
-        while (lo < hi) {
-            int mid = (lo + hi + 1) >> 1;
-            if (p.block_start[mid] <= (int64_t)b) lo = mid; else hi = mid - 1;
+        b += p.block_base;
+        // Which image owns block b: block_start is increasing, so the number of
+        // images starting at or before b, minus one.  One wave-wide probe of 64
+        // prefixes (ballot + popcount) per level instead of a dependent binary
+        // search: one load round trip for <= 64 images, two for <= 4096.
+        const int n = (int)p.n_images;
+        const int lane = (int)(threadIdx.x & 63);
+        int lo;
+        if (n <= 64) {
+            const bool le = lane < n && p.block_start[lane] <= (int64_t)b;
+            lo = __popcll(__ballot(le)) - 1;
+        } else if (n <= 64 * 64) {
+            const int ci = lane * 64;
+            const bool cle = ci < n && p.block_start[ci] <= (int64_t)b;
+            const int c = (__popcll(__ballot(cle)) - 1) * 64;
+            const int fi = c + lane;
+            const bool fle = fi < n && p.block_start[fi] <= (int64_t)b;
+            lo = c + __popcll(__ballot(fle)) - 1;
+        } else {
+            lo = 0;
+            int hi = n - 1;
+            while (lo < hi) {
+                int mid = (lo + hi + 1) >> 1;
+                if (p.block_start[mid] <= (int64_t)b) lo = mid; else hi = mid - 1;
+            }
         }
+        lo = __builtin_amdgcn_readfirstlane(lo);
         const ImageDescDev d = p.descs[lo];
         b -= (uint32_t)p.block_start[lo];
         w.src = d.src; w.dst = d.dst; w.H = d.H; w.W = d.W;

@@ -61,6 +61,10 @@
 #ifndef WICCA_K1_WG_CAP1
 #define WICCA_K1_WG_CAP1 0      // K1 at D=1: at most this many workgroups per CU (0 = no cap)
 #endif
+#ifndef WICCA_XCD_REMAP
+#define WICCA_XCD_REMAP 128   // logical blocks per XCD turn: 0 = hardware order (round-robin over
+                              // the 8 XCDs), K > 0 = runs of K, -1 = one contiguous run per XCD
+#endif
 #ifndef WICCA_STRIP_DOT
 #define WICCA_STRIP_DOT 1     // strip kernel: v_dot4 per-(icon, channel) sums on non-edge strips (neutral, fewer VGPRs)
 #endif
@@ -136,7 +140,13 @@ struct LLParams {
     const ImageDescDev* descs;
     const int64_t* block_start;  // n_images entries, prefix of blocks
     int64_t total_blocks;
+    uint32_t block_base;         // first block of this launch (grids split at the HIP limit)
 };
+
+// HIP caps gridDim.x * blockDim.x below 2^32: the most blocks one launch of
+// `threads`-wide workgroups may have.  Larger grids are split (by images for a
+// uniform batch, by block ranges for a ragged one).
+constexpr int64_t max_grid_blocks(int threads) { return (((int64_t)1 << 32) - 1) / threads; }
 
 // Multi-depth kernel parameters (icons of every wanted depth from one read).
 struct MultiParams {
@@ -155,6 +165,12 @@ struct MultiParams {
 bool multi_kernel_ok(const uint8_t* src, int64_t src_pitch, int64_t src_stride, int64_t W, int C,
                      int dmin, int dmax);
 hipError_t launch_multi(MultiParams p, int dmin, int C, hipStream_t s);
+
+// Name of the kernel launch_block_sum<uint8_t> dispatches for an aligned
+// (uniform or ragged) batch at depth L with C channels, as rocprofv3 prints it
+// without the namespace and argument list, e.g. "haar_strip_kernel<5, 3,
+// unsigned char, false>".  Empty for layouts the fast kernels do not take.
+const char* block_sum_kernel_name(int L, int C, bool ragged);
 
 int64_t segments_for(int64_t out_w, int L, int C);  // column groups per icon row
 bool fast_path_ok(const LLParams& p, int L, int C);

@@ -30,6 +30,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <mutex>
 
 #include "haar_device.h"
 
@@ -820,16 +822,35 @@ hipError_t launch_block_sum(LLParams p, int L, int C, hipStream_t stream)
     const bool out_al = ((uintptr_t)p.dst % 16 == 0) && p.dst_pitch % 16 == 0 &&
                         p.dst_image_stride % 16 == 0;
     p.aligned_out = out_al ? 1 : 0;
+    constexpr int64_t kMax = max_grid_blocks(kThreads);  // strip and segment kernels: 256 lanes
     if (p.descs == nullptr && out_al && fast_path_ok(p, L, C)) {
         p.n_seg = (int32_t)segments_for(p.out_w, L, C);
-        const int64_t blocks = p.n_images * p.out_h * p.n_seg;
-        if (blocks <= 0) return hipSuccess;
-        if (blocks >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
-        return dispatch_C<OutT>(L, C, p, blocks, stream);
+        const int64_t per_image = p.out_h * p.n_seg;
+        if (per_image <= 0 || p.n_images <= 0) return hipSuccess;
+        if (per_image > kMax) return hipErrorInvalidValue;  // one image past the grid limit
+        // at most kMax blocks per launch: consecutive image ranges
+        const int64_t imgs_per_launch = kMax / per_image;
+        const int64_t n = p.n_images;
+        for (int64_t i0 = 0; i0 < n; i0 += imgs_per_launch) {
+            LLParams q = p;
+            q.n_images = std::min(imgs_per_launch, n - i0);
+            q.src = p.src + i0 * p.src_image_stride;
+            q.dst = p.dst + i0 * p.dst_image_stride;
+            hipError_t e = dispatch_C<OutT>(L, C, q, q.n_images * per_image, stream);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
     }
     if (p.descs != nullptr) {
-        // ragged: caller guarantees alignment of every descriptor
-        return dispatch_C<OutT>(L, C, p, p.total_blocks, stream);
+        // ragged: caller guarantees alignment of every descriptor; blocks past
+        // the grid limit go to further launches that start at block_base
+        for (int64_t b0 = 0; b0 < p.total_blocks; b0 += kMax) {
+            LLParams q = p;
+            q.block_base = (uint32_t)b0;
+            hipError_t e = dispatch_C<OutT>(L, C, q, std::min(kMax, p.total_blocks - b0), stream);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
     }
     const int64_t total = p.n_images * p.out_h * p.out_w * C;
     if (total <= 0) return hipSuccess;
@@ -837,6 +858,24 @@ hipError_t launch_block_sum(LLParams p, int L, int C, hipStream_t stream)
     hipLaunchKernelGGL(haar_block_sum_generic_kernel<OutT>, dim3((uint32_t)blocks), dim3(kThreads),
                        0, stream, p, L, C);
     return hipGetLastError();
+}
+
+const char* block_sum_kernel_name(int L, int C, bool ragged)
+{
+    static const char* const kStrip = "haar_strip_kernel";
+    static const char* const kSeg = "haar_block_sum_kernel";
+    if (L < 1 || L > 8 || C < 1 || C > 4) return "";
+    // "<L, C, unsigned char, RAGGED>" as the compiler names the instantiation
+    static char names[2][9][5][64];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (int r = 0; r < 2; ++r)
+            for (int l = 1; l <= 8; ++l)
+                for (int c = 1; c <= 4; ++c)
+                    snprintf(names[r][l][c], sizeof(names[r][l][c]), "%s<%d, %d, unsigned char, %s>",
+                             use_strip_kernel(l) ? kStrip : kSeg, l, c, r ? "true" : "false");
+    });
+    return names[ragged ? 1 : 0][L][C];
 }
 
 template hipError_t launch_block_sum<uint8_t>(LLParams, int, int, hipStream_t);

@@ -52,16 +52,30 @@ hipError_t launch_multi(MultiParams p, int dmin, int C, hipStream_t s)
     const int64_t strip = 64 * strip_lane_pixels(C);
     p.n_bands = Hp / R;
     p.n_groups = (int32_t)(((Wp + strip - 1) / strip + kMultiWaves - 1) / kMultiWaves);
-    const int64_t blocks = p.n_images * p.n_bands * p.n_groups;
-    if (blocks <= 0) return hipSuccess;
-    if (blocks >= ((int64_t)1 << 32)) return hipErrorInvalidValue;
-    switch (C) {
-    case 1: return launch_multi_c<1>(dmin, p, blocks, s);
-    case 2: return launch_multi_c<2>(dmin, p, blocks, s);
-    case 3: return launch_multi_c<3>(dmin, p, blocks, s);
-    case 4: return launch_multi_c<4>(dmin, p, blocks, s);
-    default: return hipErrorInvalidValue;
+    const int64_t per_image = p.n_bands * p.n_groups;
+    if (per_image <= 0 || p.n_images <= 0) return hipSuccess;
+    // at most max_grid_blocks per launch (HIP's grid limit): image ranges
+    const int64_t kMax = max_grid_blocks(64 * kMultiWaves);
+    if (per_image > kMax) return hipErrorInvalidValue;
+    const int64_t per_launch = kMax / per_image, n = p.n_images;
+    for (int64_t i0 = 0; i0 < n; i0 += per_launch) {
+        MultiParams q = p;
+        q.n_images = std::min(per_launch, n - i0);
+        q.src = p.src + i0 * p.src_image_stride;
+        for (int t = 0; t <= 8; ++t)
+            if (q.dst[t]) q.dst[t] = p.dst[t] + i0 * p.dst_stride[t];
+        const int64_t blocks = q.n_images * per_image;
+        hipError_t e;
+        switch (C) {
+        case 1: e = launch_multi_c<1>(dmin, q, blocks, s); break;
+        case 2: e = launch_multi_c<2>(dmin, q, blocks, s); break;
+        case 3: e = launch_multi_c<3>(dmin, q, blocks, s); break;
+        case 4: e = launch_multi_c<4>(dmin, q, blocks, s); break;
+        default: e = hipErrorInvalidValue;
+        }
+        if (e != hipSuccess) return e;
     }
+    return hipSuccess;
 }
 
 }  // namespace wicca

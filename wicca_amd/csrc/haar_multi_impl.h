@@ -380,7 +380,7 @@ __global__ __launch_bounds__(64 * kMultiWaves) void haar_multi_kernel(MultiParam
     constexpr int CH = SB < 8 ? SB : 8;        // rows per load chunk (divides SB)
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    uint32_t b = blockIdx.x;
+    uint32_t b = logical_block(blockIdx.x, gridDim.x);
     const int g = (int)(b % (uint32_t)p.n_groups);
     b /= (uint32_t)p.n_groups;
     const int band = (int)(b % (uint32_t)p.n_bands);
