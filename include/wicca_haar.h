@@ -199,6 +199,46 @@ int wicca_haar_ll_u8_multi_uniform(const uint8_t* src, int64_t n, int64_t H,
                                    void* stream);
 
 /*
+ * cv2.resize(image, (out_w, out_h), interpolation) of one uint8 HWC image
+ * (C = 1..4): the resizes of the reference's caller stage,
+ * wicca/classifying_tools.py:315 (source image) and :318 (icon), which run
+ * with interpolation=cv2.INTER_AREA in the demo.  interpolation uses OpenCV's
+ * codes: 0 INTER_NEAREST, 1 INTER_LINEAR, 3 INTER_AREA (others ->
+ * WICCA_ERR_ARG).  The arithmetic restates OpenCV's resize.cpp (see
+ * oracle/resize_cv.py; parity against an OpenCV binary is unpinned here).
+ * Note OpenCV's argument order: width first.  Buffers host or device per the
+ * flags, as in wicca_haar_ll_u8.
+ */
+int wicca_resize_u8(const uint8_t* src, int64_t H, int64_t W, int64_t C,
+                    int64_t src_pitch, uint8_t* dst, int64_t out_w, int64_t out_h,
+                    int64_t dst_pitch, int interpolation, int src_is_device,
+                    int dst_is_device, int device, void* stream);
+
+/* Device-resident uniform batch of wicca_resize_u8: n images of (H, W, C). */
+int wicca_resize_u8_uniform(const uint8_t* src, int64_t n, int64_t H, int64_t W,
+                            int64_t C, int64_t src_pitch, int64_t src_image_stride,
+                            uint8_t* dst, int64_t out_w, int64_t out_h,
+                            int64_t dst_pitch, int64_t dst_image_stride,
+                            int interpolation, int device, void* stream);
+
+/*
+ * The per-image work of ClassifierProcessor._get_img_batch
+ * (wicca/classifying_tools.py:297-323) for n decoded HOST images (descs: src,
+ * height, width, src_pitch; dst unused), on one device, each image uploaded
+ * once:
+ *     resized[i]       = cv2.resize(image_i, (out_w, out_h), interpolation)  (:315)
+ *     icon             = get_small_copy(image_i, depth, border...)           (:317)
+ *     resized_icons[i] = cv2.resize(icon, (out_w, out_h), interpolation)     (:318)
+ * resized / resized_icons are dense host arrays (n, out_h, out_w, C), i.e.
+ * the np.stack of :323.  Image i+1 uploads on a second stream while image i's
+ * kernels run.
+ */
+int wicca_icon_stage_u8(const wicca_image_desc* images, int64_t n, int64_t C, int depth,
+                        int border_type, int border_constant, int64_t out_w,
+                        int64_t out_h, int interpolation, uint8_t* resized,
+                        uint8_t* resized_icons, int device);
+
+/*
  * Deterministic synthetic images on device (no PCIe in timed regions):
  * byte (i, y, x, c) = splitmix64-hash of (seed, i, y*W*C + x*C + c), see
  * wicca_amd/synth.py for the host restatement.

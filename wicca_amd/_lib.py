@@ -64,6 +64,12 @@ SIGNATURES = {
                                               ctypes.POINTER(_int), _int, _int, _int,
                                               ctypes.POINTER(_p), ctypes.POINTER(_i64),
                                               ctypes.POINTER(_i64), _int, _p]),
+    "wicca_resize_u8": (_int, [_p, _i64, _i64, _i64, _i64, _p, _i64, _i64, _i64, _int, _int,
+                               _int, _int, _p]),
+    "wicca_resize_u8_uniform": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _i64, _i64,
+                                       _i64, _i64, _int, _int, _p]),
+    "wicca_icon_stage_u8": (_int, [ctypes.POINTER(ImageDesc), _i64, _i64, _int, _int, _int, _i64,
+                                   _i64, _int, _p, _p, _int]),
     "wicca_synth_u8": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_uint64, _int,
                               _p]),
     "wicca_synth_band_u8": (_int, [_p, _i64, _i64, _i64, _i64, ctypes.c_uint64, _i64, _i64, _int,

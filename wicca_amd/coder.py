@@ -202,6 +202,46 @@ class HaarCoder(WaveletCoder):
             del keep
         return outs  # type: ignore[return-value]
 
+    def icon_stage(self, images: Sequence[np.ndarray], transform_depth: int, shape,
+                   interpolation: int = 3, border_type: int = BORDER_REPLICATE,
+                   border_constant: int = 0) -> tuple[np.ndarray, np.ndarray]:
+        """``ClassifierProcessor._get_img_batch`` (classifying_tools.py:297-323)
+        for already-decoded images, each uploaded once:
+
+        ``(np.stack([cv2.resize(im, shape, interpolation) for im in images]),
+        np.stack([cv2.resize(self.get_small_copy(im, d), shape, interpolation)
+        for im in images]))`` — INTER_NEAREST / INTER_LINEAR / INTER_AREA
+        (the demo's), computed on the GPU (``wicca_icon_stage_u8``).
+        """
+        if int(border_type) not in (BORDER_CONSTANT, BORDER_REPLICATE):
+            raise ValueError("icon_stage pads with BORDER_CONSTANT or BORDER_REPLICATE")
+        prepared = [self._prepare(im, transform_depth, border_type, border_constant)
+                    for im in images]
+        if not prepared:
+            raise ValueError("need at least one array to stack")
+        out_w, out_h = int(shape[0]), int(shape[1])
+        Cs = {img.shape[2] for img, _, _, _ in prepared}
+        if len(Cs) != 1:
+            raise ValueError("all input arrays must have the same shape")
+        C = Cs.pop()
+        _, depth, border, k = prepared[0]
+        n = len(prepared)
+        descs = (_lib.ImageDesc * n)()
+        keep = []
+        for i, (img, _, _, _) in enumerate(prepared):
+            keep.append(img)
+            descs[i] = _lib.ImageDesc(img.ctypes.data, None, img.shape[0], img.shape[1],
+                                      img.strides[0], 0)
+        resized = np.empty((n, out_h, out_w, C), np.uint8)
+        icons = np.empty((n, out_h, out_w, C), np.uint8)
+        _lib.check(self._lib.wicca_icon_stage_u8(descs, n, C, depth, border, k, out_w, out_h,
+                                                 int(interpolation), resized.ctypes.data,
+                                                 icons.ctypes.data, self.device))
+        del keep
+        if C == 1:  # cv2.resize returns single-channel images as 2-D arrays
+            return resized[..., 0].copy(), icons[..., 0].copy()
+        return resized, icons
+
     def get_small_copy_multi(self, image: np.ndarray, transform_depths: Iterable[int],
                              border_type: int = BORDER_REPLICATE,
                              border_constant: int = 0) -> dict[int, np.ndarray]:
