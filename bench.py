@@ -40,11 +40,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=["batch", "tiled", "multi", "ragged"], default="batch",
+    ap.add_argument("--config", choices=["batch", "tiled", "multi", "ragged", "stage"], default="batch",
                     help="batch: configs[2]/[3] image-parallel (default); "
                          "tiled: configs[4], one 65536^2 RGB image row-sharded at depth 8; "
                          "multi: configs[2]'s depth sweep 1..6 from one read (SURVEY 8f); "
-                         "ragged: a batch of random-size images in one launch (A7 caller)")
+                         "ragged: a batch of random-size images in one launch (A7 caller); "
+                         "stage: the caller's whole per-image stage from host arrays "
+                         "(resize + icon + icon resize, HaarCoder.icon_stage)")
+    ap.add_argument("--shape", default="224,224", help="--config stage: classifier input (w,h)")
+    ap.add_argument("--interpolation", type=int, default=3, help="--config stage: cv2.INTER_*")
     ap.add_argument("--depths", default="1,2,3,4,5,6", help="depth list of --config multi")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
@@ -361,6 +365,54 @@ def run_ragged(args, torch, rank):
     }
 
 
+def run_stage(args, torch, rank):
+    """ClassifierProcessor._get_img_batch's per-image work (classifying_tools.py:
+    312-323: source resize, icon, icon resize, stack) for a batch of decoded
+    HOST images — PCIe-inclusive, so never the headline value."""
+    from wicca_amd import HaarCoder, _lib
+    lib = _lib.load()
+    B = 25 if args.images == 128 else args.images  # the caller's batch_size default (:124)
+    H, W, C, D = args.height, args.width, args.channels, args.depth
+    shape = tuple(int(x) for x in args.shape.split(","))
+    pitch = W * C
+    dev = torch.empty(B * H * pitch, dtype=torch.uint8, device="cuda")
+    _lib.check(lib.wicca_synth_u8(ctypes.c_void_p(dev.data_ptr()), B, H, W, C, pitch, H * pitch,
+                                  args.seed, -1, None))
+    host = dev.cpu().numpy().reshape(B, H, W, C)
+    del dev
+    imgs = [host[i] for i in range(B)]
+    coder = HaarCoder()
+    for _ in range(args.warmup):
+        coder.icon_stage(imgs, D, shape, args.interpolation)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res, icons = coder.icon_stage(imgs, D, shape, args.interpolation)
+    wall = (time.perf_counter() - t0) / args.steps
+    verified = None
+    if not args.no_verify:
+        from oracle import haar_numpy, resize_cv
+        i = B - 1
+        verified = bool(np.array_equal(res[i], resize_cv.resize(imgs[i], shape, args.interpolation)))
+        icon = haar_numpy.get_small_copy(imgs[i], D)
+        verified = verified and bool(np.array_equal(icons[i], resize_cv.resize(icon, shape,
+                                                                               args.interpolation)))
+        if not verified:
+            raise SystemExit("stage bench verification FAILED")
+    mpix = B * H * W / 1e6
+    return {
+        "metric": BASELINE["metric"], "value": round(mpix / wall, 1), "unit": "MP/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(wall * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic host images (numpy, pageable), PCIe inside the timed region",
+        "config": {"workload": f"{B} host {W}x{H}x{C} images per call: cv2.resize to {shape} "
+                               f"(INTER {args.interpolation}) + icon depth {D} + icon resize "
+                               "(classifying_tools.py:312-323)",
+                   "images": B, "depth": D, "shape": shape},
+        "h2d_GBps_effective": round(B * H * W * C / wall / 1e9, 2),
+        "roofline": None, "cpu_baseline": None, "verified_vs_numpy_port": verified,
+    }
+
+
 def run_multi(args, torch, rank):
     """All depths of configs[2]'s sweep from ONE read of the batch
     (wicca_haar_ll_u8_multi_uniform), against one launch per depth."""
@@ -493,6 +545,11 @@ def main():
         raise SystemExit("no HIP device visible")
     if args.config == "multi":
         out = run_multi(args, torch, rank)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        return
+    if args.config == "stage":
+        out = run_stage(args, torch, rank)
         if rank == 0:
             print(json.dumps(out), flush=True)
         return

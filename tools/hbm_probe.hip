@@ -27,6 +27,17 @@ constexpr int kPitch = 23040;   // 8K RGB row
 constexpr int kRows = 4320;
 constexpr int kImgs = 128;
 
+// XCD-aware block order (as the icon kernels, WICCA_XCD_REMAP): XCD x runs
+// runs of K consecutive logical blocks; K = 0 keeps the hardware order
+__device__ __forceinline__ unsigned remap(unsigned b, unsigned n, unsigned K)
+{
+    if (K == 0) return b;
+    const unsigned full = n / (8 * K) * (8 * K);
+    if (b >= full) return b;
+    const unsigned x = b % 8, i = b / 8;
+    return (i / K) * (8 * K) + x * K + i % K;
+}
+
 __device__ __forceinline__ void sink(u32x4 acc, unsigned* out)
 {
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[0] = 1;
@@ -67,10 +78,11 @@ __global__ __launch_bounds__(256) void read_reduce(const u32x4* __restrict__ p, 
 // the icon kernels' read pattern: block = (image, band of `rows`, 4096-px
 // segment), 3 x dwordx4 per lane per row, buffer loads
 template <int U, bool NT>
-__global__ __launch_bounds__(256) void read_bands(const unsigned char* __restrict__ p, int rows_per_band, unsigned* out)
+__global__ __launch_bounds__(256) void read_bands(const unsigned char* __restrict__ p, int rows_per_band, unsigned* out, unsigned K)
 {
     const int n_seg = 2, bands = kRows / rows_per_band;
-    const int seg = blockIdx.x % n_seg, t = blockIdx.x / n_seg;
+    const unsigned lb = remap(blockIdx.x, gridDim.x, K);
+    const int seg = lb % n_seg, t = lb / n_seg;
     const int band = t % bands, img = t / bands;
     const unsigned char* base = p + (size_t)img * kRows * kPitch + (size_t)band * rows_per_band * kPitch;
     u32x4 acc = {0, 0, 0, 0};
@@ -94,10 +106,11 @@ __global__ __launch_bounds__(256) void read_bands(const unsigned char* __restric
 // output bytes (ROWS * 12288 / 4^D) as 16-B stores into the icon layout:
 // icon row pitch 23040 >> D, segment offset 12288 >> D, ROWS >> D icon rows.
 template <int ROWS, int D, bool NTS>
-__global__ __launch_bounds__(256) void rw_bands(const unsigned char* __restrict__ p, unsigned char* __restrict__ q, unsigned* out)
+__global__ __launch_bounds__(256) void rw_bands(const unsigned char* __restrict__ p, unsigned char* __restrict__ q, unsigned* out, unsigned K)
 {
     const int n_seg = 2, bands = kRows / ROWS;
-    const int seg = blockIdx.x % n_seg, t = blockIdx.x / n_seg;
+    const unsigned lb = remap(blockIdx.x, gridDim.x, K);
+    const int seg = lb % n_seg, t = lb / n_seg;
     const int band = t % bands, img = t / bands;
     const unsigned char* base = p + (size_t)img * kRows * kPitch + (size_t)band * ROWS * kPitch;
     u32x4 acc = {0, 0, 0, 0};
@@ -130,10 +143,11 @@ __global__ __launch_bounds__(256) void rw_bands(const unsigned char* __restrict_
 // band's bytes written contiguously per block (depths 2-6: 341/4096 = 8.3 %,
 // depths 1-6: 1365/4096 = 33 %).
 template <int ROWS, int NUM>
-__global__ __launch_bounds__(256) void rw_ratio(const unsigned char* __restrict__ p, unsigned char* __restrict__ q, unsigned* out)
+__global__ __launch_bounds__(256) void rw_ratio(const unsigned char* __restrict__ p, unsigned char* __restrict__ q, unsigned* out, unsigned K)
 {
     const int n_seg = 2, bands = kRows / ROWS;
-    const int seg = blockIdx.x % n_seg, t = blockIdx.x / n_seg;
+    const unsigned lb = remap(blockIdx.x, gridDim.x, K);
+    const int seg = lb % n_seg, t = lb / n_seg;
     const int band = t % bands, img = t / bands;
     const unsigned char* base = p + (size_t)img * kRows * kPitch + (size_t)band * ROWS * kPitch;
     u32x4 acc = {0, 0, 0, 0};
@@ -154,7 +168,7 @@ __global__ __launch_bounds__(256) void rw_ratio(const unsigned char* __restrict_
     sink(acc, out);
     constexpr int OUTB = (int)((long long)ROWS * 12288 * NUM / 4096);
     static_assert(OUTB % 16 == 0, "16-B stores");
-    unsigned char* o = q + (size_t)blockIdx.x * OUTB;
+    unsigned char* o = q + (size_t)lb * OUTB;
     for (int i = threadIdx.x * 16; i < OUTB; i += 256 * 16) st16<true>(o + i, acc);
 }
 
@@ -240,6 +254,7 @@ int main(int argc, char** argv)
     CK(hipMemset(p, 1, bytes));
     CK(hipMemset(q, 0, bytes / 2));
     const int reps = 10;
+    for (unsigned XK : {0u, 128u}) {
     if (!quick) {
         for (int blocks : {2048, 8192}) {
 #define RR(U, NT) { float ms = timeit([&] { hipLaunchKernelGGL((read_reduce<U, NT>), dim3(blocks), dim3(256), 0, 0, p, n, out); }, reps); \
@@ -248,25 +263,26 @@ int main(int argc, char** argv)
         }
         for (int rpb : {2, 4, 8, 32}) {
             int blocks = kImgs * (kRows / rpb) * 2;
-#define RB(U, NT) if (U <= rpb) { float ms = timeit([&] { hipLaunchKernelGGL((read_bands<U, NT>), dim3(blocks), dim3(256), 0, 0, (const unsigned char*)p, rpb, out); }, reps); \
-        printf("read_bands rows=%d U=%d nt=%d  %.3f ms  %.1f GB/s\n", rpb, U, (int)NT, ms, (double)bytes / ms / 1e6); }
+#define RB(U, NT) if (U <= rpb) { float ms = timeit([&] { hipLaunchKernelGGL((read_bands<U, NT>), dim3(blocks), dim3(256), 0, 0, (const unsigned char*)p, rpb, out, XK); }, reps); \
+        printf("read_bands rows=%d U=%d nt=%d xcd=%u  %.3f ms  %.1f GB/s\n", rpb, U, (int)NT, XK, ms, (double)bytes / ms / 1e6); }
             RB(2, true) RB(4, true) RB(8, true) RB(8, false)
         }
     }
     // read + write at the icon kernels' write ratios
 #define RW(ROWS, D, NTS) { int blocks = kImgs * (kRows / ROWS) * 2; \
-    float ms = timeit([&] { hipLaunchKernelGGL((rw_bands<ROWS, D, NTS>), dim3(blocks), dim3(256), 0, 0, (const unsigned char*)p, q, out); }, reps); \
+    float ms = timeit([&] { hipLaunchKernelGGL((rw_bands<ROWS, D, NTS>), dim3(blocks), dim3(256), 0, 0, (const unsigned char*)p, q, out, XK); }, reps); \
     double w = (double)bytes / (1 << (2 * D)); \
-    printf("rw_bands rows=%d D=%d nts=%d  %.3f ms  read %.1f GB/s  read+write %.1f GB/s  (write %.2f GB)\n", ROWS, D, (int)NTS, ms, bytes / ms / 1e6, (bytes + w) / ms / 1e6, w / 1e9); }
+    printf("rw_bands rows=%d D=%d nts=%d xcd=%u  %.3f ms  read %.1f GB/s  read+write %.1f GB/s  (write %.2f GB)\n", ROWS, D, (int)NTS, XK, ms, bytes / ms / 1e6, (bytes + w) / ms / 1e6, w / 1e9); }
     RW(2, 1, true) RW(4, 1, true) RW(8, 1, true) RW(2, 1, false) RW(8, 1, false)
     RW(4, 2, true) RW(8, 2, true) RW(16, 2, true) RW(4, 2, false) RW(16, 2, false)
     RW(8, 3, true) RW(16, 3, true) RW(32, 3, true) RW(8, 3, false)
     RW(32, 5, true)
 #define RQ(ROWS, NUM) { int blocks = kImgs * (kRows / ROWS) * 2; \
-    float ms = timeit([&] { hipLaunchKernelGGL((rw_ratio<ROWS, NUM>), dim3(blocks), dim3(256), 0, 0, (const unsigned char*)p, q, out); }, reps); \
+    float ms = timeit([&] { hipLaunchKernelGGL((rw_ratio<ROWS, NUM>), dim3(blocks), dim3(256), 0, 0, (const unsigned char*)p, q, out, XK); }, reps); \
     double w = (double)bytes * NUM / 4096; \
-    printf("rw_ratio rows=%d write=%d/4096  %.3f ms  read %.1f GB/s  read+write %.1f GB/s  (write %.2f GB)\n", ROWS, NUM, ms, bytes / ms / 1e6, (bytes + w) / ms / 1e6, w / 1e9); }
+    printf("rw_ratio rows=%d write=%d/4096 xcd=%u  %.3f ms  read %.1f GB/s  read+write %.1f GB/s  (write %.2f GB)\n", ROWS, NUM, XK, ms, bytes / ms / 1e6, (bytes + w) / ms / 1e6, w / 1e9); }
     RQ(64, 341) RQ(32, 341) RQ(64, 1365) RQ(32, 1365) RQ(16, 256) RQ(16, 1024)
+    }
     if (quick) return 0;
 #define RP(ROWS, D, FL, NTS, BLK) { int tb = kImgs * (kRows / ROWS) * 2; \
     float ms = timeit([&] { hipLaunchKernelGGL((rw_persist<ROWS, D, FL, NTS>), dim3(BLK), dim3(256), 0, 0, (const unsigned char*)p, q, tb, out); }, reps); \

@@ -266,13 +266,21 @@ int select_device(int device, int* out, DeviceGuard& guard)
 
 inline int64_t round_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
 
+// Row pitch of host images staged on the device: whole 128-B lines, so no
+// line is shared by two rows (rows of a ragged batch at 16-B pitches fetched
+// ~5 % extra: bench --config ragged --ragged-align 16 vs 128, r02 notes in DESIGN.md).
+constexpr int64_t kStagePitch = 128;
+
 // Upload `height` rows of `width` bytes from host memory (row pitch spitch)
-// to device memory (row pitch dpitch) on `stream`.  One hipMemcpy2DAsync from
-// pageable memory: the runtime's own staging measured 49 GB/s single-threaded
-// and 55 GB/s from 4-16 threads on MI355X (PCIe Gen5 x16, 63 GB/s spec),
-// ahead of a 2-slot pinned ring with CPU copies (32 / 51 GB/s) and of pinning
-// the caller's buffer in place (no faster, and unsafe when two threads pass
-// the same array) — tools/host_path_bench.py, profiles/r01_host_path.jsonl.
+// to device memory (row pitch dpitch), ordered before later work on `stream`:
+// one pageable hipMemcpy2DAsync.  Measured on the box
+// (tools/pcie_probe.hip, profiles/r02_pcie_probe.txt, r02_host_path_pinned_ring.jsonl):
+// pinned-memory DMA peaks at 57.5 GB/s (PCIe Gen5 x16); this path reaches
+// 49 GB/s for one 100 MB image from one thread and 54.7-56 GB/s for a batch
+// or 4-16 calling threads (95-97 % of the DMA ceiling).  A per-device ring of
+// four 32 MB pinned chunks filled by four host threads, DMA overlapped, was
+// slower (45 / 51 GB/s); so were a 2-slot single-copier ring and pinning the
+// caller's array in place (round 1, profiles/r01_host_path.jsonl).
 int upload_rows(Workspace*, void* dst, int64_t dpitch, const uint8_t* src, int64_t spitch,
                 int64_t width, int64_t height, hipStream_t stream)
 {
@@ -534,7 +542,7 @@ int single_image(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t sr
     const uint8_t* dsrc = src;
     int64_t dpitch_in = src_pitch;
     if (!src_is_device) {
-        dpitch_in = round_up(W * C, 64);
+        dpitch_in = round_up(W * C, kStagePitch);
         HIP_TRY(ws->in.reserve((size_t)(dpitch_in * H)));
         rc = upload_rows(ws, ws->in.ptr, dpitch_in, src, src_pitch, W * C, H, stream);
         if (rc) return rc;
@@ -734,14 +742,14 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
     int64_t in_bytes = 0, out_bytes = 0;
     for (int64_t i = 0; i < n; ++i) {
         icon_dims(d[i].height, d[i].width, depth, &oh[i], &ow[i]);
-        if (!src_is_device) in_bytes += round_up(d[i].width * C, 64) * d[i].height;
+        if (!src_is_device) in_bytes += round_up(d[i].width * C, kStagePitch) * d[i].height;
         if (!dst_is_device) out_bytes += round_up(ow[i] * C, 16) * oh[i];
     }
     if (!src_is_device) {
         HIP_TRY(ws->in.reserve((size_t)in_bytes));
         int64_t off = 0;
         for (int64_t i = 0; i < n; ++i) {
-            const int64_t pitch = round_up(d[i].width * C, 64);
+            const int64_t pitch = round_up(d[i].width * C, kStagePitch);
             uint8_t* p = (uint8_t*)ws->in.ptr + off;
             rc = upload_rows(ws, p, pitch, descs_in[i].src, descs_in[i].src_pitch, d[i].width * C,
                              d[i].height, stream);
@@ -920,7 +928,7 @@ int wicca_haar_ll_u8_multi(const uint8_t* src, int64_t H, int64_t W, int64_t C, 
     const uint8_t* dsrc = src;
     int64_t dpitch_in = src_pitch;
     if (!src_is_device) {  // one upload shared by every depth
-        dpitch_in = round_up(W * C, 64);
+        dpitch_in = round_up(W * C, kStagePitch);
         HIP_TRY(ws->in.reserve((size_t)(dpitch_in * H)));
         rc = upload_rows(ws, ws->in.ptr, dpitch_in, src, src_pitch, W * C, H, stream);
         if (rc) return rc;
@@ -1103,7 +1111,7 @@ int wicca_resize_u8(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t
     const uint8_t* dsrc = src;
     int64_t sp = src_pitch;
     if (!src_is_device) {
-        sp = round_up(W * C, 128);
+        sp = round_up(W * C, kStagePitch);
         HIP_TRY(ws->in.reserve((size_t)(sp * H)));
         if ((rc = upload_rows(ws, ws->in.ptr, sp, src, src_pitch, W * C, H, stream))) return rc;
         dsrc = (const uint8_t*)ws->in.ptr;
@@ -1171,7 +1179,7 @@ int wicca_icon_stage_u8(const wicca_image_desc* images, int64_t n, int64_t C, in
             return rc;
         icon_dims(images[i].height, images[i].width, depth, &ih[i], &iw[i]);
         if ((rc = check_resize(ih[i], iw[i], C, out_w, out_h, interpolation, &probe))) return rc;
-        max_in = std::max(max_in, round_up(images[i].width * C, 128) * images[i].height);
+        max_in = std::max(max_in, round_up(images[i].width * C, kStagePitch) * images[i].height);
         max_icon = std::max(max_icon, round_up(iw[i] * C, 16) * ih[i]);
     }
     DeviceGuard dg;
@@ -1195,7 +1203,7 @@ int wicca_icon_stage_u8(const wicca_image_desc* images, int64_t n, int64_t C, in
     for (int64_t i = 0; i < n; ++i) {
         const int k = (int)(i & 1);
         const int64_t H = images[i].height, W = images[i].width;
-        const int64_t pitch = round_up(W * C, 128);
+        const int64_t pitch = round_up(W * C, kStagePitch);
         uint8_t* img = (uint8_t*)ws->slot[k].ptr;
         // upload image i once slot k's previous image (i - 2) is no longer read
         HIP_TRY(hipStreamWaitEvent(up, ws->slot_free[k], 0));
