@@ -54,6 +54,8 @@ extern "C" {
 #define WICCA_ERR_HIP         -7 /* HIP runtime error (message in wicca_last_error) */
 #define WICCA_ERR_NOMEM       -8 /* device allocation failed */
 #define WICCA_ERR_NODEVICE    -9 /* no HIP device visible */
+#define WICCA_ERR_DECODE     -10 /* corrupt or truncated image file */
+#define WICCA_ERR_UNSUPPORTED -11 /* valid file the GPU decoder does not handle (progressive, ...) */
 
 /* One image of a ragged batch. */
 typedef struct wicca_image_desc {
@@ -237,6 +239,44 @@ int wicca_icon_stage_u8(const wicca_image_desc* images, int64_t n, int64_t C, in
                         int border_type, int border_constant, int64_t out_w,
                         int64_t out_h, int interpolation, uint8_t* resized,
                         uint8_t* resized_icons, int device);
+
+/*
+ * JPEG decode on the GPU: the reference's load_image (wicca/data_loader.py:
+ * 31-63: cv2.imread + cv2.cvtColor(BGR2RGB)) for baseline / extended-
+ * sequential Huffman JPEG (8-bit, grayscale or YCbCr 4:4:4 / 4:2:2 / 4:2:0,
+ * restart markers allowed): libjpeg-turbo's default arithmetic (ISLOW IDCT,
+ * fancy upsampling, integer YCbCr->RGB) restated on the device, output RGB
+ * HWC uint8 (grayscale replicated to 3 channels, as IMREAD_COLOR does).
+ * Progressive / arithmetic / 12-bit / CMYK files return WICCA_ERR_UNSUPPORTED,
+ * corrupt ones WICCA_ERR_DECODE.
+ */
+
+/* Dimensions of a JPEG file (after EXIF orientation when apply_orientation;
+ * cv2.imread applies it), its component count and EXIF orientation (1..8). */
+int wicca_jpeg_info(const uint8_t* data, int64_t size, int apply_orientation,
+                    int64_t* height, int64_t* width, int* components, int* orientation);
+
+/* Decode n JPEG files (data[i], sizes[i] bytes, host memory) into RGB images
+ * dsts[i] (row pitch dst_pitches[i] >= width*3, host or device per the flag),
+ * all in one device pass. */
+int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                         uint8_t* const* dsts, const int64_t* dst_pitches,
+                         int apply_orientation, int dst_is_device, int device, void* stream);
+
+/* Synchronisation passes of the calling thread's last JPEG decode (diagnostic). */
+int wicca_jpeg_last_sync_rounds(void);
+
+/*
+ * ClassifierProcessor._get_img_batch (wicca/classifying_tools.py:297-323) from
+ * the FILE bytes: GPU decode (load_image, :313) + cv2.resize of the image
+ * (:315) + icon (:317) + cv2.resize of the icon (:318); only the compressed
+ * files cross PCIe.  resized / resized_icons: dense host arrays (n, out_h,
+ * out_w, 3), the np.stack of :323.
+ */
+int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                             int depth, int border_type, int border_constant,
+                             int64_t out_w, int64_t out_h, int interpolation,
+                             uint8_t* resized, uint8_t* resized_icons, int device);
 
 /*
  * Deterministic synthetic images on device (no PCIe in timed regions):

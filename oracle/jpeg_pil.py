@@ -1,0 +1,80 @@
+"""JPEG decode checker — TEST INFRASTRUCTURE.
+
+The reference decodes with ``cv2.imread`` (opencv-python 4.12.0.88,
+``requirements.txt:91``), i.e. libjpeg-turbo at its defaults (ISLOW integer
+IDCT, fancy upsampling, integer YCbCr -> RGB), followed by ``cvtColor(BGR2RGB)``
+(``/root/reference/wicca/data_loader.py:53-58``).  cv2 is absent here; Pillow
+12.2.0 is present and bundles libjpeg-turbo 3.1.4.1 with the same defaults
+(``dct_method`` ISLOW unless draft mode, ``do_fancy_upsampling`` on,
+``JCS_RGB`` output), so its decode is the checker for the GPU decoder
+(``wicca_amd/csrc/jpeg.hip``): parity is pinned to libjpeg-turbo 3.1.4.1 via
+Pillow, not to an OpenCV binary.  EXIF orientation is applied with
+``ImageOps.exif_transpose`` (cv2.imread's IMREAD_COLOR applies it too).
+Only ``tests/`` and the golden-fixture script use this module.
+"""
+from __future__ import annotations
+
+import io
+
+import numpy as np
+
+
+def libjpeg_version() -> str:
+    from PIL import features
+    return str(features.version("libjpeg_turbo"))
+
+
+def decode_rgb(data: bytes, apply_orientation: bool = True) -> np.ndarray:
+    """RGB (H, W, 3) uint8 decode of a JPEG file's bytes."""
+    from PIL import Image, ImageOps
+    im = Image.open(io.BytesIO(data))
+    im.load()
+    if apply_orientation:
+        im = ImageOps.exif_transpose(im)
+    return np.asarray(im.convert("RGB")).copy()
+
+
+def encode(img: np.ndarray, quality: int = 75, subsampling: int = 2, restart_blocks: int = 0,
+           restart_rows: int = 0, optimize: bool = False, progressive: bool = False,
+           orientation: int = 1) -> bytes:
+    """JPEG bytes of an (H, W, 3) RGB or (H, W) gray uint8 array (libjpeg-turbo encoder)."""
+    from PIL import Image
+    im = Image.fromarray(img)
+    kw = dict(quality=quality, optimize=optimize, progressive=progressive)
+    if img.ndim == 3:
+        kw["subsampling"] = subsampling
+    if restart_blocks:
+        kw["restart_marker_blocks"] = restart_blocks
+    if restart_rows:
+        kw["restart_marker_rows"] = restart_rows
+    if orientation != 1:
+        ex = Image.Exif()
+        ex[0x0112] = orientation
+        kw["exif"] = ex.tobytes()
+    b = io.BytesIO()
+    im.save(b, "JPEG", **kw)
+    return b.getvalue()
+
+
+def test_image(kind: str, H: int, W: int, seed: int) -> np.ndarray:
+    """Deterministic content: 'noise' (long Huffman codes), 'smooth' (many EOBs),
+    'scene' (blobs + edges + noise), 'gray' (2-D)."""
+    rng = np.random.default_rng(seed)
+    if kind == "noise":
+        return rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    y, x = np.mgrid[0:H, 0:W].astype(np.float64)
+    if kind == "smooth":
+        r = 127 + 120 * np.sin(x / max(W, 1) * 3.1 + 0.3)
+        g = 127 + 120 * np.cos(y / max(H, 1) * 2.3)
+        b = 127 + 100 * np.sin((x + y) / max(H + W, 1) * 5.0)
+        return np.clip(np.stack([r, g, b], -1), 0, 255).astype(np.uint8)
+    base = np.zeros((H, W, 3))
+    for _ in range(6):
+        cx, cy = rng.uniform(0, W), rng.uniform(0, H)
+        rad = rng.uniform(0.05, 0.4) * max(H, W)
+        col = rng.uniform(0, 255, 3)
+        m = ((x - cx) ** 2 + (y - cy) ** 2) < rad ** 2
+        base[m] = 0.5 * base[m] + 0.5 * col
+    base += rng.normal(0, 12, base.shape)
+    img = np.clip(base, 0, 255).astype(np.uint8)
+    return img[:, :, 0] if kind == "gray" else img

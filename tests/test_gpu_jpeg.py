@@ -1,0 +1,113 @@
+"""GPU JPEG decode (load_image, data_loader.py:31-63) against libjpeg-turbo
+3.1.4.1 through Pillow (oracle/jpeg_pil.py), bit for bit: the committed golden
+files, then a generated corpus over content, sizes (MCU-aligned and ragged),
+qualities, 4:4:4 / 4:2:2 / 4:2:0 / grayscale, restart intervals, optimised
+Huffman tables and EXIF orientations; batched decode; the file-based caller
+stage (_get_img_batch, classifying_tools.py:297-323)."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import wicca_amd
+from oracle import c_oracle
+from oracle import jpeg_pil as J
+from oracle import resize_cv as R
+from wicca_amd import jpeg as WJ
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden", "jpeg")
+CASES = json.load(open(os.path.join(GOLD, "cases.json")))["cases"]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_golden_files(case):
+    data = open(os.path.join(GOLD, case["file"]), "rb").read()
+    rgb = WJ.decode(data)
+    assert rgb.shape == (case["height"], case["width"], 3)
+    assert hashlib.sha256(rgb.tobytes()).hexdigest() == case["sha256_rgb"]
+
+
+GEN = []
+for kind in ("scene", "noise", "smooth"):
+    for (H, W) in ((16, 16), (17, 33), (64, 80), (135, 241), (333, 517)):
+        for sub in (0, 1, 2):
+            for q in (50, 95):
+                GEN.append((kind, H, W, sub, q, 0, False))
+GEN += [("scene", 480, 640, 2, 75, rb, opt) for rb in (1, 5, 64) for opt in (False, True)]
+GEN += [("scene", 1080, 1920, sub, 85, 0, False) for sub in (0, 1, 2)]
+GEN += [("noise", 2160, 3840, 2, 100, 0, False), ("scene", 4320, 7680, 2, 90, 0, False)]
+
+
+@pytest.mark.parametrize("kind,H,W,sub,q,rb,opt", GEN,
+                         ids=[f"{k}-{h}x{w}-s{s}-q{q}-r{r}-o{int(o)}" for k, h, w, s, q, r, o in GEN])
+def test_generated_corpus(kind, H, W, sub, q, rb, opt):
+    img = J.test_image(kind, H, W, H * 7 + W + sub)
+    data = J.encode(img, q, sub, rb, 0, opt)
+    assert np.array_equal(WJ.decode(data), J.decode_rgb(data))
+
+
+@pytest.mark.parametrize("H,W", [(9, 13), (64, 64), (250, 333)])
+@pytest.mark.parametrize("q", [40, 90, 100])
+def test_grayscale(H, W, q):
+    img = J.test_image("gray", H, W, q)
+    data = J.encode(img, q, restart_rows=1 if q == 90 else 0)
+    got = WJ.decode(data)
+    assert np.array_equal(got, J.decode_rgb(data))
+    assert np.array_equal(got[:, :, 0], got[:, :, 2])
+
+
+@pytest.mark.parametrize("orient", range(1, 9))
+def test_exif_orientation(orient):
+    img = J.test_image("scene", 37, 58, orient)
+    data = J.encode(img, 85, 2, orientation=orient)
+    assert np.array_equal(WJ.decode(data), J.decode_rgb(data, apply_orientation=True))
+    assert np.array_equal(WJ.decode(data, apply_orientation=False),
+                          J.decode_rgb(data, apply_orientation=False))
+
+
+def test_batch_decode_mixed():
+    blobs = [J.encode(J.test_image(k, h, w, i), q, s, rb)
+             for i, (k, h, w, q, s, rb) in enumerate([("scene", 100, 120, 75, 2, 0),
+                                                      ("noise", 31, 77, 90, 0, 3),
+                                                      ("gray", 50, 50, 60, 0, 0),
+                                                      ("smooth", 240, 320, 95, 1, 0)])]
+    got = WJ.decode_batch(blobs)
+    for b, g in zip(blobs, got):
+        assert np.array_equal(g, J.decode_rgb(b))
+
+
+def test_progressive_is_unsupported():
+    data = J.encode(J.test_image("scene", 40, 40, 1), progressive=True)
+    with pytest.raises(NotImplementedError, match="progressive"):
+        WJ.decode(data)
+
+
+def test_load_image_contract(tmp_path, capsys):
+    with pytest.raises(ValueError, match="File path cannot be empty"):
+        wicca_amd.load_image("")
+    assert wicca_amd.load_image(str(tmp_path / "missing.jpg")) is None
+    assert "Error loading image" in capsys.readouterr().out
+    p = tmp_path / "x.jpg"
+    data = J.encode(J.test_image("scene", 70, 90, 2), 80, 2)
+    p.write_bytes(data)
+    assert np.array_equal(wicca_amd.load_image(str(p)), J.decode_rgb(data))
+
+
+@pytest.mark.parametrize("depth,shape", [(5, (224, 224)), (2, (299, 299)), (3, (240, 240))])
+def test_file_caller_stage(tmp_path, depth, shape):
+    paths, refs = [], []
+    for i, (h, w) in enumerate([(480, 640), (1080, 1920), (333, 517), (600, 401)]):
+        data = J.encode(J.test_image("scene", h, w, i), 85, 2, orientation=6 if i == 3 else 1)
+        p = tmp_path / f"{i}.jpg"
+        p.write_bytes(data)
+        paths.append(str(p))
+        refs.append(J.decode_rgb(data))
+    imgs, icons = wicca_amd.get_img_batch(paths, shape, depth)
+    for i, rgb in enumerate(refs):
+        assert np.array_equal(imgs[i], R.resize(rgb, shape, R.INTER_AREA)), i
+        icon = c_oracle.ll_int_block(rgb, depth)[0]
+        assert np.array_equal(icons[i], R.resize(icon, shape, R.INTER_AREA)), i

@@ -23,6 +23,8 @@ WICCA_ERR_ARG = -6
 WICCA_ERR_HIP = -7
 WICCA_ERR_NOMEM = -8
 WICCA_ERR_NODEVICE = -9
+WICCA_ERR_DECODE = -10
+WICCA_ERR_UNSUPPORTED = -11
 
 _i64 = ctypes.c_int64
 _int = ctypes.c_int
@@ -70,6 +72,13 @@ SIGNATURES = {
                                        _i64, _i64, _int, _int, _p]),
     "wicca_icon_stage_u8": (_int, [ctypes.POINTER(ImageDesc), _i64, _i64, _int, _int, _int, _i64,
                                    _i64, _int, _p, _p, _int]),
+    "wicca_jpeg_info": (_int, [_p, _i64, _int, ctypes.POINTER(_i64), ctypes.POINTER(_i64),
+                               ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "wicca_jpeg_decode_u8": (_int, [ctypes.POINTER(_p), ctypes.POINTER(_i64), _i64, ctypes.POINTER(_p),
+                                    ctypes.POINTER(_i64), _int, _int, _int, _p]),
+    "wicca_jpeg_last_sync_rounds": (_int, []),
+    "wicca_jpeg_icon_stage_u8": (_int, [ctypes.POINTER(_p), ctypes.POINTER(_i64), _i64, _int, _int, _int,
+                                        _i64, _i64, _int, _p, _p, _int]),
     "wicca_synth_u8": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_uint64, _int,
                               _p]),
     "wicca_synth_band_u8": (_int, [_p, _i64, _i64, _i64, _i64, ctypes.c_uint64, _i64, _i64, _int,
@@ -145,8 +154,10 @@ def check(rc: int) -> None:
         raise ValueError(msg)
     if rc == WICCA_ERR_NOMEM:
         raise MemoryError(msg)
-    if rc == WICCA_ERR_ARG:
+    if rc in (WICCA_ERR_ARG, WICCA_ERR_DECODE):
         raise ValueError(msg)
+    if rc == WICCA_ERR_UNSUPPORTED:
+        raise NotImplementedError(msg)
     raise WiccaHipError(f"wicca_hip status {rc}: {msg}")
 
 

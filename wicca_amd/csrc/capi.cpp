@@ -28,6 +28,7 @@
 #include "../../include/wicca_haar.h"
 #include "haar_ll.h"
 #include "resize.h"
+#include "jpeg.h"
 
 namespace {
 
@@ -110,10 +111,13 @@ struct Workspace {
     hipStream_t copy_stream = nullptr;
     hipEvent_t slot_ready[2] = {nullptr, nullptr}, slot_free[2] = {nullptr, nullptr};
     DevBuf slot[2], icon[2];
+    // JPEG decode (wicca_jpeg_*): stream + tables, coefficients, planes, scratch, RGB images
+    DevBuf jmeta, jcoef, jplanes, jscratch, jrgb, jtmp;
     size_t bytes() const
     {
         return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
-               slot[0].cap + slot[1].cap + icon[0].cap + icon[1].cap;
+               slot[0].cap + slot[1].cap + icon[0].cap + icon[1].cap + jmeta.cap + jcoef.cap +
+               jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap;
     }
     hipError_t ensure_pipeline()
     {
@@ -143,6 +147,12 @@ struct Workspace {
             slot[i].release();
             icon[i].release();
         }
+        jmeta.release();
+        jcoef.release();
+        jplanes.release();
+        jscratch.release();
+        jrgb.release();
+        jtmp.release();
     }
     void destroy()
     {
@@ -1229,6 +1239,323 @@ int wicca_icon_stage_u8(const wicca_image_desc* images, int64_t n, int64_t C, in
         HIP_TRY(hipEventRecord(ws->slot_free[k], cs));
     }
     // :323  np.stack(...) of both lists: dense (n, out_h, out_w, C) each
+    HIP_TRY(hipMemcpyAsync(resized, dres, (size_t)(n * out_bytes), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(resized_icons, dico, (size_t)(n * out_bytes), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipStreamSynchronize(cs));
+    return WICCA_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// JPEG decode on the GPU (wicca/data_loader.py:31-63)
+// ---------------------------------------------------------------------------
+namespace {
+
+int jpeg_sub_bits()
+{
+    static const int v = [] {
+        const char* e = getenv("WICCA_JPEG_SUB_BITS");
+        const int b = e ? atoi(e) : 2048;
+        return std::max(256, std::min(b, 1 << 20)) & ~7;
+    }();
+    return v;
+}
+
+int parse_one(const uint8_t* data, int64_t size, wicca::JpegInfo* info, int64_t i)
+{
+    if (!data || size <= 0) return fail(WICCA_ERR_NULL_IMAGE, "Image didn't found. Please check your input.");
+    std::string err;
+    const int rc = wicca::jpeg_parse(data, (size_t)size, info, &err);
+    if (rc == -2) return fail(WICCA_ERR_UNSUPPORTED, "image %lld: %s", (long long)i, err.c_str());
+    if (rc) return fail(WICCA_ERR_DECODE, "image %lld: %s", (long long)i, err.c_str());
+    if (info->H > 65535 || info->W > 65535) return fail(WICCA_ERR_UNSUPPORTED, "image %lld too large", (long long)i);
+    return WICCA_OK;
+}
+
+void oriented_dims(const wicca::JpegInfo& in, bool apply, int64_t* h, int64_t* w)
+{
+    const bool swap = apply && in.orientation >= 5;
+    *h = swap ? in.W : in.H;
+    *w = swap ? in.H : in.W;
+}
+
+// Decode n JPEG files into device RGB images dst[i] (pitch dpitch[i]); EXIF
+// orientation applied when `orient`.  Synchronous on `stream` for the host
+// tables; the pixels are ready in stream order.
+int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                          uint8_t* const* dst, const int64_t* dpitch, bool orient, hipStream_t stream,
+                          int* rounds_out)
+{
+    std::vector<wicca::JpegInfo> info((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        int rc = parse_one(data[i], sizes[i], &info[(size_t)i], i);
+        if (rc) return rc;
+    }
+    const int S = jpeg_sub_bits();
+    std::vector<uint8_t> stream_h;
+    std::vector<wicca::JpegSegDev> segs;
+    std::vector<int32_t> sub_seg;
+    std::vector<wicca::HuffDev> huff;
+    std::vector<wicca::JpegImageDev> ims((size_t)n);
+    int64_t coef_blocks = 0, plane_bytes = 0, tmp_bytes = 0;
+    std::vector<int64_t> tmp_off((size_t)n, -1);
+    for (int64_t i = 0; i < n; ++i) {
+        const wicca::JpegInfo& f = info[(size_t)i];
+        wicca::JpegImageDev& im = ims[(size_t)i];
+        memset(&im, 0, sizeof(im));
+        im.W = f.W;
+        im.H = f.H;
+        im.ncomp = f.ncomp;
+        im.bpm = f.bpm;
+        im.mcux = f.mcux;
+        im.hmax = f.hmax;
+        im.vmax = f.vmax;
+        for (int k = 0; k < f.bpm; ++k) {
+            im.slot_comp[k] = f.slot_comp[k];
+            im.slot_h[k] = f.slot_h[k];
+            im.slot_v[k] = f.slot_v[k];
+        }
+        int tab_dc[4] = {-1, -1, -1, -1}, tab_ac[4] = {-1, -1, -1, -1};
+        for (int c = 0; c < f.ncomp; ++c) {
+            const wicca::JpegComponent& k = f.comp[c];
+            im.comp_h[c] = k.h;
+            im.comp_v[c] = k.v;
+            im.comp_bw[c] = k.bw;
+            im.comp_bh[c] = k.bh;
+            im.comp_dw[c] = k.dw;
+            im.comp_dh[c] = k.dh;
+            if (tab_dc[k.td] < 0) {
+                tab_dc[k.td] = (int)huff.size();
+                huff.emplace_back();
+                wicca::build_huff_dev(f.dc[k.td], &huff.back());
+            }
+            if (tab_ac[k.ta] < 0) {
+                tab_ac[k.ta] = (int)huff.size();
+                huff.emplace_back();
+                wicca::build_huff_dev(f.ac[k.ta], &huff.back());
+            }
+            im.dc_tab[c] = tab_dc[k.td];
+            im.ac_tab[c] = tab_ac[k.ta];
+            im.comp_block0[c] = coef_blocks;
+            coef_blocks += (int64_t)k.bw * k.bh;
+            im.comp_plane0[c] = plane_bytes;
+            plane_bytes += round_up((int64_t)k.bw * 8 * k.bh * 8, 256);
+            memcpy(im.qt[c], f.qt[k.tq], sizeof(im.qt[c]));
+        }
+        if (orient && f.orientation != 1) {  // decode into a temporary, then orient
+            tmp_off[(size_t)i] = tmp_bytes;
+            tmp_bytes += round_up((int64_t)f.W * 3, 128) * f.H;
+            im.dst_pitch = round_up((int64_t)f.W * 3, 128);
+        } else {
+            im.dst = dst[i];
+            im.dst_pitch = dpitch[i];
+        }
+        // entropy-coded segments
+        std::vector<uint8_t> bytes;
+        std::vector<int64_t> off;
+        wicca::jpeg_destuff(f, bytes, off);
+        const int64_t mcus = (int64_t)f.mcux * f.mcuy;
+        const int64_t ri = f.restart_interval > 0 ? f.restart_interval : mcus;
+        const int64_t nseg_expect = (mcus + ri - 1) / ri;
+        const int64_t nseg = std::min<int64_t>(nseg_expect, (int64_t)off.size() - 1);
+        const int64_t base = (int64_t)stream_h.size();
+        stream_h.insert(stream_h.end(), bytes.begin(), bytes.end());
+        for (int64_t sgi = 0; sgi < std::max<int64_t>(nseg, 1); ++sgi) {
+            wicca::JpegSegDev sg;
+            const int64_t b0 = sgi < (int64_t)off.size() - 1 ? off[(size_t)sgi] : (int64_t)bytes.size();
+            const int64_t b1 = sgi + 1 < (int64_t)off.size() ? off[(size_t)sgi + 1] : (int64_t)bytes.size();
+            sg.bit0 = (base + b0) * 8;
+            sg.bits = (b1 - b0) * 8;
+            sg.block0 = sgi * ri * f.bpm;
+            sg.block_end = std::min(mcus, (sgi + 1) * ri) * f.bpm;
+            sg.img = (int32_t)i;
+            sg.sub0 = (int32_t)sub_seg.size();
+            const int64_t nsub = std::max<int64_t>(1, (sg.bits + S - 1) / S);
+            for (int64_t k = 0; k < nsub; ++k) sub_seg.push_back((int32_t)segs.size());
+            segs.push_back(sg);
+        }
+    }
+    stream_h.resize(stream_h.size() + 16, 0);  // the bit reader reads ahead
+    if (sub_seg.size() >= (size_t)INT32_MAX) return fail(WICCA_ERR_ARG, "JPEG batch too large");
+    // device buffers: [stream | segs | sub_seg | imgs | huff] in jmeta
+    const size_t o_seg = (size_t)round_up((int64_t)stream_h.size(), 256);
+    const size_t o_sub = o_seg + (size_t)round_up((int64_t)(segs.size() * sizeof(wicca::JpegSegDev)), 256);
+    const size_t o_img = o_sub + (size_t)round_up((int64_t)(sub_seg.size() * sizeof(int32_t)), 256);
+    const size_t o_huf = o_img + (size_t)round_up((int64_t)(ims.size() * sizeof(wicca::JpegImageDev)), 256);
+    const size_t meta_bytes = o_huf + huff.size() * sizeof(wicca::HuffDev);
+    HIP_TRY(ws->jmeta.reserve(meta_bytes));
+    HIP_TRY(ws->jcoef.reserve((size_t)coef_blocks * 128));
+    HIP_TRY(ws->jplanes.reserve((size_t)plane_bytes));
+    HIP_TRY(ws->jscratch.reserve(wicca::jpeg_scratch_bytes((int64_t)sub_seg.size(), (int64_t)segs.size())));
+    if (tmp_bytes) HIP_TRY(ws->jtmp.reserve((size_t)tmp_bytes));
+    for (int64_t i = 0; i < n; ++i)
+        if (tmp_off[(size_t)i] >= 0) ims[(size_t)i].dst = (uint8_t*)ws->jtmp.ptr + tmp_off[(size_t)i];
+    uint8_t* m = (uint8_t*)ws->jmeta.ptr;
+    std::vector<uint8_t> packed(meta_bytes, 0);
+    memcpy(packed.data(), stream_h.data(), stream_h.size());
+    memcpy(packed.data() + o_seg, segs.data(), segs.size() * sizeof(wicca::JpegSegDev));
+    memcpy(packed.data() + o_sub, sub_seg.data(), sub_seg.size() * sizeof(int32_t));
+    memcpy(packed.data() + o_img, ims.data(), ims.size() * sizeof(wicca::JpegImageDev));
+    memcpy(packed.data() + o_huf, huff.data(), huff.size() * sizeof(wicca::HuffDev));
+    HIP_TRY(hipMemcpyAsync(m, packed.data(), meta_bytes, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemsetAsync(ws->jcoef.ptr, 0, (size_t)coef_blocks * 128, stream));
+    wicca::JpegPlan P{};
+    P.stream = m;
+    P.segs = (const wicca::JpegSegDev*)(m + o_seg);
+    P.sub_seg = (const int32_t*)(m + o_sub);
+    P.imgs = (const wicca::JpegImageDev*)(m + o_img);
+    P.huff = (const wicca::HuffDev*)(m + o_huf);
+    P.coef = (int16_t*)ws->jcoef.ptr;
+    P.planes = (uint8_t*)ws->jplanes.ptr;
+    P.n_sub = (int64_t)sub_seg.size();
+    P.n_seg = (int64_t)segs.size();
+    P.sub_bits = S;
+    int rounds = 0;
+    HIP_TRY(wicca::jpeg_decode_device(P, ims.data(), ws->jscratch.ptr, n, &rounds, stream));
+    if (rounds_out) *rounds_out = rounds;
+    for (int64_t i = 0; i < n; ++i)
+        if (tmp_off[(size_t)i] >= 0)
+            HIP_TRY(wicca::launch_orient(ims[(size_t)i].dst, ims[(size_t)i].dst_pitch, info[(size_t)i].W,
+                                         info[(size_t)i].H, info[(size_t)i].orientation, dst[i], dpitch[i],
+                                         stream));
+    // packed / stream_h are host copies consumed by the synchronous upload above
+    HIP_TRY(hipStreamSynchronize(stream));
+    return WICCA_OK;
+}
+
+thread_local int t_jpeg_rounds = 0;
+
+}  // namespace
+
+extern "C" {
+
+int wicca_jpeg_info(const uint8_t* data, int64_t size, int apply_orientation, int64_t* height, int64_t* width,
+                    int* components, int* orientation)
+{
+    wicca::JpegInfo f;
+    int rc = parse_one(data, size, &f, 0);
+    if (rc) return rc;
+    if (height && width) oriented_dims(f, apply_orientation != 0, height, width);
+    if (components) *components = f.ncomp;
+    if (orientation) *orientation = f.orientation;
+    return WICCA_OK;
+}
+
+int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, uint8_t* const* dsts,
+                         const int64_t* dst_pitches, int apply_orientation, int dst_is_device, int device,
+                         void* stream_in)
+{
+    if (n < 0 || (n > 0 && (!data || !sizes || !dsts || !dst_pitches))) return fail(WICCA_ERR_ARG, "bad arrays");
+    if (n == 0) return WICCA_OK;
+    std::vector<int64_t> oh((size_t)n), ow((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        wicca::JpegInfo f;
+        int rc = parse_one(data[i], sizes[i], &f, i);
+        if (rc) return rc;
+        oriented_dims(f, apply_orientation != 0, &oh[i], &ow[i]);
+        if (!dsts[i] || dst_pitches[i] < ow[i] * 3) return fail(WICCA_ERR_ARG, "bad output %lld", (long long)i);
+    }
+    DeviceGuard dg;
+    int dev, rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    Workspace* ws = lease.ws;
+    hipStream_t stream = stream_in ? (hipStream_t)stream_in : ws->stream;
+    std::vector<uint8_t*> d((size_t)n);
+    std::vector<int64_t> p((size_t)n);
+    int64_t off = 0;
+    if (!dst_is_device) {
+        int64_t total = 0;
+        for (int64_t i = 0; i < n; ++i) total += round_up(ow[i] * 3, 128) * oh[i];
+        HIP_TRY(ws->jrgb.reserve((size_t)total));
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        if (dst_is_device) {
+            d[(size_t)i] = dsts[i];
+            p[(size_t)i] = dst_pitches[i];
+        } else {
+            d[(size_t)i] = (uint8_t*)ws->jrgb.ptr + off;
+            p[(size_t)i] = round_up(ow[i] * 3, 128);
+            off += p[(size_t)i] * oh[i];
+        }
+    }
+    if ((rc = jpeg_decode_to_device(ws, data, sizes, n, d.data(), p.data(), apply_orientation != 0, stream,
+                                    &t_jpeg_rounds)))
+        return rc;
+    if (!dst_is_device) {
+        for (int64_t i = 0; i < n; ++i)
+            HIP_TRY(hipMemcpy2DAsync(dsts[i], dst_pitches[i], d[(size_t)i], p[(size_t)i], ow[i] * 3, oh[i],
+                                     hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+    }
+    return WICCA_OK;
+}
+
+int wicca_jpeg_last_sync_rounds(void) { return t_jpeg_rounds; }
+
+int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
+                             int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                             int interpolation, uint8_t* resized, uint8_t* resized_icons, int device)
+{
+    if (n < 0 || (n > 0 && (!data || !sizes))) return fail(WICCA_ERR_ARG, "bad arrays");
+    if (n == 0) return WICCA_OK;
+    if (!resized || !resized_icons) return fail(WICCA_ERR_ARG, "output buffer is NULL");
+    std::vector<int64_t> H((size_t)n), W((size_t)n), ih((size_t)n), iw((size_t)n);
+    int64_t max_icon = 0, rgb_total = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        wicca::JpegInfo f;
+        int rc = parse_one(data[i], sizes[i], &f, i);
+        if (rc) return rc;
+        oriented_dims(f, true, &H[i], &W[i]);
+        if ((rc = check_image((const uint8_t*)1, H[i], W[i], 3, W[i] * 3, depth, border_type))) return rc;
+        wicca::ResizeParams probe{};
+        if ((rc = check_resize(H[i], W[i], 3, out_w, out_h, interpolation, &probe))) return rc;
+        icon_dims(H[i], W[i], depth, &ih[i], &iw[i]);
+        if ((rc = check_resize(ih[i], iw[i], 3, out_w, out_h, interpolation, &probe))) return rc;
+        max_icon = std::max(max_icon, round_up(iw[i] * 3, 16) * ih[i]);
+        rgb_total += round_up(W[i] * 3, kStagePitch) * H[i];
+    }
+    DeviceGuard dg;
+    int dev, rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    Workspace* ws = lease.ws;
+    hipStream_t cs = ws->stream;
+    HIP_TRY(ws->jrgb.reserve((size_t)rgb_total));
+    HIP_TRY(ws->icon[0].reserve((size_t)max_icon));
+    const int64_t out_bytes = out_w * out_h * 3;
+    HIP_TRY(ws->out.reserve((size_t)(2 * n * out_bytes)));
+    std::vector<uint8_t*> d((size_t)n);
+    std::vector<int64_t> p((size_t)n);
+    int64_t off = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        d[(size_t)i] = (uint8_t*)ws->jrgb.ptr + off;
+        p[(size_t)i] = round_up(W[i] * 3, kStagePitch);
+        off += p[(size_t)i] * H[i];
+    }
+    // data_loader.py:53-58  cv2.imread + BGR2RGB, on the GPU (+ EXIF orientation)
+    if ((rc = jpeg_decode_to_device(ws, data, sizes, n, d.data(), p.data(), true, cs, &t_jpeg_rounds))) return rc;
+    uint8_t* dres = (uint8_t*)ws->out.ptr;
+    uint8_t* dico = dres + n * out_bytes;
+    uint8_t* ico = (uint8_t*)ws->icon[0].ptr;
+    for (int64_t i = 0; i < n; ++i) {
+        // classifying_tools.py:315, :317, :318
+        wicca::ResizeParams rp{};
+        wicca::plan_resize((int)H[i], (int)W[i], (int)out_h, (int)out_w, 3, interpolation, &rp);
+        if ((rc = run_resize(rp, d[(size_t)i], p[(size_t)i], 0, dres + i * out_bytes, out_w * 3, 0, 1, cs)))
+            return rc;
+        const int64_t ip = round_up(iw[i] * 3, 16);
+        bool scratch = false;
+        if ((rc = run_ll<uint8_t>(d[(size_t)i], 1, H[i], W[i], 3, p[(size_t)i], 0, depth, border_type,
+                                  border_constant, ico, ip, 0, ws, cs, &scratch)))
+            return rc;
+        wicca::ResizeParams ri{};
+        wicca::plan_resize((int)ih[i], (int)iw[i], (int)out_h, (int)out_w, 3, interpolation, &ri);
+        if ((rc = run_resize(ri, ico, ip, 0, dico + i * out_bytes, out_w * 3, 0, 1, cs))) return rc;
+    }
     HIP_TRY(hipMemcpyAsync(resized, dres, (size_t)(n * out_bytes), hipMemcpyDeviceToHost, cs));
     HIP_TRY(hipMemcpyAsync(resized_icons, dico, (size_t)(n * out_bytes), hipMemcpyDeviceToHost, cs));
     HIP_TRY(hipStreamSynchronize(cs));

@@ -1,0 +1,122 @@
+// jpeg.h — baseline JPEG decode on gfx950: host-side
+// stream description (jpeg_host.cpp) and the device decode plan (jpeg.hip).
+//
+// The reference decodes every file with cv2.imread + cv2.cvtColor(BGR2RGB)
+// (wicca/data_loader.py:31-63), i.e. libjpeg-turbo with its defaults: ISLOW
+// integer IDCT (jidctint.c), fancy upsampling (jdsample.c), integer YCbCr ->
+// RGB tables (jdcolor.c).  This engine restates that arithmetic on the GPU:
+//   host    marker parse (SOF0/SOF1, DQT, DHT, DRI, SOS), byte de-stuffing and
+//           restart-segment split of the entropy-coded data,
+//   device  self-synchronising parallel Huffman decode over fixed-size
+//           subsequences of each segment, segmented prefix sums of block
+//           counts and DC differences, coefficient scatter, ISLOW IDCT, fancy
+//           upsampling fused with the colour conversion, RGB HWC output.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace wicca {
+
+constexpr int kJpegMaxComp = 3;
+constexpr int kJpegMaxSlots = 10;  // blocks per MCU (baseline limit)
+
+struct JpegHuffTable {
+    uint8_t bits[17];  // bits[l] = number of codes of length l (1..16)
+    uint8_t vals[256];
+    int nvals;
+};
+
+struct JpegComponent {
+    int id, h, v, tq, td, ta;
+    int bw, bh;          // blocks per row / column (padded to whole MCUs)
+    int dw, dh;          // downsampled (real) sample width / height
+};
+
+struct JpegInfo {
+    int W = 0, H = 0, ncomp = 0;
+    JpegComponent comp[kJpegMaxComp];
+    int hmax = 1, vmax = 1, mcux = 0, mcuy = 0, bpm = 0;
+    int slot_comp[kJpegMaxSlots], slot_h[kJpegMaxSlots], slot_v[kJpegMaxSlots];
+    uint16_t qt[4][64];  // natural order
+    bool qt_present[4] = {false, false, false, false};
+    JpegHuffTable dc[4], ac[4];
+    bool dc_present[4] = {false, false, false, false}, ac_present[4] = {false, false, false, false};
+    int restart_interval = 0;   // MCUs per restart segment (0: one segment)
+    int orientation = 1;        // EXIF orientation tag (1 = as stored)
+    const uint8_t* scan = nullptr;  // entropy-coded data (stuffed, with RST markers)
+    size_t scan_len = 0;
+    int64_t total_blocks() const { return (int64_t)mcux * mcuy * bpm; }
+};
+
+// Parse up to the first SOS.  Returns 0 or a negative code with *err set:
+// -1 not a JPEG / truncated, -2 unsupported (progressive, arithmetic coding,
+// 12-bit, CMYK, non-interleaved multi-scan, unusual sampling).
+int jpeg_parse(const uint8_t* data, size_t size, JpegInfo* info, std::string* err);
+
+// Remove byte stuffing (FF 00 -> FF) and split at RSTn markers: `out` gets the
+// de-stuffed bytes of every restart segment back to back; seg_off[s] is the
+// first byte of segment s (seg_off.back() = out.size()).
+void jpeg_destuff(const JpegInfo& info, std::vector<uint8_t>& out, std::vector<int64_t>& seg_off);
+
+// ---------------------------------------------------------------------------
+// Device plan (built on the host, uploaded once per decode call).
+// ---------------------------------------------------------------------------
+constexpr int kHuffLutBits = 9;
+
+struct HuffDev {
+    uint16_t lut[1 << kHuffLutBits];  // (len << 8) | symbol for codes <= 9 bits, 0 = longer
+    int32_t maxcode[18];              // largest code of length l, -1 if none (maxcode[17] sentinel)
+    int32_t valoff[18];               // vals index of the first code of length l, minus that code
+    uint8_t vals[256];
+};
+
+struct JpegImageDev {
+    int32_t W, H, ncomp, bpm, mcux, hmax, vmax;
+    int32_t slot_comp[kJpegMaxSlots], slot_h[kJpegMaxSlots], slot_v[kJpegMaxSlots];
+    int32_t comp_h[kJpegMaxComp], comp_v[kJpegMaxComp], comp_bw[kJpegMaxComp], comp_bh[kJpegMaxComp];
+    int32_t comp_dw[kJpegMaxComp], comp_dh[kJpegMaxComp];
+    int32_t dc_tab[kJpegMaxComp], ac_tab[kJpegMaxComp];  // indices into the HuffDev array
+    int64_t comp_block0[kJpegMaxComp];  // first block of the component in the coefficient array
+    int64_t comp_plane0[kJpegMaxComp];  // first byte of the component's sample plane
+    uint16_t qt[kJpegMaxComp][64];      // natural order, per component
+    uint8_t* dst;                       // RGB HWC output
+    int64_t dst_pitch;
+};
+
+struct JpegSegDev {
+    int64_t bit0, bits;        // de-stuffed bit range of the segment
+    int64_t block0, block_end; // image-local decode-order block range
+    int32_t img, sub0;         // image; first subsequence of the segment
+};
+
+struct JpegPlan {
+    const uint8_t* stream;   // de-stuffed bytes of every segment (+ 8 zero bytes)
+    const JpegSegDev* segs;
+    const int32_t* sub_seg;  // subsequence -> segment
+    const JpegImageDev* imgs;
+    const HuffDev* huff;
+    int16_t* coef;           // (total blocks) x 64, natural order
+    uint8_t* planes;         // component sample planes
+    int64_t n_sub, n_seg;
+    int32_t sub_bits;        // subsequence length
+};
+
+// Decode every image of the plan into its dst (RGB, HWC uint8).  `ims` is the
+// host copy of plan.imgs; scratch holds the per-subsequence states (see
+// jpeg_scratch_bytes).  *sync_rounds receives the synchronisation passes run.
+constexpr int kJpegMaxJobs = 4096;  // (image, component) pairs per call
+size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg);
+hipError_t jpeg_decode_device(const JpegPlan& plan, const JpegImageDev* ims, void* scratch, int64_t n_images,
+                              int* sync_rounds, hipStream_t s);
+
+// RGB image (W x H) -> its EXIF-oriented copy (orientation 1..8; 5-8 swap W/H).
+hipError_t launch_orient(const uint8_t* src, int64_t sp, int W, int H, int orient, uint8_t* dst, int64_t dp,
+                         hipStream_t s);
+
+void build_huff_dev(const JpegHuffTable& t, HuffDev* d);
+
+}  // namespace wicca

@@ -1,0 +1,649 @@
+// jpeg.hip — device half of the baseline JPEG decoder.
+//
+// Restates libjpeg-turbo's decode with its defaults, as cv2.imread runs it for
+// the reference (wicca/data_loader.py:53; opencv-python bundles libjpeg-turbo):
+//   Huffman decode   jdhuff.c semantics (DC differences per component, reset
+//                    at every restart marker; AC run/size symbols, ZRL, EOB)
+//   IDCT             jidctint.c jpeg_idct_islow (13-bit constants, PASS1_BITS
+//                    2, DESCALE rounding, the wrapping range-limit table)
+//   upsampling       jdsample.c h2v1 / h2v2 "fancy" triangle filters (plain
+//                    replication when the downsampled width is <= 2), edge
+//                    rows duplicated as jdmainct.c does
+//   colour           jdcolor.c ycc_rgb_convert integer tables (SCALEBITS 16)
+// Output is RGB, i.e. cv2.imread's BGR after the reference's cv2.cvtColor
+// (data_loader.py:58).  tests/test_gpu_jpeg.py checks it bit for bit against
+// Pillow 12.2.0's libjpeg-turbo 3.1.4.1 decode.
+//
+// Parallel Huffman decoding: every restart segment is cut into subsequences
+// of `sub_bits` bits, one lane each.  A lane decodes codewords that START in
+// its subsequence, from a start state (bit position, MCU slot, coefficient
+// index).  Pass 0 guesses the state at each subsequence start; then each pass
+// restarts lane i from lane i-1's end state of the previous pass until no end
+// state changes (Huffman codes resynchronise within a few codewords, so 1-3
+// passes suffice in practice; every pass fixes at least one more lane, so the
+// loop always ends).  The converged pass also yields per-lane counts of blocks
+// started and per-component DC difference sums; segmented exclusive scans of
+// those give every lane its first block index and DC predictors, and a final
+// pass scatters the coefficients.  Blocks past a segment's MCU count (the
+// decode of its padding bits) are never written.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "jpeg.h"
+
+namespace wicca {
+
+namespace {
+
+constexpr int kJThreads = 64;  // one wave per workgroup: lanes run independent decodes
+
+__constant__ int kNatural[80] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                                 12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                                 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                                 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63,
+                                 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+
+struct DecState {
+    int64_t p;  // bit position of the next codeword
+    int32_t slot, k;
+};
+
+struct SubResult {
+    DecState end;
+    int64_t started;  // blocks whose DC codeword starts in the lane's range
+    int32_t dc[kJpegMaxComp];
+    int32_t pad_;
+};
+
+// MSB-first bit reader over the de-stuffed stream (bytes past the end read 0:
+// the host pads the stream with zero bytes).
+struct BitReader {
+    const uint8_t* s;
+    int64_t p, nb;
+    uint64_t buf;
+    int n;
+    __device__ void reset(const uint8_t* stream, int64_t bitpos)
+    {
+        s = stream;
+        p = bitpos;
+        nb = bitpos >> 3;
+        buf = 0;
+        n = 0;
+        fill();
+        const int skip = (int)(bitpos & 7);
+        buf <<= skip;
+        n -= skip;
+    }
+    __device__ void fill()
+    {
+        while (n <= 56) {
+            buf |= (uint64_t)s[nb++] << (56 - n);
+            n += 8;
+        }
+    }
+    __device__ uint32_t peek16()
+    {
+        if (n < 16) fill();
+        return (uint32_t)(buf >> 48);
+    }
+    __device__ void skip(int k)
+    {
+        buf <<= k;
+        n -= k;
+        p += k;
+    }
+    __device__ uint32_t get(int k)
+    {
+        if (k == 0) return 0;
+        if (n < k) fill();
+        const uint32_t v = (uint32_t)(buf >> (64 - k));
+        skip(k);
+        return v;
+    }
+};
+
+__device__ __forceinline__ int huff_decode(const HuffDev& t, BitReader& br)
+{
+    const uint32_t look = br.peek16();
+    const uint32_t e = t.lut[look >> (16 - kHuffLutBits)];
+    if (e) {
+        br.skip((int)(e >> 8));
+        return (int)(e & 255);
+    }
+    int l = kHuffLutBits + 1;
+    int32_t code = (int32_t)(look >> (16 - l));
+    while (l <= 16 && code > t.maxcode[l]) {
+        ++l;
+        code = (int32_t)(look >> (16 - l));
+    }
+    if (l > 16) {  // not a code (only off the true decode path): jdhuff returns 0
+        br.skip(16);
+        return 0;
+    }
+    br.skip(l);
+    return t.vals[(t.valoff[l] + code) & 255];
+}
+
+// HUFF_EXTEND (jdhuff.h)
+__device__ __forceinline__ int extend(uint32_t v, int s)
+{
+    return (int)v < (1 << (s - 1)) ? (int)v - (1 << s) + 1 : (int)v;
+}
+
+// Coefficient-array index of decode-order block g of an image.
+__device__ __forceinline__ int64_t block_index(const JpegImageDev& im, int64_t g)
+{
+    const int64_t mcu = g / im.bpm;
+    const int slot = (int)(g - mcu * im.bpm);
+    const int c = im.slot_comp[slot];
+    const int64_t mx = mcu % im.mcux, my = mcu / im.mcux;
+    const int64_t bx = mx * im.comp_h[c] + im.slot_h[slot];
+    const int64_t by = my * im.comp_v[c] + im.slot_v[slot];
+    return im.comp_block0[c] + by * im.comp_bw[c] + bx;
+}
+
+// Decode the codewords that start in [state.p, stop).  WRITE: scatter
+// coefficients of blocks [g0, block_end) (g = decode-order block index of the
+// block in progress), absolute DC values from the running predictors `pred`.
+template <bool WRITE>
+__device__ void decode_run(const JpegImageDev& im, const HuffDev* tabs, BitReader& br, int64_t stop,
+                           DecState& st, int64_t& started, int32_t (&dc)[kJpegMaxComp], int64_t g,
+                           int64_t block_lo, int64_t block_end, int16_t* coef)
+{
+    int64_t blk = -1;
+    if (WRITE && g >= block_lo && g < block_end) blk = block_index(im, g);
+    while (br.p < stop) {
+        const int c = im.slot_comp[st.slot];
+        if (st.k == 0) {
+            const int s = min(huff_decode(tabs[im.dc_tab[c]], br), 16);  // > 11 only in corrupt streams
+            const int diff = s ? extend(br.get(s), s) : 0;
+            ++started;
+            dc[c] += diff;
+            if (WRITE) {
+                ++g;
+                blk = (g >= block_lo && g < block_end) ? block_index(im, g) : -1;
+                if (blk >= 0) coef[blk * 64] = (int16_t)dc[c];
+            }
+            st.k = 1;
+        } else {
+            const int rs = huff_decode(tabs[im.ac_tab[c]], br);
+            const int r = rs >> 4, s = rs & 15;
+            if (s) {
+                st.k += r;
+                const int v = extend(br.get(s), s);
+                if (WRITE && blk >= 0 && st.k < 64) coef[blk * 64 + kNatural[st.k]] = (int16_t)v;
+                ++st.k;
+            } else if (r == 15) {
+                st.k += 16;
+            } else {
+                st.k = 64;  // EOB
+            }
+        }
+        if (st.k >= 64) {
+            st.slot = st.slot + 1 == im.bpm ? 0 : st.slot + 1;
+            st.k = 0;
+        }
+    }
+    st.p = br.p;
+}
+
+// Pass over every subsequence.  round 0: start from the guessed state at the
+// subsequence start; round > 0: from the previous round's end state of the
+// previous subsequence (the segment's first subsequence starts exactly).
+__global__ __launch_bounds__(kJThreads) void jpeg_sync_kernel(JpegPlan P, const SubResult* prev,
+                                                             SubResult* next, int round, int* changed)
+{
+    const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
+    if (i >= P.n_sub) return;
+    const JpegSegDev sg = P.segs[P.sub_seg[i]];
+    const int64_t j = i - sg.sub0;  // index inside the segment
+    const int64_t b0 = sg.bit0 + j * P.sub_bits;
+    const int64_t b1 = min(sg.bit0 + (j + 1) * P.sub_bits, sg.bit0 + sg.bits);
+    const JpegImageDev& im = P.imgs[sg.img];
+    DecState st;
+    if (j == 0 || round == 0) {  // exact at a segment start, a guess elsewhere in round 0
+        st.p = b0;
+        st.slot = 0;
+        st.k = 0;
+    } else {
+        st = prev[i - 1].end;
+    }
+    SubResult r;
+    r.started = 0;
+    r.pad_ = 0;
+    int32_t dc[kJpegMaxComp] = {0, 0, 0};
+    BitReader br;
+    br.reset(P.stream, st.p);
+    decode_run<false>(im, P.huff, br, b1, st, r.started, dc, 0, 0, 0, nullptr);
+    r.end = st;
+    for (int c = 0; c < kJpegMaxComp; ++c) r.dc[c] = dc[c];
+    if (round > 0) {
+        const DecState& o = prev[i].end;
+        if (o.p != st.p || o.slot != st.slot || o.k != st.k) *changed = 1;
+    }
+    next[i] = r;
+}
+
+// Segmented exclusive scan of (blocks started, DC sums) over each segment's
+// subsequences: one workgroup of 256 lanes per segment.
+struct SubBase {
+    int64_t block;
+    int32_t dc[kJpegMaxComp];
+    int32_t pad_;
+};
+
+__global__ __launch_bounds__(256) void jpeg_scan_kernel(JpegPlan P, const SubResult* res, SubBase* base)
+{
+    const JpegSegDev sg = P.segs[blockIdx.x];
+    const int64_t n = (blockIdx.x + 1 < P.n_seg) ? P.segs[blockIdx.x + 1].sub0 - sg.sub0 : P.n_sub - sg.sub0;
+    __shared__ int64_t sb[256];
+    __shared__ int32_t sd[kJpegMaxComp][256];
+    __shared__ int64_t carry_b;
+    __shared__ int32_t carry_d[kJpegMaxComp];
+    const int t = threadIdx.x;
+    if (t == 0) {
+        carry_b = 0;
+        for (int c = 0; c < kJpegMaxComp; ++c) carry_d[c] = 0;
+    }
+    __syncthreads();
+    for (int64_t c0 = 0; c0 < n; c0 += 256) {
+        const int64_t i = c0 + t;
+        int64_t vb = 0;
+        int32_t vd[kJpegMaxComp] = {0, 0, 0};
+        if (i < n) {
+            const SubResult& r = res[sg.sub0 + i];
+            vb = r.started;
+            for (int c = 0; c < kJpegMaxComp; ++c) vd[c] = r.dc[c];
+        }
+        sb[t] = vb;
+        for (int c = 0; c < kJpegMaxComp; ++c) sd[c][t] = vd[c];
+        __syncthreads();
+        for (int off = 1; off < 256; off <<= 1) {  // Hillis-Steele inclusive scan
+            int64_t ab = 0;
+            int32_t ad[kJpegMaxComp] = {0, 0, 0};
+            if (t >= off) {
+                ab = sb[t - off];
+                for (int c = 0; c < kJpegMaxComp; ++c) ad[c] = sd[c][t - off];
+            }
+            __syncthreads();
+            sb[t] += ab;
+            for (int c = 0; c < kJpegMaxComp; ++c) sd[c][t] += ad[c];
+            __syncthreads();
+        }
+        if (i < n) {
+            SubBase b;
+            b.block = carry_b + sb[t] - vb;  // exclusive
+            for (int c = 0; c < kJpegMaxComp; ++c) b.dc[c] = carry_d[c] + sd[c][t] - vd[c];
+            b.pad_ = 0;
+            base[sg.sub0 + i] = b;
+        }
+        __syncthreads();
+        if (t == 255) {
+            carry_b += sb[255];
+            for (int c = 0; c < kJpegMaxComp; ++c) carry_d[c] += sd[c][255];
+        }
+        __syncthreads();
+    }
+}
+
+// Final pass: scatter coefficients (converged start states, scanned bases).
+__global__ __launch_bounds__(kJThreads) void jpeg_write_kernel(JpegPlan P, const SubResult* res,
+                                                              const SubBase* base)
+{
+    const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
+    if (i >= P.n_sub) return;
+    const JpegSegDev sg = P.segs[P.sub_seg[i]];
+    const int64_t j = i - sg.sub0;
+    const int64_t b1 = min(sg.bit0 + (j + 1) * P.sub_bits, sg.bit0 + sg.bits);
+    const JpegImageDev& im = P.imgs[sg.img];
+    DecState st;
+    if (j == 0) {
+        st.p = sg.bit0;
+        st.slot = 0;
+        st.k = 0;
+    } else {
+        st = res[i - 1].end;
+    }
+    const SubBase b = base[i];
+    int32_t dc[kJpegMaxComp] = {b.dc[0], b.dc[1], b.dc[2]};
+    int64_t started = 0;
+    BitReader br;
+    br.reset(P.stream, st.p);
+    // the block in progress at the start was started by an earlier lane
+    decode_run<true>(im, P.huff, br, b1, st, started, dc, sg.block0 + b.block - 1, sg.block0,
+                     sg.block_end, P.coef);
+}
+
+// ---------------------------------------------------------------------------
+// ISLOW IDCT (jidctint.c) — one lane per 8x8 block of one component.
+// ---------------------------------------------------------------------------
+struct IdctJob {
+    int64_t block0, plane0;
+    int32_t bw, bh, img, comp;
+};
+
+#define FIX_0_298631336 ((int64_t)2446)
+#define FIX_0_390180644 ((int64_t)3196)
+#define FIX_0_541196100 ((int64_t)4433)
+#define FIX_0_765366865 ((int64_t)6270)
+#define FIX_0_899976223 ((int64_t)7373)
+#define FIX_1_175875602 ((int64_t)9633)
+#define FIX_1_501321110 ((int64_t)12299)
+#define FIX_1_847759065 ((int64_t)15137)
+#define FIX_1_961570560 ((int64_t)16069)
+#define FIX_2_053119869 ((int64_t)16819)
+#define FIX_2_562915447 ((int64_t)20995)
+#define FIX_3_072711026 ((int64_t)25172)
+constexpr int kConstBits = 13, kPass1Bits = 2;
+
+__device__ __forceinline__ int64_t descale(int64_t x, int n) { return (x + ((int64_t)1 << (n - 1))) >> n; }
+
+// idct_sample_range_limit[x & 1023] of jdmaster.c's prepare_range_limit_table
+__device__ __forceinline__ uint8_t idct_limit(int64_t v)
+{
+    const int x = (int)(v & 1023);
+    return (uint8_t)(x < 128 ? x + 128 : x < 512 ? 255 : x < 896 ? 0 : x - 896);
+}
+
+__global__ __launch_bounds__(256) void jpeg_idct_kernel(JpegPlan P, const IdctJob* jobs)
+{
+    const IdctJob jb = jobs[blockIdx.y];
+    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b >= (int64_t)jb.bw * jb.bh) return;
+    const int by = (int)(b / jb.bw), bx = (int)(b - (int64_t)by * jb.bw);
+    const int16_t* in = P.coef + (jb.block0 + b) * 64;
+    const uint16_t* q = P.imgs[jb.img].qt[jb.comp];
+    int ws[64];
+    int16_t cf[64];
+#pragma unroll
+    for (int i = 0; i < 64; i += 8) {
+        const uint4 v = *reinterpret_cast<const uint4*>(in + i);
+        cf[i + 0] = (int16_t)(v.x & 0xFFFF); cf[i + 1] = (int16_t)(v.x >> 16);
+        cf[i + 2] = (int16_t)(v.y & 0xFFFF); cf[i + 3] = (int16_t)(v.y >> 16);
+        cf[i + 4] = (int16_t)(v.z & 0xFFFF); cf[i + 5] = (int16_t)(v.z >> 16);
+        cf[i + 6] = (int16_t)(v.w & 0xFFFF); cf[i + 7] = (int16_t)(v.w >> 16);
+    }
+    // pass 1: columns
+#pragma unroll
+    for (int col = 0; col < 8; ++col) {
+        auto dq = [&](int row) -> int64_t { return (int64_t)cf[row * 8 + col] * (int64_t)q[row * 8 + col]; };
+        if (cf[8 + col] == 0 && cf[16 + col] == 0 && cf[24 + col] == 0 && cf[32 + col] == 0 &&
+            cf[40 + col] == 0 && cf[48 + col] == 0 && cf[56 + col] == 0) {
+            const int dcval = (int)(dq(0) * (1 << kPass1Bits));
+#pragma unroll
+            for (int r = 0; r < 8; ++r) ws[r * 8 + col] = dcval;
+            continue;
+        }
+        int64_t z2 = dq(2), z3 = dq(6);
+        int64_t z1 = (z2 + z3) * FIX_0_541196100;
+        int64_t tmp2 = z1 + z3 * (-FIX_1_847759065);
+        int64_t tmp3 = z1 + z2 * FIX_0_765366865;
+        z2 = dq(0);
+        z3 = dq(4);
+        int64_t tmp0 = (z2 + z3) * ((int64_t)1 << kConstBits);
+        int64_t tmp1 = (z2 - z3) * ((int64_t)1 << kConstBits);
+        const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+        tmp0 = dq(7);
+        tmp1 = dq(5);
+        tmp2 = dq(3);
+        tmp3 = dq(1);
+        z1 = tmp0 + tmp3;
+        z2 = tmp1 + tmp2;
+        z3 = tmp0 + tmp2;
+        int64_t z4 = tmp1 + tmp3;
+        const int64_t z5 = (z3 + z4) * FIX_1_175875602;
+        tmp0 = tmp0 * FIX_0_298631336;
+        tmp1 = tmp1 * FIX_2_053119869;
+        tmp2 = tmp2 * FIX_3_072711026;
+        tmp3 = tmp3 * FIX_1_501321110;
+        z1 = z1 * (-FIX_0_899976223);
+        z2 = z2 * (-FIX_2_562915447);
+        z3 = z3 * (-FIX_1_961570560);
+        z4 = z4 * (-FIX_0_390180644);
+        z3 += z5;
+        z4 += z5;
+        tmp0 += z1 + z3;
+        tmp1 += z2 + z4;
+        tmp2 += z2 + z3;
+        tmp3 += z1 + z4;
+        constexpr int sh = kConstBits - kPass1Bits;
+        ws[0 * 8 + col] = (int)descale(tmp10 + tmp3, sh);
+        ws[7 * 8 + col] = (int)descale(tmp10 - tmp3, sh);
+        ws[1 * 8 + col] = (int)descale(tmp11 + tmp2, sh);
+        ws[6 * 8 + col] = (int)descale(tmp11 - tmp2, sh);
+        ws[2 * 8 + col] = (int)descale(tmp12 + tmp1, sh);
+        ws[5 * 8 + col] = (int)descale(tmp12 - tmp1, sh);
+        ws[3 * 8 + col] = (int)descale(tmp13 + tmp0, sh);
+        ws[4 * 8 + col] = (int)descale(tmp13 - tmp0, sh);
+    }
+    // pass 2: rows -> samples
+    const int64_t pitch = (int64_t)jb.bw * 8;
+    uint8_t* out = P.planes + jb.plane0 + ((int64_t)by * 8) * pitch + (int64_t)bx * 8;
+#pragma unroll
+    for (int row = 0; row < 8; ++row) {
+        const int* w = ws + row * 8;
+        uint8_t o[8];
+        constexpr int sh = kConstBits + kPass1Bits + 3;
+        if (w[1] == 0 && w[2] == 0 && w[3] == 0 && w[4] == 0 && w[5] == 0 && w[6] == 0 && w[7] == 0) {
+            const uint8_t v = idct_limit(descale((int64_t)w[0], kPass1Bits + 3));
+#pragma unroll
+            for (int c = 0; c < 8; ++c) o[c] = v;
+        } else {
+            int64_t z2 = w[2], z3 = w[6];
+            int64_t z1 = (z2 + z3) * FIX_0_541196100;
+            int64_t tmp2 = z1 + z3 * (-FIX_1_847759065);
+            int64_t tmp3 = z1 + z2 * FIX_0_765366865;
+            int64_t tmp0 = ((int64_t)w[0] + (int64_t)w[4]) * ((int64_t)1 << kConstBits);
+            int64_t tmp1 = ((int64_t)w[0] - (int64_t)w[4]) * ((int64_t)1 << kConstBits);
+            const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+            tmp0 = w[7];
+            tmp1 = w[5];
+            tmp2 = w[3];
+            tmp3 = w[1];
+            z1 = tmp0 + tmp3;
+            z2 = tmp1 + tmp2;
+            z3 = tmp0 + tmp2;
+            int64_t z4 = tmp1 + tmp3;
+            const int64_t z5 = (z3 + z4) * FIX_1_175875602;
+            tmp0 = tmp0 * FIX_0_298631336;
+            tmp1 = tmp1 * FIX_2_053119869;
+            tmp2 = tmp2 * FIX_3_072711026;
+            tmp3 = tmp3 * FIX_1_501321110;
+            z1 = z1 * (-FIX_0_899976223);
+            z2 = z2 * (-FIX_2_562915447);
+            z3 = z3 * (-FIX_1_961570560);
+            z4 = z4 * (-FIX_0_390180644);
+            z3 += z5;
+            z4 += z5;
+            tmp0 += z1 + z3;
+            tmp1 += z2 + z4;
+            tmp2 += z2 + z3;
+            tmp3 += z1 + z4;
+            o[0] = idct_limit(descale(tmp10 + tmp3, sh));
+            o[7] = idct_limit(descale(tmp10 - tmp3, sh));
+            o[1] = idct_limit(descale(tmp11 + tmp2, sh));
+            o[6] = idct_limit(descale(tmp11 - tmp2, sh));
+            o[2] = idct_limit(descale(tmp12 + tmp1, sh));
+            o[5] = idct_limit(descale(tmp12 - tmp1, sh));
+            o[3] = idct_limit(descale(tmp13 + tmp0, sh));
+            o[4] = idct_limit(descale(tmp13 - tmp0, sh));
+        }
+        uint2 pk;
+        pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
+        pk.y = (uint32_t)o[4] | ((uint32_t)o[5] << 8) | ((uint32_t)o[6] << 16) | ((uint32_t)o[7] << 24);
+        *reinterpret_cast<uint2*>(out + row * pitch) = pk;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fancy upsampling + YCbCr -> RGB (jdsample.c, jdcolor.c), one lane per pixel.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int chroma_sample(const uint8_t* plane, int64_t pitch, int dw, int dh, int fh,
+                                             int fv, int x, int y)
+{
+    if (fh == 1 && fv == 1) return plane[(int64_t)y * pitch + x];
+    const int cx = x >> 1, h = x & 1;
+    if (fv == 1) {  // h2v1
+        const uint8_t* r = plane + (int64_t)y * pitch;
+        if (dw <= 2) return r[cx];  // h2v1_upsample
+        if (h == 0) return cx == 0 ? r[0] : (r[cx] * 3 + r[cx - 1] + 1) >> 2;
+        return cx == dw - 1 ? r[cx] : (r[cx] * 3 + r[cx + 1] + 2) >> 2;
+    }
+    // h2v2
+    const int iy = y >> 1;
+    if (dw <= 2) return plane[(int64_t)iy * pitch + cx];  // h2v2_upsample
+    const int oy = (y & 1) ? min(iy + 1, dh - 1) : max(iy - 1, 0);
+    const uint8_t* r0 = plane + (int64_t)iy * pitch;
+    const uint8_t* r1 = plane + (int64_t)oy * pitch;
+    auto colsum = [&](int c) { return r0[c] * 3 + r1[c]; };
+    const int t = colsum(cx);
+    if (h == 0) return cx == 0 ? (t * 4 + 8) >> 4 : (t * 3 + colsum(cx - 1) + 8) >> 4;
+    return cx == dw - 1 ? (t * 4 + 7) >> 4 : (t * 3 + colsum(cx + 1) + 7) >> 4;
+}
+
+__device__ __forceinline__ uint8_t clamp255(int v) { return (uint8_t)min(255, max(0, v)); }
+
+__global__ __launch_bounds__(256) void jpeg_color_kernel(JpegPlan P, int img)
+{
+    const JpegImageDev& im = P.imgs[img];
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= im.W) return;
+    uint8_t* o = im.dst + (int64_t)y * im.dst_pitch + (int64_t)x * 3;
+    const int64_t py = (int64_t)im.comp_bw[0] * 8;
+    const int Y = P.planes[im.comp_plane0[0] + (int64_t)y * py + x];
+    if (im.ncomp == 1) {
+        o[0] = o[1] = o[2] = (uint8_t)Y;
+        return;
+    }
+    int cc[2];
+#pragma unroll
+    for (int k = 1; k <= 2; ++k) {
+        const int fh = im.hmax / im.comp_h[k], fv = im.vmax / im.comp_v[k];
+        cc[k - 1] = chroma_sample(P.planes + im.comp_plane0[k], (int64_t)im.comp_bw[k] * 8, im.comp_dw[k],
+                                  im.comp_dh[k], fh, fv, x, y);
+    }
+    const int cb = cc[0] - 128, cr = cc[1] - 128;
+    const int crr = (int)((91881 * (int64_t)cr + 32768) >> 16);
+    const int cbb = (int)((116130 * (int64_t)cb + 32768) >> 16);
+    const int64_t crg = -46802 * (int64_t)cr, cbg = -22554 * (int64_t)cb + 32768;
+    o[0] = clamp255(Y + crr);
+    o[1] = clamp255(Y + (int)((cbg + crg) >> 16));
+    o[2] = clamp255(Y + cbb);
+}
+
+// EXIF orientation (tag 0x0112), as cv2.imread applies it for IMREAD_COLOR:
+// output pixel (x, y) of the W' x H' result reads input pixel (sx, sy).
+__global__ __launch_bounds__(256) void orient_kernel(const uint8_t* src, int64_t sp, int W, int H, int orient,
+                                                     uint8_t* dst, int64_t dp)
+{
+    const bool swap = orient >= 5;
+    const int OW = swap ? H : W, OH = swap ? W : H;
+    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
+    if (x >= OW) return;
+    int sx, sy;
+    switch (orient) {
+    case 2: sx = W - 1 - x; sy = y; break;                  // mirror horizontal
+    case 3: sx = W - 1 - x; sy = H - 1 - y; break;          // rotate 180
+    case 4: sx = x; sy = H - 1 - y; break;                  // mirror vertical
+    case 5: sx = y; sy = x; break;                          // transpose
+    case 6: sx = y; sy = H - 1 - x; break;                  // rotate 90 CW
+    case 7: sx = W - 1 - y; sy = H - 1 - x; break;          // transverse
+    case 8: sx = W - 1 - y; sy = x; break;                  // rotate 270 CW
+    default: sx = x; sy = y; break;
+    }
+    (void)OH;
+    const uint8_t* s = src + (int64_t)sy * sp + (int64_t)sx * 3;
+    uint8_t* d = dst + (int64_t)y * dp + (int64_t)x * 3;
+    d[0] = s[0];
+    d[1] = s[1];
+    d[2] = s[2];
+}
+
+}  // namespace
+
+hipError_t launch_orient(const uint8_t* src, int64_t sp, int W, int H, int orient, uint8_t* dst, int64_t dp,
+                         hipStream_t s)
+{
+    const bool swap = orient >= 5;
+    const int OW = swap ? H : W, OH = swap ? W : H;
+    if (OH > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(orient_kernel, dim3((uint32_t)((OW + 255) / 256), (uint32_t)OH), dim3(256), 0, s, src, sp,
+                       W, H, orient, dst, dp);
+    return hipGetLastError();
+}
+
+size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg)
+{
+    (void)n_seg;
+    return (size_t)n_sub * (2 * sizeof(SubResult) + sizeof(SubBase)) + 64 + kJpegMaxJobs * sizeof(IdctJob);
+}
+
+hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* scratch, int64_t n_images,
+                              int* sync_rounds, hipStream_t s)
+{
+    uint8_t* base = (uint8_t*)scratch;
+    SubResult* ra = (SubResult*)base;
+    SubResult* rb = ra + P.n_sub;
+    SubBase* sb = (SubBase*)(rb + P.n_sub);
+    int* changed = (int*)(sb + P.n_sub);
+    IdctJob* jobs = (IdctJob*)((uint8_t*)changed + 64);
+    const uint32_t grid = (uint32_t)((P.n_sub + kJThreads - 1) / kJThreads);
+    // round 0 + rounds until no end state changes
+    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(grid), dim3(kJThreads), 0, s, P, ra, ra, 0, changed);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    SubResult* cur = ra;
+    SubResult* nxt = rb;
+    int rounds = 0;
+    for (;;) {
+        int h_changed = 0;
+        e = hipMemsetAsync(changed, 0, sizeof(int), s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(jpeg_sync_kernel, dim3(grid), dim3(kJThreads), 0, s, P, cur, nxt, 1, changed);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+        std::swap(cur, nxt);
+        ++rounds;
+        if (!h_changed || rounds > P.n_sub) break;
+    }
+    if (sync_rounds) *sync_rounds = rounds;
+    hipLaunchKernelGGL(jpeg_scan_kernel, dim3((uint32_t)P.n_seg), dim3(256), 0, s, P, cur, sb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(jpeg_write_kernel, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // IDCT jobs: every (image, component)
+    std::vector<IdctJob> hj;
+    int64_t max_blocks = 0;
+    for (int64_t i = 0; i < n_images; ++i)
+        for (int c = 0; c < ims[(size_t)i].ncomp; ++c) {
+            IdctJob j;
+            j.block0 = ims[(size_t)i].comp_block0[c];
+            j.plane0 = ims[(size_t)i].comp_plane0[c];
+            j.bw = ims[(size_t)i].comp_bw[c];
+            j.bh = ims[(size_t)i].comp_bh[c];
+            j.img = (int)i;
+            j.comp = c;
+            hj.push_back(j);
+            max_blocks = std::max<int64_t>(max_blocks, (int64_t)j.bw * j.bh);
+        }
+    if (hj.size() > (size_t)kJpegMaxJobs) return hipErrorInvalidValue;
+    e = hipMemcpyAsync(jobs, hj.data(), sizeof(IdctJob) * hj.size(), hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(jpeg_idct_kernel, dim3((uint32_t)((max_blocks + 255) / 256), (uint32_t)hj.size()),
+                       dim3(256), 0, s, P, jobs);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    for (int64_t i = 0; i < n_images; ++i) {
+        const JpegImageDev& im = ims[(size_t)i];
+        hipLaunchKernelGGL(jpeg_color_kernel, dim3((uint32_t)((im.W + 255) / 256), (uint32_t)im.H), dim3(256),
+                           0, s, P, (int)i);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+}  // namespace wicca

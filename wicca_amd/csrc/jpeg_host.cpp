@@ -1,0 +1,278 @@
+// jpeg_host.cpp — host half of the GPU JPEG decoder:
+// marker parsing, Huffman decode tables and byte de-stuffing.  No pixel is
+// decoded here; the entropy-coded data goes to the device (jpeg.hip).
+//
+// Follows the JPEG standard (ITU-T T.81) as libjpeg-turbo implements it for
+// cv2.imread (wicca/data_loader.py:53): baseline / extended-sequential Huffman
+// 8-bit frames, one interleaved scan (or one grayscale component), restart
+// intervals; EXIF orientation is read so that the caller can apply it as
+// OpenCV's IMREAD_COLOR does.
+#include <algorithm>
+#include <climits>
+#include <cstring>
+
+#include "jpeg.h"
+
+namespace wicca {
+
+namespace {
+
+// zig-zag index -> natural (row-major) index
+constexpr int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                             12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                             35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                             58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+int u16be(const uint8_t* p) { return (p[0] << 8) | p[1]; }
+
+int exif_orientation(const uint8_t* p, size_t n)
+{
+    // "Exif\0\0" + TIFF header + IFD0; tag 0x0112 (SHORT)
+    if (n < 14 || memcmp(p, "Exif\0\0", 6) != 0) return 1;
+    const uint8_t* t = p + 6;
+    const size_t tn = n - 6;
+    const bool le = t[0] == 'I' && t[1] == 'I';
+    if (!le && !(t[0] == 'M' && t[1] == 'M')) return 1;
+    auto rd16 = [&](size_t o) -> int {
+        return o + 2 > tn ? -1 : le ? (t[o] | (t[o + 1] << 8)) : ((t[o] << 8) | t[o + 1]);
+    };
+    auto rd32 = [&](size_t o) -> int64_t {
+        if (o + 4 > tn) return -1;
+        return le ? ((int64_t)t[o] | ((int64_t)t[o + 1] << 8) | ((int64_t)t[o + 2] << 16) | ((int64_t)t[o + 3] << 24))
+                  : (((int64_t)t[o] << 24) | ((int64_t)t[o + 1] << 16) | ((int64_t)t[o + 2] << 8) | t[o + 3]);
+    };
+    const int64_t ifd = rd32(4);
+    if (ifd < 8) return 1;
+    const int cnt = rd16((size_t)ifd);
+    for (int i = 0; i < cnt && cnt > 0; ++i) {
+        const size_t e = (size_t)ifd + 2 + 12 * (size_t)i;
+        if (rd16(e) == 0x0112) {
+            const int v = rd16(e + 8);
+            return (v >= 1 && v <= 8) ? v : 1;
+        }
+    }
+    return 1;
+}
+
+}  // namespace
+
+int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
+{
+    auto bad = [&](int code, const char* m) {
+        *err = m;
+        return code;
+    };
+    if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return bad(-1, "not a JPEG file (no SOI marker)");
+    size_t pos = 2;
+    bool have_sof = false;
+    int scan_ids[kJpegMaxComp] = {0, 0, 0};
+    for (;;) {
+        while (pos < n && d[pos] != 0xFF) ++pos;  // tolerate garbage between segments
+        while (pos < n && d[pos] == 0xFF) ++pos;  // fill bytes
+        if (pos >= n) return bad(-1, "truncated JPEG (no SOS)");
+        const int m = d[pos++];
+        if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;  // no length
+        if (m == 0xD9) return bad(-1, "EOI before SOS");
+        if (pos + 2 > n) return bad(-1, "truncated marker segment");
+        const int len = u16be(d + pos);
+        if (len < 2 || pos + (size_t)len > n) return bad(-1, "truncated marker segment");
+        const uint8_t* s = d + pos + 2;
+        const int sl = len - 2;
+        pos += (size_t)len;
+        if (m == 0xC0 || m == 0xC1) {  // baseline / extended sequential, Huffman
+            if (sl < 6) return bad(-1, "bad SOF");
+            if (s[0] != 8) return bad(-2, "only 8-bit JPEG is supported");
+            info->H = u16be(s + 1);
+            info->W = u16be(s + 3);
+            info->ncomp = s[5];
+            if (info->H <= 0 || info->W <= 0) return bad(-2, "JPEG with DNL height is not supported");
+            if (info->ncomp != 1 && info->ncomp != 3)
+                return bad(-2, "only grayscale and 3-component (YCbCr) JPEG is supported");
+            if (sl < 6 + 3 * info->ncomp) return bad(-1, "bad SOF");
+            for (int c = 0; c < info->ncomp; ++c) {
+                JpegComponent& k = info->comp[c];
+                k.id = s[6 + 3 * c];
+                k.h = s[7 + 3 * c] >> 4;
+                k.v = s[7 + 3 * c] & 15;
+                k.tq = s[8 + 3 * c];
+                if (k.h < 1 || k.h > 4 || k.v < 1 || k.v > 4 || k.tq > 3) return bad(-1, "bad SOF component");
+            }
+            have_sof = true;
+        } else if ((m >= 0xC2 && m <= 0xC3) || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
+                   (m >= 0xCD && m <= 0xCF)) {
+            return bad(-2, "progressive, lossless, hierarchical and arithmetic-coded JPEG are not supported");
+        } else if (m == 0xC4) {  // DHT
+            int o = 0;
+            while (o < sl) {
+                if (o + 17 > sl) return bad(-1, "bad DHT");
+                const int tc = s[o] >> 4, th = s[o] & 15;
+                if (tc > 1 || th > 3) return bad(-1, "bad DHT class/id");
+                JpegHuffTable& t = tc ? info->ac[th] : info->dc[th];
+                t.bits[0] = 0;
+                int total = 0;
+                for (int l = 1; l <= 16; ++l) {
+                    t.bits[l] = s[o + l];
+                    total += t.bits[l];
+                }
+                if (total > 256 || o + 17 + total > sl) return bad(-1, "bad DHT counts");
+                memcpy(t.vals, s + o + 17, (size_t)total);
+                t.nvals = total;
+                (tc ? info->ac_present : info->dc_present)[th] = true;
+                o += 17 + total;
+            }
+        } else if (m == 0xDB) {  // DQT
+            int o = 0;
+            while (o < sl) {
+                const int pq = s[o] >> 4, tq = s[o] & 15;
+                if (tq > 3 || pq > 1 || o + 1 + 64 * (pq + 1) > sl) return bad(-1, "bad DQT");
+                for (int i = 0; i < 64; ++i)
+                    info->qt[tq][kZigzag[i]] = pq ? (uint16_t)u16be(s + o + 1 + 2 * i) : s[o + 1 + i];
+                info->qt_present[tq] = true;
+                o += 1 + 64 * (pq + 1);
+            }
+        } else if (m == 0xDD) {  // DRI
+            if (sl < 2) return bad(-1, "bad DRI");
+            info->restart_interval = u16be(s);
+        } else if (m == 0xE1) {  // APP1: EXIF orientation
+            const int o = exif_orientation(s, (size_t)sl);
+            if (o != 1) info->orientation = o;
+        } else if (m == 0xDA) {  // SOS
+            if (!have_sof) return bad(-1, "SOS before SOF");
+            const int ns = s[0];
+            if (ns != info->ncomp)
+                return bad(-2, "multi-scan (non-interleaved) JPEG is not supported");
+            if (sl < 1 + 2 * ns + 3) return bad(-1, "bad SOS");
+            for (int i = 0; i < ns; ++i) {
+                const int id = s[1 + 2 * i];
+                int c = -1;
+                for (int k = 0; k < info->ncomp; ++k)
+                    if (info->comp[k].id == id) c = k;
+                if (c < 0) return bad(-1, "SOS names an unknown component");
+                scan_ids[i] = c;
+                info->comp[c].td = s[2 + 2 * i] >> 4;
+                info->comp[c].ta = s[2 + 2 * i] & 15;
+                if (info->comp[c].td > 3 || info->comp[c].ta > 3) return bad(-1, "bad SOS table id");
+            }
+            const int ss = s[1 + 2 * ns], se = s[2 + 2 * ns], ahl = s[3 + 2 * ns];
+            if (ss != 0 || se != 63 || ahl != 0) return bad(-2, "spectral selection / successive approximation");
+            info->scan = d + pos;
+            info->scan_len = n - pos;
+            break;
+        }
+        // other APPn, COM, ...: skipped
+    }
+    // tables present?
+    for (int c = 0; c < info->ncomp; ++c) {
+        const JpegComponent& k = info->comp[c];
+        if (!info->qt_present[k.tq]) return bad(-1, "missing quantisation table");
+        if (!info->dc_present[k.td] || !info->ac_present[k.ta]) return bad(-1, "missing Huffman table");
+    }
+    // geometry
+    if (info->ncomp == 1) {
+        JpegComponent& k = info->comp[0];
+        info->hmax = info->vmax = 1;
+        info->mcux = (info->W + 7) / 8;
+        info->mcuy = (info->H + 7) / 8;
+        k.h = k.v = 1;  // a single-component scan has one block per MCU
+        k.bw = info->mcux;
+        k.bh = info->mcuy;
+        k.dw = info->W;
+        k.dh = info->H;
+        info->bpm = 1;
+        info->slot_comp[0] = 0;
+        info->slot_h[0] = info->slot_v[0] = 0;
+    } else {
+        int hmax = 1, vmax = 1;
+        for (int c = 0; c < 3; ++c) {
+            hmax = std::max(hmax, info->comp[c].h);
+            vmax = std::max(vmax, info->comp[c].v);
+        }
+        info->hmax = hmax;
+        info->vmax = vmax;
+        for (int c = 0; c < 3; ++c) {
+            const int fh = hmax / info->comp[c].h, fv = vmax / info->comp[c].v;
+            if (hmax % info->comp[c].h || vmax % info->comp[c].v || fh > 2 || fv > 2 || (fh == 1 && fv == 2))
+                return bad(-2, "only 4:4:4, 4:2:2 and 4:2:0 sampling is supported");
+        }
+        info->mcux = (info->W + 8 * hmax - 1) / (8 * hmax);
+        info->mcuy = (info->H + 8 * vmax - 1) / (8 * vmax);
+        int slot = 0;
+        for (int i = 0; i < 3; ++i) {
+            const int c = scan_ids[i];
+            JpegComponent& k = info->comp[c];
+            k.bw = info->mcux * k.h;
+            k.bh = info->mcuy * k.v;
+            k.dw = (int)(((int64_t)info->W * k.h + hmax - 1) / hmax);
+            k.dh = (int)(((int64_t)info->H * k.v + vmax - 1) / vmax);
+            for (int v = 0; v < k.v; ++v)
+                for (int h = 0; h < k.h; ++h) {
+                    if (slot >= kJpegMaxSlots) return bad(-1, "too many blocks per MCU");
+                    info->slot_comp[slot] = c;
+                    info->slot_h[slot] = h;
+                    info->slot_v[slot] = v;
+                    ++slot;
+                }
+        }
+        info->bpm = slot;
+    }
+    return 0;
+}
+
+void jpeg_destuff(const JpegInfo& info, std::vector<uint8_t>& out, std::vector<int64_t>& seg_off)
+{
+    const uint8_t* s = info.scan;
+    const size_t n = info.scan_len;
+    out.clear();
+    out.reserve(n);
+    seg_off.assign(1, 0);
+    size_t i = 0;
+    while (i < n) {
+        const uint8_t* ff = (const uint8_t*)memchr(s + i, 0xFF, n - i);
+        const size_t run = ff ? (size_t)(ff - (s + i)) : n - i;
+        out.insert(out.end(), s + i, s + i + run);
+        i += run;
+        if (i >= n) break;
+        // s[i] == 0xFF
+        if (i + 1 >= n) break;
+        const uint8_t nx = s[i + 1];
+        if (nx == 0x00) {  // stuffed data byte
+            out.push_back(0xFF);
+            i += 2;
+        } else if (nx == 0xFF) {  // fill byte
+            i += 1;
+        } else if (nx >= 0xD0 && nx <= 0xD7) {  // RSTn: next segment starts byte-aligned
+            seg_off.push_back((int64_t)out.size());
+            i += 2;
+        } else {
+            break;  // EOI or another marker: end of the scan
+        }
+    }
+    seg_off.push_back((int64_t)out.size());
+}
+
+void build_huff_dev(const JpegHuffTable& t, HuffDev* d)
+{
+    memset(d, 0, sizeof(*d));
+    int code = 0, k = 0;
+    for (int l = 1; l <= 16; ++l) {
+        if (t.bits[l] == 0) {
+            d->maxcode[l] = -1;
+            d->valoff[l] = 0;
+        } else {
+            d->valoff[l] = k - code;
+            for (int i = 0; i < t.bits[l]; ++i, ++k, ++code) {
+                if (l <= kHuffLutBits) {
+                    const int lo = code << (kHuffLutBits - l), hi = (code + 1) << (kHuffLutBits - l);
+                    for (int e = lo; e < hi; ++e) d->lut[e] = (uint16_t)((l << 8) | t.vals[k]);
+                }
+            }
+            d->maxcode[l] = code - 1;
+        }
+        code <<= 1;
+    }
+    d->maxcode[0] = -1;
+    d->maxcode[17] = INT_MAX;  // sentinel
+    memcpy(d->vals, t.vals, 256);
+}
+
+}  // namespace wicca

@@ -1,0 +1,108 @@
+"""GPU JPEG decode: the reference's ``load_image``.
+
+``/root/reference/wicca/data_loader.py:31-63`` reads every file with
+``cv2.imread`` (libjpeg-turbo, BGR) and converts it to RGB.  Here baseline
+JPEG files are decoded on the GPU (``wicca_jpeg_decode_u8``,
+``wicca_amd/csrc/jpeg.hip``), restating libjpeg-turbo's default arithmetic
+bit for bit (checked against Pillow 12.2.0 / libjpeg-turbo 3.1.4.1,
+``tests/test_gpu_jpeg.py``), EXIF orientation applied as ``cv2.imread`` does.
+
+:func:`load_image` keeps the reference's contract: empty path ->
+``ValueError("File path cannot be empty")``; any failure -> prints
+``Error loading image {path}: {err}`` and returns ``None``.  Files the GPU
+decoder does not handle (PNG, progressive JPEG, ...) fail that way too —
+there is no CPU decoder behind it.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Sequence
+
+import numpy as np
+
+from . import _lib
+
+
+def _buffers(blobs: Sequence[bytes]):
+    n = len(blobs)
+    keep = [np.frombuffer(b, np.uint8) for b in blobs]
+    ptrs = (ctypes.c_void_p * n)(*[k.ctypes.data for k in keep])
+    sizes = (ctypes.c_int64 * n)(*[k.size for k in keep])
+    return keep, ptrs, sizes
+
+
+def info(data: bytes, apply_orientation: bool = True) -> tuple[int, int, int, int]:
+    """(height, width, components, exif_orientation) of a JPEG file's bytes."""
+    arr = np.frombuffer(data, np.uint8)
+    h, w = ctypes.c_int64(), ctypes.c_int64()
+    c, o = ctypes.c_int(), ctypes.c_int()
+    _lib.check(_lib.load().wicca_jpeg_info(arr.ctypes.data, arr.size, int(apply_orientation),
+                                           ctypes.byref(h), ctypes.byref(w), ctypes.byref(c),
+                                           ctypes.byref(o)))
+    return h.value, w.value, c.value, o.value
+
+
+def decode_batch(blobs: Sequence[bytes], apply_orientation: bool = True,
+                 device: int | None = None) -> list[np.ndarray]:
+    """RGB (H, W, 3) uint8 arrays of JPEG files, decoded in one GPU pass."""
+    if not blobs:
+        return []
+    outs = []
+    for b in blobs:
+        h, w, _, _ = info(b, apply_orientation)
+        outs.append(np.empty((h, w, 3), np.uint8))
+    keep, ptrs, sizes = _buffers(blobs)
+    n = len(blobs)
+    dsts = (ctypes.c_void_p * n)(*[o.ctypes.data for o in outs])
+    pitches = (ctypes.c_int64 * n)(*[o.shape[1] * 3 for o in outs])
+    _lib.check(_lib.load().wicca_jpeg_decode_u8(ptrs, sizes, n, dsts, pitches, int(apply_orientation),
+                                                0, -1 if device is None else int(device), None))
+    del keep
+    return outs
+
+
+def decode(data: bytes, apply_orientation: bool = True, device: int | None = None) -> np.ndarray:
+    """RGB (H, W, 3) uint8 array of one JPEG file's bytes."""
+    return decode_batch([data], apply_orientation, device)[0]
+
+
+def load_image(file_path: str) -> np.ndarray | None:
+    """``wicca.data_loader.load_image`` (data_loader.py:31-63) with the decode on the GPU."""
+    if not file_path:
+        raise ValueError("File path cannot be empty")
+    try:
+        with open(file_path, "rb") as f:
+            data = f.read()
+        return decode(data)
+    except Exception as e:  # the reference prints and returns None (data_loader.py:61-63)
+        print(f"Error loading image {file_path}: {str(e)}")
+        return None
+
+
+def get_img_batch(file_paths: Sequence[str], shape, transform_depth: int, interpolation: int = 3,
+                  border_type: int = 1, border_constant: int = 0,
+                  device: int | None = None) -> tuple[np.ndarray, np.ndarray]:
+    """``ClassifierProcessor._get_img_batch`` (classifying_tools.py:297-323)
+    from file paths: GPU decode + resize + icon + icon resize; only the
+    compressed files cross PCIe.  Returns ``(batch_images, batch_icons)``."""
+    from .coder import _border_value, _depth_index
+    blobs = []
+    for p in file_paths:
+        if not p:
+            raise ValueError("File path cannot be empty")
+        with open(p, "rb") as f:
+            blobs.append(f.read())
+    if not blobs:
+        raise ValueError("need at least one array to stack")
+    out_w, out_h = int(shape[0]), int(shape[1])
+    n = len(blobs)
+    resized = np.empty((n, out_h, out_w, 3), np.uint8)
+    icons = np.empty((n, out_h, out_w, 3), np.uint8)
+    keep, ptrs, sizes = _buffers(blobs)
+    k = _border_value(border_constant) if int(border_type) == 0 else 0
+    _lib.check(_lib.load().wicca_jpeg_icon_stage_u8(
+        ptrs, sizes, n, _depth_index(transform_depth), int(border_type), k, out_w, out_h,
+        int(interpolation), resized.ctypes.data, icons.ctypes.data,
+        -1 if device is None else int(device)))
+    del keep
+    return resized, icons
