@@ -40,13 +40,17 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=["batch", "tiled", "multi", "ragged", "stage"], default="batch",
+    ap.add_argument("--config", choices=["batch", "tiled", "multi", "ragged", "stage", "jpeg"],
+                    default="batch",
                     help="batch: configs[2]/[3] image-parallel (default); "
                          "tiled: configs[4], one 65536^2 RGB image row-sharded at depth 8; "
                          "multi: configs[2]'s depth sweep 1..6 from one read (SURVEY 8f); "
                          "ragged: a batch of random-size images in one launch (A7 caller); "
                          "stage: the caller's whole per-image stage from host arrays "
-                         "(resize + icon + icon resize, HaarCoder.icon_stage)")
+                         "(resize + icon + icon resize, HaarCoder.icon_stage); "
+                         "jpeg: GPU decode of 8K JPEG files (load_image) and the file-based "
+                         "caller stage (decode + resize + icon + icon resize)")
+    ap.add_argument("--quality", type=int, default=90, help="--config jpeg: encoder quality")
     ap.add_argument("--shape", default="224,224", help="--config stage: classifier input (w,h)")
     ap.add_argument("--interpolation", type=int, default=3, help="--config stage: cv2.INTER_*")
     ap.add_argument("--depths", default="1,2,3,4,5,6", help="depth list of --config multi")
@@ -413,6 +417,96 @@ def run_stage(args, torch, rank):
     }
 
 
+def run_jpeg(args, torch, rank):
+    """load_image (data_loader.py:31-63) on the GPU: B JPEG files of the
+    configs[2] size decoded in one call into device RGB buffers, then the whole
+    file-based _get_img_batch stage (classifying_tools.py:297-323).  The files
+    are already in host memory (no disk I/O); the CPU baseline is libjpeg-turbo
+    itself through Pillow (the decoder cv2.imread wraps)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from oracle import jpeg_pil
+    from wicca_amd import _lib
+    lib = _lib.load()
+    B = 25 if args.images == 128 else args.images
+    H, W, D = args.height, args.width, args.depth
+    distinct = [jpeg_pil.encode(jpeg_pil.test_image("scene", H, W, 40 + k), args.quality, 2)
+                for k in range(4)]
+    blobs = [distinct[i % 4] for i in range(B)]
+    keep = [np.frombuffer(b, np.uint8) for b in blobs]
+    ptrs = (ctypes.c_void_p * B)(*[k.ctypes.data for k in keep])
+    sizes = (ctypes.c_int64 * B)(*[k.size for k in keep])
+    pitch = (W * 3 + 127) // 128 * 128
+    dev = torch.empty(B * H * pitch, dtype=torch.uint8, device="cuda")
+    dsts = (ctypes.c_void_p * B)(*[dev.data_ptr() + i * H * pitch for i in range(B)])
+    pitches = (ctypes.c_int64 * B)(*([pitch] * B))
+    stream = torch.cuda.Stream()
+    sh = ctypes.c_void_p(stream.cuda_stream)
+
+    def decode():
+        _lib.check(lib.wicca_jpeg_decode_u8(ptrs, sizes, B, dsts, pitches, 1, 1, -1, sh))
+        stream.synchronize()
+
+    for _ in range(args.warmup):
+        decode()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        decode()
+    dec_s = (time.perf_counter() - t0) / args.steps
+    rounds = int(lib.wicca_jpeg_last_sync_rounds())
+    verified = None
+    if not args.no_verify:
+        got = dev[:H * pitch].view(H, pitch)[:, :W * 3].cpu().numpy().reshape(H, W, 3)
+        verified = bool(np.array_equal(got, jpeg_pil.decode_rgb(blobs[0])))
+        if not verified:
+            raise SystemExit("jpeg bench verification FAILED")
+    shape = tuple(int(x) for x in args.shape.split(","))
+    res = np.empty((B, shape[1], shape[0], 3), np.uint8)
+    ico = np.empty_like(res)
+
+    def stage():
+        _lib.check(lib.wicca_jpeg_icon_stage_u8(ptrs, sizes, B, D, 1, 0, shape[0], shape[1],
+                                                args.interpolation, res.ctypes.data, ico.ctypes.data, -1))
+
+    stage()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        stage()
+    stage_s = (time.perf_counter() - t0) / args.steps
+    mpix = B * H * W / 1e6
+    # CPU: libjpeg-turbo (Pillow) decode, one thread and a pool over the affinity set
+    n1, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 3.0 and n1 < 8:
+        jpeg_pil.decode_rgb(blobs[n1 % 4], apply_orientation=False)
+        n1 += 1
+    single = n1 * H * W / 1e6 / (time.perf_counter() - t0)
+    threads = min(16, len(os.sched_getaffinity(0)))
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda b: jpeg_pil.decode_rgb(b, False), blobs[:threads]))
+        t0 = time.perf_counter()
+        list(ex.map(lambda b: jpeg_pil.decode_rgb(b, False), blobs * 2))
+        pool = 2 * B * H * W / 1e6 / (time.perf_counter() - t0)
+    return {
+        "metric": "megapixels/sec JPEG decode (load_image) on the GPU", "value": round(mpix / dec_s, 1),
+        "unit": "MP/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(dec_s * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": f"synthetic scenes encoded by libjpeg-turbo (q{args.quality}, 4:2:0), files in host "
+                "memory; decode into device RGB (compressed bytes cross PCIe inside the timed region)",
+        "config": {"workload": f"{B} x {W}x{H} JPEG files per call, EXIF orientation applied",
+                   "images": B, "mean_file_MB": round(sum(len(b) for b in blobs) / B / 1e6, 2)},
+        "sync_rounds": rounds,
+        "file_stage": {"ms_per_batch": round(stage_s * 1e3, 3), "MP_per_s": round(mpix / stage_s, 1),
+                       "what": f"decode + cv2.resize to {shape} + icon depth {D} + icon resize, "
+                               "outputs to host (classifying_tools.py:312-323)"},
+        "cpu_baseline": {"value": round(pool, 1), "unit": "MP/s", "cores": threads, "kind": "reference",
+                         "sample": f"Pillow/libjpeg-turbo {jpeg_pil.libjpeg_version()} decode of the same "
+                                   f"files, ThreadPoolExecutor({threads}), {2 * B} files",
+                         "single_thread_value": round(single, 1)},
+        "roofline": None, "verified_vs_libjpeg_turbo": verified,
+    }
+
+
 def run_multi(args, torch, rank):
     """All depths of configs[2]'s sweep from ONE read of the batch
     (wicca_haar_ll_u8_multi_uniform), against one launch per depth."""
@@ -545,6 +639,11 @@ def main():
         raise SystemExit("no HIP device visible")
     if args.config == "multi":
         out = run_multi(args, torch, rank)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        return
+    if args.config == "jpeg":
+        out = run_jpeg(args, torch, rank)
         if rank == 0:
             print(json.dumps(out), flush=True)
         return

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdarg>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -113,6 +114,20 @@ struct Workspace {
     DevBuf slot[2], icon[2];
     // JPEG decode (wicca_jpeg_*): stream + tables, coefficients, planes, scratch, RGB images
     DevBuf jmeta, jcoef, jplanes, jscratch, jrgb, jtmp;
+    uint8_t* jhost = nullptr;  // pinned host staging of the de-stuffed JPEG streams
+    size_t jhost_cap = 0;
+    bool reserve_jhost(size_t n)
+    {
+        if (n <= jhost_cap) return true;
+        if (jhost) (void)hipHostFree(jhost);
+        jhost = nullptr;
+        jhost_cap = 0;
+        void* p = nullptr;
+        if (hipHostMalloc(&p, std::max<size_t>(n, 16 << 20), hipHostMallocDefault) != hipSuccess) return false;
+        jhost = (uint8_t*)p;
+        jhost_cap = std::max<size_t>(n, 16 << 20);
+        return true;
+    }
     size_t bytes() const
     {
         return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
@@ -153,6 +168,9 @@ struct Workspace {
         jscratch.release();
         jrgb.release();
         jtmp.release();
+        if (jhost) (void)hipHostFree(jhost);
+        jhost = nullptr;
+        jhost_cap = 0;
     }
     void destroy()
     {
@@ -1252,14 +1270,22 @@ int wicca_icon_stage_u8(const wicca_image_desc* images, int64_t n, int64_t C, in
 // ---------------------------------------------------------------------------
 namespace {
 
-int jpeg_sub_bits()
+// Subsequence length (bits) of the parallel Huffman decode: long enough that a
+// lane started at a guessed state resynchronises (bit alignment AND MCU slot)
+// inside its own subsequence — 2048 bits needed 9 passes on 8K photos — and
+// short enough to keep ~256 K lanes in flight (the passes are latency-bound).
+// Measured on 25 x 8K q90 4:2:0 files (profiles/r02_jpeg_sub_bits.jsonl):
+// 4096 bits 3 passes 27.0 GP/s, 8192 2 passes 28.4, 16384 1 pass 27.2, 32768
+// 1 pass 22.2.  WICCA_JPEG_SUB_BITS overrides.
+int64_t jpeg_sub_bits(int64_t total_bits)
 {
-    static const int v = [] {
+    static const int64_t env = [] {
         const char* e = getenv("WICCA_JPEG_SUB_BITS");
-        const int b = e ? atoi(e) : 2048;
-        return std::max(256, std::min(b, 1 << 20)) & ~7;
+        return e ? (int64_t)atoll(e) : (int64_t)0;
     }();
-    return v;
+    int64_t b = env > 0 ? env : total_bits / 262144;
+    b = std::max<int64_t>(env > 0 ? 256 : 8192, std::min<int64_t>(b, 65536));
+    return (b + 255) & ~(int64_t)255;
 }
 
 int parse_one(const uint8_t* data, int64_t size, wicca::JpegInfo* info, int64_t i)
@@ -1292,10 +1318,40 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         int rc = parse_one(data[i], sizes[i], &info[(size_t)i], i);
         if (rc) return rc;
     }
-    const int S = jpeg_sub_bits();
-    std::vector<uint8_t> stream_h;
+    // de-stuff every image's scan in parallel into its own region of one buffer
+    std::vector<int64_t> img_off((size_t)n + 1, 0);
+    for (int64_t i = 0; i < n; ++i)
+        img_off[(size_t)i + 1] = img_off[(size_t)i] + round_up((int64_t)info[(size_t)i].scan_len, 16);
+    // pinned staging, reused across calls; the bit reader reads ahead past the end
+    const size_t stream_bytes = (size_t)img_off[(size_t)n] + 64;
+    if (!ws->reserve_jhost(stream_bytes)) return fail(WICCA_ERR_NOMEM, "pinned staging of %zu bytes", stream_bytes);
+    uint8_t* stream_h = ws->jhost;
+    for (int64_t i = 0; i < n; ++i)  // the tail of each region past its de-stuffed data stays zero
+        memset(stream_h + img_off[(size_t)i] + (int64_t)info[(size_t)i].scan_len, 0,
+               (size_t)(img_off[(size_t)i + 1] - img_off[(size_t)i] - (int64_t)info[(size_t)i].scan_len));
+    memset(stream_h + img_off[(size_t)n], 0, 64);
+    std::vector<std::vector<int64_t>> seg_off((size_t)n);
+    {
+        const int nt = (int)std::min<int64_t>(n, 16);
+        std::atomic<int64_t> next{0};
+        auto work = [&] {
+            for (int64_t i; (i = next.fetch_add(1)) < n;)
+            {
+                const size_t got = wicca::jpeg_destuff_into(info[(size_t)i], stream_h + img_off[(size_t)i],
+                                                            seg_off[(size_t)i]);
+                memset(stream_h + img_off[(size_t)i] + got, 0, info[(size_t)i].scan_len - got);
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+    }
+    int64_t total_bits = 0;
+    for (int64_t i = 0; i < n; ++i) total_bits += seg_off[(size_t)i].back() * 8;
+    const int64_t S = jpeg_sub_bits(total_bits);
     std::vector<wicca::JpegSegDev> segs;
-    std::vector<int32_t> sub_seg;
+    std::vector<int32_t> sub_seg, sub_img;
     std::vector<wicca::HuffDev> huff;
     std::vector<wicca::JpegImageDev> ims((size_t)n);
     int64_t coef_blocks = 0, plane_bytes = 0, tmp_bytes = 0;
@@ -1351,37 +1407,34 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
             im.dst = dst[i];
             im.dst_pitch = dpitch[i];
         }
-        // entropy-coded segments
-        std::vector<uint8_t> bytes;
-        std::vector<int64_t> off;
-        wicca::jpeg_destuff(f, bytes, off);
+        // restart segments and their subsequences; the image's subsequences
+        // are padded to whole workgroups (padding lanes: segment -1)
+        const std::vector<int64_t>& off = seg_off[(size_t)i];
         const int64_t mcus = (int64_t)f.mcux * f.mcuy;
         const int64_t ri = f.restart_interval > 0 ? f.restart_interval : mcus;
-        const int64_t nseg_expect = (mcus + ri - 1) / ri;
-        const int64_t nseg = std::min<int64_t>(nseg_expect, (int64_t)off.size() - 1);
-        const int64_t base = (int64_t)stream_h.size();
-        stream_h.insert(stream_h.end(), bytes.begin(), bytes.end());
-        for (int64_t sgi = 0; sgi < std::max<int64_t>(nseg, 1); ++sgi) {
+        const int64_t nseg = std::max<int64_t>(1, std::min<int64_t>((mcus + ri - 1) / ri, (int64_t)off.size() - 1));
+        for (int64_t sgi = 0; sgi < nseg; ++sgi) {
             wicca::JpegSegDev sg;
-            const int64_t b0 = sgi < (int64_t)off.size() - 1 ? off[(size_t)sgi] : (int64_t)bytes.size();
-            const int64_t b1 = sgi + 1 < (int64_t)off.size() ? off[(size_t)sgi + 1] : (int64_t)bytes.size();
-            sg.bit0 = (base + b0) * 8;
+            const int64_t b0 = off[(size_t)sgi], b1 = off[(size_t)sgi + 1];
+            sg.bit0 = (img_off[(size_t)i] + b0) * 8;
             sg.bits = (b1 - b0) * 8;
             sg.block0 = sgi * ri * f.bpm;
             sg.block_end = std::min(mcus, (sgi + 1) * ri) * f.bpm;
             sg.img = (int32_t)i;
             sg.sub0 = (int32_t)sub_seg.size();
-            const int64_t nsub = std::max<int64_t>(1, (sg.bits + S - 1) / S);
-            for (int64_t k = 0; k < nsub; ++k) sub_seg.push_back((int32_t)segs.size());
+            sg.n_sub = std::max<int64_t>(1, (sg.bits + S - 1) / S);
+            for (int64_t k = 0; k < sg.n_sub; ++k) sub_seg.push_back((int32_t)segs.size());
             segs.push_back(sg);
         }
+        while (sub_seg.size() % wicca::kJpegLanes) sub_seg.push_back(-1);
+        while (sub_img.size() < sub_seg.size() / wicca::kJpegLanes) sub_img.push_back((int32_t)i);
     }
-    stream_h.resize(stream_h.size() + 16, 0);  // the bit reader reads ahead
     if (sub_seg.size() >= (size_t)INT32_MAX) return fail(WICCA_ERR_ARG, "JPEG batch too large");
     // device buffers: [stream | segs | sub_seg | imgs | huff] in jmeta
-    const size_t o_seg = (size_t)round_up((int64_t)stream_h.size(), 256);
+    const size_t o_seg = (size_t)round_up((int64_t)stream_bytes, 256);
     const size_t o_sub = o_seg + (size_t)round_up((int64_t)(segs.size() * sizeof(wicca::JpegSegDev)), 256);
-    const size_t o_img = o_sub + (size_t)round_up((int64_t)(sub_seg.size() * sizeof(int32_t)), 256);
+    const size_t o_sim = o_sub + (size_t)round_up((int64_t)(sub_seg.size() * sizeof(int32_t)), 256);
+    const size_t o_img = o_sim + (size_t)round_up((int64_t)(sub_img.size() * sizeof(int32_t)), 256);
     const size_t o_huf = o_img + (size_t)round_up((int64_t)(ims.size() * sizeof(wicca::JpegImageDev)), 256);
     const size_t meta_bytes = o_huf + huff.size() * sizeof(wicca::HuffDev);
     HIP_TRY(ws->jmeta.reserve(meta_bytes));
@@ -1392,25 +1445,28 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     for (int64_t i = 0; i < n; ++i)
         if (tmp_off[(size_t)i] >= 0) ims[(size_t)i].dst = (uint8_t*)ws->jtmp.ptr + tmp_off[(size_t)i];
     uint8_t* m = (uint8_t*)ws->jmeta.ptr;
-    std::vector<uint8_t> packed(meta_bytes, 0);
-    memcpy(packed.data(), stream_h.data(), stream_h.size());
-    memcpy(packed.data() + o_seg, segs.data(), segs.size() * sizeof(wicca::JpegSegDev));
-    memcpy(packed.data() + o_sub, sub_seg.data(), sub_seg.size() * sizeof(int32_t));
-    memcpy(packed.data() + o_img, ims.data(), ims.size() * sizeof(wicca::JpegImageDev));
-    memcpy(packed.data() + o_huf, huff.data(), huff.size() * sizeof(wicca::HuffDev));
-    HIP_TRY(hipMemcpyAsync(m, packed.data(), meta_bytes, hipMemcpyHostToDevice, stream));
+    // the de-stuffed streams go up as they are; the small tables packed behind them
+    std::vector<uint8_t> packed(meta_bytes - o_seg, 0);
+    memcpy(packed.data(), segs.data(), segs.size() * sizeof(wicca::JpegSegDev));
+    memcpy(packed.data() + (o_sub - o_seg), sub_seg.data(), sub_seg.size() * sizeof(int32_t));
+    memcpy(packed.data() + (o_sim - o_seg), sub_img.data(), sub_img.size() * sizeof(int32_t));
+    memcpy(packed.data() + (o_img - o_seg), ims.data(), ims.size() * sizeof(wicca::JpegImageDev));
+    memcpy(packed.data() + (o_huf - o_seg), huff.data(), huff.size() * sizeof(wicca::HuffDev));
+    HIP_TRY(hipMemcpyAsync(m, stream_h, stream_bytes, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(m + o_seg, packed.data(), packed.size(), hipMemcpyHostToDevice, stream));
     HIP_TRY(hipMemsetAsync(ws->jcoef.ptr, 0, (size_t)coef_blocks * 128, stream));
     wicca::JpegPlan P{};
     P.stream = m;
     P.segs = (const wicca::JpegSegDev*)(m + o_seg);
     P.sub_seg = (const int32_t*)(m + o_sub);
+    P.sub_img = (const int32_t*)(m + o_sim);
     P.imgs = (const wicca::JpegImageDev*)(m + o_img);
     P.huff = (const wicca::HuffDev*)(m + o_huf);
     P.coef = (int16_t*)ws->jcoef.ptr;
     P.planes = (uint8_t*)ws->jplanes.ptr;
     P.n_sub = (int64_t)sub_seg.size();
     P.n_seg = (int64_t)segs.size();
-    P.sub_bits = S;
+    P.sub_bits = (int32_t)S;
     int rounds = 0;
     HIP_TRY(wicca::jpeg_decode_device(P, ims.data(), ws->jscratch.ptr, n, &rounds, stream));
     if (rounds_out) *rounds_out = rounds;

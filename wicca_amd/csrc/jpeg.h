@@ -61,6 +61,9 @@ int jpeg_parse(const uint8_t* data, size_t size, JpegInfo* info, std::string* er
 // de-stuffed bytes of every restart segment back to back; seg_off[s] is the
 // first byte of segment s (seg_off.back() = out.size()).
 void jpeg_destuff(const JpegInfo& info, std::vector<uint8_t>& out, std::vector<int64_t>& seg_off);
+// The same into out[0 .. info.scan_len) (the de-stuffed data is never longer);
+// returns the de-stuffed length.
+size_t jpeg_destuff_into(const JpegInfo& info, uint8_t* out, std::vector<int64_t>& seg_off);
 
 // ---------------------------------------------------------------------------
 // Device plan (built on the host, uploaded once per decode call).
@@ -91,6 +94,7 @@ struct JpegSegDev {
     int64_t bit0, bits;        // de-stuffed bit range of the segment
     int64_t block0, block_end; // image-local decode-order block range
     int32_t img, sub0;         // image; first subsequence of the segment
+    int64_t n_sub;             // its subsequences
 };
 
 struct JpegPlan {
@@ -103,7 +107,12 @@ struct JpegPlan {
     uint8_t* planes;         // component sample planes
     int64_t n_sub, n_seg;
     int32_t sub_bits;        // subsequence length
+    const int32_t* sub_img;  // per workgroup of kJpegLanes subsequences: its image (uniform)
 };
+
+// Lanes per decode workgroup; an image's subsequences are padded to whole
+// workgroups so that a workgroup serves one image (its Huffman tables go to LDS).
+constexpr int kJpegLanes = 256;
 
 // Decode every image of the plan into its dst (RGB, HWC uint8).  `ims` is the
 // host copy of plan.imgs; scratch holds the per-subsequence states (see

@@ -38,7 +38,7 @@ namespace wicca {
 
 namespace {
 
-constexpr int kJThreads = 64;  // one wave per workgroup: lanes run independent decodes
+constexpr int kJThreads = kJpegLanes;  // lanes run independent decodes; a workgroup shares LDS tables
 
 __constant__ int kNatural[80] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
                                  12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
@@ -58,47 +58,57 @@ struct SubResult {
     int32_t pad_;
 };
 
-// MSB-first bit reader over the de-stuffed stream (bytes past the end read 0:
-// the host pads the stream with zero bytes).
+// MSB-first bit reader over the de-stuffed stream: aligned 32-bit loads (one
+// per 32 bits consumed) issued two words ahead of use, so the load latency
+// overlaps the decode of the bits already buffered.  The host pads the stream
+// with zero bytes past its end.
 struct BitReader {
-    const uint8_t* s;
-    int64_t p, nb;
-    uint64_t buf;
+    const uint32_t* w;
+    int64_t p;     // absolute position of the next unconsumed bit
+    int64_t wi;    // index of the word in n0
+    uint64_t buf;  // n valid bits, MSB-aligned
     int n;
+    uint32_t n0, n1;
+    __device__ __forceinline__ static uint32_t be(uint32_t x) { return __builtin_bswap32(x); }
     __device__ void reset(const uint8_t* stream, int64_t bitpos)
     {
-        s = stream;
+        w = reinterpret_cast<const uint32_t*>(stream);
         p = bitpos;
-        nb = bitpos >> 3;
-        buf = 0;
-        n = 0;
-        fill();
-        const int skip = (int)(bitpos & 7);
+        const int64_t word = bitpos >> 5;
+        buf = ((uint64_t)be(w[word]) << 32) | be(w[word + 1]);
+        n = 64;
+        wi = word + 2;
+        n0 = be(w[wi]);
+        n1 = be(w[wi + 1]);
+        const int skip = (int)(bitpos & 31);
         buf <<= skip;
         n -= skip;
     }
-    __device__ void fill()
+    __device__ __forceinline__ void refill()
     {
-        while (n <= 56) {
-            buf |= (uint64_t)s[nb++] << (56 - n);
-            n += 8;
+        if (n <= 32) {
+            buf |= (uint64_t)n0 << (32 - n);
+            n += 32;
+            n0 = n1;
+            ++wi;
+            n1 = be(w[wi + 1]);
         }
     }
-    __device__ uint32_t peek16()
+    __device__ __forceinline__ uint32_t peek16()
     {
-        if (n < 16) fill();
+        refill();
         return (uint32_t)(buf >> 48);
     }
-    __device__ void skip(int k)
+    __device__ __forceinline__ void skip(int k)
     {
         buf <<= k;
         n -= k;
         p += k;
     }
-    __device__ uint32_t get(int k)
+    __device__ __forceinline__ uint32_t get(int k)
     {
         if (k == 0) return 0;
-        if (n < k) fill();
+        refill();
         const uint32_t v = (uint32_t)(buf >> (64 - k));
         skip(k);
         return v;
@@ -133,8 +143,18 @@ __device__ __forceinline__ int extend(uint32_t v, int s)
     return (int)v < (1 << (s - 1)) ? (int)v - (1 << s) + 1 : (int)v;
 }
 
+// What the Huffman passes need of an image, staged in LDS per workgroup (a
+// register copy of the whole JpegImageDev spilled 712 B per lane to scratch).
+struct DecGeom {
+    int64_t comp_block0[kJpegMaxComp];
+    int32_t bpm, mcux;
+    int32_t slot_comp[kJpegMaxSlots], slot_h[kJpegMaxSlots], slot_v[kJpegMaxSlots];
+    int32_t comp_h[kJpegMaxComp], comp_v[kJpegMaxComp], comp_bw[kJpegMaxComp];
+    int32_t dc_tab[kJpegMaxComp], ac_tab[kJpegMaxComp];  // LDS table slots
+};
+
 // Coefficient-array index of decode-order block g of an image.
-__device__ __forceinline__ int64_t block_index(const JpegImageDev& im, int64_t g)
+__device__ __forceinline__ int64_t block_index(const DecGeom& im, int64_t g)
 {
     const int64_t mcu = g / im.bpm;
     const int slot = (int)(g - mcu * im.bpm);
@@ -149,7 +169,7 @@ __device__ __forceinline__ int64_t block_index(const JpegImageDev& im, int64_t g
 // coefficients of blocks [g0, block_end) (g = decode-order block index of the
 // block in progress), absolute DC values from the running predictors `pred`.
 template <bool WRITE>
-__device__ void decode_run(const JpegImageDev& im, const HuffDev* tabs, BitReader& br, int64_t stop,
+__device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br, int64_t stop,
                            DecState& st, int64_t& started, int32_t (&dc)[kJpegMaxComp], int64_t g,
                            int64_t block_lo, int64_t block_end, int16_t* coef)
 {
@@ -157,8 +177,10 @@ __device__ void decode_run(const JpegImageDev& im, const HuffDev* tabs, BitReade
     if (WRITE && g >= block_lo && g < block_end) blk = block_index(im, g);
     while (br.p < stop) {
         const int c = im.slot_comp[st.slot];
+        // one table lookup for both symbol kinds keeps the lanes of a wave together
+        const int sym = huff_decode(tabs[st.k == 0 ? im.dc_tab[c] : im.ac_tab[c]], br);
         if (st.k == 0) {
-            const int s = min(huff_decode(tabs[im.dc_tab[c]], br), 16);  // > 11 only in corrupt streams
+            const int s = min(sym, 16);  // > 11 only in corrupt streams
             const int diff = s ? extend(br.get(s), s) : 0;
             ++started;
             dc[c] += diff;
@@ -169,8 +191,7 @@ __device__ void decode_run(const JpegImageDev& im, const HuffDev* tabs, BitReade
             }
             st.k = 1;
         } else {
-            const int rs = huff_decode(tabs[im.ac_tab[c]], br);
-            const int r = rs >> 4, s = rs & 15;
+            const int r = sym >> 4, s = sym & 15;
             if (s) {
                 st.k += r;
                 const int v = extend(br.get(s), s);
@@ -190,6 +211,50 @@ __device__ void decode_run(const JpegImageDev& im, const HuffDev* tabs, BitReade
     st.p = br.p;
 }
 
+// The image's Huffman tables, staged in LDS: slot 2c = DC table of component
+// c, 2c + 1 = its AC table.  Every workgroup serves one image (the host pads
+// each image's subsequences to whole workgroups).
+struct ImgTabs {
+    HuffDev t[2 * kJpegMaxComp];
+    DecGeom g;
+};
+
+__device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageDev* imp, ImgTabs& lds)
+{
+    constexpr int kWords = sizeof(HuffDev) / 4;
+    static_assert(sizeof(HuffDev) % 4 == 0, "word copy");
+    const int ncomp = imp->ncomp;
+    for (int c = 0; c < ncomp; ++c) {
+        const uint32_t* sdc = reinterpret_cast<const uint32_t*>(P.huff + imp->dc_tab[c]);
+        const uint32_t* sac = reinterpret_cast<const uint32_t*>(P.huff + imp->ac_tab[c]);
+        uint32_t* ddc = reinterpret_cast<uint32_t*>(&lds.t[2 * c]);
+        uint32_t* dac = reinterpret_cast<uint32_t*>(&lds.t[2 * c + 1]);
+        for (int w = threadIdx.x; w < kWords; w += kJThreads) {
+            ddc[w] = sdc[w];
+            dac[w] = sac[w];
+        }
+    }
+    if (threadIdx.x == 0) {
+        DecGeom& g = lds.g;
+        g.bpm = imp->bpm;
+        g.mcux = imp->mcux;
+        for (int k = 0; k < kJpegMaxSlots; ++k) {
+            g.slot_comp[k] = imp->slot_comp[k];
+            g.slot_h[k] = imp->slot_h[k];
+            g.slot_v[k] = imp->slot_v[k];
+        }
+        for (int c = 0; c < kJpegMaxComp; ++c) {
+            g.comp_block0[c] = imp->comp_block0[c];
+            g.comp_h[c] = imp->comp_h[c];
+            g.comp_v[c] = imp->comp_v[c];
+            g.comp_bw[c] = imp->comp_bw[c];
+            g.dc_tab[c] = 2 * c;
+            g.ac_tab[c] = 2 * c + 1;
+        }
+    }
+    __syncthreads();
+}
+
 // Pass over every subsequence.  round 0: start from the guessed state at the
 // subsequence start; round > 0: from the previous round's end state of the
 // previous subsequence (the segment's first subsequence starts exactly).
@@ -197,12 +262,14 @@ __global__ __launch_bounds__(kJThreads) void jpeg_sync_kernel(JpegPlan P, const 
                                                              SubResult* next, int round, int* changed)
 {
     const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
-    if (i >= P.n_sub) return;
+    __shared__ ImgTabs tabs;
+    stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);
+    const DecGeom& im = tabs.g;
+    if (i >= P.n_sub || P.sub_seg[i] < 0) return;  // padding lane
     const JpegSegDev sg = P.segs[P.sub_seg[i]];
     const int64_t j = i - sg.sub0;  // index inside the segment
     const int64_t b0 = sg.bit0 + j * P.sub_bits;
     const int64_t b1 = min(sg.bit0 + (j + 1) * P.sub_bits, sg.bit0 + sg.bits);
-    const JpegImageDev& im = P.imgs[sg.img];
     DecState st;
     if (j == 0 || round == 0) {  // exact at a segment start, a guess elsewhere in round 0
         st.p = b0;
@@ -217,7 +284,7 @@ __global__ __launch_bounds__(kJThreads) void jpeg_sync_kernel(JpegPlan P, const 
     int32_t dc[kJpegMaxComp] = {0, 0, 0};
     BitReader br;
     br.reset(P.stream, st.p);
-    decode_run<false>(im, P.huff, br, b1, st, r.started, dc, 0, 0, 0, nullptr);
+    decode_run<false>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr);
     r.end = st;
     for (int c = 0; c < kJpegMaxComp; ++c) r.dc[c] = dc[c];
     if (round > 0) {
@@ -238,7 +305,7 @@ struct SubBase {
 __global__ __launch_bounds__(256) void jpeg_scan_kernel(JpegPlan P, const SubResult* res, SubBase* base)
 {
     const JpegSegDev sg = P.segs[blockIdx.x];
-    const int64_t n = (blockIdx.x + 1 < P.n_seg) ? P.segs[blockIdx.x + 1].sub0 - sg.sub0 : P.n_sub - sg.sub0;
+    const int64_t n = sg.n_sub;
     __shared__ int64_t sb[256];
     __shared__ int32_t sd[kJpegMaxComp][256];
     __shared__ int64_t carry_b;
@@ -294,11 +361,13 @@ __global__ __launch_bounds__(kJThreads) void jpeg_write_kernel(JpegPlan P, const
                                                               const SubBase* base)
 {
     const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
-    if (i >= P.n_sub) return;
+    __shared__ ImgTabs tabs;
+    stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);
+    const DecGeom& im = tabs.g;
+    if (i >= P.n_sub || P.sub_seg[i] < 0) return;  // padding lane
     const JpegSegDev sg = P.segs[P.sub_seg[i]];
     const int64_t j = i - sg.sub0;
     const int64_t b1 = min(sg.bit0 + (j + 1) * P.sub_bits, sg.bit0 + sg.bits);
-    const JpegImageDev& im = P.imgs[sg.img];
     DecState st;
     if (j == 0) {
         st.p = sg.bit0;
@@ -313,7 +382,7 @@ __global__ __launch_bounds__(kJThreads) void jpeg_write_kernel(JpegPlan P, const
     BitReader br;
     br.reset(P.stream, st.p);
     // the block in progress at the start was started by an earlier lane
-    decode_run<true>(im, P.huff, br, b1, st, started, dc, sg.block0 + b.block - 1, sg.block0,
+    decode_run<true>(im, tabs.t, br, b1, st, started, dc, sg.block0 + b.block - 1, sg.block0,
                      sg.block_end, P.coef);
 }
 

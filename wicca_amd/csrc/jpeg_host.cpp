@@ -218,36 +218,43 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
     return 0;
 }
 
-void jpeg_destuff(const JpegInfo& info, std::vector<uint8_t>& out, std::vector<int64_t>& seg_off)
+size_t jpeg_destuff_into(const JpegInfo& info, uint8_t* out, std::vector<int64_t>& seg_off)
 {
     const uint8_t* s = info.scan;
     const size_t n = info.scan_len;
-    out.clear();
-    out.reserve(n);
+    size_t o = 0;
     seg_off.assign(1, 0);
     size_t i = 0;
     while (i < n) {
         const uint8_t* ff = (const uint8_t*)memchr(s + i, 0xFF, n - i);
         const size_t run = ff ? (size_t)(ff - (s + i)) : n - i;
-        out.insert(out.end(), s + i, s + i + run);
+        memcpy(out + o, s + i, run);
+        o += run;
         i += run;
         if (i >= n) break;
         // s[i] == 0xFF
         if (i + 1 >= n) break;
         const uint8_t nx = s[i + 1];
         if (nx == 0x00) {  // stuffed data byte
-            out.push_back(0xFF);
+            out[o++] = 0xFF;
             i += 2;
         } else if (nx == 0xFF) {  // fill byte
             i += 1;
         } else if (nx >= 0xD0 && nx <= 0xD7) {  // RSTn: next segment starts byte-aligned
-            seg_off.push_back((int64_t)out.size());
+            seg_off.push_back((int64_t)o);
             i += 2;
         } else {
             break;  // EOI or another marker: end of the scan
         }
     }
-    seg_off.push_back((int64_t)out.size());
+    seg_off.push_back((int64_t)o);
+    return o;
+}
+
+void jpeg_destuff(const JpegInfo& info, std::vector<uint8_t>& out, std::vector<int64_t>& seg_off)
+{
+    out.resize(info.scan_len);
+    out.resize(jpeg_destuff_into(info, out.data(), seg_off));
 }
 
 void build_huff_dev(const JpegHuffTable& t, HuffDev* d)
