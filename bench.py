@@ -73,7 +73,7 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--dry-run", action="store_true",
                     help="print each rank's (rank, world) and exit before touching the GPU")
-    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r01b.json"),
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r02.json"),
                     help="PMC summary (rocprofv3 FETCH_SIZE/WRITE_SIZE) for roofline.traffic")
     return ap.parse_args()
 
