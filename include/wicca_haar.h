@@ -91,7 +91,9 @@ int wicca_balance_ranges(const int64_t* weights, int64_t n, int n_ranges, int64_
 
 /* Device memory held by idle pooled workspaces of `device` (-1: all devices).
  * The pool keeps at most WICCA_WORKSPACE_CAP_MB (default 4096) idle per
- * device; a workspace returned above the cap frees its buffers first. */
+ * device: when a returned workspace takes the device above the cap, the least
+ * recently used other workspaces free their buffers (the returned one keeps
+ * its own, so a batch larger than the cap does not re-allocate every call). */
 int64_t wicca_workspace_bytes(int device);
 
 /* Set the idle-pool cap in bytes (bytes < 0: leave it); returns the previous

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <thread>
 #include <cstdio>
@@ -219,18 +220,38 @@ size_t idle_bytes_locked(int device)
     return b;
 }
 
+// Returning a workspace: it goes to the back of the idle pool (most recent);
+// if the device's idle buffers then exceed the cap, the least recently used
+// OTHER idle workspaces give theirs back (streams and events stay pooled).
+// The returned workspace keeps its buffers even when it alone exceeds the cap:
+// releasing it made every large batch re-allocate its device and pinned
+// buffers on every call (the JPEG stage lost 16 ms a call that way).
 struct WorkspaceLease {
     Workspace* ws = nullptr;
     ~WorkspaceLease()
     {
         if (!ws) return;
-        std::unique_lock<std::mutex> g(g_pool_mu);
-        if (idle_bytes_locked(ws->device) + ws->bytes() > pool_cap_bytes()) {
-            g.unlock();
-            ws->release_buffers();  // its stream and events stay pooled
-            g.lock();
+        std::vector<std::unique_ptr<Workspace>> trim;
+        {
+            std::lock_guard<std::mutex> g(g_pool_mu);
+            g_pool.emplace_back(ws);
+            size_t idle = idle_bytes_locked(ws->device);
+            for (size_t i = 0; i + 1 < g_pool.size() && idle > pool_cap_bytes();) {
+                Workspace* w = g_pool[i].get();
+                if (w->device == ws->device && w->bytes() > 0) {
+                    idle -= w->bytes();
+                    trim.push_back(std::move(g_pool[i]));
+                    g_pool.erase(g_pool.begin() + i);
+                } else {
+                    ++i;
+                }
+            }
         }
-        g_pool.emplace_back(ws);
+        for (auto& w : trim) w->release_buffers();  // not in the pool: nobody can lease it meanwhile
+        if (!trim.empty()) {
+            std::lock_guard<std::mutex> g(g_pool_mu);
+            for (auto& w : trim) g_pool.insert(g_pool.begin(), std::move(w));
+        }
     }
 };
 
@@ -1309,10 +1330,22 @@ void oriented_dims(const wicca::JpegInfo& in, bool apply, int64_t* h, int64_t* w
 // Decode n JPEG files into device RGB images dst[i] (pitch dpitch[i]); EXIF
 // orientation applied when `orient`.  Synchronous on `stream` for the host
 // tables; the pixels are ready in stream order.
+bool jpeg_timing()
+{
+    static const bool on = getenv("WICCA_JPEG_TIMING") != nullptr;
+    return on;
+}
+
+double now_ms()
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
                           uint8_t* const* dst, const int64_t* dpitch, bool orient, hipStream_t stream,
                           int* rounds_out)
 {
+    const double t_start = now_ms();
     std::vector<wicca::JpegInfo> info((size_t)n);
     for (int64_t i = 0; i < n; ++i) {
         int rc = parse_one(data[i], sizes[i], &info[(size_t)i], i);
@@ -1347,6 +1380,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         work();
         for (auto& t : th) t.join();
     }
+    const double t_destuffed = now_ms();
     int64_t total_bits = 0;
     for (int64_t i = 0; i < n; ++i) total_bits += seg_off[(size_t)i].back() * 8;
     const int64_t S = jpeg_sub_bits(total_bits);
@@ -1468,6 +1502,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     P.n_seg = (int64_t)segs.size();
     P.sub_bits = (int32_t)S;
     int rounds = 0;
+    const double t_upload = now_ms();
     HIP_TRY(wicca::jpeg_decode_device(P, ims.data(), ws->jscratch.ptr, n, &rounds, stream));
     if (rounds_out) *rounds_out = rounds;
     for (int64_t i = 0; i < n; ++i)
@@ -1477,6 +1512,10 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
                                          stream));
     // packed / stream_h are host copies consumed by the synchronous upload above
     HIP_TRY(hipStreamSynchronize(stream));
+    if (jpeg_timing())
+        fprintf(stderr, "[wicca jpeg] %lld files: parse+destuff %.2f ms, tables+upload issue %.2f ms, "
+                "device decode %.2f ms (%d sync passes), sub_bits %lld\n", (long long)n, t_destuffed - t_start,
+                t_upload - t_destuffed, now_ms() - t_upload, rounds, (long long)S);
     return WICCA_OK;
 }
 

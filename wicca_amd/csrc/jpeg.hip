@@ -153,28 +153,50 @@ struct DecGeom {
     int32_t dc_tab[kJpegMaxComp], ac_tab[kJpegMaxComp];  // LDS table slots
 };
 
-// Coefficient-array index of decode-order block g of an image.
-__device__ __forceinline__ int64_t block_index(const DecGeom& im, int64_t g)
-{
-    const int64_t mcu = g / im.bpm;
-    const int slot = (int)(g - mcu * im.bpm);
-    const int c = im.slot_comp[slot];
-    const int64_t mx = mcu % im.mcux, my = mcu / im.mcux;
-    const int64_t bx = mx * im.comp_h[c] + im.slot_h[slot];
-    const int64_t by = my * im.comp_v[c] + im.slot_v[slot];
-    return im.comp_block0[c] + by * im.comp_bw[c] + bx;
-}
+// Position of a decode-order block: MCU column / row and slot, advanced
+// incrementally (one division per lane instead of three 64-bit ones per block).
+struct BlockPos {
+    uint32_t mx, my, slot;
+    __device__ void init(const DecGeom& im, int64_t g)
+    {
+        const uint32_t gg = (uint32_t)g, bpm = (uint32_t)im.bpm, mcu = gg / bpm;
+        slot = gg - mcu * bpm;
+        my = mcu / (uint32_t)im.mcux;
+        mx = mcu - my * (uint32_t)im.mcux;
+    }
+    __device__ void next(const DecGeom& im)
+    {
+        if (++slot == (uint32_t)im.bpm) {
+            slot = 0;
+            if (++mx == (uint32_t)im.mcux) {
+                mx = 0;
+                ++my;
+            }
+        }
+    }
+    __device__ int64_t index(const DecGeom& im) const
+    {
+        const int c = im.slot_comp[slot];
+        const int64_t bx = (int64_t)mx * im.comp_h[c] + im.slot_h[slot];
+        const int64_t by = (int64_t)my * im.comp_v[c] + im.slot_v[slot];
+        return im.comp_block0[c] + by * im.comp_bw[c] + bx;
+    }
+};
 
 // Decode the codewords that start in [state.p, stop).  WRITE: scatter
-// coefficients of blocks [g0, block_end) (g = decode-order block index of the
-// block in progress), absolute DC values from the running predictors `pred`.
+// coefficients of blocks [block_lo, block_end) (g = decode-order block index of
+// the block in progress), absolute DC values from the running predictors.
 template <bool WRITE>
 __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br, int64_t stop,
                            DecState& st, int64_t& started, int32_t (&dc)[kJpegMaxComp], int64_t g,
                            int64_t block_lo, int64_t block_end, int16_t* coef)
 {
     int64_t blk = -1;
-    if (WRITE && g >= block_lo && g < block_end) blk = block_index(im, g);
+    BlockPos pos;
+    if (WRITE) {
+        pos.init(im, g < 0 ? 0 : g);
+        if (g >= block_lo && g < block_end) blk = pos.index(im);
+    }
     while (br.p < stop) {
         const int c = im.slot_comp[st.slot];
         // one table lookup for both symbol kinds keeps the lanes of a wave together
@@ -185,8 +207,9 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
             ++started;
             dc[c] += diff;
             if (WRITE) {
+                if (g >= 0) pos.next(im);
                 ++g;
-                blk = (g >= block_lo && g < block_end) ? block_index(im, g) : -1;
+                blk = (g >= block_lo && g < block_end) ? pos.index(im) : -1;
                 if (blk >= 0) coef[blk * 64] = (int16_t)dc[c];
             }
             st.k = 1;
@@ -575,32 +598,51 @@ __device__ __forceinline__ int chroma_sample(const uint8_t* plane, int64_t pitch
 
 __device__ __forceinline__ uint8_t clamp255(int v) { return (uint8_t)min(255, max(0, v)); }
 
+// Four output pixels per lane: one dword of Y, the chroma samples of the four
+// (shared neighbours hit in L1), 12 bytes of RGB as three dword stores.
 __global__ __launch_bounds__(256) void jpeg_color_kernel(JpegPlan P, int img)
 {
     const JpegImageDev& im = P.imgs[img];
-    const int x = blockIdx.x * 256 + threadIdx.x, y = blockIdx.y;
-    if (x >= im.W) return;
-    uint8_t* o = im.dst + (int64_t)y * im.dst_pitch + (int64_t)x * 3;
-    const int64_t py = (int64_t)im.comp_bw[0] * 8;
-    const int Y = P.planes[im.comp_plane0[0] + (int64_t)y * py + x];
+    const int x0 = (blockIdx.x * 256 + threadIdx.x) * 4, y = blockIdx.y;
+    if (x0 >= im.W) return;
+    const int nx = min(4, im.W - x0);
+    // the Y plane is whole 8x8 blocks wide and 256-B aligned: x0..x0+3 is inside
+    const uint32_t y4 = *reinterpret_cast<const uint32_t*>(
+        P.planes + im.comp_plane0[0] + (int64_t)y * ((int64_t)im.comp_bw[0] * 8) + x0);
+    uint8_t o[12];
     if (im.ncomp == 1) {
-        o[0] = o[1] = o[2] = (uint8_t)Y;
-        return;
-    }
-    int cc[2];
 #pragma unroll
-    for (int k = 1; k <= 2; ++k) {
-        const int fh = im.hmax / im.comp_h[k], fv = im.vmax / im.comp_v[k];
-        cc[k - 1] = chroma_sample(P.planes + im.comp_plane0[k], (int64_t)im.comp_bw[k] * 8, im.comp_dw[k],
-                                  im.comp_dh[k], fh, fv, x, y);
+        for (int q = 0; q < 4; ++q) o[3 * q] = o[3 * q + 1] = o[3 * q + 2] = (uint8_t)(y4 >> (8 * q));
+    } else {
+        const int fh1 = im.hmax / im.comp_h[1], fv1 = im.vmax / im.comp_v[1];
+        const int fh2 = im.hmax / im.comp_h[2], fv2 = im.vmax / im.comp_v[2];
+        const uint8_t* pb = P.planes + im.comp_plane0[1];
+        const uint8_t* pr = P.planes + im.comp_plane0[2];
+        const int64_t sb = (int64_t)im.comp_bw[1] * 8, sr = (int64_t)im.comp_bw[2] * 8;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int x = min(x0 + q, im.W - 1);
+            const int Y = (int)((y4 >> (8 * q)) & 255);
+            const int cb = chroma_sample(pb, sb, im.comp_dw[1], im.comp_dh[1], fh1, fv1, x, y) - 128;
+            const int cr = chroma_sample(pr, sr, im.comp_dw[2], im.comp_dh[2], fh2, fv2, x, y) - 128;
+            const int crr = (int)((91881 * (int64_t)cr + 32768) >> 16);
+            const int cbb = (int)((116130 * (int64_t)cb + 32768) >> 16);
+            const int64_t crg = -46802 * (int64_t)cr, cbg = -22554 * (int64_t)cb + 32768;
+            o[3 * q] = clamp255(Y + crr);
+            o[3 * q + 1] = clamp255(Y + (int)((cbg + crg) >> 16));
+            o[3 * q + 2] = clamp255(Y + cbb);
+        }
     }
-    const int cb = cc[0] - 128, cr = cc[1] - 128;
-    const int crr = (int)((91881 * (int64_t)cr + 32768) >> 16);
-    const int cbb = (int)((116130 * (int64_t)cb + 32768) >> 16);
-    const int64_t crg = -46802 * (int64_t)cr, cbg = -22554 * (int64_t)cb + 32768;
-    o[0] = clamp255(Y + crr);
-    o[1] = clamp255(Y + (int)((cbg + crg) >> 16));
-    o[2] = clamp255(Y + cbb);
+    uint8_t* d = im.dst + (int64_t)y * im.dst_pitch + (int64_t)x0 * 3;
+    if (nx == 4 && ((uintptr_t)d & 3) == 0) {
+        uint32_t* d32 = reinterpret_cast<uint32_t*>(d);
+#pragma unroll
+        for (int w = 0; w < 3; ++w)
+            d32[w] = (uint32_t)o[4 * w] | ((uint32_t)o[4 * w + 1] << 8) | ((uint32_t)o[4 * w + 2] << 16) |
+                     ((uint32_t)o[4 * w + 3] << 24);
+    } else {
+        for (int i = 0; i < 3 * nx; ++i) d[i] = o[i];
+    }
 }
 
 // EXIF orientation (tag 0x0112), as cv2.imread applies it for IMREAD_COLOR:
@@ -708,7 +750,7 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     for (int64_t i = 0; i < n_images; ++i) {
         const JpegImageDev& im = ims[(size_t)i];
-        hipLaunchKernelGGL(jpeg_color_kernel, dim3((uint32_t)((im.W + 255) / 256), (uint32_t)im.H), dim3(256),
+        hipLaunchKernelGGL(jpeg_color_kernel, dim3((uint32_t)((im.W + 1023) / 1024), (uint32_t)im.H), dim3(256),
                            0, s, P, (int)i);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
