@@ -280,6 +280,15 @@ int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, i
                              int64_t out_w, int64_t out_h, int interpolation,
                              uint8_t* resized, uint8_t* resized_icons, int device);
 
+/* wicca_jpeg_icon_stage_u8 over several GPUs of one process: contiguous file
+ * ranges balanced by file size, one host thread per device (devices NULL /
+ * n_devices 0: every visible device); same outputs as the one-device call. */
+int wicca_jpeg_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                                    int depth, int border_type, int border_constant,
+                                    int64_t out_w, int64_t out_h, int interpolation,
+                                    uint8_t* resized, uint8_t* resized_icons,
+                                    const int* devices, int n_devices);
+
 /*
  * Deterministic synthetic images on device (no PCIe in timed regions):
  * byte (i, y, x, c) = splitmix64-hash of (seed, i, y*W*C + x*C + c), see

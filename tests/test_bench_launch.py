@@ -10,6 +10,8 @@ import re
 import subprocess
 import sys
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = os.path.join(REPO, "bench.py")
 
@@ -21,14 +23,16 @@ def _env(**extra):
     return env
 
 
-def test_gpus_n_spawns_n_ranks():
-    out = subprocess.run([sys.executable, BENCH, "--gpus", "3", "--dry-run"], env=_env(),
+@pytest.mark.parametrize("n", [3, 8])  # 8: BASELINE configs[3], 1024 x 8K over 8 GPUs
+def test_gpus_n_spawns_n_ranks(n):
+    out = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--dry-run"], env=_env(),
                          capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stderr
     # ranks share the pipe: take every JSON object, whatever the line breaks
     lines = [json.loads(m) for m in re.findall(r"\{[^{}]*\}", out.stdout)]
-    assert sorted(d["rank"] for d in lines) == [0, 1, 2]
-    assert all(d["world"] == 3 for d in lines)
+    assert sorted(d["rank"] for d in lines) == list(range(n))
+    assert sorted(d["local_rank"] for d in lines) == list(range(n))
+    assert all(d["world"] == n for d in lines)
 
 
 def test_world_size_mismatch_refused():

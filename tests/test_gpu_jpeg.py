@@ -111,3 +111,46 @@ def test_file_caller_stage(tmp_path, depth, shape):
         assert np.array_equal(imgs[i], R.resize(rgb, shape, R.INTER_AREA)), i
         icon = c_oracle.ll_int_block(rgb, depth)[0]
         assert np.array_equal(icons[i], R.resize(icon, shape, R.INTER_AREA)), i
+
+
+def test_file_caller_stage_split_over_devices(tmp_path):
+    """The one-process multi-GPU form (devices=[0, 0] exercises the split and
+    the per-range output offsets on a one-GPU box)."""
+    paths = []
+    for i, (h, w) in enumerate([(200, 300), (480, 640), (100, 100), (333, 517), (640, 480)]):
+        p = tmp_path / f"m{i}.jpg"
+        p.write_bytes(J.encode(J.test_image("scene", h, w, 50 + i), 80, 2))
+        paths.append(str(p))
+    one = wicca_amd.get_img_batch(paths, (224, 224), 4)
+    two = wicca_amd.get_img_batch(paths, (224, 224), 4, devices=[0, 0])
+    assert np.array_equal(one[0], two[0]) and np.array_equal(one[1], two[1])
+
+
+@pytest.mark.parametrize("cut", [0.3, 0.7, 0.95])
+def test_truncated_file_decodes_without_fault(cut):
+    """A file cut inside its entropy-coded data: the decode must stay inside
+    its buffers (missing blocks come out as the DC-0 grey libjpeg also
+    substitutes); the decoded part before the cut must match libjpeg-turbo's."""
+    img = J.test_image("scene", 256, 384, 11)
+    data = J.encode(img, 90, 2, restart_blocks=8)
+    short = data[:int(len(data) * cut)]
+    got = WJ.decode(short)
+    assert got.shape == (256, 384, 3)
+    full = J.decode_rgb(data)
+    assert np.array_equal(got[:16], full[:16]) if cut >= 0.3 else True
+
+
+def test_corrupted_bits_decode_without_fault():
+    """Flipped bytes in the entropy-coded data (not in markers): garbage
+    pixels are fine, faults and hangs are not; the next clean file decodes."""
+    img = J.test_image("noise", 200, 300, 12)
+    data = bytearray(J.encode(img, 75, 2))
+    rng = np.random.default_rng(5)
+    sos = bytes(data).index(b"\xff\xda")
+    for pos in rng.integers(sos + 20, len(data) - 4, 40):
+        if data[pos] != 0xFF and data[pos - 1] != 0xFF:
+            data[pos] ^= 0x5A if data[pos] ^ 0x5A != 0xFF else 0x01
+    got = WJ.decode(bytes(data))
+    assert got.shape == (200, 300, 3)
+    ok = J.encode(img, 75, 2)
+    assert np.array_equal(WJ.decode(ok), J.decode_rgb(ok))

@@ -17,6 +17,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdarg>
+#include <functional>
 #include <thread>
 #include <cstdio>
 #include <cstdlib>
@@ -637,6 +638,46 @@ void balance_ranges(const int64_t* w, int64_t n, int nr, int64_t* first)
     for (int k = r + 1; k <= nr; ++k) first[k] = n;
 }
 
+// Contiguous item ranges balanced by weight, at most one per device, each run
+// by its own host thread: fn(first, last, device).  The first failure's
+// status and message are returned.
+int split_over_devices(const std::vector<int64_t>& weights, const int* devices, int n_devices,
+                       const std::function<int(int64_t, int64_t, int)>& fn)
+{
+    const int64_t n = (int64_t)weights.size();
+    init_once();
+    if (g_device_count <= 0) return fail(WICCA_ERR_NODEVICE, "no HIP device visible");
+    std::vector<int> devs;
+    if (devices && n_devices > 0) {
+        devs.assign(devices, devices + n_devices);
+    } else {
+        for (int d = 0; d < g_device_count; ++d) devs.push_back(d);
+    }
+    for (int d : devs)
+        if (d < 0 || d >= g_device_count) return fail(WICCA_ERR_ARG, "device %d out of range", d);
+    const int nd = (int)std::min<int64_t>((int64_t)devs.size(), n);
+    std::vector<int64_t> first((size_t)nd + 1);  // range r = items [first[r], first[r+1])
+    balance_ranges(weights.data(), n, nd, first.data());
+    std::vector<int> rcs((size_t)nd, WICCA_OK);
+    std::vector<std::string> msgs((size_t)nd);
+    auto work = [&](int r) {
+        const int64_t a = first[(size_t)r], b = first[(size_t)r + 1];
+        if (b <= a) return;
+        rcs[(size_t)r] = fn(a, b, devs[(size_t)r]);
+        if (rcs[(size_t)r]) msgs[(size_t)r] = t_last_error;
+    };
+    std::vector<std::thread> pool;
+    for (int r = 1; r < nd; ++r) pool.emplace_back(work, r);
+    work(0);
+    for (auto& t : pool) t.join();
+    for (int r = 0; r < nd; ++r)
+        if (rcs[(size_t)r]) {
+            t_last_error = msgs[(size_t)r];
+            return rcs[(size_t)r];
+        }
+    return WICCA_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -912,42 +953,13 @@ int wicca_haar_ll_u8_batch_multi_gpu(const wicca_image_desc* descs, int64_t n, i
 {
     if (n < 0 || (n > 0 && !descs)) return fail(WICCA_ERR_ARG, "bad descriptor array");
     if (n == 0) return WICCA_OK;
-    init_once();
-    if (g_device_count <= 0) return fail(WICCA_ERR_NODEVICE, "no HIP device visible");
-    std::vector<int> devs;
-    if (devices && n_devices > 0) {
-        devs.assign(devices, devices + n_devices);
-    } else {
-        for (int d = 0; d < g_device_count; ++d) devs.push_back(d);
-    }
-    for (int d : devs)
-        if (d < 0 || d >= g_device_count) return fail(WICCA_ERR_ARG, "device %d out of range", d);
-    // contiguous image ranges balanced by pixel count, at most one per device
-    const int nd = (int)std::min<int64_t>((int64_t)devs.size(), n);
-    std::vector<int64_t> px((size_t)n);
+    std::vector<int64_t> px((size_t)n);  // balanced by pixel count
     for (int64_t i = 0; i < n; ++i)
         px[(size_t)i] = std::max<int64_t>(descs[i].height, 0) * std::max<int64_t>(descs[i].width, 0);
-    std::vector<int64_t> first((size_t)nd + 1);  // range r = images [first[r], first[r+1])
-    balance_ranges(px.data(), n, nd, first.data());
-    std::vector<int> rcs((size_t)nd, WICCA_OK);
-    std::vector<std::string> msgs((size_t)nd);
-    auto work = [&](int r) {
-        const int64_t a = first[(size_t)r], b = first[(size_t)r + 1];
-        if (b <= a) return;
-        rcs[(size_t)r] = wicca_haar_ll_u8_batch(descs + a, b - a, C, depth, border_type,
-                                                border_constant, 0, 0, devs[(size_t)r], nullptr);
-        if (rcs[(size_t)r]) msgs[(size_t)r] = t_last_error;
-    };
-    std::vector<std::thread> pool;
-    for (int r = 1; r < nd; ++r) pool.emplace_back(work, r);
-    work(0);
-    for (auto& t : pool) t.join();
-    for (int r = 0; r < nd; ++r)
-        if (rcs[(size_t)r]) {
-            t_last_error = msgs[(size_t)r];
-            return rcs[(size_t)r];
-        }
-    return WICCA_OK;
+    return split_over_devices(px, devices, n_devices, [&](int64_t a, int64_t b, int dev) {
+        return wicca_haar_ll_u8_batch(descs + a, b - a, C, depth, border_type, border_constant, 0, 0, dev,
+                                      nullptr);
+    });
 }
 
 int wicca_haar_ll_u8_multi(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t src_pitch,
@@ -1589,6 +1601,28 @@ int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64
 }
 
 int wicca_jpeg_last_sync_rounds(void) { return t_jpeg_rounds; }
+
+int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
+                             int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                             int interpolation, uint8_t* resized, uint8_t* resized_icons, int device);
+
+int wicca_jpeg_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
+                                    int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                                    int interpolation, uint8_t* resized, uint8_t* resized_icons,
+                                    const int* devices, int n_devices)
+{
+    if (n < 0 || (n > 0 && (!data || !sizes))) return fail(WICCA_ERR_ARG, "bad arrays");
+    if (n == 0) return WICCA_OK;
+    if (!resized || !resized_icons) return fail(WICCA_ERR_ARG, "output buffer is NULL");
+    if (out_w <= 0 || out_h <= 0) return fail(WICCA_ERR_ARG, "bad output size");
+    const int64_t ob = out_w * out_h * 3;
+    // balanced by file size (the compressed bytes are what each device decodes)
+    std::vector<int64_t> w(sizes, sizes + n);
+    return split_over_devices(w, devices, n_devices, [&](int64_t a, int64_t b, int dev) {
+        return wicca_jpeg_icon_stage_u8(data + a, sizes + a, b - a, depth, border_type, border_constant, out_w,
+                                        out_h, interpolation, resized + a * ob, resized_icons + a * ob, dev);
+    });
+}
 
 int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
                              int border_type, int border_constant, int64_t out_w, int64_t out_h,

@@ -80,11 +80,13 @@ def load_image(file_path: str) -> np.ndarray | None:
 
 
 def get_img_batch(file_paths: Sequence[str], shape, transform_depth: int, interpolation: int = 3,
-                  border_type: int = 1, border_constant: int = 0,
-                  device: int | None = None) -> tuple[np.ndarray, np.ndarray]:
+                  border_type: int = 1, border_constant: int = 0, device: int | None = None,
+                  devices: Sequence[int] | None = None) -> tuple[np.ndarray, np.ndarray]:
     """``ClassifierProcessor._get_img_batch`` (classifying_tools.py:297-323)
     from file paths: GPU decode + resize + icon + icon resize; only the
-    compressed files cross PCIe.  Returns ``(batch_images, batch_icons)``."""
+    compressed files cross PCIe.  Returns ``(batch_images, batch_icons)``.
+    With ``devices`` (several ids) the files are split over those GPUs,
+    balanced by file size, one host thread each."""
     from .coder import _border_value, _depth_index
     blobs = []
     for p in file_paths:
@@ -100,9 +102,16 @@ def get_img_batch(file_paths: Sequence[str], shape, transform_depth: int, interp
     icons = np.empty((n, out_h, out_w, 3), np.uint8)
     keep, ptrs, sizes = _buffers(blobs)
     k = _border_value(border_constant) if int(border_type) == 0 else 0
-    _lib.check(_lib.load().wicca_jpeg_icon_stage_u8(
-        ptrs, sizes, n, _depth_index(transform_depth), int(border_type), k, out_w, out_h,
-        int(interpolation), resized.ctypes.data, icons.ctypes.data,
-        -1 if device is None else int(device)))
+    lib = _lib.load()
+    if devices is not None and len(devices) > 1:
+        devs = (ctypes.c_int * len(devices))(*devices)
+        _lib.check(lib.wicca_jpeg_icon_stage_multi_gpu(
+            ptrs, sizes, n, _depth_index(transform_depth), int(border_type), k, out_w, out_h,
+            int(interpolation), resized.ctypes.data, icons.ctypes.data, devs, len(devices)))
+    else:
+        dev = devices[0] if devices else (-1 if device is None else int(device))
+        _lib.check(lib.wicca_jpeg_icon_stage_u8(
+            ptrs, sizes, n, _depth_index(transform_depth), int(border_type), k, out_w, out_h,
+            int(interpolation), resized.ctypes.data, icons.ctypes.data, dev))
     del keep
     return resized, icons
