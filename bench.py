@@ -272,7 +272,7 @@ def run_tiled(args, torch, dist, world, rank, local_rank):
         "roofline": {"bound": "hbm", "achieved": round(band_bytes / (kernel_ms / 1e3) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(band_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": None, "kernel": f"block_sum<L={D},C={C},u8> (rank-0 band)",
+                     "traffic": None, "kernel": lib.wicca_kernel_name(D, C, 0).decode() + " (rank-0 band)",
                      "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": band_bytes},
         "cpu_baseline": None,
         "verified_vs_numpy_port": verified,

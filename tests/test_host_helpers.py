@@ -64,7 +64,7 @@ def test_split_properties(weights, nr):
 def test_kernel_name_matches_dispatch_table(depth):
     lib = _lib.load()
     name = lib.wicca_kernel_name(depth, 3, 0).decode()
-    strip = depth in (2, 3, 5, 6)  # use_strip_kernel (haar_ll.h)
+    strip = depth in (2, 3, 5, 6, 7, 8)  # use_strip_kernel (haar_ll.h)
     assert name == ("haar_strip_kernel" if strip else "haar_block_sum_kernel") + \
         f"<{depth}, 3, unsigned char, false>"
     assert lib.wicca_kernel_name(depth, 1, 1).decode().endswith(f"<{depth}, 1, unsigned char, true>")

@@ -72,12 +72,14 @@
 namespace wicca {
 
 // Which K1 variant serves depth L (in-process A/B, profiles/r01_ab_v7.json,
-// r01_ab_strip_caps.json): the wave-strip kernel at depths 2-3, and at 5-6 when
-// capped at 2 waves/SIMD (+0.4-1.1 % over the LDS-segment kernel); the
-// LDS-segment kernel at depths 1, 4, 7, 8.
+// r01_ab_strip_caps.json; re-measured under the XCD block order,
+// r02_ab_kernel_choice.json, r02_ab_strip78.json): the wave-strip kernel at
+// depths 2-3, and at 5-8 when capped at 2 waves/SIMD (D = 7 +3.2 %, D = 8
+// +2.8 % over the LDS-segment kernel with the XCD order; it lost before); the
+// LDS-segment kernel at depths 1 and 4.
 constexpr bool use_strip_kernel(int L)
 {
-    return WICCA_STRIP >= 0 ? WICCA_STRIP == 1 : (L == 2 || L == 3 || L == 5 || L == 6);
+    return WICCA_STRIP >= 0 ? WICCA_STRIP == 1 : (L == 2 || L == 3 || L >= 5);
 }
 
 // Pixels a strip-kernel lane owns: whole pixels in 12 or 16 contiguous bytes,
