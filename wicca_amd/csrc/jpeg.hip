@@ -619,12 +619,43 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(JpegPlan P, int img)
         const uint8_t* pb = P.planes + im.comp_plane0[1];
         const uint8_t* pr = P.planes + im.comp_plane0[2];
         const int64_t sb = (int64_t)im.comp_bw[1] * 8, sr = (int64_t)im.comp_bw[2] * 8;
+        int cbv[4], crv[4];
+        const bool fast420 = fh1 == 2 && fv1 == 2 && fh2 == 2 && fv2 == 2 && im.comp_dw[1] > 2 &&
+                             im.comp_dw[2] > 2 && im.comp_dw[1] == im.comp_dw[2] && im.comp_dh[1] == im.comp_dh[2];
+        if (fast420) {
+            // h2v2 fancy upsampling of 4 output pixels from chroma columns c-1 .. c+2
+            // of the nearest and the next-nearest chroma row (jdsample.c)
+            const int dw = im.comp_dw[1], dh = im.comp_dh[1];
+            const int c = x0 >> 1, iy = y >> 1;
+            const int oy = (y & 1) ? min(iy + 1, dh - 1) : max(iy - 1, 0);
+            int cc[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cc[k] = min(max(c - 1 + k, 0), dw - 1);
+            auto four = [&](const uint8_t* plane, int64_t pitch, int (&out)[4]) {
+                const uint8_t* r0 = plane + (int64_t)iy * pitch;
+                const uint8_t* r1 = plane + (int64_t)oy * pitch;
+                int t[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) t[k] = r0[cc[k]] * 3 + r1[cc[k]];
+                out[0] = c == 0 ? (t[1] * 4 + 8) >> 4 : (t[1] * 3 + t[0] + 8) >> 4;
+                out[1] = c == dw - 1 ? (t[1] * 4 + 7) >> 4 : (t[1] * 3 + t[2] + 7) >> 4;
+                out[2] = (t[2] * 3 + t[1] + 8) >> 4;
+                out[3] = c + 1 >= dw - 1 ? (t[2] * 4 + 7) >> 4 : (t[2] * 3 + t[3] + 7) >> 4;
+            };
+            four(pb, sb, cbv);
+            four(pr, sr, crv);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int x = min(x0 + q, im.W - 1);
+                cbv[q] = chroma_sample(pb, sb, im.comp_dw[1], im.comp_dh[1], fh1, fv1, x, y);
+                crv[q] = chroma_sample(pr, sr, im.comp_dw[2], im.comp_dh[2], fh2, fv2, x, y);
+            }
+        }
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const int x = min(x0 + q, im.W - 1);
             const int Y = (int)((y4 >> (8 * q)) & 255);
-            const int cb = chroma_sample(pb, sb, im.comp_dw[1], im.comp_dh[1], fh1, fv1, x, y) - 128;
-            const int cr = chroma_sample(pr, sr, im.comp_dw[2], im.comp_dh[2], fh2, fv2, x, y) - 128;
+            const int cb = cbv[q] - 128, cr = crv[q] - 128;
             const int crr = (int)((91881 * (int64_t)cr + 32768) >> 16);
             const int cbb = (int)((116130 * (int64_t)cb + 32768) >> 16);
             const int64_t crg = -46802 * (int64_t)cr, cbg = -22554 * (int64_t)cb + 32768;
