@@ -186,12 +186,22 @@ struct BlockPos {
 // Decode the codewords that start in [state.p, stop).  WRITE: scatter
 // coefficients of blocks [block_lo, block_end) (g = decode-order block index of
 // the block in progress), absolute DC values from the running predictors.
+// Blocks that start AND end inside the lane's range are assembled in the
+// lane's LDS block `lb` and leave as eight 16-B stores (2-byte scattered
+// stores cost 4.5 of the pass's 7 ms); the block in progress at the start
+// (begun by the previous lane) is written coefficient by coefficient, and so
+// is the nonzero part of a block the range ends inside (the next lane writes
+// its other coefficients): no two lanes ever write the same bytes.
+constexpr int kLaneBlock = 72;  // int16 per lane in LDS (144 B: 16-B aligned, spreads banks)
+
 template <bool WRITE>
 __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br, int64_t stop,
                            DecState& st, int64_t& started, int32_t (&dc)[kJpegMaxComp], int64_t g,
-                           int64_t block_lo, int64_t block_end, int16_t* coef)
+                           int64_t block_lo, int64_t block_end, int16_t* coef, int16_t* lb = nullptr)
 {
     int64_t blk = -1;
+    bool staged = false;
+    uint64_t nz = 0;
     BlockPos pos;
     if (WRITE) {
         pos.init(im, g < 0 ? 0 : g);
@@ -210,7 +220,16 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
                 if (g >= 0) pos.next(im);
                 ++g;
                 blk = (g >= block_lo && g < block_end) ? pos.index(im) : -1;
-                if (blk >= 0) coef[blk * 64] = (int16_t)dc[c];
+                if (blk >= 0) {
+#ifndef WICCA_JPEG_ABLATE_STORES
+                    uint4* z = reinterpret_cast<uint4*>(lb);
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) z[q] = make_uint4(0, 0, 0, 0);
+                    lb[0] = (int16_t)dc[c];
+                    nz = 1;
+                    staged = true;
+#endif
+                }
             }
             st.k = 1;
         } else {
@@ -218,7 +237,19 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
             if (s) {
                 st.k += r;
                 const int v = extend(br.get(s), s);
-                if (WRITE && blk >= 0 && st.k < 64) coef[blk * 64 + kNatural[st.k]] = (int16_t)v;
+                if (WRITE && blk >= 0 && st.k < 64) {
+                    const int n = kNatural[st.k];
+#ifndef WICCA_JPEG_ABLATE_STORES
+                    if (staged) {
+                        lb[n] = (int16_t)v;
+                        nz |= 1ull << n;
+                    } else {
+                        coef[blk * 64 + n] = (int16_t)v;
+                    }
+#else
+                    asm volatile("" ::"v"(v), "v"(n));
+#endif
+                }
                 ++st.k;
             } else if (r == 15) {
                 st.k += 16;
@@ -227,8 +258,22 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
             }
         }
         if (st.k >= 64) {
+            if (WRITE && staged) {  // a whole block of this lane: eight 16-B stores
+                const uint4* src = reinterpret_cast<const uint4*>(lb);
+                uint4* dst = reinterpret_cast<uint4*>(coef + blk * 64);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) dst[q] = src[q];
+                staged = false;
+            }
             st.slot = st.slot + 1 == im.bpm ? 0 : st.slot + 1;
             st.k = 0;
+        }
+    }
+    if (WRITE && staged) {  // the range ends inside this block: its nonzero coefficients only
+        while (nz) {
+            const int n = __builtin_ctzll(nz);
+            nz &= nz - 1;
+            coef[blk * 64 + n] = lb[n];
         }
     }
     st.p = br.p;
@@ -385,6 +430,7 @@ __global__ __launch_bounds__(kJThreads) void jpeg_write_kernel(JpegPlan P, const
 {
     const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
     __shared__ ImgTabs tabs;
+    __shared__ __attribute__((aligned(16))) int16_t lanes[kJThreads * kLaneBlock];
     stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);
     const DecGeom& im = tabs.g;
     if (i >= P.n_sub || P.sub_seg[i] < 0) return;  // padding lane
@@ -406,7 +452,7 @@ __global__ __launch_bounds__(kJThreads) void jpeg_write_kernel(JpegPlan P, const
     br.reset(P.stream, st.p);
     // the block in progress at the start was started by an earlier lane
     decode_run<true>(im, tabs.t, br, b1, st, started, dc, sg.block0 + b.block - 1, sg.block0,
-                     sg.block_end, P.coef);
+                     sg.block_end, P.coef, lanes + threadIdx.x * kLaneBlock);
 }
 
 // ---------------------------------------------------------------------------
