@@ -259,11 +259,12 @@ struct WorkspaceLease {
 int acquire(int device, WorkspaceLease& lease)
 {
     {
+        // most recently returned first: its buffers are the ones still allocated
         std::lock_guard<std::mutex> g(g_pool_mu);
-        for (size_t i = 0; i < g_pool.size(); ++i) {
+        for (size_t i = g_pool.size(); i-- > 0;) {
             if (g_pool[i]->device == device) {
                 lease.ws = g_pool[i].release();
-                g_pool.erase(g_pool.begin() + i);
+                g_pool.erase(g_pool.begin() + (std::ptrdiff_t)i);
                 return WICCA_OK;
             }
         }
