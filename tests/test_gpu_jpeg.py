@@ -154,3 +154,12 @@ def test_corrupted_bits_decode_without_fault():
     assert got.shape == (200, 300, 3)
     ok = J.encode(img, 75, 2)
     assert np.array_equal(WJ.decode(ok), J.decode_rgb(ok))
+
+
+def test_batch_larger_than_one_device_pass():
+    """More files than one pass takes (4096 IDCT jobs / 3 components)."""
+    blobs = [J.encode(J.test_image("scene", 16 + i % 5, 24 + i % 7, i), 70 + i % 25, i % 3)
+             for i in range(1400)]
+    got = WJ.decode_batch(blobs)
+    for i in (0, 1364, 1365, 1366, 1399):
+        assert np.array_equal(got[i], J.decode_rgb(blobs[i])), i

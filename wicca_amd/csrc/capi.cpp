@@ -1358,6 +1358,17 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
                           uint8_t* const* dst, const int64_t* dpitch, bool orient, hipStream_t stream,
                           int* rounds_out)
 {
+    // at most kJpegMaxJobs (image, component) IDCT jobs per device pass
+    constexpr int64_t kChunk = wicca::kJpegMaxJobs / wicca::kJpegMaxComp;
+    if (n > kChunk) {
+        for (int64_t a = 0; a < n; a += kChunk) {
+            const int64_t m = std::min(kChunk, n - a);
+            int rc = jpeg_decode_to_device(ws, data + a, sizes + a, m, dst + a, dpitch + a, orient, stream,
+                                           rounds_out);
+            if (rc) return rc;
+        }
+        return WICCA_OK;
+    }
     const double t_start = now_ms();
     std::vector<wicca::JpegInfo> info((size_t)n);
     for (int64_t i = 0; i < n; ++i) {
