@@ -1,0 +1,222 @@
+// capi_internal.h — what the C-ABI translation units share (capi.cpp: pool,
+// device selection, icon entry points; capi_resize.cpp: cv2.resize and the
+// decoded-image caller stage; capi_jpeg.cpp: JPEG decode and the file stage).
+// Internal to libwicca_hip.so; the public boundary is include/wicca_haar.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../../include/wicca_haar.h"
+#include "haar_ll.h"
+#include "resize.h"
+
+namespace wicca_capi {
+
+extern thread_local std::string t_last_error;
+
+// Set the thread's last error (printf format) and return `code`.
+int fail(int code, const char* fmt, ...);
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess)                                                             \
+            return ::wicca_capi::fail(e_ == hipErrorOutOfMemory ? WICCA_ERR_NOMEM : WICCA_ERR_HIP, \
+                                      "HIP error %d (%s) in %s", (int)e_, hipGetErrorString(e_), #expr); \
+    } while (0)
+
+extern int g_device_count;
+void init_once();
+
+// Growable device buffer.
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t n)
+    {
+        if (n <= cap) return hipSuccess;
+        release();
+        size_t want = std::max<size_t>(n, 1 << 20);
+        hipError_t e = hipMalloc(&ptr, want);
+        if (e == hipSuccess) cap = want;
+        else ptr = nullptr;
+        return e;
+    }
+    void release()
+    {
+        if (ptr) (void)hipFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+    }
+};
+
+// One call's worth of resources; pooled per device, never shared concurrently.
+//   in / out      staging of host images and icons
+//   t0..t2        scratch planes (depth > 8 tail, generic multi-depth pyramid)
+//   meta[2]       ragged-batch descriptors, two slots used alternately: a slot
+//                 is rewritten only after the launch that read it has finished
+//                 (meta_done[slot]), so a ragged call on a caller's stream does
+//                 not have to wait for its own kernel; meta_host[slot] keeps the
+//                 bytes the slot holds, and an identical descriptor set (the same
+//                 batch again: the reference runs every batch once per
+//                 classifier and depth, classifying_tools.py:339-352, 546-551)
+//                 skips the upload.
+struct Workspace {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DevBuf in, out, t0, t1, t2;
+    DevBuf meta[2];
+    hipEvent_t meta_done[2] = {nullptr, nullptr};
+    std::vector<uint8_t> meta_host[2];
+    int meta_slot = 0;
+    // caller-stage pipeline (wicca_icon_stage_u8): a second stream uploads
+    // image k+1 into one of two slots while the compute stream works on image k
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t slot_ready[2] = {nullptr, nullptr}, slot_free[2] = {nullptr, nullptr};
+    DevBuf slot[2], icon[2];
+    // JPEG decode (wicca_jpeg_*): stream + tables, coefficients, planes, scratch, RGB images
+    DevBuf jmeta, jcoef, jplanes, jscratch, jrgb, jtmp;
+    uint8_t* jhost = nullptr;  // pinned host staging of the de-stuffed JPEG streams
+    size_t jhost_cap = 0;
+    bool reserve_jhost(size_t n)
+    {
+        if (n <= jhost_cap) return true;
+        if (jhost) (void)hipHostFree(jhost);
+        jhost = nullptr;
+        jhost_cap = 0;
+        void* p = nullptr;
+        if (hipHostMalloc(&p, std::max<size_t>(n, 16 << 20), hipHostMallocDefault) != hipSuccess) return false;
+        jhost = (uint8_t*)p;
+        jhost_cap = std::max<size_t>(n, 16 << 20);
+        return true;
+    }
+    size_t bytes() const
+    {
+        return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
+               slot[0].cap + slot[1].cap + icon[0].cap + icon[1].cap + jmeta.cap + jcoef.cap +
+               jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap;
+    }
+    hipError_t ensure_pipeline()
+    {
+        if (copy_stream) return hipSuccess;
+        hipError_t e = hipStreamCreateWithFlags(&copy_stream, hipStreamNonBlocking);
+        for (int i = 0; i < 2 && e == hipSuccess; ++i) {
+            e = hipEventCreateWithFlags(&slot_ready[i], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&slot_free[i], hipEventDisableTiming);
+        }
+        return e;
+    }
+    void release_buffers()
+    {
+        for (int i = 0; i < 2; ++i) {
+            if (meta_done[i]) (void)hipEventSynchronize(meta_done[i]);
+            meta[i].release();
+            meta_host[i].clear();
+        }
+        if (copy_stream) (void)hipStreamSynchronize(copy_stream);
+        if (stream) (void)hipStreamSynchronize(stream);
+        in.release();
+        out.release();
+        t0.release();
+        t1.release();
+        t2.release();
+        for (int i = 0; i < 2; ++i) {
+            slot[i].release();
+            icon[i].release();
+        }
+        jmeta.release();
+        jcoef.release();
+        jplanes.release();
+        jscratch.release();
+        jrgb.release();
+        jtmp.release();
+        if (jhost) (void)hipHostFree(jhost);
+        jhost = nullptr;
+        jhost_cap = 0;
+    }
+    void destroy()
+    {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != device) (void)hipSetDevice(device);
+        release_buffers();
+        for (int i = 0; i < 2; ++i) {
+            if (meta_done[i]) (void)hipEventDestroy(meta_done[i]);
+            if (slot_ready[i]) (void)hipEventDestroy(slot_ready[i]);
+            if (slot_free[i]) (void)hipEventDestroy(slot_free[i]);
+        }
+        if (copy_stream) (void)hipStreamDestroy(copy_stream);
+        if (stream) (void)hipStreamDestroy(stream);
+        if (cur >= 0 && cur != device) (void)hipSetDevice(cur);
+    }
+};
+
+// Returning a workspace: it goes to the back of the idle pool (most recent);
+// if the device's idle buffers then exceed the cap, the least recently used
+// OTHER idle workspaces give theirs back (streams and events stay pooled).
+// The returned workspace keeps its buffers even when it alone exceeds the cap:
+// releasing it made every large batch re-allocate its device and pinned
+// buffers on every call (the JPEG stage lost 16 ms a call that way).
+struct WorkspaceLease {
+    Workspace* ws = nullptr;
+    WorkspaceLease() = default;
+    WorkspaceLease(const WorkspaceLease&) = delete;
+    WorkspaceLease& operator=(const WorkspaceLease&) = delete;
+    ~WorkspaceLease();
+};
+
+// Lease a workspace of `device` (the most recently returned one first).
+int acquire(int device, WorkspaceLease& lease);
+
+// Restores the calling thread's current HIP device when an entry point
+// returns: entries switch to the requested device, the caller's selection
+// (e.g. torch's) is left as it was.
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard() = default;
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+int select_device(int device, int* out, DeviceGuard& guard);
+
+inline int64_t round_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+// Row pitch of host images staged on the device: whole 128-B lines, so no
+// line is shared by two rows (rows of a ragged batch at 16-B pitches fetched
+// ~5 % extra: bench --config ragged --ragged-align 16 vs 128).
+constexpr int64_t kStagePitch = 128;
+
+int upload_rows(Workspace* ws, void* dst, int64_t dpitch, const uint8_t* src, int64_t spitch,
+                int64_t width, int64_t height, hipStream_t stream);
+void icon_dims(int64_t H, int64_t W, int depth, int64_t* oh, int64_t* ow);
+inline uint32_t saturate_k(int k) { return (uint32_t)std::min(255, std::max(0, k)); }
+int check_image(const void* src, int64_t H, int64_t W, int64_t C, int64_t pitch, int depth,
+                int border_type);
+
+// Device-resident uniform batch: n images -> n icons (OutT = uint8_t or float).
+template <typename OutT>
+int run_ll(const uint8_t* src, int64_t n, int64_t H, int64_t W, int64_t C, int64_t src_pitch,
+           int64_t src_stride, int depth, int border, int k, void* dst, int64_t dst_pitch,
+           int64_t dst_stride, Workspace* ws, hipStream_t stream, bool* used_scratch);
+
+// Contiguous item ranges balanced by weight over devices, one host thread each.
+int split_over_devices(const std::vector<int64_t>& weights, const int* devices, int n_devices,
+                       const std::function<int(int64_t, int64_t, int)>& fn);
+
+// cv2.resize plumbing (capi_resize.cpp), also used by the JPEG file stage
+int check_resize(int64_t H, int64_t W, int64_t C, int64_t out_w, int64_t out_h, int interpolation,
+                 wicca::ResizeParams* rp);
+int run_resize(wicca::ResizeParams rp, const uint8_t* src, int64_t src_pitch, int64_t src_stride,
+               uint8_t* dst, int64_t dst_pitch, int64_t dst_stride, int64_t n, hipStream_t stream);
+
+}  // namespace wicca_capi

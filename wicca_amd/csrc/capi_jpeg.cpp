@@ -1,0 +1,425 @@
+// capi_jpeg.cpp — baseline JPEG decode on device (wicca_jpeg_*) and the file stage
+// (bytes -> pixels -> resize -> icons).
+// Part of the C ABI declared in include/wicca_haar.h; shared plumbing
+// (workspace pool, staging, error reporting) lives in capi.cpp / capi_internal.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "capi_internal.h"
+#include "jpeg.h"
+
+using namespace wicca_capi;
+
+// ---------------------------------------------------------------------------
+// JPEG decode on the GPU (wicca/data_loader.py:31-63)
+// ---------------------------------------------------------------------------
+namespace {
+
+// Subsequence length (bits) of the parallel Huffman decode: long enough that a
+// lane started at a guessed state resynchronises (bit alignment AND MCU slot)
+// inside its own subsequence — 2048 bits needed 9 passes on 8K photos — and
+// short enough to keep ~256 K lanes in flight (the passes are latency-bound).
+// Measured on 25 x 8K q90 4:2:0 files (profiles/r02_jpeg_sub_bits.jsonl):
+// 4096 bits 3 passes 27.0 GP/s, 8192 2 passes 28.4, 16384 1 pass 27.2, 32768
+// 1 pass 22.2.  WICCA_JPEG_SUB_BITS overrides.
+int64_t jpeg_sub_bits(int64_t total_bits)
+{
+    static const int64_t env = [] {
+        const char* e = getenv("WICCA_JPEG_SUB_BITS");
+        return e ? (int64_t)atoll(e) : (int64_t)0;
+    }();
+    int64_t b = env > 0 ? env : total_bits / 262144;
+    b = std::max<int64_t>(env > 0 ? 256 : 8192, std::min<int64_t>(b, 65536));
+    return (b + 255) & ~(int64_t)255;
+}
+
+int parse_one(const uint8_t* data, int64_t size, wicca::JpegInfo* info, int64_t i)
+{
+    if (!data || size <= 0) return fail(WICCA_ERR_NULL_IMAGE, "Image didn't found. Please check your input.");
+    std::string err;
+    const int rc = wicca::jpeg_parse(data, (size_t)size, info, &err);
+    if (rc == -2) return fail(WICCA_ERR_UNSUPPORTED, "image %lld: %s", (long long)i, err.c_str());
+    if (rc) return fail(WICCA_ERR_DECODE, "image %lld: %s", (long long)i, err.c_str());
+    if (info->H > 65535 || info->W > 65535) return fail(WICCA_ERR_UNSUPPORTED, "image %lld too large", (long long)i);
+    return WICCA_OK;
+}
+
+void oriented_dims(const wicca::JpegInfo& in, bool apply, int64_t* h, int64_t* w)
+{
+    const bool swap = apply && in.orientation >= 5;
+    *h = swap ? in.W : in.H;
+    *w = swap ? in.H : in.W;
+}
+
+// Decode n JPEG files into device RGB images dst[i] (pitch dpitch[i]); EXIF
+// orientation applied when `orient`.  Synchronous on `stream` for the host
+// tables; the pixels are ready in stream order.
+bool jpeg_timing()
+{
+    static const bool on = getenv("WICCA_JPEG_TIMING") != nullptr;
+    return on;
+}
+
+double now_ms()
+{
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                          uint8_t* const* dst, const int64_t* dpitch, bool orient, hipStream_t stream,
+                          int* rounds_out)
+{
+    // at most kJpegMaxJobs (image, component) IDCT jobs per device pass
+    constexpr int64_t kChunk = wicca::kJpegMaxJobs / wicca::kJpegMaxComp;
+    if (n > kChunk) {
+        for (int64_t a = 0; a < n; a += kChunk) {
+            const int64_t m = std::min(kChunk, n - a);
+            int rc = jpeg_decode_to_device(ws, data + a, sizes + a, m, dst + a, dpitch + a, orient, stream,
+                                           rounds_out);
+            if (rc) return rc;
+        }
+        return WICCA_OK;
+    }
+    const double t_start = now_ms();
+    std::vector<wicca::JpegInfo> info((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        int rc = parse_one(data[i], sizes[i], &info[(size_t)i], i);
+        if (rc) return rc;
+    }
+    // de-stuff every image's scan in parallel into its own region of one buffer
+    std::vector<int64_t> img_off((size_t)n + 1, 0);
+    for (int64_t i = 0; i < n; ++i)
+        img_off[(size_t)i + 1] = img_off[(size_t)i] + round_up((int64_t)info[(size_t)i].scan_len, 16);
+    // pinned staging, reused across calls; the bit reader reads ahead past the end
+    const size_t stream_bytes = (size_t)img_off[(size_t)n] + 64;
+    if (!ws->reserve_jhost(stream_bytes)) return fail(WICCA_ERR_NOMEM, "pinned staging of %zu bytes", stream_bytes);
+    uint8_t* stream_h = ws->jhost;
+    for (int64_t i = 0; i < n; ++i)  // the tail of each region past its de-stuffed data stays zero
+        memset(stream_h + img_off[(size_t)i] + (int64_t)info[(size_t)i].scan_len, 0,
+               (size_t)(img_off[(size_t)i + 1] - img_off[(size_t)i] - (int64_t)info[(size_t)i].scan_len));
+    memset(stream_h + img_off[(size_t)n], 0, 64);
+    std::vector<std::vector<int64_t>> seg_off((size_t)n);
+    {
+        const int nt = (int)std::min<int64_t>(n, 16);
+        std::atomic<int64_t> next{0};
+        auto work = [&] {
+            for (int64_t i; (i = next.fetch_add(1)) < n;)
+            {
+                const size_t got = wicca::jpeg_destuff_into(info[(size_t)i], stream_h + img_off[(size_t)i],
+                                                            seg_off[(size_t)i]);
+                memset(stream_h + img_off[(size_t)i] + got, 0, info[(size_t)i].scan_len - got);
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(work);
+        work();
+        for (auto& t : th) t.join();
+    }
+    const double t_destuffed = now_ms();
+    int64_t total_bits = 0;
+    for (int64_t i = 0; i < n; ++i) total_bits += seg_off[(size_t)i].back() * 8;
+    const int64_t S = jpeg_sub_bits(total_bits);
+    std::vector<wicca::JpegSegDev> segs;
+    std::vector<int32_t> sub_seg, sub_img;
+    std::vector<wicca::HuffDev> huff;
+    std::vector<wicca::JpegImageDev> ims((size_t)n);
+    int64_t coef_blocks = 0, plane_bytes = 0, tmp_bytes = 0;
+    std::vector<int64_t> tmp_off((size_t)n, -1);
+    for (int64_t i = 0; i < n; ++i) {
+        const wicca::JpegInfo& f = info[(size_t)i];
+        wicca::JpegImageDev& im = ims[(size_t)i];
+        memset(&im, 0, sizeof(im));
+        im.W = f.W;
+        im.H = f.H;
+        im.ncomp = f.ncomp;
+        im.bpm = f.bpm;
+        im.mcux = f.mcux;
+        im.hmax = f.hmax;
+        im.vmax = f.vmax;
+        for (int k = 0; k < f.bpm; ++k) {
+            im.slot_comp[k] = f.slot_comp[k];
+            im.slot_h[k] = f.slot_h[k];
+            im.slot_v[k] = f.slot_v[k];
+        }
+        int tab_dc[4] = {-1, -1, -1, -1}, tab_ac[4] = {-1, -1, -1, -1};
+        for (int c = 0; c < f.ncomp; ++c) {
+            const wicca::JpegComponent& k = f.comp[c];
+            im.comp_h[c] = k.h;
+            im.comp_v[c] = k.v;
+            im.comp_bw[c] = k.bw;
+            im.comp_bh[c] = k.bh;
+            im.comp_dw[c] = k.dw;
+            im.comp_dh[c] = k.dh;
+            if (tab_dc[k.td] < 0) {
+                tab_dc[k.td] = (int)huff.size();
+                huff.emplace_back();
+                wicca::build_huff_dev(f.dc[k.td], &huff.back());
+            }
+            if (tab_ac[k.ta] < 0) {
+                tab_ac[k.ta] = (int)huff.size();
+                huff.emplace_back();
+                wicca::build_huff_dev(f.ac[k.ta], &huff.back());
+            }
+            im.dc_tab[c] = tab_dc[k.td];
+            im.ac_tab[c] = tab_ac[k.ta];
+            im.comp_block0[c] = coef_blocks;
+            coef_blocks += (int64_t)k.bw * k.bh;
+            im.comp_plane0[c] = plane_bytes;
+            plane_bytes += round_up((int64_t)k.bw * 8 * k.bh * 8, 256);
+            memcpy(im.qt[c], f.qt[k.tq], sizeof(im.qt[c]));
+        }
+        if (orient && f.orientation != 1) {  // decode into a temporary, then orient
+            tmp_off[(size_t)i] = tmp_bytes;
+            tmp_bytes += round_up((int64_t)f.W * 3, 128) * f.H;
+            im.dst_pitch = round_up((int64_t)f.W * 3, 128);
+        } else {
+            im.dst = dst[i];
+            im.dst_pitch = dpitch[i];
+        }
+        // restart segments and their subsequences; the image's subsequences
+        // are padded to whole workgroups (padding lanes: segment -1)
+        const std::vector<int64_t>& off = seg_off[(size_t)i];
+        const int64_t mcus = (int64_t)f.mcux * f.mcuy;
+        const int64_t ri = f.restart_interval > 0 ? f.restart_interval : mcus;
+        const int64_t nseg = std::max<int64_t>(1, std::min<int64_t>((mcus + ri - 1) / ri, (int64_t)off.size() - 1));
+        for (int64_t sgi = 0; sgi < nseg; ++sgi) {
+            wicca::JpegSegDev sg;
+            const int64_t b0 = off[(size_t)sgi], b1 = off[(size_t)sgi + 1];
+            sg.bit0 = (img_off[(size_t)i] + b0) * 8;
+            sg.bits = (b1 - b0) * 8;
+            sg.block0 = sgi * ri * f.bpm;
+            sg.block_end = std::min(mcus, (sgi + 1) * ri) * f.bpm;
+            sg.img = (int32_t)i;
+            sg.sub0 = (int32_t)sub_seg.size();
+            sg.n_sub = std::max<int64_t>(1, (sg.bits + S - 1) / S);
+            for (int64_t k = 0; k < sg.n_sub; ++k) sub_seg.push_back((int32_t)segs.size());
+            segs.push_back(sg);
+        }
+        while (sub_seg.size() % wicca::kJpegLanes) sub_seg.push_back(-1);
+        while (sub_img.size() < sub_seg.size() / wicca::kJpegLanes) sub_img.push_back((int32_t)i);
+    }
+    if (sub_seg.size() >= (size_t)INT32_MAX) return fail(WICCA_ERR_ARG, "JPEG batch too large");
+    // device buffers: [stream | segs | sub_seg | imgs | huff] in jmeta
+    const size_t o_seg = (size_t)round_up((int64_t)stream_bytes, 256);
+    const size_t o_sub = o_seg + (size_t)round_up((int64_t)(segs.size() * sizeof(wicca::JpegSegDev)), 256);
+    const size_t o_sim = o_sub + (size_t)round_up((int64_t)(sub_seg.size() * sizeof(int32_t)), 256);
+    const size_t o_img = o_sim + (size_t)round_up((int64_t)(sub_img.size() * sizeof(int32_t)), 256);
+    const size_t o_huf = o_img + (size_t)round_up((int64_t)(ims.size() * sizeof(wicca::JpegImageDev)), 256);
+    const size_t meta_bytes = o_huf + huff.size() * sizeof(wicca::HuffDev);
+    HIP_TRY(ws->jmeta.reserve(meta_bytes));
+    HIP_TRY(ws->jcoef.reserve((size_t)coef_blocks * 128));
+    HIP_TRY(ws->jplanes.reserve((size_t)plane_bytes));
+    HIP_TRY(ws->jscratch.reserve(wicca::jpeg_scratch_bytes((int64_t)sub_seg.size(), (int64_t)segs.size())));
+    if (tmp_bytes) HIP_TRY(ws->jtmp.reserve((size_t)tmp_bytes));
+    for (int64_t i = 0; i < n; ++i)
+        if (tmp_off[(size_t)i] >= 0) ims[(size_t)i].dst = (uint8_t*)ws->jtmp.ptr + tmp_off[(size_t)i];
+    uint8_t* m = (uint8_t*)ws->jmeta.ptr;
+    // the de-stuffed streams go up as they are; the small tables packed behind them
+    std::vector<uint8_t> packed(meta_bytes - o_seg, 0);
+    memcpy(packed.data(), segs.data(), segs.size() * sizeof(wicca::JpegSegDev));
+    memcpy(packed.data() + (o_sub - o_seg), sub_seg.data(), sub_seg.size() * sizeof(int32_t));
+    memcpy(packed.data() + (o_sim - o_seg), sub_img.data(), sub_img.size() * sizeof(int32_t));
+    memcpy(packed.data() + (o_img - o_seg), ims.data(), ims.size() * sizeof(wicca::JpegImageDev));
+    memcpy(packed.data() + (o_huf - o_seg), huff.data(), huff.size() * sizeof(wicca::HuffDev));
+    HIP_TRY(hipMemcpyAsync(m, stream_h, stream_bytes, hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemcpyAsync(m + o_seg, packed.data(), packed.size(), hipMemcpyHostToDevice, stream));
+    HIP_TRY(hipMemsetAsync(ws->jcoef.ptr, 0, (size_t)coef_blocks * 128, stream));
+    wicca::JpegPlan P{};
+    P.stream = m;
+    P.segs = (const wicca::JpegSegDev*)(m + o_seg);
+    P.sub_seg = (const int32_t*)(m + o_sub);
+    P.sub_img = (const int32_t*)(m + o_sim);
+    P.imgs = (const wicca::JpegImageDev*)(m + o_img);
+    P.huff = (const wicca::HuffDev*)(m + o_huf);
+    P.coef = (int16_t*)ws->jcoef.ptr;
+    P.planes = (uint8_t*)ws->jplanes.ptr;
+    P.n_sub = (int64_t)sub_seg.size();
+    P.n_seg = (int64_t)segs.size();
+    P.sub_bits = (int32_t)S;
+    int rounds = 0;
+    const double t_upload = now_ms();
+    HIP_TRY(wicca::jpeg_decode_device(P, ims.data(), ws->jscratch.ptr, n, &rounds, stream));
+    if (rounds_out) *rounds_out = rounds;
+    for (int64_t i = 0; i < n; ++i)
+        if (tmp_off[(size_t)i] >= 0)
+            HIP_TRY(wicca::launch_orient(ims[(size_t)i].dst, ims[(size_t)i].dst_pitch, info[(size_t)i].W,
+                                         info[(size_t)i].H, info[(size_t)i].orientation, dst[i], dpitch[i],
+                                         stream));
+    // packed / stream_h are host copies consumed by the synchronous upload above
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (jpeg_timing())
+        fprintf(stderr, "[wicca jpeg] %lld files: parse+destuff %.2f ms, tables+upload issue %.2f ms, "
+                "device decode %.2f ms (%d sync passes), sub_bits %lld\n", (long long)n, t_destuffed - t_start,
+                t_upload - t_destuffed, now_ms() - t_upload, rounds, (long long)S);
+    return WICCA_OK;
+}
+
+thread_local int t_jpeg_rounds = 0;
+
+}  // namespace
+
+extern "C" {
+
+int wicca_jpeg_info(const uint8_t* data, int64_t size, int apply_orientation, int64_t* height, int64_t* width,
+                    int* components, int* orientation)
+{
+    wicca::JpegInfo f;
+    int rc = parse_one(data, size, &f, 0);
+    if (rc) return rc;
+    if (height && width) oriented_dims(f, apply_orientation != 0, height, width);
+    if (components) *components = f.ncomp;
+    if (orientation) *orientation = f.orientation;
+    return WICCA_OK;
+}
+
+int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, uint8_t* const* dsts,
+                         const int64_t* dst_pitches, int apply_orientation, int dst_is_device, int device,
+                         void* stream_in)
+{
+    if (n < 0 || (n > 0 && (!data || !sizes || !dsts || !dst_pitches))) return fail(WICCA_ERR_ARG, "bad arrays");
+    if (n == 0) return WICCA_OK;
+    std::vector<int64_t> oh((size_t)n), ow((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        wicca::JpegInfo f;
+        int rc = parse_one(data[i], sizes[i], &f, i);
+        if (rc) return rc;
+        oriented_dims(f, apply_orientation != 0, &oh[i], &ow[i]);
+        if (!dsts[i] || dst_pitches[i] < ow[i] * 3) return fail(WICCA_ERR_ARG, "bad output %lld", (long long)i);
+    }
+    DeviceGuard dg;
+    int dev, rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    Workspace* ws = lease.ws;
+    hipStream_t stream = stream_in ? (hipStream_t)stream_in : ws->stream;
+    std::vector<uint8_t*> d((size_t)n);
+    std::vector<int64_t> p((size_t)n);
+    int64_t off = 0;
+    if (!dst_is_device) {
+        int64_t total = 0;
+        for (int64_t i = 0; i < n; ++i) total += round_up(ow[i] * 3, 128) * oh[i];
+        HIP_TRY(ws->jrgb.reserve((size_t)total));
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        if (dst_is_device) {
+            d[(size_t)i] = dsts[i];
+            p[(size_t)i] = dst_pitches[i];
+        } else {
+            d[(size_t)i] = (uint8_t*)ws->jrgb.ptr + off;
+            p[(size_t)i] = round_up(ow[i] * 3, 128);
+            off += p[(size_t)i] * oh[i];
+        }
+    }
+    if ((rc = jpeg_decode_to_device(ws, data, sizes, n, d.data(), p.data(), apply_orientation != 0, stream,
+                                    &t_jpeg_rounds)))
+        return rc;
+    if (!dst_is_device) {
+        for (int64_t i = 0; i < n; ++i)
+            HIP_TRY(hipMemcpy2DAsync(dsts[i], dst_pitches[i], d[(size_t)i], p[(size_t)i], ow[i] * 3, oh[i],
+                                     hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+    }
+    return WICCA_OK;
+}
+
+int wicca_jpeg_last_sync_rounds(void) { return t_jpeg_rounds; }
+
+int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
+                             int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                             int interpolation, uint8_t* resized, uint8_t* resized_icons, int device);
+
+int wicca_jpeg_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
+                                    int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                                    int interpolation, uint8_t* resized, uint8_t* resized_icons,
+                                    const int* devices, int n_devices)
+{
+    if (n < 0 || (n > 0 && (!data || !sizes))) return fail(WICCA_ERR_ARG, "bad arrays");
+    if (n == 0) return WICCA_OK;
+    if (!resized || !resized_icons) return fail(WICCA_ERR_ARG, "output buffer is NULL");
+    if (out_w <= 0 || out_h <= 0) return fail(WICCA_ERR_ARG, "bad output size");
+    const int64_t ob = out_w * out_h * 3;
+    // balanced by file size (the compressed bytes are what each device decodes)
+    std::vector<int64_t> w(sizes, sizes + n);
+    return split_over_devices(w, devices, n_devices, [&](int64_t a, int64_t b, int dev) {
+        return wicca_jpeg_icon_stage_u8(data + a, sizes + a, b - a, depth, border_type, border_constant, out_w,
+                                        out_h, interpolation, resized + a * ob, resized_icons + a * ob, dev);
+    });
+}
+
+int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
+                             int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                             int interpolation, uint8_t* resized, uint8_t* resized_icons, int device)
+{
+    if (n < 0 || (n > 0 && (!data || !sizes))) return fail(WICCA_ERR_ARG, "bad arrays");
+    if (n == 0) return WICCA_OK;
+    if (!resized || !resized_icons) return fail(WICCA_ERR_ARG, "output buffer is NULL");
+    std::vector<int64_t> H((size_t)n), W((size_t)n), ih((size_t)n), iw((size_t)n);
+    int64_t max_icon = 0, rgb_total = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        wicca::JpegInfo f;
+        int rc = parse_one(data[i], sizes[i], &f, i);
+        if (rc) return rc;
+        oriented_dims(f, true, &H[i], &W[i]);
+        if ((rc = check_image((const uint8_t*)1, H[i], W[i], 3, W[i] * 3, depth, border_type))) return rc;
+        wicca::ResizeParams probe{};
+        if ((rc = check_resize(H[i], W[i], 3, out_w, out_h, interpolation, &probe))) return rc;
+        icon_dims(H[i], W[i], depth, &ih[i], &iw[i]);
+        if ((rc = check_resize(ih[i], iw[i], 3, out_w, out_h, interpolation, &probe))) return rc;
+        max_icon = std::max(max_icon, round_up(iw[i] * 3, 16) * ih[i]);
+        rgb_total += round_up(W[i] * 3, kStagePitch) * H[i];
+    }
+    DeviceGuard dg;
+    int dev, rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    Workspace* ws = lease.ws;
+    hipStream_t cs = ws->stream;
+    HIP_TRY(ws->jrgb.reserve((size_t)rgb_total));
+    HIP_TRY(ws->icon[0].reserve((size_t)max_icon));
+    const int64_t out_bytes = out_w * out_h * 3;
+    HIP_TRY(ws->out.reserve((size_t)(2 * n * out_bytes)));
+    std::vector<uint8_t*> d((size_t)n);
+    std::vector<int64_t> p((size_t)n);
+    int64_t off = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        d[(size_t)i] = (uint8_t*)ws->jrgb.ptr + off;
+        p[(size_t)i] = round_up(W[i] * 3, kStagePitch);
+        off += p[(size_t)i] * H[i];
+    }
+    // data_loader.py:53-58  cv2.imread + BGR2RGB, on the GPU (+ EXIF orientation)
+    if ((rc = jpeg_decode_to_device(ws, data, sizes, n, d.data(), p.data(), true, cs, &t_jpeg_rounds))) return rc;
+    uint8_t* dres = (uint8_t*)ws->out.ptr;
+    uint8_t* dico = dres + n * out_bytes;
+    uint8_t* ico = (uint8_t*)ws->icon[0].ptr;
+    for (int64_t i = 0; i < n; ++i) {
+        // classifying_tools.py:315, :317, :318
+        wicca::ResizeParams rp{};
+        wicca::plan_resize((int)H[i], (int)W[i], (int)out_h, (int)out_w, 3, interpolation, &rp);
+        if ((rc = run_resize(rp, d[(size_t)i], p[(size_t)i], 0, dres + i * out_bytes, out_w * 3, 0, 1, cs)))
+            return rc;
+        const int64_t ip = round_up(iw[i] * 3, 16);
+        bool scratch = false;
+        if ((rc = run_ll<uint8_t>(d[(size_t)i], 1, H[i], W[i], 3, p[(size_t)i], 0, depth, border_type,
+                                  border_constant, ico, ip, 0, ws, cs, &scratch)))
+            return rc;
+        wicca::ResizeParams ri{};
+        wicca::plan_resize((int)ih[i], (int)iw[i], (int)out_h, (int)out_w, 3, interpolation, &ri);
+        if ((rc = run_resize(ri, ico, ip, 0, dico + i * out_bytes, out_w * 3, 0, 1, cs))) return rc;
+    }
+    HIP_TRY(hipMemcpyAsync(resized, dres, (size_t)(n * out_bytes), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(resized_icons, dico, (size_t)(n * out_bytes), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipStreamSynchronize(cs));
+    return WICCA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,213 @@
+// capi_resize.cpp — cv2.resize (INTER_NEAREST / INTER_LINEAR / INTER_AREA) on device and the
+// decoded-image caller stage (resize + icons, data_loader.py / classifying_tools.py).
+// Part of the C ABI declared in include/wicca_haar.h; shared plumbing
+// (workspace pool, staging, error reporting) lives in capi.cpp / capi_internal.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "capi_internal.h"
+
+using namespace wicca_capi;
+
+// ---------------------------------------------------------------------------
+// cv2.resize and the caller stage of _get_img_batch
+// ---------------------------------------------------------------------------
+namespace wicca_capi {
+
+int check_resize(int64_t H, int64_t W, int64_t C, int64_t out_w, int64_t out_h, int interpolation,
+                 wicca::ResizeParams* rp)
+{
+    if (H <= 0 || W <= 0 || C <= 0) return fail(WICCA_ERR_EMPTY, "Image is empty");
+    if (C > 4) return fail(WICCA_ERR_ARG, "resize takes 1-4 channels (got %lld)", (long long)C);
+    if (out_w <= 0 || out_h <= 0 || out_w > 65535 || out_h > 65535)
+        return fail(WICCA_ERR_ARG, "bad output size %lldx%lld", (long long)out_w, (long long)out_h);
+    if (H >= ((int64_t)1 << 31) || W * C >= ((int64_t)1 << 31))
+        return fail(WICCA_ERR_ARG, "image too large to resize");
+    if (!wicca::plan_resize((int)H, (int)W, (int)out_h, (int)out_w, (int)C, interpolation, rp))
+        return fail(WICCA_ERR_ARG, "interpolation %d is not implemented (INTER_NEAREST, "
+                    "INTER_LINEAR and INTER_AREA are)", interpolation);
+    return WICCA_OK;
+}
+
+// Device-resident resize of n images (uniform shape) on `stream`.
+int run_resize(wicca::ResizeParams rp, const uint8_t* src, int64_t src_pitch, int64_t src_stride,
+               uint8_t* dst, int64_t dst_pitch, int64_t dst_stride, int64_t n, hipStream_t stream)
+{
+    if (rp.mode == wicca::RS_COPY) {
+        for (int64_t i = 0; i < n; ++i)
+            HIP_TRY(hipMemcpy2DAsync(dst + i * dst_stride, dst_pitch, src + i * src_stride, src_pitch,
+                                     (size_t)rp.W * rp.C, rp.H, hipMemcpyDeviceToDevice, stream));
+        return WICCA_OK;
+    }
+    rp.src = src;
+    rp.src_pitch = src_pitch;
+    rp.src_stride = src_stride;
+    rp.dst = dst;
+    rp.dst_pitch = dst_pitch;
+    rp.dst_stride = dst_stride;
+    for (int64_t i0 = 0; i0 < n; i0 += 65535) {  // grid.z limit
+        wicca::ResizeParams q = rp;
+        q.src = src + i0 * src_stride;
+        q.dst = dst + i0 * dst_stride;
+        HIP_TRY(wicca::launch_resize(q, std::min<int64_t>(65535, n - i0), stream));
+    }
+    return WICCA_OK;
+}
+
+}  // namespace wicca_capi
+
+extern "C" {
+
+int wicca_resize_u8(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t src_pitch,
+                    uint8_t* dst, int64_t out_w, int64_t out_h, int64_t dst_pitch, int interpolation,
+                    int src_is_device, int dst_is_device, int device, void* stream_in)
+{
+    if (!src) return fail(WICCA_ERR_NULL_IMAGE, "Image didn't found. Please check your input.");
+    if (!dst) return fail(WICCA_ERR_ARG, "dst is NULL");
+    wicca::ResizeParams rp{};
+    int rc = check_resize(H, W, C, out_w, out_h, interpolation, &rp);
+    if (rc) return rc;
+    if (src_pitch < W * C || dst_pitch < out_w * C) return fail(WICCA_ERR_ARG, "pitch too small");
+    DeviceGuard dg;
+    int dev;
+    if ((rc = select_device(device, &dev, dg))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    Workspace* ws = lease.ws;
+    hipStream_t stream = stream_in ? (hipStream_t)stream_in : ws->stream;
+    const uint8_t* dsrc = src;
+    int64_t sp = src_pitch;
+    if (!src_is_device) {
+        sp = round_up(W * C, kStagePitch);
+        HIP_TRY(ws->in.reserve((size_t)(sp * H)));
+        if ((rc = upload_rows(ws, ws->in.ptr, sp, src, src_pitch, W * C, H, stream))) return rc;
+        dsrc = (const uint8_t*)ws->in.ptr;
+    }
+    uint8_t* ddst = dst;
+    int64_t dp = dst_pitch;
+    if (!dst_is_device) {
+        dp = round_up(out_w * C, 16);
+        HIP_TRY(ws->out.reserve((size_t)(dp * out_h)));
+        ddst = (uint8_t*)ws->out.ptr;
+    }
+    if ((rc = run_resize(rp, dsrc, sp, 0, ddst, dp, 0, 1, stream))) return rc;
+    if (!dst_is_device)
+        HIP_TRY(hipMemcpy2DAsync(dst, dst_pitch, ddst, dp, out_w * C, out_h, hipMemcpyDeviceToHost,
+                                 stream));
+    if (!stream_in || !src_is_device || !dst_is_device) HIP_TRY(hipStreamSynchronize(stream));
+    return WICCA_OK;
+}
+
+int wicca_resize_u8_uniform(const uint8_t* src, int64_t n, int64_t H, int64_t W, int64_t C,
+                            int64_t src_pitch, int64_t src_image_stride, uint8_t* dst, int64_t out_w,
+                            int64_t out_h, int64_t dst_pitch, int64_t dst_image_stride,
+                            int interpolation, int device, void* stream_in)
+{
+    if (n < 0) return fail(WICCA_ERR_ARG, "negative batch size");
+    if (n == 0) return WICCA_OK;
+    if (!src) return fail(WICCA_ERR_NULL_IMAGE, "Image didn't found. Please check your input.");
+    if (!dst) return fail(WICCA_ERR_ARG, "dst is NULL");
+    wicca::ResizeParams rp{};
+    int rc = check_resize(H, W, C, out_w, out_h, interpolation, &rp);
+    if (rc) return rc;
+    if (src_pitch < W * C || dst_pitch < out_w * C ||
+        (n > 1 && (src_image_stride < src_pitch * H || dst_image_stride < dst_pitch * out_h)))
+        return fail(WICCA_ERR_ARG, "pitch/stride too small");
+    DeviceGuard dg;
+    int dev;
+    if ((rc = select_device(device, &dev, dg))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    hipStream_t stream = stream_in ? (hipStream_t)stream_in : lease.ws->stream;
+    if ((rc = run_resize(rp, src, src_pitch, src_image_stride, dst, dst_pitch, dst_image_stride, n,
+                         stream)))
+        return rc;
+    if (!stream_in) HIP_TRY(hipStreamSynchronize(stream));
+    return WICCA_OK;
+}
+
+int wicca_icon_stage_u8(const wicca_image_desc* images, int64_t n, int64_t C, int depth,
+                        int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                        int interpolation, uint8_t* resized, uint8_t* resized_icons, int device)
+{
+    if (n < 0 || (n > 0 && !images)) return fail(WICCA_ERR_ARG, "bad image array");
+    if (n == 0) return WICCA_OK;
+    if (!resized || !resized_icons) return fail(WICCA_ERR_ARG, "output buffer is NULL");
+    if (C <= 0) return fail(WICCA_ERR_EMPTY, "Image is empty");
+    int64_t max_in = 0, max_icon = 0;
+    std::vector<int64_t> ih((size_t)n), iw((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        int rc = check_image(images[i].src, images[i].height, images[i].width, C, images[i].src_pitch,
+                             depth, border_type);
+        if (rc) return rc;
+        wicca::ResizeParams probe{};
+        if ((rc = check_resize(images[i].height, images[i].width, C, out_w, out_h, interpolation,
+                               &probe)))
+            return rc;
+        icon_dims(images[i].height, images[i].width, depth, &ih[i], &iw[i]);
+        if ((rc = check_resize(ih[i], iw[i], C, out_w, out_h, interpolation, &probe))) return rc;
+        max_in = std::max(max_in, round_up(images[i].width * C, kStagePitch) * images[i].height);
+        max_icon = std::max(max_icon, round_up(iw[i] * C, 16) * ih[i]);
+    }
+    DeviceGuard dg;
+    int dev, rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    Workspace* ws = lease.ws;
+    HIP_TRY(ws->ensure_pipeline());
+    hipStream_t cs = ws->stream, up = ws->copy_stream;
+    const int64_t out_bytes = out_w * out_h * C;  // dense (out_h, out_w, C) per image
+    for (int k = 0; k < 2; ++k) {
+        HIP_TRY(ws->slot[k].reserve((size_t)max_in));
+        HIP_TRY(ws->icon[k].reserve((size_t)max_icon));
+    }
+    HIP_TRY(ws->out.reserve((size_t)(2 * n * out_bytes)));
+    uint8_t* dres = (uint8_t*)ws->out.ptr;
+    uint8_t* dico = dres + n * out_bytes;
+    // the slots may still be read by an earlier call's kernels on `cs`
+    HIP_TRY(hipStreamSynchronize(cs));
+    for (int64_t i = 0; i < n; ++i) {
+        const int k = (int)(i & 1);
+        const int64_t H = images[i].height, W = images[i].width;
+        const int64_t pitch = round_up(W * C, kStagePitch);
+        uint8_t* img = (uint8_t*)ws->slot[k].ptr;
+        // upload image i once slot k's previous image (i - 2) is no longer read
+        HIP_TRY(hipStreamWaitEvent(up, ws->slot_free[k], 0));
+        if ((rc = upload_rows(ws, img, pitch, images[i].src, images[i].src_pitch, W * C, H, up)))
+            return rc;
+        HIP_TRY(hipEventRecord(ws->slot_ready[k], up));
+        HIP_TRY(hipStreamWaitEvent(cs, ws->slot_ready[k], 0));
+        // classifying_tools.py:315  resized = cv2.resize(image, shape, interpolation)
+        wicca::ResizeParams rp{};
+        wicca::plan_resize((int)H, (int)W, (int)out_h, (int)out_w, (int)C, interpolation, &rp);
+        if ((rc = run_resize(rp, img, pitch, 0, dres + i * out_bytes, out_w * C, 0, 1, cs))) return rc;
+        // :317  icon = coder.get_small_copy(image, depth)
+        const int64_t ip = round_up(iw[i] * C, 16);
+        uint8_t* ico = (uint8_t*)ws->icon[k].ptr;
+        bool scratch = false;
+        if ((rc = run_ll<uint8_t>(img, 1, H, W, C, pitch, 0, depth, border_type, border_constant, ico,
+                                  ip, 0, ws, cs, &scratch)))
+            return rc;
+        // :318  resized_icon = cv2.resize(icon, shape, interpolation)
+        wicca::ResizeParams ri{};
+        wicca::plan_resize((int)ih[i], (int)iw[i], (int)out_h, (int)out_w, (int)C, interpolation, &ri);
+        if ((rc = run_resize(ri, ico, ip, 0, dico + i * out_bytes, out_w * C, 0, 1, cs))) return rc;
+        HIP_TRY(hipEventRecord(ws->slot_free[k], cs));
+    }
+    // :323  np.stack(...) of both lists: dense (n, out_h, out_w, C) each
+    HIP_TRY(hipMemcpyAsync(resized, dres, (size_t)(n * out_bytes), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipMemcpyAsync(resized_icons, dico, (size_t)(n * out_bytes), hipMemcpyDeviceToHost, cs));
+    HIP_TRY(hipStreamSynchronize(cs));
+    return WICCA_OK;
+}
+
+}  // extern "C"
