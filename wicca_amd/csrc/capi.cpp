@@ -86,6 +86,20 @@ size_t idle_bytes_locked(int device)
     return b;
 }
 
+// Ragged descriptor upload (WICCA_META_UPLOAD, read once): 0 = copy kernel
+// from the slot's pinned buffer (default), 1 = hipMemcpyAsync from it,
+// 2 = hipMemcpyAsync from pageable memory (the round-2 path; the host waits
+// for the stream there, leaving a gap between back-to-back ragged launches).
+int meta_upload_mode()
+{
+    static const int mode = [] {
+        const char* e = getenv("WICCA_META_UPLOAD");
+        const int m = e ? atoi(e) : 0;
+        return (m >= 0 && m <= 2) ? m : 0;
+    }();
+    return mode;
+}
+
 WorkspaceLease::~WorkspaceLease()
 {
     if (!ws) return;
@@ -734,7 +748,7 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
             e.dst_pitch = d[i].dst_pitch;
             e.out_h = oh[i];
             e.out_w = ow[i];
-            e.n_seg = (int32_t)wicca::segments_for(e.out_w, depth, (int)C);
+            e.n_seg = (int32_t)wicca::segments_for(e.out_w, depth, (int)C, true);
             e.pad_ = 0;
             starts[(size_t)i] = total;
             total += e.out_h * e.n_seg;
@@ -745,7 +759,7 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
         // next meta slot unless that slot already holds these exact bytes
         const size_t bytes_d = sizeof(wicca::ImageDescDev) * (size_t)n;
         const size_t off_s = (size_t)round_up((int64_t)bytes_d, 16);
-        const size_t meta_bytes = off_s + sizeof(int64_t) * (size_t)n;
+        const size_t meta_bytes = (size_t)round_up((int64_t)(off_s + sizeof(int64_t) * (size_t)n), 16);
         std::vector<uint8_t> packed(meta_bytes, 0);
         memcpy(packed.data(), dd.data(), bytes_d);
         memcpy(packed.data() + off_s, starts.data(), sizeof(int64_t) * (size_t)n);
@@ -759,8 +773,20 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
             HIP_TRY(hipEventSynchronize(ws->meta_done[slot]));
             ws->meta_host[slot].clear();
             HIP_TRY(ws->meta[slot].reserve(meta_bytes));
-            HIP_TRY(hipMemcpyAsync(ws->meta[slot].ptr, packed.data(), meta_bytes,
-                                   hipMemcpyHostToDevice, stream));
+            const int mode = meta_upload_mode();
+            if (mode == 2) {  // pageable copy (timing reference)
+                HIP_TRY(hipMemcpyAsync(ws->meta[slot].ptr, packed.data(), meta_bytes,
+                                       hipMemcpyHostToDevice, stream));
+            } else {
+                HIP_TRY(ws->meta_pin[slot].reserve(meta_bytes, 64 << 10));
+                memcpy(ws->meta_pin[slot].ptr, packed.data(), meta_bytes);
+                if (mode == 1)
+                    HIP_TRY(hipMemcpyAsync(ws->meta[slot].ptr, ws->meta_pin[slot].ptr, meta_bytes,
+                                           hipMemcpyHostToDevice, stream));
+                else
+                    HIP_TRY(wicca::launch_copy16(ws->meta[slot].ptr, ws->meta_pin[slot].ptr,
+                                                 (int64_t)meta_bytes, stream));
+            }
             ws->meta_host[slot] = std::move(packed);
         } else {
             // uploaded by an earlier call, possibly on another stream

@@ -56,6 +56,30 @@ struct DevBuf {
     }
 };
 
+// Growable pinned host buffer (device-readable).
+struct HostBuf {
+    uint8_t* ptr = nullptr;
+    size_t cap = 0;
+    hipError_t reserve(size_t n, size_t min_bytes)
+    {
+        if (n <= cap) return hipSuccess;
+        release();
+        void* p = nullptr;
+        const size_t want = std::max(n, min_bytes);
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e != hipSuccess) return e;
+        ptr = (uint8_t*)p;
+        cap = want;
+        return hipSuccess;
+    }
+    void release()
+    {
+        if (ptr) (void)hipHostFree(ptr);
+        ptr = nullptr;
+        cap = 0;
+    }
+};
+
 // One call's worth of resources; pooled per device, never shared concurrently.
 //   in / out      staging of host images and icons
 //   t0..t2        scratch planes (depth > 8 tail, generic multi-depth pyramid)
@@ -66,7 +90,10 @@ struct DevBuf {
 //                 bytes the slot holds, and an identical descriptor set (the same
 //                 batch again: the reference runs every batch once per
 //                 classifier and depth, classifying_tools.py:339-352, 546-551)
-//                 skips the upload.
+//                 skips the upload.  A new set is written into the slot's
+//                 pinned host buffer (meta_pin) and pulled onto the device by a
+//                 copy kernel on the call's stream: no copy-engine round trip
+//                 and no host wait between back-to-back ragged launches.
 struct Workspace {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -74,6 +101,7 @@ struct Workspace {
     DevBuf meta[2];
     hipEvent_t meta_done[2] = {nullptr, nullptr};
     std::vector<uint8_t> meta_host[2];
+    HostBuf meta_pin[2];
     int meta_slot = 0;
     // caller-stage pipeline (wicca_icon_stage_u8): a second stream uploads
     // image k+1 into one of two slots while the compute stream works on image k
@@ -82,20 +110,7 @@ struct Workspace {
     DevBuf slot[2], icon[2];
     // JPEG decode (wicca_jpeg_*): stream + tables, coefficients, planes, scratch, RGB images
     DevBuf jmeta, jcoef, jplanes, jscratch, jrgb, jtmp;
-    uint8_t* jhost = nullptr;  // pinned host staging of the de-stuffed JPEG streams
-    size_t jhost_cap = 0;
-    bool reserve_jhost(size_t n)
-    {
-        if (n <= jhost_cap) return true;
-        if (jhost) (void)hipHostFree(jhost);
-        jhost = nullptr;
-        jhost_cap = 0;
-        void* p = nullptr;
-        if (hipHostMalloc(&p, std::max<size_t>(n, 16 << 20), hipHostMallocDefault) != hipSuccess) return false;
-        jhost = (uint8_t*)p;
-        jhost_cap = std::max<size_t>(n, 16 << 20);
-        return true;
-    }
+    HostBuf jhost;  // pinned host staging of the de-stuffed JPEG streams
     size_t bytes() const
     {
         return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
@@ -118,6 +133,7 @@ struct Workspace {
             if (meta_done[i]) (void)hipEventSynchronize(meta_done[i]);
             meta[i].release();
             meta_host[i].clear();
+            meta_pin[i].release();
         }
         if (copy_stream) (void)hipStreamSynchronize(copy_stream);
         if (stream) (void)hipStreamSynchronize(stream);
@@ -136,9 +152,7 @@ struct Workspace {
         jscratch.release();
         jrgb.release();
         jtmp.release();
-        if (jhost) (void)hipHostFree(jhost);
-        jhost = nullptr;
-        jhost_cap = 0;
+        jhost.release();
     }
     void destroy()
     {

@@ -100,8 +100,9 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         img_off[(size_t)i + 1] = img_off[(size_t)i] + round_up((int64_t)info[(size_t)i].scan_len, 16);
     // pinned staging, reused across calls; the bit reader reads ahead past the end
     const size_t stream_bytes = (size_t)img_off[(size_t)n] + 64;
-    if (!ws->reserve_jhost(stream_bytes)) return fail(WICCA_ERR_NOMEM, "pinned staging of %zu bytes", stream_bytes);
-    uint8_t* stream_h = ws->jhost;
+    if (ws->jhost.reserve(stream_bytes, 16 << 20) != hipSuccess)
+        return fail(WICCA_ERR_NOMEM, "pinned staging of %zu bytes", stream_bytes);
+    uint8_t* stream_h = ws->jhost.ptr;
     for (int64_t i = 0; i < n; ++i)  // the tail of each region past its de-stuffed data stays zero
         memset(stream_h + img_off[(size_t)i] + (int64_t)info[(size_t)i].scan_len, 0,
                (size_t)(img_off[(size_t)i + 1] - img_off[(size_t)i] - (int64_t)info[(size_t)i].scan_len));

@@ -56,13 +56,14 @@ struct BlockWork {
     int32_t oy, seg, n_seg;
 };
 
+// Work unit b (a segment of an icon row, or one wave strip with
+// WICCA_STRIP_FLAT) -> image, icon row, segment.  Ragged: b counts from the
+// batch's first unit; wave-uniform.
 template <int L, bool RAGGED>
-__device__ __forceinline__ BlockWork resolve_block(const LLParams& p)
+__device__ __forceinline__ BlockWork resolve_unit(const LLParams& p, uint32_t b)
 {
     BlockWork w;
-    uint32_t b = logical_block(blockIdx.x, gridDim.x);
     if constexpr (RAGGED) {
-        b += p.block_base;
         // Which image owns block b: block_start is increasing, so the number of
         // images starting at or before b, minus one.  One wave-wide probe of 64
         // prefixes (ballot + popcount) per level instead of a dependent binary
@@ -108,6 +109,12 @@ __device__ __forceinline__ BlockWork resolve_block(const LLParams& p)
         w.seg = (int32_t)seg; w.oy = (int32_t)oy;
     }
     return w;
+}
+
+template <int L, bool RAGGED>
+__device__ __forceinline__ BlockWork resolve_block(const LLParams& p)
+{
+    return resolve_unit<L, RAGGED>(p, logical_block(blockIdx.x, gridDim.x) + (RAGGED ? p.block_base : 0u));
 }
 
 // Packed column sums: lo holds bytes 0,2 of each dword, hi bytes 1,3.

@@ -55,6 +55,12 @@
 #ifndef WICCA_STRIP_WG_CAP3
 #define WICCA_STRIP_WG_CAP3 4   // K1s at D=3: at most this many workgroups (= waves/SIMD) per CU
 #endif
+#ifndef WICCA_STRIP_FLAT
+#define WICCA_STRIP_FLAT -1   // K1s: a workgroup takes 4 consecutive strips of the (image, band, strip) order; -1: table
+#endif
+#ifndef WICCA_STRIP_WG_CAP3_RAGGED
+#define WICCA_STRIP_WG_CAP3_RAGGED 0  // the same cap for ragged batches (0: uncapped)
+#endif
 #ifndef WICCA_STRIP_WG_CAP_HI
 #define WICCA_STRIP_WG_CAP_HI 2 // K1s at D>=4 (when selected): at most this many workgroups per CU
 #endif
@@ -99,10 +105,21 @@ constexpr int strip_min_lds(int L, bool ragged)
 {
     // a ragged batch at D = 3 (smaller images, descriptor search per block)
     // runs faster uncapped
-    return L == 3 ? (ragged ? 0 : lds_for_cap(WICCA_STRIP_WG_CAP3))
+    return L == 3 ? lds_for_cap(ragged ? WICCA_STRIP_WG_CAP3_RAGGED : WICCA_STRIP_WG_CAP3)
                   : L >= 4 ? lds_for_cap(WICCA_STRIP_WG_CAP_HI) : 0;
 }
 constexpr int k1_min_lds(int L) { return L == 1 ? lds_for_cap(WICCA_K1_WG_CAP1) : 0; }
+
+// Work units of the strip kernel: groups of kStripWaves strips of one band
+// (idle waves where a band's strips do not fill the last group), or single
+// strips in (image, band, strip) order, four per workgroup.  Single strips
+// measured +2.6 % (D = 3) / +3.3 % (D = 2) on ragged batches of random widths
+// and -4.5 % / -1 % on uniform 4K batches, -3 % on ragged D = 5
+// (profiles/r02_ab_flat*.json).
+constexpr bool strip_flat(int L, bool ragged)
+{
+    return WICCA_STRIP_FLAT >= 0 ? WICCA_STRIP_FLAT == 1 : (ragged && L <= 3);
+}
 
 constexpr int strip_chunk_rows(int L)
 {
@@ -140,8 +157,8 @@ struct LLParams {
     int32_t aligned_out; // set by the launcher
     // ragged batch (descs != nullptr): device arrays
     const ImageDescDev* descs;
-    const int64_t* block_start;  // n_images entries, prefix of blocks
-    int64_t total_blocks;
+    const int64_t* block_start;  // n_images entries, prefix of work units
+    int64_t total_blocks;        // work units (units_per_block(L) per workgroup)
     uint32_t block_base;         // first block of this launch (grids split at the HIP limit)
 };
 
@@ -174,7 +191,8 @@ hipError_t launch_multi(MultiParams p, int dmin, int C, hipStream_t s);
 // unsigned char, false>".  Empty for layouts the fast kernels do not take.
 const char* block_sum_kernel_name(int L, int C, bool ragged);
 
-int64_t segments_for(int64_t out_w, int L, int C);  // column groups per icon row
+int64_t segments_for(int64_t out_w, int L, int C, bool ragged);  // work units per icon row
+int units_per_block(int L, bool ragged);                         // work units per workgroup
 bool fast_path_ok(const LLParams& p, int L, int C);
 
 // Block sums of the padded 2^L x 2^L blocks, finished as OutT:
@@ -195,6 +213,10 @@ hipError_t launch_pyramid_step(const uint32_t* in, int64_t in_pitch, int64_t in_
                                int64_t w, int C, int64_t n_img, int t, uint8_t* icon,
                                int64_t icon_h, int64_t icon_w, int64_t icon_pitch,
                                int64_t icon_stride, uint32_t* next, hipStream_t s);
+
+// Copy n_bytes (a multiple of 16, both ends 16-B aligned) with a kernel on
+// stream s; `src` may be pinned host memory (small descriptor sets).
+hipError_t launch_copy16(void* dst, const void* src, int64_t n_bytes, hipStream_t s);
 
 hipError_t launch_synth(uint8_t* dst, int64_t n, int64_t H, int64_t WC, int64_t pitch,
                         int64_t image_stride, uint64_t seed, int64_t first_image,

@@ -342,8 +342,21 @@ __global__ __launch_bounds__(64 * kStripWaves) void haar_strip_kernel(LLParams p
     // ---- work: block -> (image, icon row, group of kStripWaves strips); wave -> strip
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    BlockWork w = resolve_block<L, RAGGED>(p);
-    const int strip = w.seg * kStripWaves + wave;
+    BlockWork w;
+    int strip;
+    if constexpr (strip_flat(L, RAGGED)) {
+        // unit = one wave strip; the workgroup's waves take consecutive units, so
+        // only the batch's last workgroup can hold idle waves
+        const uint64_t unit = ((uint64_t)logical_block(blockIdx.x, gridDim.x) + (RAGGED ? p.block_base : 0u)) *
+                                  kStripWaves + (uint64_t)wave;
+        const int64_t n_units = RAGGED ? p.total_blocks : p.n_images * p.out_h * p.n_seg;
+        if ((int64_t)unit >= n_units) return;  // wave-uniform; no workgroup barriers in this kernel
+        w = resolve_unit<L, RAGGED>(p, (uint32_t)unit);
+        strip = w.seg;
+    } else {
+        w = resolve_block<L, RAGGED>(p);
+        strip = w.seg * kStripWaves + wave;
+    }
     const int64_t spx0 = (int64_t)strip * STRIP;     // first pixel of the strip
     const int64_t Wp = w.out_w << L;                 // padded width
     uint8_t* stage = smem + wave * STAGE;
@@ -745,6 +758,26 @@ __global__ __launch_bounds__(kThreads) void synth_u8_kernel(uint8_t* dst, int64_
     }
 }
 
+// Small copies on the compute queue (ragged descriptor sets from pinned host
+// memory): a kernel keeps the upload in stream order with the launch that
+// reads it, without a copy-engine hand-off between the two.
+__global__ __launch_bounds__(kThreads) void copy16_kernel(u32x4* dst, const u32x4* src, int64_t n)
+{
+    for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads)
+        dst[i] = src[i];
+}
+
+hipError_t launch_copy16(void* dst, const void* src, int64_t n_bytes, hipStream_t s)
+{
+    if (n_bytes <= 0) return hipSuccess;
+    if (n_bytes % 16 || (uintptr_t)dst % 16 || (uintptr_t)src % 16) return hipErrorInvalidValue;
+    const int64_t n = n_bytes / 16;
+    const int64_t blocks = std::min<int64_t>((n + kThreads - 1) / kThreads, 64);
+    hipLaunchKernelGGL(copy16_kernel, dim3((uint32_t)blocks), dim3(kThreads), 0, s, (u32x4*)dst,
+                       (const u32x4*)src, n);
+    return hipGetLastError();
+}
+
 // ----------------------------------------------------------------------------
 // Launchers
 // ----------------------------------------------------------------------------
@@ -800,14 +833,19 @@ static hipError_t dispatch_C(int L, int C, const LLParams& p, int64_t blocks, hi
     }
 }
 
-int64_t segments_for(int64_t out_w, int L, int C)
+int64_t segments_for(int64_t out_w, int L, int C, bool ragged)
 {
-    if (use_strip_kernel(L)) {  // groups of kStripWaves wave strips of 64*P pixels
+    if (use_strip_kernel(L)) {  // wave strips of 64*P pixels (groups of kStripWaves unless flat)
         const int64_t strip = 64 * strip_lane_pixels(std::max(1, std::min(C, 4)));
         const int64_t strips = ((out_w << L) + strip - 1) / strip;
-        return (strips + kStripWaves - 1) / kStripWaves;
+        return strip_flat(L, ragged) ? strips : (strips + kStripWaves - 1) / kStripWaves;
     }
     return ((out_w << L) + kSegPx - 1) / kSegPx;  // 4,096-pixel segments
+}
+
+int units_per_block(int L, bool ragged)
+{
+    return use_strip_kernel(L) && strip_flat(L, ragged) ? kStripWaves : 1;
 }
 
 bool fast_path_ok(const LLParams& p, int L, int C)
@@ -824,19 +862,20 @@ hipError_t launch_block_sum(LLParams p, int L, int C, hipStream_t stream)
     p.aligned_out = out_al ? 1 : 0;
     constexpr int64_t kMax = max_grid_blocks(kThreads);  // strip and segment kernels: 256 lanes
     if (p.descs == nullptr && out_al && fast_path_ok(p, L, C)) {
-        p.n_seg = (int32_t)segments_for(p.out_w, L, C);
-        const int64_t per_image = p.out_h * p.n_seg;
+        p.n_seg = (int32_t)segments_for(p.out_w, L, C, false);
+        const int64_t per_image = p.out_h * p.n_seg;  // work units
+        const int64_t upb = units_per_block(L, false);
         if (per_image <= 0 || p.n_images <= 0) return hipSuccess;
-        if (per_image > kMax) return hipErrorInvalidValue;  // one image past the grid limit
+        if (per_image > kMax * upb) return hipErrorInvalidValue;  // one image past the grid limit
         // at most kMax blocks per launch: consecutive image ranges
-        const int64_t imgs_per_launch = kMax / per_image;
+        const int64_t imgs_per_launch = kMax * upb / per_image;
         const int64_t n = p.n_images;
         for (int64_t i0 = 0; i0 < n; i0 += imgs_per_launch) {
             LLParams q = p;
             q.n_images = std::min(imgs_per_launch, n - i0);
             q.src = p.src + i0 * p.src_image_stride;
             q.dst = p.dst + i0 * p.dst_image_stride;
-            hipError_t e = dispatch_C<OutT>(L, C, q, q.n_images * per_image, stream);
+            hipError_t e = dispatch_C<OutT>(L, C, q, (q.n_images * per_image + upb - 1) / upb, stream);
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
@@ -844,10 +883,12 @@ hipError_t launch_block_sum(LLParams p, int L, int C, hipStream_t stream)
     if (p.descs != nullptr) {
         // ragged: caller guarantees alignment of every descriptor; blocks past
         // the grid limit go to further launches that start at block_base
-        for (int64_t b0 = 0; b0 < p.total_blocks; b0 += kMax) {
+        const int64_t upb = units_per_block(L, true);
+        const int64_t blocks = (p.total_blocks + upb - 1) / upb;
+        for (int64_t b0 = 0; b0 < blocks; b0 += kMax) {
             LLParams q = p;
             q.block_base = (uint32_t)b0;
-            hipError_t e = dispatch_C<OutT>(L, C, q, std::min(kMax, p.total_blocks - b0), stream);
+            hipError_t e = dispatch_C<OutT>(L, C, q, std::min(kMax, blocks - b0), stream);
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
