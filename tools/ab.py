@@ -37,6 +37,12 @@ def main():
                     help="> 0: a ragged batch, H, W drawn from [ragged * size, size], one "
                          "wicca_haar_ll_u8_batch call with device descriptors")
     ap.add_argument("--ragged-align", type=int, default=16, help="row pitch alignment (bytes)")
+    ap.add_argument("--ragged-wmult", type=int, default=1,
+                    help="round ragged widths down to a multiple of this many pixels")
+    ap.add_argument("--ragged-hmult", type=int, default=1,
+                    help="round ragged heights down to a multiple of this many rows")
+    ap.add_argument("--pitch-pad", type=int, default=0,
+                    help="uniform batch: bytes added to the 16-B aligned row pitch")
     ap.add_argument("--no-check", action="store_true",
                     help="skip the identical-icons check (ablation builds compute garbage)")
     args = ap.parse_args()
@@ -60,13 +66,15 @@ def main():
     first = next(iter(libs.values()))
     if args.ragged > 0:
         rng = np.random.default_rng(0)
-        Hs = [int(x) for x in rng.integers(int(H * args.ragged), H + 1, B)]
-        Ws = [int(x) for x in rng.integers(int(W * args.ragged), W + 1, B)]
+        Hs = [int(x) // args.ragged_hmult * args.ragged_hmult
+              for x in rng.integers(int(H * args.ragged), H + 1, B)]
+        Ws = [int(x) // args.ragged_wmult * args.ragged_wmult
+              for x in rng.integers(int(W * args.ragged), W + 1, B)]
         al = args.ragged_align
         pitches = [(w * C + al - 1) // al * al for w in Ws]
     else:
         Hs, Ws = [H] * B, [W] * B
-        pitches = [(W * C + 15) // 16 * 16] * B
+        pitches = [(W * C + 15) // 16 * 16 + args.pitch_pad] * B
     offs = np.concatenate([[0], np.cumsum([p * h for p, h in zip(pitches, Hs)])]).astype(np.int64)
     src = torch.empty(int(offs[-1]), dtype=torch.uint8, device="cuda")
     for i in range(B):

@@ -737,7 +737,7 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
     } else {
         std::vector<wicca::ImageDescDev> dd((size_t)n);
         std::vector<int64_t> starts((size_t)n);
-        int64_t total = 0;
+        int64_t total = 0, min_units = INT64_MAX;
         for (int64_t i = 0; i < n; ++i) {
             auto& e = dd[(size_t)i];
             e.src = d[i].src;
@@ -752,6 +752,7 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
             e.pad_ = 0;
             starts[(size_t)i] = total;
             total += e.out_h * e.n_seg;
+            min_units = std::min<int64_t>(min_units, e.out_h * e.n_seg);
         }
         if (total >= ((int64_t)1 << 32))
             return fail(WICCA_ERR_ARG, "batch too large for one launch");
@@ -760,6 +761,10 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
         const size_t bytes_d = sizeof(wicca::ImageDescDev) * (size_t)n;
         const size_t off_s = (size_t)round_up((int64_t)bytes_d, 16);
         const size_t meta_bytes = (size_t)round_up((int64_t)(off_s + sizeof(int64_t) * (size_t)n), 16);
+        // unit -> image map after the uploaded bytes, built on device
+        const int map_shift = wicca::ragged_map_shift(min_units, total);
+        const int64_t n_groups = (total >> map_shift) + 1;
+        const size_t slot_bytes = meta_bytes + sizeof(uint32_t) * (size_t)n_groups;
         std::vector<uint8_t> packed(meta_bytes, 0);
         memcpy(packed.data(), dd.data(), bytes_d);
         memcpy(packed.data() + off_s, starts.data(), sizeof(int64_t) * (size_t)n);
@@ -772,7 +777,7 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
             // the launch that last read this slot must be done before it is rewritten
             HIP_TRY(hipEventSynchronize(ws->meta_done[slot]));
             ws->meta_host[slot].clear();
-            HIP_TRY(ws->meta[slot].reserve(meta_bytes));
+            HIP_TRY(ws->meta[slot].reserve(slot_bytes));
             const int mode = meta_upload_mode();
             if (mode == 2) {  // pageable copy (timing reference)
                 HIP_TRY(hipMemcpyAsync(ws->meta[slot].ptr, packed.data(), meta_bytes,
@@ -787,6 +792,9 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
                     HIP_TRY(wicca::launch_copy16(ws->meta[slot].ptr, ws->meta_pin[slot].ptr,
                                                  (int64_t)meta_bytes, stream));
             }
+            HIP_TRY(wicca::launch_ragged_map((uint32_t*)((uint8_t*)ws->meta[slot].ptr + meta_bytes),
+                                             (const int64_t*)((uint8_t*)ws->meta[slot].ptr + off_s), n,
+                                             n_groups, map_shift, stream));
             ws->meta_host[slot] = std::move(packed);
         } else {
             // uploaded by an earlier call, possibly on another stream
@@ -800,6 +808,8 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
         p.dst = d[0].dst;  // alignment probe only; every descriptor is aligned
         p.descs = (const wicca::ImageDescDev*)meta;
         p.block_start = (const int64_t*)(meta + off_s);
+        p.unit_map = (const uint32_t*)(meta + meta_bytes);
+        p.map_shift = map_shift;
         p.total_blocks = total;
         HIP_TRY(wicca::launch_block_sum<uint8_t>(p, depth, (int)C, stream));
         HIP_TRY(hipEventRecord(ws->meta_done[slot], stream));

@@ -71,7 +71,28 @@ __device__ __forceinline__ BlockWork resolve_unit(const LLParams& p, uint32_t b)
         const int n = (int)p.n_images;
         const int lane = (int)(threadIdx.x & 63);
         int lo;
-        if (n <= 64) {
+        if constexpr (ragged_probe(L) == 2) {
+            // the group map names the first image of b's group; a group is no
+            // longer than the smallest image (unless the map had to be
+            // coarsened), so the scalar step below runs at most once
+            typedef __attribute__((address_space(4))) const int64_t* cptr;
+            typedef __attribute__((address_space(4))) const uint32_t* cmap;
+            const cptr bs = (cptr)p.block_start;
+            lo = (int)((cmap)p.unit_map)[b >> p.map_shift];
+            while (lo + 1 < n && bs[lo + 1] <= (int64_t)b) ++lo;
+        } else if (ragged_probe(L) == 1) {
+            // scalar binary search: the prefix table is read through the
+            // constant address space (s_load, scalar cache), off the vector
+            // memory queues the streaming loads keep full
+            typedef __attribute__((address_space(4))) const int64_t* cptr;
+            const cptr bs = (cptr)p.block_start;
+            lo = 0;
+            int hi = n - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (bs[mid] <= (int64_t)b) lo = mid; else hi = mid - 1;
+            }
+        } else if (n <= 64) {
             const bool le = lane < n && p.block_start[lane] <= (int64_t)b;
             lo = __popcll(__ballot(le)) - 1;
         } else if (n <= 64 * 64) {

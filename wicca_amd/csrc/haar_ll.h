@@ -55,8 +55,12 @@
 #ifndef WICCA_STRIP_WG_CAP3
 #define WICCA_STRIP_WG_CAP3 4   // K1s at D=3: at most this many workgroups (= waves/SIMD) per CU
 #endif
+#ifndef WICCA_RAGGED_PROBE
+#define WICCA_RAGGED_PROBE 2  // ragged unit -> image: 0 wave ballot over vector loads, 1 scalar binary search,
+                              // 2 unit-group map + scalar step, -1 table (ragged_probe)
+#endif
 #ifndef WICCA_STRIP_FLAT
-#define WICCA_STRIP_FLAT -1   // K1s: a workgroup takes 4 consecutive strips of the (image, band, strip) order; -1: table
+#define WICCA_STRIP_FLAT 0    // K1s: a workgroup takes 4 consecutive strips of the (image, band, strip) order; -1: table
 #endif
 #ifndef WICCA_STRIP_WG_CAP3_RAGGED
 #define WICCA_STRIP_WG_CAP3_RAGGED 0  // the same cap for ragged batches (0: uncapped)
@@ -121,6 +125,16 @@ constexpr bool strip_flat(int L, bool ragged)
     return WICCA_STRIP_FLAT >= 0 ? WICCA_STRIP_FLAT == 1 : (ragged && L <= 3);
 }
 
+// Ragged unit -> image lookup (profiles/r02_ab_map_*.json, ab_sprobe_*): the
+// group map read through the scalar cache beats the wave ballot over vector
+// loads by 6-8 % at D = 1 and 4-7 % at D = 5 (the ballot's loads queue behind
+// the streaming loads); with single-strip units (D <= 3) the ballot is 1-3 %
+// ahead (three dependent scalar loads per short wave).
+constexpr int ragged_probe(int L)
+{
+    return WICCA_RAGGED_PROBE >= 0 ? WICCA_RAGGED_PROBE : (use_strip_kernel(L) && strip_flat(L, true) ? 0 : 2);
+}
+
 constexpr int strip_chunk_rows(int L)
 {
     return WICCA_STRIP_CHUNK > 0 ? WICCA_STRIP_CHUNK : 16;
@@ -159,6 +173,8 @@ struct LLParams {
     const ImageDescDev* descs;
     const int64_t* block_start;  // n_images entries, prefix of work units
     int64_t total_blocks;        // work units (units_per_block(L) per workgroup)
+    const uint32_t* unit_map;    // first image of every group of 2^map_shift units
+    int32_t map_shift;
     uint32_t block_base;         // first block of this launch (grids split at the HIP limit)
 };
 
@@ -213,6 +229,12 @@ hipError_t launch_pyramid_step(const uint32_t* in, int64_t in_pitch, int64_t in_
                                int64_t w, int C, int64_t n_img, int t, uint8_t* icon,
                                int64_t icon_h, int64_t icon_w, int64_t icon_pitch,
                                int64_t icon_stride, uint32_t* next, hipStream_t s);
+
+// Ragged batches: group size (log2) of the unit -> image map, and the map
+// (built on device from the block_start prefix; n_groups = (total >> shift) + 1).
+int ragged_map_shift(int64_t min_units, int64_t total_units);
+hipError_t launch_ragged_map(uint32_t* map, const int64_t* block_start, int64_t n_images,
+                             int64_t n_groups, int shift, hipStream_t s);
 
 // Copy n_bytes (a multiple of 16, both ends 16-B aligned) with a kernel on
 // stream s; `src` may be pinned host memory (small descriptor sets).

@@ -758,6 +758,38 @@ __global__ __launch_bounds__(kThreads) void synth_u8_kernel(uint8_t* dst, int64_
     }
 }
 
+// Unit -> image map of a ragged batch: entry g = the image owning unit g << shift.
+__global__ __launch_bounds__(kThreads) void ragged_map_kernel(uint32_t* map, const int64_t* bs, int64_t n,
+                                                              int64_t n_groups, int shift)
+{
+    const int64_t g = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (g >= n_groups) return;
+    const int64_t u = g << shift;
+    int64_t lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (bs[mid] <= u) lo = mid; else hi = mid - 1;
+    }
+    map[g] = (uint32_t)lo;
+}
+
+int ragged_map_shift(int64_t min_units, int64_t total_units)
+{
+    int shift = 0;
+    while (shift < 40 && ((int64_t)2 << shift) <= min_units) ++shift;  // 2^shift <= min_units
+    while ((total_units >> shift) >= ((int64_t)1 << 22)) ++shift;       // map <= 16 MiB
+    return shift;
+}
+
+hipError_t launch_ragged_map(uint32_t* map, const int64_t* block_start, int64_t n_images,
+                             int64_t n_groups, int shift, hipStream_t s)
+{
+    if (n_groups <= 0 || n_images <= 0) return hipSuccess;
+    hipLaunchKernelGGL(ragged_map_kernel, dim3((uint32_t)((n_groups + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, s, map, block_start, n_images, n_groups, shift);
+    return hipGetLastError();
+}
+
 // Small copies on the compute queue (ragged descriptor sets from pinned host
 // memory): a kernel keeps the upload in stream order with the launch that
 // reads it, without a copy-engine hand-off between the two.
