@@ -174,3 +174,37 @@ def test_ragged_descriptor_reuse_follows_content(D):
                                               ctypes.c_void_p(stream.cuda_stream)))
         stream.synchronize()
         _check(dsts, hosts, C, D, border, k)
+
+
+def test_ragged_group_map_spans_many_images(tall):
+    """Tall and tiny images interleaved: 36 M work units force a coarsened
+    unit -> image map (groups of 16 units), so one group spans up to 16 tiny
+    images and the lookup has to step across them."""
+    n, H, W = tall.shape
+    rng = np.random.default_rng(11)
+    tiny_src, tiny_dst, tiny_host = [], [], []
+    for _ in range(100):
+        h, w = int(rng.integers(1, 6)), int(rng.integers(1, 17))
+        im = rng.integers(0, 256, (h, w, 1), dtype=np.uint8)
+        s = torch.zeros((h, 16), dtype=torch.uint8, device="cuda")
+        s[:, :w] = torch.from_numpy(im[:, :, 0])
+        tiny_src.append(s)
+        tiny_dst.append(torch.full((-(-h // 2), 16), 7, dtype=torch.uint8, device="cuda"))
+        tiny_host.append(im)
+    out = torch.empty((n, H // 2, 16), dtype=torch.uint8, device="cuda")
+    order = [("t", i) for i in range(4)] + [("s", i) for i in range(50)] + \
+        [("t", i) for i in range(4, 8)] + [("s", i) for i in range(50, 100)]
+    descs = (_lib.ImageDesc * len(order))()
+    for j, (kind, i) in enumerate(order):
+        if kind == "t":
+            descs[j] = _lib.ImageDesc(tall[i].data_ptr(), out[i].data_ptr(), H, W, W, 16)
+        else:
+            h, w = tiny_host[i].shape[:2]
+            descs[j] = _lib.ImageDesc(tiny_src[i].data_ptr(), tiny_dst[i].data_ptr(), h, w, 16, 16)
+    _lib.check(_lib.load().wicca_haar_ll_u8_batch(descs, len(order), 1, 1, 1, 0, 1, 1, -1, None))
+    torch.cuda.synchronize()
+    assert torch.equal(out[:, :, :8], _expect(tall, 1))
+    for d, im in zip(tiny_dst, tiny_host):
+        h, w = im.shape[:2]
+        got = d[:, :-(-w // 2)].cpu().numpy().reshape(-(-h // 2), -(-w // 2), 1)
+        assert np.array_equal(got, c_oracle.ll_int_block(im, 1)[0])

@@ -1,5 +1,10 @@
 set -e
-V=tools/variants
-A="--libs $V/lib_cur.so $V/lib_rcap4.so $V/lib_rcap6.so $V/lib_strip.so --depths 1 3 --rounds 5 --images 256 --height 2160 --width 3840 --ragged-align 128"
-timeout -k 10 150 python -u tools/ab.py $A --ragged 1.0 --out gpurun_out/ab_rcap_r10.json | sed 's/^/r1.0 /'
-timeout -k 10 150 python -u tools/ab.py $A --ragged 0.5 --out gpurun_out/ab_rcap_r05.json | sed 's/^/r0.5 /'
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_suite.log 2>&1
+tail -1 gpurun_out/gpu_suite.log
+R3="--config ragged --depth 3 --images 256 --height 2160 --width 3840 --ragged-align 128 --steps 30 --no-cpu-baseline"
+R5="--config ragged --depth 5 --images 128 --ragged-align 128 --steps 20 --no-cpu-baseline"
+timeout -k 10 120 python -u bench.py $R3 > gpurun_out/r02_bench_ragged_d3.json
+timeout -k 10 120 python -u bench.py $R5 > gpurun_out/r02_bench_ragged_d5.json
+timeout -k 10 120 python -u bench.py --config ragged --depth 1 --images 256 --height 2160 --width 3840 --ragged-align 128 --steps 30 --no-cpu-baseline > gpurun_out/r02_bench_ragged_d1.json
+timeout -k 10 120 python -u bench.py --config ragged --depth 2 --images 256 --height 2160 --width 3840 --ragged-align 128 --steps 30 --no-cpu-baseline > gpurun_out/r02_bench_ragged_d2.json
+cat gpurun_out/r02_bench_ragged_d*.json

@@ -63,7 +63,7 @@
 #define WICCA_STRIP_FLAT 0    // K1s: a workgroup takes 4 consecutive strips of the (image, band, strip) order; -1: table
 #endif
 #ifndef WICCA_STRIP_WG_CAP3_RAGGED
-#define WICCA_STRIP_WG_CAP3_RAGGED 0  // the same cap for ragged batches (0: uncapped)
+#define WICCA_STRIP_WG_CAP3_RAGGED 6  // K1s at D=3 on ragged batches (0: uncapped; r02_ab_rcap_*.json)
 #endif
 #ifndef WICCA_STRIP_WG_CAP_HI
 #define WICCA_STRIP_WG_CAP_HI 2 // K1s at D>=4 (when selected): at most this many workgroups per CU
@@ -107,8 +107,7 @@ constexpr int kLdsPerCU = 160 * 1024;
 constexpr int lds_for_cap(int cap) { return cap > 0 ? kLdsPerCU / (cap + 1) + 16 : 0; }
 constexpr int strip_min_lds(int L, bool ragged)
 {
-    // a ragged batch at D = 3 (smaller images, descriptor search per block)
-    // runs faster uncapped
+    // ragged batches at D = 3: 6 per CU (+2-2.5 % over uncapped, 4 is mixed)
     return L == 3 ? lds_for_cap(ragged ? WICCA_STRIP_WG_CAP3_RAGGED : WICCA_STRIP_WG_CAP3)
                   : L >= 4 ? lds_for_cap(WICCA_STRIP_WG_CAP_HI) : 0;
 }
