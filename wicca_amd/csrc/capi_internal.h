@@ -109,12 +109,13 @@ struct Workspace {
     hipEvent_t slot_ready[2] = {nullptr, nullptr}, slot_free[2] = {nullptr, nullptr};
     DevBuf slot[2], icon[2];
     // JPEG decode (wicca_jpeg_*): stream + tables, coefficients, planes, scratch, RGB images
-    DevBuf jmeta, jcoef, jplanes, jscratch, jrgb, jtmp;
+    DevBuf jstream, jmeta, jcoef, jplanes, jscratch, jrgb, jtmp;
     HostBuf jhost;  // pinned host staging of the de-stuffed JPEG streams
+    HostBuf jtab;   // pinned host staging of the decode tables
     size_t bytes() const
     {
         return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
-               slot[0].cap + slot[1].cap + icon[0].cap + icon[1].cap + jmeta.cap + jcoef.cap +
+               slot[0].cap + slot[1].cap + icon[0].cap + icon[1].cap + jstream.cap + jmeta.cap + jcoef.cap +
                jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap;
     }
     hipError_t ensure_pipeline()
@@ -146,6 +147,7 @@ struct Workspace {
             slot[i].release();
             icon[i].release();
         }
+        jstream.release();
         jmeta.release();
         jcoef.release();
         jplanes.release();
@@ -153,6 +155,7 @@ struct Workspace {
         jrgb.release();
         jtmp.release();
         jhost.release();
+        jtab.release();
     }
     void destroy()
     {

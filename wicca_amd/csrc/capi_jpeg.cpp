@@ -107,7 +107,14 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         memset(stream_h + img_off[(size_t)i] + (int64_t)info[(size_t)i].scan_len, 0,
                (size_t)(img_off[(size_t)i + 1] - img_off[(size_t)i] - (int64_t)info[(size_t)i].scan_len));
     memset(stream_h + img_off[(size_t)n], 0, 64);
+    // each image's region goes up as soon as it is de-stuffed (pinned source:
+    // the copies run while the other threads are still de-stuffing)
+    HIP_TRY(ws->jstream.reserve(stream_bytes));
+    uint8_t* stream_d = (uint8_t*)ws->jstream.ptr;
+    HIP_TRY(hipMemcpyAsync(stream_d + img_off[(size_t)n], stream_h + img_off[(size_t)n], 64,
+                           hipMemcpyHostToDevice, stream));
     std::vector<std::vector<int64_t>> seg_off((size_t)n);
+    std::atomic<int> upload_err{0};
     {
         const int nt = (int)std::min<int64_t>(n, 16);
         std::atomic<int64_t> next{0};
@@ -117,12 +124,20 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
                 const size_t got = wicca::jpeg_destuff_into(info[(size_t)i], stream_h + img_off[(size_t)i],
                                                             seg_off[(size_t)i]);
                 memset(stream_h + img_off[(size_t)i] + got, 0, info[(size_t)i].scan_len - got);
+                const int64_t a = img_off[(size_t)i], len = img_off[(size_t)i + 1] - a;
+                if (hipMemcpyAsync(stream_d + a, stream_h + a, (size_t)len, hipMemcpyHostToDevice, stream) !=
+                    hipSuccess)
+                    upload_err = 1;
             }
         };
         std::vector<std::thread> th;
         for (int t = 1; t < nt; ++t) th.emplace_back(work);
         work();
         for (auto& t : th) t.join();
+    }
+    if (upload_err) {
+        (void)hipStreamSynchronize(stream);  // the staging is reused by the next call
+        return fail(WICCA_ERR_HIP, "JPEG stream upload failed");
     }
     const double t_destuffed = now_ms();
     int64_t total_bits = 0;
@@ -208,8 +223,8 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         while (sub_img.size() < sub_seg.size() / wicca::kJpegLanes) sub_img.push_back((int32_t)i);
     }
     if (sub_seg.size() >= (size_t)INT32_MAX) return fail(WICCA_ERR_ARG, "JPEG batch too large");
-    // device buffers: [stream | segs | sub_seg | imgs | huff] in jmeta
-    const size_t o_seg = (size_t)round_up((int64_t)stream_bytes, 256);
+    // device buffers: the streams in jstream, [segs | sub_seg | sub_img | imgs | huff] in jmeta
+    const size_t o_seg = 0;
     const size_t o_sub = o_seg + (size_t)round_up((int64_t)(segs.size() * sizeof(wicca::JpegSegDev)), 256);
     const size_t o_sim = o_sub + (size_t)round_up((int64_t)(sub_seg.size() * sizeof(int32_t)), 256);
     const size_t o_img = o_sim + (size_t)round_up((int64_t)(sub_img.size() * sizeof(int32_t)), 256);
@@ -223,18 +238,20 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     for (int64_t i = 0; i < n; ++i)
         if (tmp_off[(size_t)i] >= 0) ims[(size_t)i].dst = (uint8_t*)ws->jtmp.ptr + tmp_off[(size_t)i];
     uint8_t* m = (uint8_t*)ws->jmeta.ptr;
-    // the de-stuffed streams go up as they are; the small tables packed behind them
-    std::vector<uint8_t> packed(meta_bytes - o_seg, 0);
-    memcpy(packed.data(), segs.data(), segs.size() * sizeof(wicca::JpegSegDev));
-    memcpy(packed.data() + (o_sub - o_seg), sub_seg.data(), sub_seg.size() * sizeof(int32_t));
-    memcpy(packed.data() + (o_sim - o_seg), sub_img.data(), sub_img.size() * sizeof(int32_t));
-    memcpy(packed.data() + (o_img - o_seg), ims.data(), ims.size() * sizeof(wicca::JpegImageDev));
-    memcpy(packed.data() + (o_huf - o_seg), huff.data(), huff.size() * sizeof(wicca::HuffDev));
-    HIP_TRY(hipMemcpyAsync(m, stream_h, stream_bytes, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemcpyAsync(m + o_seg, packed.data(), packed.size(), hipMemcpyHostToDevice, stream));
+    // the small tables, packed in pinned memory (a pageable copy would make the
+    // host wait for the stream uploads before issuing the decode)
+    HIP_TRY(ws->jtab.reserve(meta_bytes, 1 << 20));
+    uint8_t* packed = ws->jtab.ptr;
+    memset(packed, 0, meta_bytes);
+    memcpy(packed, segs.data(), segs.size() * sizeof(wicca::JpegSegDev));
+    memcpy(packed + o_sub, sub_seg.data(), sub_seg.size() * sizeof(int32_t));
+    memcpy(packed + o_sim, sub_img.data(), sub_img.size() * sizeof(int32_t));
+    memcpy(packed + o_img, ims.data(), ims.size() * sizeof(wicca::JpegImageDev));
+    memcpy(packed + o_huf, huff.data(), huff.size() * sizeof(wicca::HuffDev));
+    HIP_TRY(hipMemcpyAsync(m, packed, meta_bytes, hipMemcpyHostToDevice, stream));
     HIP_TRY(hipMemsetAsync(ws->jcoef.ptr, 0, (size_t)coef_blocks * 128, stream));
     wicca::JpegPlan P{};
-    P.stream = m;
+    P.stream = stream_d;
     P.segs = (const wicca::JpegSegDev*)(m + o_seg);
     P.sub_seg = (const int32_t*)(m + o_sub);
     P.sub_img = (const int32_t*)(m + o_sim);
@@ -254,7 +271,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
             HIP_TRY(wicca::launch_orient(ims[(size_t)i].dst, ims[(size_t)i].dst_pitch, info[(size_t)i].W,
                                          info[(size_t)i].H, info[(size_t)i].orientation, dst[i], dpitch[i],
                                          stream));
-    // packed / stream_h are host copies consumed by the synchronous upload above
+    // the pinned staging (streams, tables) is reused by the next call
     HIP_TRY(hipStreamSynchronize(stream));
     if (jpeg_timing())
         fprintf(stderr, "[wicca jpeg] %lld files: parse+destuff %.2f ms, tables+upload issue %.2f ms, "

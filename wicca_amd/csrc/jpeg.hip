@@ -325,9 +325,20 @@ __device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageD
 
 // Pass over every subsequence.  round 0: start from the guessed state at the
 // subsequence start; round > 0: from the previous round's end state of the
-// previous subsequence (the segment's first subsequence starts exactly).
+// previous subsequence (the segment's first subsequence starts exactly).  A
+// lane whose start state is the one it started from in the previous round
+// (`older`: the results of round - 2; the guess in round 1) repeats that
+// round's result without decoding: after the first sync pass nearly every
+// lane has synchronised, so the confirming pass costs only the lanes whose
+// predecessor still moved.
+__device__ __forceinline__ bool same_state(const DecState& a, const DecState& b)
+{
+    return a.p == b.p && a.slot == b.slot && a.k == b.k;
+}
+
 __global__ __launch_bounds__(kJThreads) void jpeg_sync_kernel(JpegPlan P, const SubResult* prev,
-                                                             SubResult* next, int round, int* changed)
+                                                             SubResult* next, int round, int* changed,
+                                                             const SubResult* older)
 {
     const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
     __shared__ ImgTabs tabs;
@@ -346,6 +357,20 @@ __global__ __launch_bounds__(kJThreads) void jpeg_sync_kernel(JpegPlan P, const 
     } else {
         st = prev[i - 1].end;
     }
+    if (round > 0) {
+        DecState before;  // this lane's start state in the previous round
+        if (j == 0 || round == 1) {
+            before.p = b0;
+            before.slot = 0;
+            before.k = 0;
+        } else {
+            before = older[i - 1].end;
+        }
+        if (same_state(st, before)) {  // same input, same result
+            next[i] = prev[i];
+            return;
+        }
+    }
     SubResult r;
     r.started = 0;
     r.pad_ = 0;
@@ -355,10 +380,7 @@ __global__ __launch_bounds__(kJThreads) void jpeg_sync_kernel(JpegPlan P, const 
     decode_run<false>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr);
     r.end = st;
     for (int c = 0; c < kJpegMaxComp; ++c) r.dc[c] = dc[c];
-    if (round > 0) {
-        const DecState& o = prev[i].end;
-        if (o.p != st.p || o.slot != st.slot || o.k != st.k) *changed = 1;
-    }
+    if (round > 0 && !same_state(prev[i].end, st)) *changed = 1;
     next[i] = r;
 }
 
@@ -766,7 +788,7 @@ hipError_t launch_orient(const uint8_t* src, int64_t sp, int W, int H, int orien
 size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg)
 {
     (void)n_seg;
-    return (size_t)n_sub * (2 * sizeof(SubResult) + sizeof(SubBase)) + 64 + kJpegMaxJobs * sizeof(IdctJob);
+    return (size_t)n_sub * (3 * sizeof(SubResult) + sizeof(SubBase)) + 64 + kJpegMaxJobs * sizeof(IdctJob);
 }
 
 hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* scratch, int64_t n_images,
@@ -775,36 +797,12 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     uint8_t* base = (uint8_t*)scratch;
     SubResult* ra = (SubResult*)base;
     SubResult* rb = ra + P.n_sub;
-    SubBase* sb = (SubBase*)(rb + P.n_sub);
+    SubResult* rc = rb + P.n_sub;
+    SubBase* sb = (SubBase*)(rc + P.n_sub);
     int* changed = (int*)(sb + P.n_sub);
     IdctJob* jobs = (IdctJob*)((uint8_t*)changed + 64);
-    const uint32_t grid = (uint32_t)((P.n_sub + kJThreads - 1) / kJThreads);
-    // round 0 + rounds until no end state changes
-    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(grid), dim3(kJThreads), 0, s, P, ra, ra, 0, changed);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    SubResult* cur = ra;
-    SubResult* nxt = rb;
-    int rounds = 0;
-    for (;;) {
-        int h_changed = 0;
-        e = hipMemsetAsync(changed, 0, sizeof(int), s);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(jpeg_sync_kernel, dim3(grid), dim3(kJThreads), 0, s, P, cur, nxt, 1, changed);
-        e = hipGetLastError();
-        if (e == hipSuccess) e = hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (e != hipSuccess) return e;
-        std::swap(cur, nxt);
-        ++rounds;
-        if (!h_changed || rounds > P.n_sub) break;
-    }
-    if (sync_rounds) *sync_rounds = rounds;
-    hipLaunchKernelGGL(jpeg_scan_kernel, dim3((uint32_t)P.n_seg), dim3(256), 0, s, P, cur, sb);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(jpeg_write_kernel, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    // IDCT jobs: every (image, component)
+    // IDCT jobs: every (image, component); uploaded first, while the stream
+    // still waits for the entropy-coded data
     std::vector<IdctJob> hj;
     int64_t max_blocks = 0;
     for (int64_t i = 0; i < n_images; ++i)
@@ -820,8 +818,41 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             max_blocks = std::max<int64_t>(max_blocks, (int64_t)j.bw * j.bh);
         }
     if (hj.size() > (size_t)kJpegMaxJobs) return hipErrorInvalidValue;
-    e = hipMemcpyAsync(jobs, hj.data(), sizeof(IdctJob) * hj.size(), hipMemcpyHostToDevice, s);
+    hipError_t e = hipMemcpyAsync(jobs, hj.data(), sizeof(IdctJob) * hj.size(), hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return e;
+    const uint32_t grid = (uint32_t)((P.n_sub + kJThreads - 1) / kJThreads);
+    // round 0 + rounds until no end state changes; results rotate through
+    // three buffers (older = round - 2, cur = round - 1, nxt = this round)
+    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(grid), dim3(kJThreads), 0, s, P, ra, ra, 0, changed,
+                       (const SubResult*)nullptr);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    SubResult* older = rc;
+    SubResult* cur = ra;
+    SubResult* nxt = rb;
+    int rounds = 0;
+    for (;;) {
+        int h_changed = 0;
+        e = hipMemsetAsync(changed, 0, sizeof(int), s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(jpeg_sync_kernel, dim3(grid), dim3(kJThreads), 0, s, P, cur, nxt, rounds + 1, changed,
+                           (const SubResult*)older);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return e;
+        SubResult* t = older;
+        older = cur;
+        cur = nxt;
+        nxt = t;
+        ++rounds;
+        if (!h_changed || rounds > P.n_sub) break;
+    }
+    if (sync_rounds) *sync_rounds = rounds;
+    hipLaunchKernelGGL(jpeg_scan_kernel, dim3((uint32_t)P.n_seg), dim3(256), 0, s, P, cur, sb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(jpeg_write_kernel, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(jpeg_idct_kernel, dim3((uint32_t)((max_blocks + 255) / 256), (uint32_t)hj.size()),
                        dim3(256), 0, s, P, jobs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
