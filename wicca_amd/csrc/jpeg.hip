@@ -187,23 +187,89 @@ struct BlockPos {
 // coefficients of blocks [block_lo, block_end) (g = decode-order block index of
 // the block in progress), absolute DC values from the running predictors.
 // Blocks that start AND end inside the lane's range are assembled in the
-// lane's LDS block `lb` and leave as eight 16-B stores (2-byte scattered
-// stores cost 4.5 of the pass's 7 ms); the block in progress at the start
-// (begun by the previous lane) is written coefficient by coefficient, and so
-// is the nonzero part of a block the range ends inside (the next lane writes
-// its other coefficients): no two lanes ever write the same bytes.
+// lane's LDS block `lb` (only the coefficients it sets, tracked in the 64-bit
+// mask `nz`: no zeroing) and leave through the wave's cooperative flush; the
+// block in progress at the start (begun by the previous lane) is written
+// coefficient by coefficient, and so is the nonzero part of a block the range
+// ends inside (the next lane writes its other coefficients): no two lanes ever
+// write the same bytes.
 constexpr int kLaneBlock = 72;  // int16 per lane in LDS (144 B: 16-B aligned, spreads banks)
+#ifndef WICCA_JPEG_STAGE
+#define WICCA_JPEG_STAGE 1  // 0: every coefficient leaves as its own 2-B store (no LDS staging)
+#endif
+
+// Per-wave LDS of the write pass: every lane's block under assembly, and the
+// flush list (owner lane, block index, coefficient mask) of blocks completed
+// in the current iteration.
+struct WaveStage {
+    int16_t* blocks;  // 64 * kLaneBlock
+    int32_t* owner;   // 64
+    int64_t* blk;     // 64
+    uint64_t* nz;     // 64
+};
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Blocks completed by lanes of this wave in this iteration leave as full
+// 128-B blocks: the wave's active lanes deal the 8 16-B chunks of every such
+// block among themselves, so one store instruction writes up to 8 blocks
+// (a lane storing its own block issued 8 mostly-empty instructions per block,
+// on nearly every iteration of every wave: 2.4 -> 6.2 ms for the pass).
+// Coefficients the block did not set come out as zeros (mask `nz`).
+__device__ __forceinline__ void flush_blocks(bool done, int64_t blk, uint64_t nz, const WaveStage& ws,
+                                             int16_t* coef)
+{
+    const uint64_t pend = __ballot(done);
+    if (pend == 0) return;  // uniform over the active lanes
+    const uint64_t act = __ballot(true);
+    const int lane = (int)(threadIdx.x & 63);
+    const uint64_t below = (1ull << lane) - 1;
+    if (done) {
+        const int r = __popcll(pend & below);
+        ws.owner[r] = lane;
+        ws.blk[r] = blk;
+        ws.nz[r] = nz;
+    }
+    wave_lds_sync();
+    const int n_act = __popcll(act), n_chunks = 8 * __popcll(pend);
+#pragma unroll 1
+    for (int c = __popcll(act & below); c < n_chunks; c += n_act) {
+        const int b = c >> 3, q = c & 7;
+        uint4 v = *reinterpret_cast<const uint4*>(ws.blocks + ws.owner[b] * kLaneBlock + q * 8);
+        const uint32_t m = (uint32_t)(ws.nz[b] >> (q * 8)) & 0xFFu;
+        auto keep = [&](uint32_t w, int d) -> uint32_t {
+            return w & (((m >> (2 * d)) & 1u ? 0x0000FFFFu : 0u) | ((m >> (2 * d + 1)) & 1u ? 0xFFFF0000u : 0u));
+        };
+        v.x = keep(v.x, 0);
+        v.y = keep(v.y, 1);
+        v.z = keep(v.z, 2);
+        v.w = keep(v.w, 3);
+#ifndef WICCA_JPEG_ABLATE_STORES
+        *reinterpret_cast<uint4*>(coef + ws.blk[b] * 64 + q * 8) = v;
+#else
+        asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+#endif
+    }
+    wave_lds_sync();  // the owners reuse their blocks and the list next iteration
+}
 
 template <bool WRITE>
 __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br, int64_t stop,
                            DecState& st, int64_t& started, int32_t (&dc)[kJpegMaxComp], int64_t g,
-                           int64_t block_lo, int64_t block_end, int16_t* coef, int16_t* lb = nullptr)
+                           int64_t block_lo, int64_t block_end, int16_t* coef, const WaveStage* ws = nullptr)
 {
     int64_t blk = -1;
     bool staged = false;
     uint64_t nz = 0;
     BlockPos pos;
+    int16_t* lb = nullptr;
     if (WRITE) {
+        if (WICCA_JPEG_STAGE) lb = ws->blocks + (threadIdx.x & 63) * kLaneBlock;
         pos.init(im, g < 0 ? 0 : g);
         if (g >= block_lo && g < block_end) blk = pos.index(im);
     }
@@ -221,14 +287,13 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
                 ++g;
                 blk = (g >= block_lo && g < block_end) ? pos.index(im) : -1;
                 if (blk >= 0) {
-#ifndef WICCA_JPEG_ABLATE_STORES
-                    uint4* z = reinterpret_cast<uint4*>(lb);
-#pragma unroll
-                    for (int q = 0; q < 8; ++q) z[q] = make_uint4(0, 0, 0, 0);
-                    lb[0] = (int16_t)dc[c];
-                    nz = 1;
-                    staged = true;
-#endif
+                    if (WICCA_JPEG_STAGE) {
+                        lb[0] = (int16_t)dc[c];
+                        nz = 1;
+                        staged = true;
+                    } else {
+                        coef[blk * 64] = (int16_t)dc[c];
+                    }
                 }
             }
             st.k = 1;
@@ -239,16 +304,12 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
                 const int v = extend(br.get(s), s);
                 if (WRITE && blk >= 0 && st.k < 64) {
                     const int n = kNatural[st.k];
-#ifndef WICCA_JPEG_ABLATE_STORES
                     if (staged) {
                         lb[n] = (int16_t)v;
                         nz |= 1ull << n;
                     } else {
                         coef[blk * 64 + n] = (int16_t)v;
                     }
-#else
-                    asm volatile("" ::"v"(v), "v"(n));
-#endif
                 }
                 ++st.k;
             } else if (r == 15) {
@@ -257,17 +318,14 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
                 st.k = 64;  // EOB
             }
         }
+        bool done = false;
         if (st.k >= 64) {
-            if (WRITE && staged) {  // a whole block of this lane: eight 16-B stores
-                const uint4* src = reinterpret_cast<const uint4*>(lb);
-                uint4* dst = reinterpret_cast<uint4*>(coef + blk * 64);
-#pragma unroll
-                for (int q = 0; q < 8; ++q) dst[q] = src[q];
-                staged = false;
-            }
+            done = WRITE && staged;  // a whole block of this lane
+            staged = false;
             st.slot = st.slot + 1 == im.bpm ? 0 : st.slot + 1;
             st.k = 0;
         }
+        if (WRITE && WICCA_JPEG_STAGE) flush_blocks(done, blk, nz, *ws, coef);
     }
     if (WRITE && staged) {  // the range ends inside this block: its nonzero coefficients only
         while (nz) {
@@ -452,7 +510,12 @@ __global__ __launch_bounds__(kJThreads) void jpeg_write_kernel(JpegPlan P, const
 {
     const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
     __shared__ ImgTabs tabs;
+#if WICCA_JPEG_STAGE
     __shared__ __attribute__((aligned(16))) int16_t lanes[kJThreads * kLaneBlock];
+    __shared__ int64_t s_blk[kJThreads];
+    __shared__ uint64_t s_nz[kJThreads];
+    __shared__ int32_t s_owner[kJThreads];
+#endif
     stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);
     const DecGeom& im = tabs.g;
     if (i >= P.n_sub || P.sub_seg[i] < 0) return;  // padding lane
@@ -473,8 +536,14 @@ __global__ __launch_bounds__(kJThreads) void jpeg_write_kernel(JpegPlan P, const
     BitReader br;
     br.reset(P.stream, st.p);
     // the block in progress at the start was started by an earlier lane
+#if WICCA_JPEG_STAGE
+    const int w0 = (int)(threadIdx.x & ~63u);  // the wave's first lane
+    const WaveStage ws{lanes + w0 * kLaneBlock, s_owner + w0, s_blk + w0, s_nz + w0};
+#else
+    const WaveStage ws{nullptr, nullptr, nullptr, nullptr};
+#endif
     decode_run<true>(im, tabs.t, br, b1, st, started, dc, sg.block0 + b.block - 1, sg.block0,
-                     sg.block_end, P.coef, lanes + threadIdx.x * kLaneBlock);
+                     sg.block_end, P.coef, &ws);
 }
 
 // ---------------------------------------------------------------------------
