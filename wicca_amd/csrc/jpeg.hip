@@ -735,81 +735,143 @@ __device__ __forceinline__ int chroma_sample(const uint8_t* plane, int64_t pitch
 
 __device__ __forceinline__ uint8_t clamp255(int v) { return (uint8_t)min(255, max(0, v)); }
 
-// Four output pixels per lane: one dword of Y, the chroma samples of the four
-// (shared neighbours hit in L1), 12 bytes of RGB as three dword stores.
-__global__ __launch_bounds__(256) void jpeg_color_kernel(JpegPlan P, int img)
+// Four bytes c0..c0+3 of a plane row (c0 >= 0, the 8 bytes from c0 & ~3 inside
+// the row's allocation): two aligned dword loads and a funnel shift.
+__device__ __forceinline__ uint32_t load4_unaligned(const uint8_t* row, int c0)
 {
-    const JpegImageDev& im = P.imgs[img];
-    const int x0 = (blockIdx.x * 256 + threadIdx.x) * 4, y = blockIdx.y;
-    if (x0 >= im.W) return;
-    const int nx = min(4, im.W - x0);
-    // the Y plane is whole 8x8 blocks wide and 256-B aligned: x0..x0+3 is inside
-    const uint32_t y4 = *reinterpret_cast<const uint32_t*>(
-        P.planes + im.comp_plane0[0] + (int64_t)y * ((int64_t)im.comp_bw[0] * 8) + x0);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(row + (c0 & ~3));
+    const uint64_t v = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+    return (uint32_t)(v >> (8 * (c0 & 3)));
+}
+
+// Four output pixels per lane: one dword of Y, the chroma samples of the four
+// (4:2:0: one 4-byte window per chroma row), colour in 32-bit integers
+// (jdcolor.c's JLONG products fit: |91881 * 128| < 2^24).  The workgroup's
+// 3,072 RGB bytes are staged in LDS and leave as 16-B stores when the output
+// row is 16-B aligned (12-B lane stores at a 12-B stride before: 99 us per 8K
+// image).
+constexpr int kColorRows = 1;  // output rows per workgroup (4, or a row loop even at 1: 118 vs 87 us per 8K image)
+
+__device__ __forceinline__ void color_row(const JpegPlan& P, const JpegImageDev& im, int xb, int y,
+                                          uint32_t* stage)
+{
+    const int x0 = xb + threadIdx.x * 4;
+    const int nx = max(0, min(4, im.W - x0));
     uint8_t o[12];
-    if (im.ncomp == 1) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) o[3 * q] = o[3 * q + 1] = o[3 * q + 2] = (uint8_t)(y4 >> (8 * q));
-    } else {
-        const int fh1 = im.hmax / im.comp_h[1], fv1 = im.vmax / im.comp_v[1];
-        const int fh2 = im.hmax / im.comp_h[2], fv2 = im.vmax / im.comp_v[2];
-        const uint8_t* pb = P.planes + im.comp_plane0[1];
-        const uint8_t* pr = P.planes + im.comp_plane0[2];
-        const int64_t sb = (int64_t)im.comp_bw[1] * 8, sr = (int64_t)im.comp_bw[2] * 8;
-        int cbv[4], crv[4];
-        const bool fast420 = fh1 == 2 && fv1 == 2 && fh2 == 2 && fv2 == 2 && im.comp_dw[1] > 2 &&
-                             im.comp_dw[2] > 2 && im.comp_dw[1] == im.comp_dw[2] && im.comp_dh[1] == im.comp_dh[2];
-        if (fast420) {
-            // h2v2 fancy upsampling of 4 output pixels from chroma columns c-1 .. c+2
-            // of the nearest and the next-nearest chroma row (jdsample.c)
-            const int dw = im.comp_dw[1], dh = im.comp_dh[1];
-            const int c = x0 >> 1, iy = y >> 1;
-            const int oy = (y & 1) ? min(iy + 1, dh - 1) : max(iy - 1, 0);
-            int cc[4];
+    for (int i = 0; i < 12; ++i) o[i] = 0;
+    if (nx > 0) {
+        // the Y plane is whole 8x8 blocks wide and 256-B aligned: x0..x0+3 is inside
+        const uint32_t y4 = *reinterpret_cast<const uint32_t*>(
+            P.planes + im.comp_plane0[0] + (int64_t)y * ((int64_t)im.comp_bw[0] * 8) + x0);
+        if (im.ncomp == 1) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) cc[k] = min(max(c - 1 + k, 0), dw - 1);
-            auto four = [&](const uint8_t* plane, int64_t pitch, int (&out)[4]) {
-                const uint8_t* r0 = plane + (int64_t)iy * pitch;
-                const uint8_t* r1 = plane + (int64_t)oy * pitch;
-                int t[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) t[k] = r0[cc[k]] * 3 + r1[cc[k]];
-                out[0] = c == 0 ? (t[1] * 4 + 8) >> 4 : (t[1] * 3 + t[0] + 8) >> 4;
-                out[1] = c == dw - 1 ? (t[1] * 4 + 7) >> 4 : (t[1] * 3 + t[2] + 7) >> 4;
-                out[2] = (t[2] * 3 + t[1] + 8) >> 4;
-                out[3] = c + 1 >= dw - 1 ? (t[2] * 4 + 7) >> 4 : (t[2] * 3 + t[3] + 7) >> 4;
-            };
-            four(pb, sb, cbv);
-            four(pr, sr, crv);
+            for (int q = 0; q < 4; ++q) o[3 * q] = o[3 * q + 1] = o[3 * q + 2] = (uint8_t)(y4 >> (8 * q));
         } else {
+            const int fh1 = im.hmax / im.comp_h[1], fv1 = im.vmax / im.comp_v[1];
+            const int fh2 = im.hmax / im.comp_h[2], fv2 = im.vmax / im.comp_v[2];
+            const uint8_t* pb = P.planes + im.comp_plane0[1];
+            const uint8_t* pr = P.planes + im.comp_plane0[2];
+            const int64_t sb = (int64_t)im.comp_bw[1] * 8, sr = (int64_t)im.comp_bw[2] * 8;
+            int cbv[4], crv[4];
+            const bool fast420 = fh1 == 2 && fv1 == 2 && fh2 == 2 && fv2 == 2 && im.comp_dw[1] > 2 &&
+                                 im.comp_dw[2] > 2 && im.comp_dw[1] == im.comp_dw[2] &&
+                                 im.comp_dh[1] == im.comp_dh[2] && sb == sr;
+            if (fast420) {
+                // h2v2 fancy upsampling of 4 output pixels from chroma columns c-1 .. c+2
+                // of the nearest and the next-nearest chroma row (jdsample.c)
+                const int dw = im.comp_dw[1], dh = im.comp_dh[1];
+                const int c = x0 >> 1, iy = y >> 1;
+                const int oy = (y & 1) ? min(iy + 1, dh - 1) : max(iy - 1, 0);
+                // interior: the window c-1 .. c+2 needs no clamping and its two
+                // aligned dwords lie inside the row (pitch sb, a multiple of 8)
+                const bool interior = c >= 1 && c + 2 <= dw - 1 && ((c - 1) & ~3) + 8 <= sb;
+                auto four = [&](const uint8_t* plane, int (&out)[4]) {
+                    const uint8_t* r0 = plane + (int64_t)iy * sb;
+                    const uint8_t* r1 = plane + (int64_t)oy * sb;
+                    int t[4];
+                    if (interior) {
+                        const uint32_t a = load4_unaligned(r0, c - 1), b = load4_unaligned(r1, c - 1);
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) t[k] = (int)((a >> (8 * k)) & 255) * 3 + (int)((b >> (8 * k)) & 255);
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const int cc = min(max(c - 1 + k, 0), dw - 1);
+                            t[k] = r0[cc] * 3 + r1[cc];
+                        }
+                    }
+                    out[0] = c == 0 ? (t[1] * 4 + 8) >> 4 : (t[1] * 3 + t[0] + 8) >> 4;
+                    out[1] = c == dw - 1 ? (t[1] * 4 + 7) >> 4 : (t[1] * 3 + t[2] + 7) >> 4;
+                    out[2] = (t[2] * 3 + t[1] + 8) >> 4;
+                    out[3] = c + 1 >= dw - 1 ? (t[2] * 4 + 7) >> 4 : (t[2] * 3 + t[3] + 7) >> 4;
+                };
+                four(pb, cbv);
+                four(pr, crv);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int x = min(x0 + q, im.W - 1);
+                    cbv[q] = chroma_sample(pb, sb, im.comp_dw[1], im.comp_dh[1], fh1, fv1, x, y);
+                    crv[q] = chroma_sample(pr, sr, im.comp_dw[2], im.comp_dh[2], fh2, fv2, x, y);
+                }
+            }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const int x = min(x0 + q, im.W - 1);
-                cbv[q] = chroma_sample(pb, sb, im.comp_dw[1], im.comp_dh[1], fh1, fv1, x, y);
-                crv[q] = chroma_sample(pr, sr, im.comp_dw[2], im.comp_dh[2], fh2, fv2, x, y);
+                const int Y = (int)((y4 >> (8 * q)) & 255);
+                const int cb = cbv[q] - 128, cr = crv[q] - 128;
+                const int crr = (91881 * cr + 32768) >> 16;
+                const int cbb = (116130 * cb + 32768) >> 16;
+                const int g = (-46802 * cr + (-22554 * cb + 32768)) >> 16;
+                o[3 * q] = clamp255(Y + crr);
+                o[3 * q + 1] = clamp255(Y + g);
+                o[3 * q + 2] = clamp255(Y + cbb);
             }
         }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int Y = (int)((y4 >> (8 * q)) & 255);
-            const int cb = cbv[q] - 128, cr = crv[q] - 128;
-            const int crr = (int)((91881 * (int64_t)cr + 32768) >> 16);
-            const int cbb = (int)((116130 * (int64_t)cb + 32768) >> 16);
-            const int64_t crg = -46802 * (int64_t)cr, cbg = -22554 * (int64_t)cb + 32768;
-            o[3 * q] = clamp255(Y + crr);
-            o[3 * q + 1] = clamp255(Y + (int)((cbg + crg) >> 16));
-            o[3 * q + 2] = clamp255(Y + cbb);
-        }
     }
-    uint8_t* d = im.dst + (int64_t)y * im.dst_pitch + (int64_t)x0 * 3;
+    uint32_t w3[3];
+#pragma unroll
+    for (int w = 0; w < 3; ++w)
+        w3[w] = (uint32_t)o[4 * w] | ((uint32_t)o[4 * w + 1] << 8) | ((uint32_t)o[4 * w + 2] << 16) |
+                ((uint32_t)o[4 * w + 3] << 24);
+    uint8_t* drow = im.dst + (int64_t)y * im.dst_pitch;
+    uint8_t* d0 = drow + (int64_t)xb * 3;  // the workgroup's first byte
+    if ((((uintptr_t)d0) & 15) == 0) {     // uniform over the workgroup
+#pragma unroll
+        for (int w = 0; w < 3; ++w) stage[threadIdx.x * 3 + w] = w3[w];
+        __syncthreads();
+        const int nbytes = max(0, min(1024, im.W - xb)) * 3;
+        const uint4* s16 = reinterpret_cast<const uint4*>(stage);
+        if ((int)threadIdx.x * 16 + 16 <= nbytes) {
+            reinterpret_cast<uint4*>(d0)[threadIdx.x] = s16[threadIdx.x];
+        } else if ((int)threadIdx.x * 16 < nbytes) {  // the row's last partial chunk
+            const uint8_t* sb8 = reinterpret_cast<const uint8_t*>(stage);
+            for (int i = threadIdx.x * 16; i < nbytes; ++i) d0[i] = sb8[i];
+        }
+        if (kColorRows > 1)  // the stage is rewritten by the next row (LDS-only barrier: a
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // full one waits for the stores)
+        return;
+    }
+    uint8_t* d = drow + (int64_t)x0 * 3;
     if (nx == 4 && ((uintptr_t)d & 3) == 0) {
         uint32_t* d32 = reinterpret_cast<uint32_t*>(d);
 #pragma unroll
-        for (int w = 0; w < 3; ++w)
-            d32[w] = (uint32_t)o[4 * w] | ((uint32_t)o[4 * w + 1] << 8) | ((uint32_t)o[4 * w + 2] << 16) |
-                     ((uint32_t)o[4 * w + 3] << 24);
+        for (int w = 0; w < 3; ++w) d32[w] = w3[w];
     } else {
         for (int i = 0; i < 3 * nx; ++i) d[i] = o[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void jpeg_color_kernel(JpegPlan P, int img)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t stage[256 * 3];
+    const JpegImageDev& im = P.imgs[img];
+    if constexpr (kColorRows == 1) {
+        color_row(P, im, blockIdx.x * 1024, blockIdx.y, stage);
+    } else {
+        const int y0 = blockIdx.y * kColorRows;
+        const int y1 = min(y0 + kColorRows, im.H);
+        for (int y = y0; y < y1; ++y) color_row(P, im, blockIdx.x * 1024, y, stage);  // uniform bounds
     }
 }
 
@@ -927,8 +989,9 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     for (int64_t i = 0; i < n_images; ++i) {
         const JpegImageDev& im = ims[(size_t)i];
-        hipLaunchKernelGGL(jpeg_color_kernel, dim3((uint32_t)((im.W + 1023) / 1024), (uint32_t)im.H), dim3(256),
-                           0, s, P, (int)i);
+        hipLaunchKernelGGL(jpeg_color_kernel, dim3((uint32_t)((im.W + 1023) / 1024),
+                                                   (uint32_t)((im.H + kColorRows - 1) / kColorRows)),
+                           dim3(256), 0, s, P, (int)i);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
