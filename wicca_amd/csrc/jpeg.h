@@ -85,10 +85,12 @@ struct JpegImageDev {
     int32_t dc_tab[kJpegMaxComp], ac_tab[kJpegMaxComp];  // indices into the HuffDev array
     int64_t comp_block0[kJpegMaxComp];  // first block of the component in the coefficient array
     int64_t comp_plane0[kJpegMaxComp];  // first byte of the component's sample plane
-    uint16_t qt[kJpegMaxComp][64];      // natural order, per component
+    alignas(16) uint16_t qt[kJpegMaxComp][64];  // natural order, per component (16-B rows for the IDCT)
     uint8_t* dst;                       // RGB HWC output
     int64_t dst_pitch;
 };
+static_assert(sizeof(JpegImageDev) % 16 == 0, "16-B aligned qt rows in an array of images");
+
 
 struct JpegSegDev {
     int64_t bit0, bits;        // de-stuffed bit range of the segment

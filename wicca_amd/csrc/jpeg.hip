@@ -577,133 +577,129 @@ __device__ __forceinline__ uint8_t idct_limit(int64_t v)
     return (uint8_t)(x < 128 ? x + 128 : x < 512 ? 255 : x < 896 ? 0 : x - 896);
 }
 
+// jidctint.c's 1-D butterfly on 8 values (rows 0..7 of a column in pass 1,
+// columns 0..7 of a row in pass 2), JLONG = 64-bit products as libjpeg-turbo
+// computes them on LP64.  Returns the 8 outputs before descaling.  (A 32-bit
+// variant, exact while every input is below 2^13.5 — intermediates stay under
+// 2^17.45 times the input bound — ran slower: 1.81 vs 1.43 ms per 25 x 8K,
+// both paths taken within waves.)
+template <typename T>
+__device__ __forceinline__ void islow_1d(const T (&v)[8], T (&o)[8])
+{
+    T z2 = v[2], z3 = v[6];
+    T z1 = (z2 + z3) * (T)FIX_0_541196100;
+    T tmp2 = z1 + z3 * (T)(-FIX_1_847759065);
+    T tmp3 = z1 + z2 * (T)FIX_0_765366865;
+    z2 = v[0];
+    z3 = v[4];
+    T tmp0 = (z2 + z3) * ((T)1 << kConstBits);
+    T tmp1 = (z2 - z3) * ((T)1 << kConstBits);
+    const T tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+    tmp0 = v[7];
+    tmp1 = v[5];
+    tmp2 = v[3];
+    tmp3 = v[1];
+    z1 = tmp0 + tmp3;
+    z2 = tmp1 + tmp2;
+    z3 = tmp0 + tmp2;
+    T z4 = tmp1 + tmp3;
+    const T z5 = (z3 + z4) * (T)FIX_1_175875602;
+    tmp0 = tmp0 * (T)FIX_0_298631336;
+    tmp1 = tmp1 * (T)FIX_2_053119869;
+    tmp2 = tmp2 * (T)FIX_3_072711026;
+    tmp3 = tmp3 * (T)FIX_1_501321110;
+    z1 = z1 * (T)(-FIX_0_899976223);
+    z2 = z2 * (T)(-FIX_2_562915447);
+    z3 = z3 * (T)(-FIX_1_961570560);
+    z4 = z4 * (T)(-FIX_0_390180644);
+    z3 += z5;
+    z4 += z5;
+    tmp0 += z1 + z3;
+    tmp1 += z2 + z4;
+    tmp2 += z2 + z3;
+    tmp3 += z1 + z4;
+    o[0] = tmp10 + tmp3;
+    o[7] = tmp10 - tmp3;
+    o[1] = tmp11 + tmp2;
+    o[6] = tmp11 - tmp2;
+    o[2] = tmp12 + tmp1;
+    o[5] = tmp12 - tmp1;
+    o[3] = tmp13 + tmp0;
+    o[4] = tmp13 - tmp0;
+}
+
+// Eight lanes per 8x8 block (a lane per row, then per column, then per row):
+// a block's 128 coefficient bytes are one coalesced read, every lane holds 8
+// values instead of 128 (one lane per block ran at 156 VGPRs, 3 waves per
+// SIMD), and the two transposes go through the wave's LDS.  The all-zero-AC
+// shortcuts of jidctint.c give the same values as the full butterfly, so
+// they are not needed for bit-exactness.
+constexpr int kIdctBlocksPerWg = 32;
+
+__device__ __forceinline__ void idct_group(const JpegPlan& P, const IdctJob& jb, int64_t group, int32_t* tr)
+{
+    const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;  // block of the group, row / column
+    const int64_t b = group * kIdctBlocksPerWg + lb;
+    const bool live = b < (int64_t)jb.bw * jb.bh;  // uniform over the block's 8 lanes
+    int32_t* t = tr + lb * 64;
+    if (live) {
+        const uint4 v = *reinterpret_cast<const uint4*>(P.coef + (jb.block0 + b) * 64 + r * 8);
+        const uint4 qv = *reinterpret_cast<const uint4*>(P.imgs[jb.img].qt[jb.comp] + r * 8);
+        const uint32_t cw[4] = {v.x, v.y, v.z, v.w}, qw[4] = {qv.x, qv.y, qv.z, qv.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // dequantised row r (coefficient * quantiser fits in int32)
+            t[r * 8 + 2 * k] = (int32_t)(int16_t)(cw[k] & 0xFFFF) * (int32_t)(qw[k] & 0xFFFF);
+            t[r * 8 + 2 * k + 1] = (int32_t)(int16_t)(cw[k] >> 16) * (int32_t)(qw[k] >> 16);
+        }
+    }
+    wave_lds_sync();
+    int64_t col[8], o[8];
+    if (live) {  // pass 1: column r
+#pragma unroll
+        for (int k = 0; k < 8; ++k) col[k] = t[k * 8 + r];
+        islow_1d<int64_t>(col, o);
+    }
+    wave_lds_sync();
+    if (live) {
+        constexpr int sh = kConstBits - kPass1Bits;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) t[k * 8 + r] = (int32_t)descale(o[k], sh);
+    }
+    wave_lds_sync();
+    if (!live) return;
+    // pass 2: row r -> samples
+    int64_t row[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) row[k] = t[r * 8 + k];
+    islow_1d<int64_t>(row, o);
+    constexpr int sh = kConstBits + kPass1Bits + 3;
+    uint8_t px[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) px[k] = idct_limit(descale(o[k], sh));
+    const int by = (int)(b / jb.bw), bx = (int)(b - (int64_t)by * jb.bw);
+    const int64_t pitch = (int64_t)jb.bw * 8;
+    uint2 pk;
+    pk.x = (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16) | ((uint32_t)px[3] << 24);
+    pk.y = (uint32_t)px[4] | ((uint32_t)px[5] << 8) | ((uint32_t)px[6] << 16) | ((uint32_t)px[7] << 24);
+    *reinterpret_cast<uint2*>(P.planes + jb.plane0 + ((int64_t)by * 8 + r) * pitch + (int64_t)bx * 8) = pk;
+}
+
+// kIdctGroups groups of 32 blocks per workgroup: one-group workgroups were
+// bound by workgroup dispatch (1.2 M per 25 x 8K call, half of them past the
+// chroma planes' ends).
+constexpr int kIdctGroups = 8;
+
 __global__ __launch_bounds__(256) void jpeg_idct_kernel(JpegPlan P, const IdctJob* jobs)
 {
+    __shared__ int32_t tr[kIdctBlocksPerWg * 64];
     const IdctJob jb = jobs[blockIdx.y];
-    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (b >= (int64_t)jb.bw * jb.bh) return;
-    const int by = (int)(b / jb.bw), bx = (int)(b - (int64_t)by * jb.bw);
-    const int16_t* in = P.coef + (jb.block0 + b) * 64;
-    const uint16_t* q = P.imgs[jb.img].qt[jb.comp];
-    int ws[64];
-    int16_t cf[64];
-#pragma unroll
-    for (int i = 0; i < 64; i += 8) {
-        const uint4 v = *reinterpret_cast<const uint4*>(in + i);
-        cf[i + 0] = (int16_t)(v.x & 0xFFFF); cf[i + 1] = (int16_t)(v.x >> 16);
-        cf[i + 2] = (int16_t)(v.y & 0xFFFF); cf[i + 3] = (int16_t)(v.y >> 16);
-        cf[i + 4] = (int16_t)(v.z & 0xFFFF); cf[i + 5] = (int16_t)(v.z >> 16);
-        cf[i + 6] = (int16_t)(v.w & 0xFFFF); cf[i + 7] = (int16_t)(v.w >> 16);
-    }
-    // pass 1: columns
-#pragma unroll
-    for (int col = 0; col < 8; ++col) {
-        auto dq = [&](int row) -> int64_t { return (int64_t)cf[row * 8 + col] * (int64_t)q[row * 8 + col]; };
-        if (cf[8 + col] == 0 && cf[16 + col] == 0 && cf[24 + col] == 0 && cf[32 + col] == 0 &&
-            cf[40 + col] == 0 && cf[48 + col] == 0 && cf[56 + col] == 0) {
-            const int dcval = (int)(dq(0) * (1 << kPass1Bits));
-#pragma unroll
-            for (int r = 0; r < 8; ++r) ws[r * 8 + col] = dcval;
-            continue;
-        }
-        int64_t z2 = dq(2), z3 = dq(6);
-        int64_t z1 = (z2 + z3) * FIX_0_541196100;
-        int64_t tmp2 = z1 + z3 * (-FIX_1_847759065);
-        int64_t tmp3 = z1 + z2 * FIX_0_765366865;
-        z2 = dq(0);
-        z3 = dq(4);
-        int64_t tmp0 = (z2 + z3) * ((int64_t)1 << kConstBits);
-        int64_t tmp1 = (z2 - z3) * ((int64_t)1 << kConstBits);
-        const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
-        tmp0 = dq(7);
-        tmp1 = dq(5);
-        tmp2 = dq(3);
-        tmp3 = dq(1);
-        z1 = tmp0 + tmp3;
-        z2 = tmp1 + tmp2;
-        z3 = tmp0 + tmp2;
-        int64_t z4 = tmp1 + tmp3;
-        const int64_t z5 = (z3 + z4) * FIX_1_175875602;
-        tmp0 = tmp0 * FIX_0_298631336;
-        tmp1 = tmp1 * FIX_2_053119869;
-        tmp2 = tmp2 * FIX_3_072711026;
-        tmp3 = tmp3 * FIX_1_501321110;
-        z1 = z1 * (-FIX_0_899976223);
-        z2 = z2 * (-FIX_2_562915447);
-        z3 = z3 * (-FIX_1_961570560);
-        z4 = z4 * (-FIX_0_390180644);
-        z3 += z5;
-        z4 += z5;
-        tmp0 += z1 + z3;
-        tmp1 += z2 + z4;
-        tmp2 += z2 + z3;
-        tmp3 += z1 + z4;
-        constexpr int sh = kConstBits - kPass1Bits;
-        ws[0 * 8 + col] = (int)descale(tmp10 + tmp3, sh);
-        ws[7 * 8 + col] = (int)descale(tmp10 - tmp3, sh);
-        ws[1 * 8 + col] = (int)descale(tmp11 + tmp2, sh);
-        ws[6 * 8 + col] = (int)descale(tmp11 - tmp2, sh);
-        ws[2 * 8 + col] = (int)descale(tmp12 + tmp1, sh);
-        ws[5 * 8 + col] = (int)descale(tmp12 - tmp1, sh);
-        ws[3 * 8 + col] = (int)descale(tmp13 + tmp0, sh);
-        ws[4 * 8 + col] = (int)descale(tmp13 - tmp0, sh);
-    }
-    // pass 2: rows -> samples
-    const int64_t pitch = (int64_t)jb.bw * 8;
-    uint8_t* out = P.planes + jb.plane0 + ((int64_t)by * 8) * pitch + (int64_t)bx * 8;
-#pragma unroll
-    for (int row = 0; row < 8; ++row) {
-        const int* w = ws + row * 8;
-        uint8_t o[8];
-        constexpr int sh = kConstBits + kPass1Bits + 3;
-        if (w[1] == 0 && w[2] == 0 && w[3] == 0 && w[4] == 0 && w[5] == 0 && w[6] == 0 && w[7] == 0) {
-            const uint8_t v = idct_limit(descale((int64_t)w[0], kPass1Bits + 3));
-#pragma unroll
-            for (int c = 0; c < 8; ++c) o[c] = v;
-        } else {
-            int64_t z2 = w[2], z3 = w[6];
-            int64_t z1 = (z2 + z3) * FIX_0_541196100;
-            int64_t tmp2 = z1 + z3 * (-FIX_1_847759065);
-            int64_t tmp3 = z1 + z2 * FIX_0_765366865;
-            int64_t tmp0 = ((int64_t)w[0] + (int64_t)w[4]) * ((int64_t)1 << kConstBits);
-            int64_t tmp1 = ((int64_t)w[0] - (int64_t)w[4]) * ((int64_t)1 << kConstBits);
-            const int64_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
-            tmp0 = w[7];
-            tmp1 = w[5];
-            tmp2 = w[3];
-            tmp3 = w[1];
-            z1 = tmp0 + tmp3;
-            z2 = tmp1 + tmp2;
-            z3 = tmp0 + tmp2;
-            int64_t z4 = tmp1 + tmp3;
-            const int64_t z5 = (z3 + z4) * FIX_1_175875602;
-            tmp0 = tmp0 * FIX_0_298631336;
-            tmp1 = tmp1 * FIX_2_053119869;
-            tmp2 = tmp2 * FIX_3_072711026;
-            tmp3 = tmp3 * FIX_1_501321110;
-            z1 = z1 * (-FIX_0_899976223);
-            z2 = z2 * (-FIX_2_562915447);
-            z3 = z3 * (-FIX_1_961570560);
-            z4 = z4 * (-FIX_0_390180644);
-            z3 += z5;
-            z4 += z5;
-            tmp0 += z1 + z3;
-            tmp1 += z2 + z4;
-            tmp2 += z2 + z3;
-            tmp3 += z1 + z4;
-            o[0] = idct_limit(descale(tmp10 + tmp3, sh));
-            o[7] = idct_limit(descale(tmp10 - tmp3, sh));
-            o[1] = idct_limit(descale(tmp11 + tmp2, sh));
-            o[6] = idct_limit(descale(tmp11 - tmp2, sh));
-            o[2] = idct_limit(descale(tmp12 + tmp1, sh));
-            o[5] = idct_limit(descale(tmp12 - tmp1, sh));
-            o[3] = idct_limit(descale(tmp13 + tmp0, sh));
-            o[4] = idct_limit(descale(tmp13 - tmp0, sh));
-        }
-        uint2 pk;
-        pk.x = (uint32_t)o[0] | ((uint32_t)o[1] << 8) | ((uint32_t)o[2] << 16) | ((uint32_t)o[3] << 24);
-        pk.y = (uint32_t)o[4] | ((uint32_t)o[5] << 8) | ((uint32_t)o[6] << 16) | ((uint32_t)o[7] << 24);
-        *reinterpret_cast<uint2*>(out + row * pitch) = pk;
+    const int64_t n_groups = ((int64_t)jb.bw * jb.bh + kIdctBlocksPerWg - 1) / kIdctBlocksPerWg;
+#pragma unroll 1
+    for (int k = 0; k < kIdctGroups; ++k) {
+        const int64_t g = (int64_t)blockIdx.x * kIdctGroups + k;
+        if (g >= n_groups) break;  // uniform
+        idct_group(P, jb, g, tr);
+        wave_lds_sync();  // the wave's transposes are rewritten by the next group
     }
 }
 
@@ -984,7 +980,8 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     if ((e = hipGetLastError()) != hipSuccess) return e;
     hipLaunchKernelGGL(jpeg_write_kernel, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(jpeg_idct_kernel, dim3((uint32_t)((max_blocks + 255) / 256), (uint32_t)hj.size()),
+    const int64_t per_wg = (int64_t)kIdctBlocksPerWg * kIdctGroups;
+    hipLaunchKernelGGL(jpeg_idct_kernel, dim3((uint32_t)((max_blocks + per_wg - 1) / per_wg), (uint32_t)hj.size()),
                        dim3(256), 0, s, P, jobs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     for (int64_t i = 0; i < n_images; ++i) {
