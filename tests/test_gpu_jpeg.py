@@ -163,3 +163,26 @@ def test_batch_larger_than_one_device_pass():
     got = WJ.decode_batch(blobs)
     for i in (0, 1364, 1365, 1366, 1399):
         assert np.array_equal(got[i], J.decode_rgb(blobs[i])), i
+
+
+def test_six_table_write_kernel_subprocess():
+    """The write pass has a 4-table build (every baseline file) and a 6-table
+    one (extended-sequential files with separate tables per component); force
+    the 6-table kernel in a child process and check the golden files."""
+    import subprocess
+    import sys
+    code = (
+        "import hashlib, json, os, sys\n"
+        "from wicca_amd import jpeg as WJ\n"
+        f"gold = {GOLD!r}\n"
+        "cases = json.load(open(os.path.join(gold, 'cases.json')))['cases']\n"
+        "data = [open(os.path.join(gold, c['file']), 'rb').read() for c in cases]\n"
+        "outs = WJ.decode_batch(data)\n"
+        "bad = [c['name'] for c, o in zip(cases, outs)\n"
+        "       if hashlib.sha256(o.tobytes()).hexdigest() != c['sha256_rgb']]\n"
+        "print('BAD', bad)\n"
+        "sys.exit(1 if bad else 0)\n")
+    env = dict(os.environ, WICCA_JPEG_WRITE_SLOTS="6")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -262,6 +262,16 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     P.n_sub = (int64_t)sub_seg.size();
     P.n_seg = (int64_t)segs.size();
     P.sub_bits = (int32_t)S;
+    // an image's tables are consecutive in `huff`: its count is max - min + 1
+    P.max_tabs = 1;
+    for (const auto& im : ims) {
+        int lo = INT32_MAX, hi = -1;
+        for (int c = 0; c < im.ncomp; ++c) {
+            lo = std::min({lo, im.dc_tab[c], im.ac_tab[c]});
+            hi = std::max({hi, im.dc_tab[c], im.ac_tab[c]});
+        }
+        P.max_tabs = std::max(P.max_tabs, hi - lo + 1);
+    }
     int rounds = 0;
     const double t_upload = now_ms();
     HIP_TRY(wicca::jpeg_decode_device(P, ims.data(), ws->jscratch.ptr, n, &rounds, stream));

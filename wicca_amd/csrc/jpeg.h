@@ -110,6 +110,7 @@ struct JpegPlan {
     int64_t n_sub, n_seg;
     int32_t sub_bits;        // subsequence length
     const int32_t* sub_img;  // per workgroup of kJpegLanes subsequences: its image (uniform)
+    int32_t max_tabs;        // most Huffman tables one image of the batch uses (<= 2 * kJpegMaxComp)
 };
 
 // Lanes per decode workgroup; an image's subsequences are padded to whole

@@ -30,6 +30,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "jpeg.h"
@@ -193,19 +194,16 @@ struct BlockPos {
 // coefficient by coefficient, and so is the nonzero part of a block the range
 // ends inside (the next lane writes its other coefficients): no two lanes ever
 // write the same bytes.
-constexpr int kLaneBlock = 72;  // int16 per lane in LDS (144 B: 16-B aligned, spreads banks)
+constexpr int kLaneBlock = 64;  // int16 per lane in LDS: one block
 #ifndef WICCA_JPEG_STAGE
 #define WICCA_JPEG_STAGE 1  // 0: every coefficient leaves as its own 2-B store (no LDS staging)
 #endif
 
 // Per-wave LDS of the write pass: every lane's block under assembly, and the
-// flush list (owner lane, block index, coefficient mask) of blocks completed
-// in the current iteration.
+// owner lanes of the blocks completed in the current iteration.
 struct WaveStage {
     int16_t* blocks;  // 64 * kLaneBlock
-    int32_t* owner;   // 64
-    int64_t* blk;     // 64
-    uint64_t* nz;     // 64
+    uint8_t* owner;   // 64
 };
 
 __device__ __forceinline__ void wave_lds_sync()
@@ -215,12 +213,20 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+__device__ __forceinline__ int64_t shfl64(int64_t v, int src)
+{
+    const int lo = __shfl((int)(uint32_t)v, src, 64), hi = __shfl((int)(uint32_t)((uint64_t)v >> 32), src, 64);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
 // Blocks completed by lanes of this wave in this iteration leave as full
 // 128-B blocks: the wave's active lanes deal the 8 16-B chunks of every such
 // block among themselves, so one store instruction writes up to 8 blocks
 // (a lane storing its own block issued 8 mostly-empty instructions per block,
-// on nearly every iteration of every wave: 2.4 -> 6.2 ms for the pass).
-// Coefficients the block did not set come out as zeros (mask `nz`).
+// on nearly every iteration of every wave).  Coefficients the block did not
+// set come out as zeros (mask `nz`).  Block index and mask come from the owner
+// lane by shuffle; every active lane runs every round of the loop (owners are
+// active), only the stores are predicated.
 __device__ __forceinline__ void flush_blocks(bool done, int64_t blk, uint64_t nz, const WaveStage& ws,
                                              int16_t* coef)
 {
@@ -229,31 +235,34 @@ __device__ __forceinline__ void flush_blocks(bool done, int64_t blk, uint64_t nz
     const uint64_t act = __ballot(true);
     const int lane = (int)(threadIdx.x & 63);
     const uint64_t below = (1ull << lane) - 1;
-    if (done) {
-        const int r = __popcll(pend & below);
-        ws.owner[r] = lane;
-        ws.blk[r] = blk;
-        ws.nz[r] = nz;
-    }
+    if (done) ws.owner[__popcll(pend & below)] = (uint8_t)lane;
     wave_lds_sync();
     const int n_act = __popcll(act), n_chunks = 8 * __popcll(pend);
+    const int rounds = (n_chunks + n_act - 1) / n_act;
+    int c = __popcll(act & below);
 #pragma unroll 1
-    for (int c = __popcll(act & below); c < n_chunks; c += n_act) {
-        const int b = c >> 3, q = c & 7;
-        uint4 v = *reinterpret_cast<const uint4*>(ws.blocks + ws.owner[b] * kLaneBlock + q * 8);
-        const uint32_t m = (uint32_t)(ws.nz[b] >> (q * 8)) & 0xFFu;
-        auto keep = [&](uint32_t w, int d) -> uint32_t {
-            return w & (((m >> (2 * d)) & 1u ? 0x0000FFFFu : 0u) | ((m >> (2 * d + 1)) & 1u ? 0xFFFF0000u : 0u));
-        };
-        v.x = keep(v.x, 0);
-        v.y = keep(v.y, 1);
-        v.z = keep(v.z, 2);
-        v.w = keep(v.w, 3);
+    for (int t = 0; t < rounds; ++t, c += n_act) {
+        const bool valid = c < n_chunks;
+        const int bi = valid ? c >> 3 : 0, q = c & 7;
+        const int o = ws.owner[bi];
+        const int64_t ob = shfl64(blk, o);
+        const uint64_t onz = (uint64_t)shfl64((int64_t)nz, o);
+        if (valid) {
+            uint4 v = *reinterpret_cast<const uint4*>(ws.blocks + o * kLaneBlock + q * 8);
+            const uint32_t m = (uint32_t)(onz >> (q * 8)) & 0xFFu;
+            auto keep = [&](uint32_t w, int d) -> uint32_t {
+                return w & (((m >> (2 * d)) & 1u ? 0x0000FFFFu : 0u) | ((m >> (2 * d + 1)) & 1u ? 0xFFFF0000u : 0u));
+            };
+            v.x = keep(v.x, 0);
+            v.y = keep(v.y, 1);
+            v.z = keep(v.z, 2);
+            v.w = keep(v.w, 3);
 #ifndef WICCA_JPEG_ABLATE_STORES
-        *reinterpret_cast<uint4*>(coef + ws.blk[b] * 64 + q * 8) = v;
+            *reinterpret_cast<uint4*>(coef + ob * 64 + q * 8) = v;
 #else
-        asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+            asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w), "v"(ob));
 #endif
+        }
     }
     wave_lds_sync();  // the owners reuse their blocks and the list next iteration
 }
@@ -337,29 +346,31 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
     st.p = br.p;
 }
 
-// The image's Huffman tables, staged in LDS: slot 2c = DC table of component
-// c, 2c + 1 = its AC table.  Every workgroup serves one image (the host pads
-// each image's subsequences to whole workgroups).
+// The image's Huffman tables, staged in LDS: the host stores an image's
+// distinct tables consecutively in P.huff (at most NS of them here), slot s =
+// table first + s.  Every workgroup serves one image (the host pads each
+// image's subsequences to whole workgroups).
+template <int NS>
 struct ImgTabs {
-    HuffDev t[2 * kJpegMaxComp];
+    HuffDev t[NS];
     DecGeom g;
 };
 
-__device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageDev* imp, ImgTabs& lds)
+template <int NS>
+__device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageDev* imp, ImgTabs<NS>& lds)
 {
     constexpr int kWords = sizeof(HuffDev) / 4;
     static_assert(sizeof(HuffDev) % 4 == 0, "word copy");
     const int ncomp = imp->ncomp;
+    int first = imp->dc_tab[0], last = imp->dc_tab[0];
     for (int c = 0; c < ncomp; ++c) {
-        const uint32_t* sdc = reinterpret_cast<const uint32_t*>(P.huff + imp->dc_tab[c]);
-        const uint32_t* sac = reinterpret_cast<const uint32_t*>(P.huff + imp->ac_tab[c]);
-        uint32_t* ddc = reinterpret_cast<uint32_t*>(&lds.t[2 * c]);
-        uint32_t* dac = reinterpret_cast<uint32_t*>(&lds.t[2 * c + 1]);
-        for (int w = threadIdx.x; w < kWords; w += kJThreads) {
-            ddc[w] = sdc[w];
-            dac[w] = sac[w];
-        }
+        first = min(first, min(imp->dc_tab[c], imp->ac_tab[c]));
+        last = max(last, max(imp->dc_tab[c], imp->ac_tab[c]));
     }
+    const int n = min(last - first + 1, NS);  // the launcher picked NS >= every image's count
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(P.huff + first);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&lds.t[0]);
+    for (int w = threadIdx.x; w < n * kWords; w += kJThreads) dst[w] = src[w];
     if (threadIdx.x == 0) {
         DecGeom& g = lds.g;
         g.bpm = imp->bpm;
@@ -374,8 +385,8 @@ __device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageD
             g.comp_h[c] = imp->comp_h[c];
             g.comp_v[c] = imp->comp_v[c];
             g.comp_bw[c] = imp->comp_bw[c];
-            g.dc_tab[c] = 2 * c;
-            g.ac_tab[c] = 2 * c + 1;
+            g.dc_tab[c] = c < ncomp ? imp->dc_tab[c] - first : 0;
+            g.ac_tab[c] = c < ncomp ? imp->ac_tab[c] - first : 0;
         }
     }
     __syncthreads();
@@ -399,7 +410,7 @@ __global__ __launch_bounds__(kJThreads) void jpeg_sync_kernel(JpegPlan P, const 
                                                              const SubResult* older)
 {
     const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
-    __shared__ ImgTabs tabs;
+    __shared__ ImgTabs<2 * kJpegMaxComp> tabs;
     stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);
     const DecGeom& im = tabs.g;
     if (i >= P.n_sub || P.sub_seg[i] < 0) return;  // padding lane
@@ -505,16 +516,17 @@ __global__ __launch_bounds__(256) void jpeg_scan_kernel(JpegPlan P, const SubRes
 }
 
 // Final pass: scatter coefficients (converged start states, scanned bases).
-__global__ __launch_bounds__(kJThreads) void jpeg_write_kernel(JpegPlan P, const SubResult* res,
-                                                              const SubBase* base)
+// NS table slots: 4 (every baseline image: 2 DC + 2 AC tables) keeps the
+// workgroup's LDS under 40 KB, i.e. 4 workgroups per CU instead of 3.
+template <int NS>
+__global__ __launch_bounds__(kJThreads, NS <= 4 ? 4 : 1) void jpeg_write_kernel(JpegPlan P, const SubResult* res,
+                                                                 const SubBase* base)
 {
     const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
-    __shared__ ImgTabs tabs;
+    __shared__ ImgTabs<NS> tabs;
 #if WICCA_JPEG_STAGE
     __shared__ __attribute__((aligned(16))) int16_t lanes[kJThreads * kLaneBlock];
-    __shared__ int64_t s_blk[kJThreads];
-    __shared__ uint64_t s_nz[kJThreads];
-    __shared__ int32_t s_owner[kJThreads];
+    __shared__ uint8_t s_owner[kJThreads];
 #endif
     stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);
     const DecGeom& im = tabs.g;
@@ -535,13 +547,13 @@ __global__ __launch_bounds__(kJThreads) void jpeg_write_kernel(JpegPlan P, const
     int64_t started = 0;
     BitReader br;
     br.reset(P.stream, st.p);
-    // the block in progress at the start was started by an earlier lane
 #if WICCA_JPEG_STAGE
     const int w0 = (int)(threadIdx.x & ~63u);  // the wave's first lane
-    const WaveStage ws{lanes + w0 * kLaneBlock, s_owner + w0, s_blk + w0, s_nz + w0};
+    const WaveStage ws{lanes + w0 * kLaneBlock, s_owner + w0};
 #else
-    const WaveStage ws{nullptr, nullptr, nullptr, nullptr};
+    const WaveStage ws{nullptr, nullptr};
 #endif
+    // the block in progress at the start was started by an earlier lane
     decode_run<true>(im, tabs.t, br, b1, st, started, dc, sg.block0 + b.block - 1, sg.block0,
                      sg.block_end, P.coef, &ws);
 }
@@ -978,7 +990,14 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     if (sync_rounds) *sync_rounds = rounds;
     hipLaunchKernelGGL(jpeg_scan_kernel, dim3((uint32_t)P.n_seg), dim3(256), 0, s, P, cur, sb);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(jpeg_write_kernel, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
+    static const bool force6 = [] {  // WICCA_JPEG_WRITE_SLOTS=6: the 6-table kernel for every batch (tests)
+        const char* e = getenv("WICCA_JPEG_WRITE_SLOTS");
+        return e && atoi(e) == 6;
+    }();
+    if (P.max_tabs <= 4 && !force6)
+        hipLaunchKernelGGL(jpeg_write_kernel<4>, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
+    else
+        hipLaunchKernelGGL(jpeg_write_kernel<2 * kJpegMaxComp>, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const int64_t per_wg = (int64_t)kIdctBlocksPerWg * kIdctGroups;
     hipLaunchKernelGGL(jpeg_idct_kernel, dim3((uint32_t)((max_blocks + per_wg - 1) / per_wg), (uint32_t)hj.size()),
