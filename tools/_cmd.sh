@@ -1,7 +1,5 @@
 set -e
-timeout -k 10 400 python -u -m pytest tests/test_gpu_jpeg.py -x -q --timeout 300 --timeout-method thread 2>&1 | tail -2
-WICCA_JPEG_TIMING=1 timeout -k 10 300 python -u bench.py --config jpeg --steps 10 --no-cpu-baseline > gpurun_out/jpeg_bench.json 2> gpurun_out/jpeg_bench.err
-tail -1 gpurun_out/jpeg_bench.err
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_jpeg -- python3 -u bench.py --config jpeg --steps 10 --no-cpu-baseline > gpurun_out/jpeg_prof.json
-find gpurun_out/prof_jpeg -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/jpeg_kernel_stats.csv
+for sb in 8192 4096 2048 8192 4096 2048; do
+WICCA_JPEG_SUB_BITS=$sb WICCA_JPEG_TIMING=1 timeout -k 10 300 python -u bench.py --config jpeg --steps 10 --no-cpu-baseline 2> gpurun_out/jpeg_sb.err | python3 -c "import sys,json; d=json.loads(sys.stdin.read()); print('$sb', d['value'], d['ms_per_step'], d['sync_rounds'], d['file_stage']['ms_per_batch'])"
+tail -1 gpurun_out/jpeg_sb.err
+done

@@ -26,18 +26,19 @@ namespace {
 // Subsequence length (bits) of the parallel Huffman decode: long enough that a
 // lane started at a guessed state resynchronises (bit alignment AND MCU slot)
 // inside its own subsequence — 2048 bits needed 9 passes on 8K photos — and
-// short enough to keep ~256 K lanes in flight (the passes are latency-bound).
-// Measured on 25 x 8K q90 4:2:0 files (profiles/r02_jpeg_sub_bits.jsonl):
-// 4096 bits 3 passes 27.0 GP/s, 8192 2 passes 28.4, 16384 1 pass 27.2, 32768
-// 1 pass 22.2.  WICCA_JPEG_SUB_BITS overrides.
+// short enough to keep ~512 K lanes in flight (the passes are latency-bound).
+// Measured on 25 x 8K q90 4:2:0 files since the sync passes skip lanes whose
+// start did not move (profiles/r02u_jpeg_sub_bits.log): 2048 bits 9 passes
+// 40.7 GP/s, 4096 3 passes 45.6, 8192 2 passes 43.0 (before the skip:
+// r02_jpeg_sub_bits.jsonl).  WICCA_JPEG_SUB_BITS overrides.
 int64_t jpeg_sub_bits(int64_t total_bits)
 {
     static const int64_t env = [] {
         const char* e = getenv("WICCA_JPEG_SUB_BITS");
         return e ? (int64_t)atoll(e) : (int64_t)0;
     }();
-    int64_t b = env > 0 ? env : total_bits / 262144;
-    b = std::max<int64_t>(env > 0 ? 256 : 8192, std::min<int64_t>(b, 65536));
+    int64_t b = env > 0 ? env : total_bits / 524288;
+    b = std::max<int64_t>(env > 0 ? 256 : 4096, std::min<int64_t>(b, 65536));
     return (b + 255) & ~(int64_t)255;
 }
 
