@@ -41,6 +41,9 @@ def main():
                     help="round ragged widths down to a multiple of this many pixels")
     ap.add_argument("--ragged-hmult", type=int, default=1,
                     help="round ragged heights down to a multiple of this many rows")
+    ap.add_argument("--multi", default="",
+                    help="comma-separated depth list: time wicca_haar_ll_u8_multi_uniform (K5) "
+                         "instead of single depths (uniform batch)")
     ap.add_argument("--pitch-pad", type=int, default=0,
                     help="uniform batch: bytes added to the 16-B aligned row pitch")
     ap.add_argument("--no-check", action="store_true",
@@ -84,6 +87,46 @@ def main():
                                         Ws[i], C, pitches[i], Hs[i] * pitches[i], i, -1, sh) == 0
     pitch = pitches[0]
     results = []
+    if args.multi:
+        ds = [int(x) for x in args.multi.split(",")]
+        outs, c_p, c_pi, c_s = [], [], [], []
+        alg = B * H * W * C
+        for d in ds:
+            oh, ow = -(-H // (1 << d)), -(-W // (1 << d))
+            op = (ow * C + 15) // 16 * 16
+            outs.append(torch.empty(B * oh * op, dtype=torch.uint8, device="cuda"))
+            c_p.append(outs[-1].data_ptr())
+            c_pi.append(op)
+            c_s.append(oh * op)
+            alg += B * oh * ow * C
+        arr_d = (ctypes.c_int * len(ds))(*ds)
+        arr_p = (ctypes.c_void_p * len(ds))(*c_p)
+        arr_pi = (ctypes.c_int64 * len(ds))(*c_pi)
+        arr_s = (ctypes.c_int64 * len(ds))(*c_s)
+        samples = {k: [] for k in libs}
+        for rnd in range(args.rounds):
+            for name, h in libs.items():
+                def mstep():
+                    rc = h.wicca_haar_ll_u8_multi_uniform(
+                        ctypes.c_void_p(src.data_ptr()), B, H, W, C, pitch, H * pitch, arr_d, len(ds),
+                        args.border, 0, arr_p, arr_pi, arr_s, -1, sh)
+                    assert rc == 0, rc
+                for _ in range(2):
+                    mstep()
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(args.steps):
+                    mstep()
+                e1.record(stream)
+                e1.synchronize()
+                samples[name].append(alg / (e0.elapsed_time(e1) / args.steps / 1e3) / 1e9)
+        for name, v in samples.items():
+            row = {"lib": name, "depths": ds, "median_gbs": round(statistics.median(v), 1),
+                   "min_gbs": round(min(v), 1), "max_gbs": round(max(v), 1), "rounds": len(v)}
+            results.append(row)
+            print(json.dumps(row), flush=True)
+        args.depths = []
     for D in args.depths:
         r = 1 << D
         oh, ow = -(-H // r), -(-W // r)

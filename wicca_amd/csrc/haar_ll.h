@@ -44,7 +44,7 @@
                               // separate K1 launch for depth 1 (profiles/r01_ab_k5_depth1.json)
 #endif
 #ifndef WICCA_MULTI_FW
-#define WICCA_MULTI_FW 16     // K5: level-DMIN blocks per flush window (power of 2)
+#define WICCA_MULTI_FW 0      // K5: level-DMIN blocks per flush window (power of 2); 0: multi_fw table
 #endif
 #ifndef WICCA_MULTI_CHUNK
 #define WICCA_MULTI_CHUNK 8   // K5 interior strips: rows per load chunk (double-buffered)
@@ -196,6 +196,10 @@ struct MultiParams {
     uint8_t* dst[9];   // per depth t: icon base, row pitch, image stride
     int64_t dst_pitch[9], dst_stride[9];
 };
+// K5 flush window (level-DMIN blocks): 8 at DMIN = 1 (depths 1-6 +1.5 %), 16
+// otherwise (depths 2-6: 8 was -1.7 %; profiles/r02_ab_fw_*.json).
+constexpr int multi_fw(int dmin) { return WICCA_MULTI_FW > 0 ? WICCA_MULTI_FW : (dmin == 1 ? 8 : 16); }
+
 bool multi_kernel_ok(const uint8_t* src, int64_t src_pitch, int64_t src_stride, int64_t W, int C,
                      int dmin, int dmax);
 hipError_t launch_multi(MultiParams p, int dmin, int C, hipStream_t s);

@@ -163,7 +163,7 @@ constexpr int lane_icons()
 // every block (16 per 64-row band) cost K5 ~30 % of its time.
 template <int DMIN, int DMAX, int C>
 struct MultiStage {
-    static constexpr int FW = (1 << (DMAX - DMIN)) < WICCA_MULTI_FW ? (1 << (DMAX - DMIN)) : WICCA_MULTI_FW;
+    static constexpr int FW = (1 << (DMAX - DMIN)) < multi_fw(DMIN) ? (1 << (DMAX - DMIN)) : multi_fw(DMIN);
     static constexpr int WINDOWS = (1 << (DMAX - DMIN)) / FW;  // flush windows per band
     static constexpr int NBUF = WINDOWS > 1 ? 2 : 1;
     static constexpr int per(int t) { return 1 << (t - DMIN); }  // level-DMIN blocks per level-t row
