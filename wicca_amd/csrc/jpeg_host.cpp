@@ -11,6 +11,8 @@
 #include <climits>
 #include <cstring>
 
+#include <immintrin.h>
+
 #include "jpeg.h"
 
 namespace wicca {
@@ -218,37 +220,86 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
     return 0;
 }
 
-size_t jpeg_destuff_into(const JpegInfo& info, uint8_t* out, std::vector<int64_t>& seg_off)
+namespace {
+
+// One 0xFF at s[*i] (i + 1 < n): a stuffed data byte, a fill byte, an RSTn
+// (the next restart segment starts at the current output length) or the end
+// of the scan.  Returns false at the end of the scan.
+inline bool destuff_marker(const uint8_t* s, size_t& i, uint8_t* out, size_t& o, std::vector<int64_t>& seg_off)
 {
-    const uint8_t* s = info.scan;
-    const size_t n = info.scan_len;
-    size_t o = 0;
-    seg_off.assign(1, 0);
-    size_t i = 0;
+    const uint8_t nx = s[i + 1];
+    if (nx == 0x00) {  // stuffed data byte
+        out[o++] = 0xFF;
+        i += 2;
+    } else if (nx == 0xFF) {  // fill byte
+        i += 1;
+    } else if (nx >= 0xD0 && nx <= 0xD7) {  // RSTn: next segment starts byte-aligned
+        seg_off.push_back((int64_t)o);
+        i += 2;
+    } else {
+        return false;  // EOI or another marker: end of the scan
+    }
+    return true;
+}
+
+// Scalar tail / fallback: memchr to the next 0xFF, memcpy the run.
+size_t destuff_scalar(const uint8_t* s, size_t n, size_t i, uint8_t* out, size_t o, std::vector<int64_t>& seg_off)
+{
     while (i < n) {
         const uint8_t* ff = (const uint8_t*)memchr(s + i, 0xFF, n - i);
         const size_t run = ff ? (size_t)(ff - (s + i)) : n - i;
         memcpy(out + o, s + i, run);
         o += run;
         i += run;
-        if (i >= n) break;
-        // s[i] == 0xFF
-        if (i + 1 >= n) break;
-        const uint8_t nx = s[i + 1];
-        if (nx == 0x00) {  // stuffed data byte
-            out[o++] = 0xFF;
-            i += 2;
-        } else if (nx == 0xFF) {  // fill byte
-            i += 1;
-        } else if (nx >= 0xD0 && nx <= 0xD7) {  // RSTn: next segment starts byte-aligned
-            seg_off.push_back((int64_t)o);
-            i += 2;
-        } else {
-            break;  // EOI or another marker: end of the scan
-        }
+        if (i + 1 >= n) break;  // end of data (a lone trailing 0xFF is dropped)
+        if (!destuff_marker(s, i, out, o, seg_off)) break;
     }
     seg_off.push_back((int64_t)o);
     return o;
+}
+
+// 32 bytes per step: a 0xFF appears about once per 256 entropy-coded bytes,
+// so the memchr + memcpy pair per run cost ~1.6 ms per 10 MB file; whole
+// 32-byte vectors without 0xFF are copied as they are.  The output never runs
+// ahead of the input (o <= i), so a full 32-byte store at out + o stays inside
+// the caller's n-byte region.
+__attribute__((target("avx2"))) size_t destuff_avx2(const uint8_t* s, size_t n, uint8_t* out,
+                                                    std::vector<int64_t>& seg_off)
+{
+    size_t i = 0, o = 0;
+    const __m256i ff = _mm256_set1_epi8((char)0xFF);
+    while (i + 32 <= n) {
+        const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(s + i));
+        const uint32_t m = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, ff));
+        _mm256_storeu_si256(reinterpret_cast<__m256i*>(out + o), v);
+        if (m == 0) {
+            i += 32;
+            o += 32;
+            continue;
+        }
+        const int k = __builtin_ctz(m);  // bytes before the first 0xFF are already stored
+        i += (size_t)k;
+        o += (size_t)k;
+        if (i + 1 >= n) {
+            seg_off.push_back((int64_t)o);
+            return o;
+        }
+        if (!destuff_marker(s, i, out, o, seg_off)) {
+            seg_off.push_back((int64_t)o);
+            return o;
+        }
+    }
+    return destuff_scalar(s, n, i, out, o, seg_off);
+}
+
+}  // namespace
+
+size_t jpeg_destuff_into(const JpegInfo& info, uint8_t* out, std::vector<int64_t>& seg_off)
+{
+    seg_off.assign(1, 0);
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2) return destuff_avx2(info.scan, info.scan_len, out, seg_off);
+    return destuff_scalar(info.scan, info.scan_len, 0, out, 0, seg_off);
 }
 
 void jpeg_destuff(const JpegInfo& info, std::vector<uint8_t>& out, std::vector<int64_t>& seg_off)
