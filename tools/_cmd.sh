@@ -1,5 +1,4 @@
 set -e
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "multi" 2>&1 | tail -1
-timeout -k 10 100 python -u bench.py --config multi --depths 1,2,3,4,5,6 --steps 10 --no-cpu-baseline > gpurun_out/r02u_bench_multi16.json
-timeout -k 10 100 python -u bench.py --config multi --depths 2,3,4,5,6 --steps 10 --no-cpu-baseline > gpurun_out/r02u_bench_multi26.json
-python3 -c "import json; [print(f, json.load(open('gpurun_out/'+f))['ms_per_step']) for f in ('r02u_bench_multi16.json','r02u_bench_multi26.json')]"
+V=tools/variants
+timeout -k 10 200 python -u tools/ab.py --libs $V/lib_base.so $V/lib_c4.so $V/lib_c6.so $V/lib_c8.so --depths 2 --rounds 7 --out gpurun_out/ab_cap2_8k.json
+timeout -k 10 200 python -u tools/ab.py --libs $V/lib_base.so $V/lib_c4.so $V/lib_c6.so $V/lib_c8.so --depths 2 --rounds 7 --images 256 --height 2160 --width 3840 --out gpurun_out/ab_cap2_4k.json

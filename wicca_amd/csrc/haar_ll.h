@@ -62,6 +62,9 @@
 #ifndef WICCA_STRIP_FLAT
 #define WICCA_STRIP_FLAT 0    // K1s: a workgroup takes 4 consecutive strips of the (image, band, strip) order; -1: table
 #endif
+#ifndef WICCA_STRIP_WG_CAP2
+#define WICCA_STRIP_WG_CAP2 0   // K1s at D=2: workgroups per CU (0: uncapped; 4/6/8 were -15/-6/0 %, r02_ab_cap2_*.json)
+#endif
 #ifndef WICCA_STRIP_WG_CAP3_RAGGED
 #define WICCA_STRIP_WG_CAP3_RAGGED 6  // K1s at D=3 on ragged batches (0: uncapped; r02_ab_rcap_*.json)
 #endif
@@ -108,7 +111,8 @@ constexpr int lds_for_cap(int cap) { return cap > 0 ? kLdsPerCU / (cap + 1) + 16
 constexpr int strip_min_lds(int L, bool ragged)
 {
     // ragged batches at D = 3: 6 per CU (+2-2.5 % over uncapped, 4 is mixed)
-    return L == 3 ? lds_for_cap(ragged ? WICCA_STRIP_WG_CAP3_RAGGED : WICCA_STRIP_WG_CAP3)
+    return L == 2 ? lds_for_cap(WICCA_STRIP_WG_CAP2)
+         : L == 3 ? lds_for_cap(ragged ? WICCA_STRIP_WG_CAP3_RAGGED : WICCA_STRIP_WG_CAP3)
                   : L >= 4 ? lds_for_cap(WICCA_STRIP_WG_CAP_HI) : 0;
 }
 constexpr int k1_min_lds(int L) { return L == 1 ? lds_for_cap(WICCA_K1_WG_CAP1) : 0; }
