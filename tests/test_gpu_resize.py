@@ -103,3 +103,24 @@ def test_icon_stage_constant_border(coder):
     for i, im in enumerate(imgs):
         icon = c_oracle.ll_int_block(im, 3, 0, 77)[0]
         assert np.array_equal(got_icon[i], R.resize(icon, (224, 224), 3)), i
+
+
+def test_resize_uniform_device_batch_area_two_pass():
+    """INTER_AREA downscales of a device batch take the two-pass path (row sums
+    in workspace scratch, several images per launch); rows wider than the LDS
+    stage (W * C > 24 KiB) take the one-pass kernel."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(12)
+    for (n, H, W, dw, dh) in ((5, 540, 960, 224, 224), (2, 41, 8500, 100, 20)):
+        C = 3
+        host = rng.integers(0, 256, (n, H, W, C), dtype=np.uint8)
+        pitch = (W * C + 15) // 16 * 16
+        src = torch.zeros((n, H, pitch), dtype=torch.uint8, device="cuda")
+        src[:, :, :W * C] = torch.from_numpy(host.reshape(n, H, W * C)).cuda()
+        dst = torch.empty((n, dh, dw, C), dtype=torch.uint8, device="cuda")
+        _lib.check(_lib.load().wicca_resize_u8_uniform(
+            ctypes.c_void_p(src.data_ptr()), n, H, W, C, pitch, H * pitch,
+            ctypes.c_void_p(dst.data_ptr()), dw, dh, dw * C, dh * dw * C, R.INTER_AREA, -1, None))
+        got = dst.cpu().numpy()
+        for i in range(n):
+            assert np.array_equal(got[i], R.resize(host[i], (dw, dh), R.INTER_AREA)), (H, W, i)

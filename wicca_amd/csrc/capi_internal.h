@@ -110,13 +110,14 @@ struct Workspace {
     DevBuf slot[2], icon[2];
     // JPEG decode (wicca_jpeg_*): stream + tables, coefficients, planes, scratch, RGB images
     DevBuf jstream, jmeta, jcoef, jplanes, jscratch, jrgb, jtmp;
+    DevBuf rscratch;  // two-pass INTER_AREA row sums (float)
     HostBuf jhost;  // pinned host staging of the de-stuffed JPEG streams
     HostBuf jtab;   // pinned host staging of the decode tables
     size_t bytes() const
     {
         return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
                slot[0].cap + slot[1].cap + icon[0].cap + icon[1].cap + jstream.cap + jmeta.cap + jcoef.cap +
-               jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap;
+               jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap + rscratch.cap;
     }
     hipError_t ensure_pipeline()
     {
@@ -148,6 +149,7 @@ struct Workspace {
             icon[i].release();
         }
         jstream.release();
+        rscratch.release();
         jmeta.release();
         jcoef.release();
         jplanes.release();
@@ -234,6 +236,7 @@ int split_over_devices(const std::vector<int64_t>& weights, const int* devices, 
 int check_resize(int64_t H, int64_t W, int64_t C, int64_t out_w, int64_t out_h, int interpolation,
                  wicca::ResizeParams* rp);
 int run_resize(wicca::ResizeParams rp, const uint8_t* src, int64_t src_pitch, int64_t src_stride,
-               uint8_t* dst, int64_t dst_pitch, int64_t dst_stride, int64_t n, hipStream_t stream);
+               uint8_t* dst, int64_t dst_pitch, int64_t dst_stride, int64_t n, hipStream_t stream,
+               Workspace* ws);
 
 }  // namespace wicca_capi

@@ -434,7 +434,7 @@ int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, i
         // classifying_tools.py:315, :317, :318
         wicca::ResizeParams rp{};
         wicca::plan_resize((int)H[i], (int)W[i], (int)out_h, (int)out_w, 3, interpolation, &rp);
-        if ((rc = run_resize(rp, d[(size_t)i], p[(size_t)i], 0, dres + i * out_bytes, out_w * 3, 0, 1, cs)))
+        if ((rc = run_resize(rp, d[(size_t)i], p[(size_t)i], 0, dres + i * out_bytes, out_w * 3, 0, 1, cs, ws)))
             return rc;
         const int64_t ip = round_up(iw[i] * 3, 16);
         bool scratch = false;
@@ -443,7 +443,7 @@ int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, i
             return rc;
         wicca::ResizeParams ri{};
         wicca::plan_resize((int)ih[i], (int)iw[i], (int)out_h, (int)out_w, 3, interpolation, &ri);
-        if ((rc = run_resize(ri, ico, ip, 0, dico + i * out_bytes, out_w * 3, 0, 1, cs))) return rc;
+        if ((rc = run_resize(ri, ico, ip, 0, dico + i * out_bytes, out_w * 3, 0, 1, cs, ws))) return rc;
     }
     HIP_TRY(hipMemcpyAsync(resized, dres, (size_t)(n * out_bytes), hipMemcpyDeviceToHost, cs));
     HIP_TRY(hipMemcpyAsync(resized_icons, dico, (size_t)(n * out_bytes), hipMemcpyDeviceToHost, cs));

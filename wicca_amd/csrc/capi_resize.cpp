@@ -39,7 +39,8 @@ int check_resize(int64_t H, int64_t W, int64_t C, int64_t out_w, int64_t out_h, 
 
 // Device-resident resize of n images (uniform shape) on `stream`.
 int run_resize(wicca::ResizeParams rp, const uint8_t* src, int64_t src_pitch, int64_t src_stride,
-               uint8_t* dst, int64_t dst_pitch, int64_t dst_stride, int64_t n, hipStream_t stream)
+               uint8_t* dst, int64_t dst_pitch, int64_t dst_stride, int64_t n, hipStream_t stream,
+               Workspace* ws)
 {
     if (rp.mode == wicca::RS_COPY) {
         for (int64_t i = 0; i < n; ++i)
@@ -53,11 +54,30 @@ int run_resize(wicca::ResizeParams rp, const uint8_t* src, int64_t src_pitch, in
     rp.dst = dst;
     rp.dst_pitch = dst_pitch;
     rp.dst_stride = dst_stride;
-    for (int64_t i0 = 0; i0 < n; i0 += 65535) {  // grid.z limit
+    // the two-pass INTER_AREA path: at most ~256 MiB of row sums per launch
+    // (an 8K RGB source to 224 x 224: 11.6 MB per image); without scratch the
+    // one-pass kernel runs
+    const size_t per_image = wicca::resize_scratch_bytes(rp, 1);
+    int64_t step = 65535;  // grid.z limit
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+    constexpr size_t kScratchCap = (size_t)256 << 20;
+    if (per_image > 0 && per_image <= kScratchCap && ws) {
+        step = std::min<int64_t>(step, (int64_t)(kScratchCap / per_image));
+        const size_t want = per_image * (size_t)std::min<int64_t>(step, n);
+        if (ws->rscratch.reserve(want) == hipSuccess) {
+            scratch = ws->rscratch.ptr;
+            scratch_bytes = ws->rscratch.cap;
+        } else {
+            (void)hipGetLastError();
+            step = 65535;
+        }
+    }
+    for (int64_t i0 = 0; i0 < n; i0 += step) {
         wicca::ResizeParams q = rp;
         q.src = src + i0 * src_stride;
         q.dst = dst + i0 * dst_stride;
-        HIP_TRY(wicca::launch_resize(q, std::min<int64_t>(65535, n - i0), stream));
+        HIP_TRY(wicca::launch_resize(q, std::min<int64_t>(step, n - i0), stream, scratch, scratch_bytes));
     }
     return WICCA_OK;
 }
@@ -98,7 +118,7 @@ int wicca_resize_u8(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t
         HIP_TRY(ws->out.reserve((size_t)(dp * out_h)));
         ddst = (uint8_t*)ws->out.ptr;
     }
-    if ((rc = run_resize(rp, dsrc, sp, 0, ddst, dp, 0, 1, stream))) return rc;
+    if ((rc = run_resize(rp, dsrc, sp, 0, ddst, dp, 0, 1, stream, ws))) return rc;
     if (!dst_is_device)
         HIP_TRY(hipMemcpy2DAsync(dst, dst_pitch, ddst, dp, out_w * C, out_h, hipMemcpyDeviceToHost,
                                  stream));
@@ -127,8 +147,10 @@ int wicca_resize_u8_uniform(const uint8_t* src, int64_t n, int64_t H, int64_t W,
     WorkspaceLease lease;
     if ((rc = acquire(dev, lease))) return rc;
     hipStream_t stream = stream_in ? (hipStream_t)stream_in : lease.ws->stream;
+    // on a caller's stream the call returns before the kernels finish: no
+    // workspace scratch then (one-pass INTER_AREA kernel)
     if ((rc = run_resize(rp, src, src_pitch, src_image_stride, dst, dst_pitch, dst_image_stride, n,
-                         stream)))
+                         stream, stream_in ? nullptr : lease.ws)))
         return rc;
     if (!stream_in) HIP_TRY(hipStreamSynchronize(stream));
     return WICCA_OK;
@@ -189,7 +211,7 @@ int wicca_icon_stage_u8(const wicca_image_desc* images, int64_t n, int64_t C, in
         // classifying_tools.py:315  resized = cv2.resize(image, shape, interpolation)
         wicca::ResizeParams rp{};
         wicca::plan_resize((int)H, (int)W, (int)out_h, (int)out_w, (int)C, interpolation, &rp);
-        if ((rc = run_resize(rp, img, pitch, 0, dres + i * out_bytes, out_w * C, 0, 1, cs))) return rc;
+        if ((rc = run_resize(rp, img, pitch, 0, dres + i * out_bytes, out_w * C, 0, 1, cs, ws))) return rc;
         // :317  icon = coder.get_small_copy(image, depth)
         const int64_t ip = round_up(iw[i] * C, 16);
         uint8_t* ico = (uint8_t*)ws->icon[k].ptr;
@@ -200,7 +222,7 @@ int wicca_icon_stage_u8(const wicca_image_desc* images, int64_t n, int64_t C, in
         // :318  resized_icon = cv2.resize(icon, shape, interpolation)
         wicca::ResizeParams ri{};
         wicca::plan_resize((int)ih[i], (int)iw[i], (int)out_h, (int)out_w, (int)C, interpolation, &ri);
-        if ((rc = run_resize(ri, ico, ip, 0, dico + i * out_bytes, out_w * C, 0, 1, cs))) return rc;
+        if ((rc = run_resize(ri, ico, ip, 0, dico + i * out_bytes, out_w * C, 0, 1, cs, ws))) return rc;
         HIP_TRY(hipEventRecord(ws->slot_free[k], cs));
     }
     // :323  np.stack(...) of both lists: dense (n, out_h, out_w, C) each

@@ -79,6 +79,10 @@ inline bool plan_resize(int H, int W, int dh, int dw, int C, int interpolation, 
 }
 
 // n images of (H, W, C) at src + i * src_stride -> (dh, dw, C) at dst + i * dst_stride.
-hipError_t launch_resize(const ResizeParams& p, int64_t n_images, hipStream_t s);
+// Scratch the two-pass INTER_AREA path needs (0: the path does not apply);
+// without it (scratch == nullptr or too small) the one-pass kernel runs.
+size_t resize_scratch_bytes(const ResizeParams& p, int64_t n_images);
+hipError_t launch_resize(const ResizeParams& p, int64_t n_images, hipStream_t s, void* scratch = nullptr,
+                         size_t scratch_bytes = 0);
 
 }  // namespace wicca

@@ -30,6 +30,8 @@
 
 #include "resize.h"
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
 namespace wicca {
 
 namespace {
@@ -172,13 +174,91 @@ __global__ __launch_bounds__(kRsThreads) void resize_u8_kernel(ResizeParams p)
     out[e] = v;
 }
 
+// RS_AREA in two passes with a float scratch plane (H rows x dw*C per image):
+//   1. one workgroup per source row: the row passes through LDS once (16-B
+//      loads by the whole workgroup) and every output element's horizontal
+//      sum of that row (computeResizeAreaTab weights, column order) goes to
+//      scratch[sy][e];
+//   2. one lane per output element: sum = beta * buf over the rows of its
+//      window, in row order.
+// Each element's arithmetic is the per-lane kernel's, in the same order, so
+// the result is the same bit for bit; the per-lane kernel reads every source
+// row as strided bytes, 3 lanes per pixel (62 us for an 8K RGB image to
+// 224 x 224).  A workgroup per output row staging its rows through LDS ran
+// 157 us (224 workgroups, one row in flight each).
+constexpr int kAreaRowMax = 24 * 1024;  // source row bytes staged in LDS
+
+__global__ __launch_bounds__(kRsThreads) void area_hsum_kernel(ResizeParams p, float* scratch)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t row[kAreaRowMax];
+    const int sy = blockIdx.x, C = p.C;
+    const int n_el = p.dw * C;
+    const int row16 = (p.W * C + 15) >> 4;
+    const u32x4* src = reinterpret_cast<const u32x4*>(p.src + (int64_t)blockIdx.y * p.src_stride +
+                                                      (int64_t)sy * p.src_pitch);
+    for (int i = threadIdx.x; i < row16; i += kRsThreads)
+        reinterpret_cast<u32x4*>(row)[i] = __builtin_nontemporal_load(src + i);
+    __syncthreads();
+    float* out = scratch + ((int64_t)blockIdx.y * p.H + sy) * n_el;
+    for (int e = threadIdx.x; e < n_el; e += kRsThreads) {
+        const int dx = e / C, c = e - dx * C;
+        const AreaTab t = area_tab(dx, p.W, p.scale_x);
+        const uint8_t* r = row + c;
+        float buf = 0.f;
+        if (t.has_a) buf = buf + (float)r[(t.s1 - 1) * C] * t.wa;
+        for (int sx = t.s1; sx < t.s2; ++sx) buf = buf + (float)r[sx * C] * t.wm;
+        if (t.has_b) buf = buf + (float)r[t.s2 * C] * t.wb;
+        out[e] = buf;
+    }
+}
+
+__global__ __launch_bounds__(kRsThreads) void area_vsum_kernel(ResizeParams p, const float* scratch)
+{
+    const int e = blockIdx.x * kRsThreads + threadIdx.x;
+    const int n_el = p.dw * p.C;
+    if (e >= n_el) return;
+    const int dy = blockIdx.y;
+    const AreaTab ty = area_tab(dy, p.H, p.scale_y);
+    const float* col = scratch + (int64_t)blockIdx.z * p.H * n_el + e;
+    float sum = 0.f;
+    bool first = true;
+    auto term = [&](int sy, float beta) {
+        const float v = beta * col[(int64_t)sy * n_el];
+        sum = first ? v : sum + v;
+        first = false;
+    };
+    if (ty.has_a) term(ty.s1 - 1, ty.wa);
+    for (int sy = ty.s1; sy < ty.s2; ++sy) term(sy, ty.wm);
+    if (ty.has_b) term(ty.s2, ty.wb);
+    p.dst[(int64_t)blockIdx.z * p.dst_stride + (int64_t)dy * p.dst_pitch + e] = sat_u8(round_f32(sum));
+}
+
 }  // namespace
 
-hipError_t launch_resize(const ResizeParams& p, int64_t n_images, hipStream_t s)
+size_t resize_scratch_bytes(const ResizeParams& p, int64_t n_images)
+{
+    const bool two_pass = p.mode == RS_AREA && (int64_t)p.W * p.C <= kAreaRowMax;
+    return two_pass ? (size_t)n_images * (size_t)p.H * (size_t)p.dw * (size_t)p.C * sizeof(float) : 0;
+}
+
+hipError_t launch_resize(const ResizeParams& p, int64_t n_images, hipStream_t s, void* scratch,
+                         size_t scratch_bytes)
 {
     if (n_images <= 0 || p.dw <= 0 || p.dh <= 0) return hipSuccess;
     const int64_t row = (int64_t)p.dw * p.C;
     if (n_images > 65535 || p.dh > 65535) return hipErrorInvalidValue;
+    const size_t need = resize_scratch_bytes(p, n_images);
+    if (need > 0 && scratch != nullptr && scratch_bytes >= need && p.H <= 65535 && (uintptr_t)p.src % 16 == 0 &&
+        p.src_pitch % 16 == 0 && p.src_stride % 16 == 0) {
+        float* sc = static_cast<float*>(scratch);
+        hipLaunchKernelGGL(area_hsum_kernel, dim3((uint32_t)p.H, (uint32_t)n_images), dim3(kRsThreads), 0, s, p, sc);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(area_vsum_kernel, dim3((uint32_t)((row + kRsThreads - 1) / kRsThreads), (uint32_t)p.dh,
+                                                  (uint32_t)n_images),
+                           dim3(kRsThreads), 0, s, p, (const float*)sc);
+        return hipGetLastError();
+    }
     dim3 grid((uint32_t)((row + kRsThreads - 1) / kRsThreads), (uint32_t)p.dh, (uint32_t)n_images);
     hipLaunchKernelGGL(resize_u8_kernel, grid, dim3(kRsThreads), 0, s, p);
     return hipGetLastError();
