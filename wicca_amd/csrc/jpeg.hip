@@ -870,10 +870,13 @@ __device__ __forceinline__ void color_row(const JpegPlan& P, const JpegImageDev&
     }
 }
 
-__global__ __launch_bounds__(256) void jpeg_color_kernel(JpegPlan P, int img)
+// One launch for the batch: grid.z = image, the grid sized for the largest
+// image (workgroups past an image's width or height return at once).
+__global__ __launch_bounds__(256) void jpeg_color_kernel(JpegPlan P)
 {
     __shared__ __attribute__((aligned(16))) uint32_t stage[256 * 3];
-    const JpegImageDev& im = P.imgs[img];
+    const JpegImageDev& im = P.imgs[blockIdx.z];
+    if ((int)blockIdx.x * 1024 >= im.W || (int)blockIdx.y * kColorRows >= im.H) return;  // uniform
     if constexpr (kColorRows == 1) {
         color_row(P, im, blockIdx.x * 1024, blockIdx.y, stage);
     } else {
@@ -1003,11 +1006,26 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     hipLaunchKernelGGL(jpeg_idct_kernel, dim3((uint32_t)((max_blocks + per_wg - 1) / per_wg), (uint32_t)hj.size()),
                        dim3(256), 0, s, P, jobs);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    // one launch over the batch unless the images differ so much in size that
+    // the padded grid would be mostly empty workgroups
+    int max_w = 0, max_h = 0;
+    int64_t real_wg = 0;
     for (int64_t i = 0; i < n_images; ++i) {
-        const JpegImageDev& im = ims[(size_t)i];
-        hipLaunchKernelGGL(jpeg_color_kernel, dim3((uint32_t)((im.W + 1023) / 1024),
-                                                   (uint32_t)((im.H + kColorRows - 1) / kColorRows)),
-                           dim3(256), 0, s, P, (int)i);
+        max_w = std::max(max_w, ims[(size_t)i].W);
+        max_h = std::max(max_h, ims[(size_t)i].H);
+        real_wg += (int64_t)((ims[(size_t)i].W + 1023) / 1024) * ((ims[(size_t)i].H + kColorRows - 1) / kColorRows);
+    }
+    const int64_t gx = (max_w + 1023) / 1024, gy = (max_h + kColorRows - 1) / kColorRows;
+    const bool batched = gx * gy * n_images <= 2 * real_wg + 65536;
+    const int64_t per_launch = batched ? 65535 : 1;  // grid.z limit
+    for (int64_t i0 = 0; i0 < n_images; i0 += per_launch) {
+        JpegPlan Q = P;
+        Q.imgs = P.imgs + i0;
+        const JpegImageDev& im = ims[(size_t)i0];
+        const uint32_t x = (uint32_t)(batched ? gx : (im.W + 1023) / 1024);
+        const uint32_t y = (uint32_t)(batched ? gy : (im.H + kColorRows - 1) / kColorRows);
+        hipLaunchKernelGGL(jpeg_color_kernel, dim3(x, y, (uint32_t)std::min<int64_t>(per_launch, n_images - i0)),
+                           dim3(256), 0, s, Q);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
