@@ -758,7 +758,7 @@ __device__ __forceinline__ uint32_t load4_unaligned(const uint8_t* row, int c0)
 // 3,072 RGB bytes are staged in LDS and leave as 16-B stores when the output
 // row is 16-B aligned (12-B lane stores at a 12-B stride before: 99 us per 8K
 // image).
-constexpr int kColorRows = 1;  // output rows per workgroup (4, or a row loop even at 1: 118 vs 87 us per 8K image)
+constexpr int kColorRows = 1;  // output rows per workgroup (batched launch: 2 -> 2.39, 4 -> 2.57 vs 2.07 ms per 25 x 8K)
 
 __device__ __forceinline__ void color_row(const JpegPlan& P, const JpegImageDev& im, int xb, int y,
                                           uint32_t* stage)
@@ -881,8 +881,9 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(JpegPlan P)
         color_row(P, im, blockIdx.x * 1024, blockIdx.y, stage);
     } else {
         const int y0 = blockIdx.y * kColorRows;
-        const int y1 = min(y0 + kColorRows, im.H);
-        for (int y = y0; y < y1; ++y) color_row(P, im, blockIdx.x * 1024, y, stage);  // uniform bounds
+#pragma unroll
+        for (int r = 0; r < kColorRows; ++r)
+            if (y0 + r < im.H) color_row(P, im, blockIdx.x * 1024, y0 + r, stage);  // uniform
     }
 }
 
