@@ -1,6 +1,7 @@
 set -e
+timeout -k 10 400 python -u -m pytest tests/test_gpu_jpeg.py -x -q --timeout 300 --timeout-method thread 2>&1 | tail -1
+timeout -k 10 300 python -u bench.py --config jpeg --steps 10 --no-cpu-baseline > gpurun_out/jpeg_bench.json
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-for v in r1 r2 r4; do
-WICCA_HIP_LIB=tools/variants/lib_$v.so timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c_$v -- python3 -u bench.py --config jpeg --steps 5 --no-cpu-baseline > gpurun_out/jpeg_c_$v.json
-f=$(find gpurun_out/prof_c_$v -name "*kernel_stats.csv" | head -1); grep color $f | cut -d, -f1-5 | sed "s/^/$v /"
-done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_jpeg -- python3 -u bench.py --config jpeg --steps 5 --no-cpu-baseline > gpurun_out/jpeg_prof.json
+find gpurun_out/prof_jpeg -name "*kernel_stats.csv" | head -1 | xargs -I{} cp {} gpurun_out/jpeg_kernel_stats.csv
+find gpurun_out/prof_jpeg -name "*kernel_trace.csv" | head -1 | xargs -I{} cp {} gpurun_out/jpeg_kernel_trace.csv

@@ -411,35 +411,45 @@ __global__ __launch_bounds__(kJThreads) void jpeg_sync_kernel(JpegPlan P, const 
 {
     const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
     __shared__ ImgTabs<2 * kJpegMaxComp> tabs;
-    stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);
-    const DecGeom& im = tabs.g;
-    if (i >= P.n_sub || P.sub_seg[i] < 0) return;  // padding lane
-    const JpegSegDev sg = P.segs[P.sub_seg[i]];
-    const int64_t j = i - sg.sub0;  // index inside the segment
-    const int64_t b0 = sg.bit0 + j * P.sub_bits;
-    const int64_t b1 = min(sg.bit0 + (j + 1) * P.sub_bits, sg.bit0 + sg.bits);
-    DecState st;
-    if (j == 0 || round == 0) {  // exact at a segment start, a guess elsewhere in round 0
-        st.p = b0;
-        st.slot = 0;
-        st.k = 0;
-    } else {
-        st = prev[i - 1].end;
-    }
-    if (round > 0) {
-        DecState before;  // this lane's start state in the previous round
-        if (j == 0 || round == 1) {
-            before.p = b0;
-            before.slot = 0;
-            before.k = 0;
+    // this lane's start state, and whether it has to decode at all (every
+    // lane of a workgroup that repeats its result skips the table staging too)
+    const bool lane_live = i < P.n_sub && P.sub_seg[i] >= 0;  // else a padding lane
+    JpegSegDev sg{};
+    int64_t j = 0, b0 = 0, b1 = 0;
+    DecState st{};
+    bool decode = false;
+    if (lane_live) {
+        sg = P.segs[P.sub_seg[i]];
+        j = i - sg.sub0;  // index inside the segment
+        b0 = sg.bit0 + j * P.sub_bits;
+        b1 = min(sg.bit0 + (j + 1) * P.sub_bits, sg.bit0 + sg.bits);
+        if (j == 0 || round == 0) {  // exact at a segment start, a guess elsewhere in round 0
+            st.p = b0;
+            st.slot = 0;
+            st.k = 0;
         } else {
-            before = older[i - 1].end;
+            st = prev[i - 1].end;
         }
-        if (same_state(st, before)) {  // same input, same result
-            next[i] = prev[i];
-            return;
+        decode = true;
+        if (round > 0) {
+            DecState before;  // this lane's start state in the previous round
+            if (j == 0 || round == 1) {
+                before.p = b0;
+                before.slot = 0;
+                before.k = 0;
+            } else {
+                before = older[i - 1].end;
+            }
+            if (same_state(st, before)) {  // same input, same result
+                next[i] = prev[i];
+                decode = false;
+            }
         }
     }
+    if (!__syncthreads_or(decode)) return;  // uniform: nothing to decode in this workgroup
+    stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);
+    if (!decode) return;
+    const DecGeom& im = tabs.g;
     SubResult r;
     r.started = 0;
     r.pad_ = 0;
