@@ -374,7 +374,8 @@ def test_batch_multi_gpu_entry(coder):
 def test_batch_ragged_device_descriptors(coder):
     """wicca_haar_ll_u8_batch with device-resident images and icons (the
     bench's --config ragged path): one launch over random sizes, the strip
-    kernel (D = 2, 3) and the segment kernel (D = 1, 4-6), both borders."""
+    kernel (D = 2, 3) and the segment kernel (D = 1 with two-band units, 4-6), both
+    borders."""
     import ctypes
     from wicca_amd import _lib
     torch = pytest.importorskip("torch")
@@ -389,7 +390,8 @@ def test_batch_ragged_device_descriptors(coder):
             host = np.zeros((im.shape[0], p), np.uint8)
             host[:, :im.shape[1] * C] = im.reshape(im.shape[0], -1)
             srcs.append(torch.from_numpy(host).cuda())
-        for d, border, k in ((1, 1, 0), (2, 0, 9), (3, 1, 0), (4, 0, 250), (5, 1, 0), (6, 0, 3)):
+        for d, border, k in ((1, 1, 0), (1, 0, 200), (2, 0, 9), (3, 1, 0), (4, 0, 250), (5, 1, 0),
+                             (6, 0, 3)):
             r = 1 << d
             descs = (_lib.ImageDesc * len(imgs))()
             outs = []

@@ -751,8 +751,9 @@ int wicca_haar_ll_u8_batch(const wicca_image_desc* descs_in, int64_t n, int64_t 
             e.n_seg = (int32_t)wicca::segments_for(e.out_w, depth, (int)C, true);
             e.pad_ = 0;
             starts[(size_t)i] = total;
-            total += e.out_h * e.n_seg;
-            min_units = std::min<int64_t>(min_units, e.out_h * e.n_seg);
+            const int64_t units = wicca::unit_rows(e.out_h, depth, true) * e.n_seg;
+            total += units;
+            min_units = std::min<int64_t>(min_units, units);
         }
         if (total >= ((int64_t)1 << 32))
             return fail(WICCA_ERR_ARG, "batch too large for one launch");

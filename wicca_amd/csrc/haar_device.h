@@ -56,8 +56,8 @@ struct BlockWork {
     int32_t oy, seg, n_seg;
 };
 
-// Work unit b (a segment of an icon row, or one wave strip with
-// WICCA_STRIP_FLAT) -> image, icon row, segment.  Ragged: b counts from the
+// Work unit b (a segment of an icon row — of k1_bands consecutive icon rows
+// for K1 — or one wave strip with WICCA_STRIP_FLAT) -> image, unit row, segment.  Ragged: b counts from the
 // batch's first unit; wave-uniform.
 template <int L, bool RAGGED>
 __device__ __forceinline__ BlockWork resolve_unit(const LLParams& p, uint32_t b)
@@ -121,8 +121,9 @@ __device__ __forceinline__ BlockWork resolve_unit(const LLParams& p, uint32_t b)
     } else {
         uint32_t seg = b % (uint32_t)p.n_seg;
         uint32_t t = b / (uint32_t)p.n_seg;
-        uint32_t oy = t % (uint32_t)p.out_h;
-        uint32_t img = t / (uint32_t)p.out_h;
+        const uint32_t rows = (uint32_t)unit_rows(p.out_h, L, false);
+        uint32_t oy = t % rows;
+        uint32_t img = t / rows;
         w.src = p.src + (int64_t)img * p.src_image_stride;
         w.dst = p.dst + (int64_t)img * p.dst_image_stride;
         w.H = p.H; w.W = p.W; w.src_pitch = p.src_pitch; w.dst_pitch = p.dst_pitch;

@@ -74,6 +74,17 @@
 #ifndef WICCA_K1_WG_CAP1
 #define WICCA_K1_WG_CAP1 0      // K1 at D=1: at most this many workgroups per CU (0 = no cap)
 #endif
+#ifndef WICCA_K1_BANDS1
+#define WICCA_K1_BANDS1 1       // K1 at D=1, uniform batches: icon rows (bands) per work unit; the next
+                                // band's loads are issued before the current band's LDS epilogue
+                                // (2 / 4: -3 / -8 %, profiles/r02_ab_k1_bands.json)
+#endif
+#ifndef WICCA_K1_BANDS1R
+#define WICCA_K1_BANDS1R 2      // the same for ragged batches (2 / 4: +4.4 / +4.0 %)
+#endif
+#ifndef WICCA_K1_BANDS4
+#define WICCA_K1_BANDS4 1       // the same at D=4 (2 / 4: -12 / -7 %: 192 VGPRs of loads stay live)
+#endif
 #ifndef WICCA_XCD_REMAP
 #define WICCA_XCD_REMAP 128   // logical blocks per XCD turn: 0 = hardware order (round-robin over
                               // the 8 XCDs), K > 0 = runs of K, -1 = one contiguous run per XCD
@@ -116,6 +127,20 @@ constexpr int strip_min_lds(int L, bool ragged)
                   : L >= 4 ? lds_for_cap(WICCA_STRIP_WG_CAP_HI) : 0;
 }
 constexpr int k1_min_lds(int L) { return L == 1 ? lds_for_cap(WICCA_K1_WG_CAP1) : 0; }
+
+// Icon rows (bands) one K1 work unit covers, top to bottom.
+constexpr int k1_bands(int L, bool ragged)
+{
+    return use_strip_kernel(L) ? 1
+         : L == 1              ? (ragged ? WICCA_K1_BANDS1R : WICCA_K1_BANDS1)
+         : L == 4              ? WICCA_K1_BANDS4
+                               : 1;
+}
+// Work-unit rows of an image with out_h icon rows (groups of k1_bands bands).
+constexpr int64_t unit_rows(int64_t out_h, int L, bool ragged)
+{
+    return (out_h + k1_bands(L, ragged) - 1) / k1_bands(L, ragged);
+}
 
 // Work units of the strip kernel: groups of kStripWaves strips of one band
 // (idle waves where a band's strips do not fill the last group), or single

@@ -239,9 +239,9 @@ void haar_block_sum_kernel(LLParams p)
     const int tid = threadIdx.x;
     const int64_t row_bytes = w.W * C;
     const int64_t px0 = (int64_t)w.seg * kSegPx;          // first pixel of segment
-    const int oy = w.oy;                                  // icon row (band) of the block
-    const int64_t y0 = (int64_t)oy << L;                  // its first input row
-    const int rows_real = (int)min<int64_t>(max<int64_t>(w.H - y0, 0), R);
+    constexpr int NB = k1_bands(L, RAGGED);                       // icon rows (bands) of this unit
+    const int oy0 = w.oy * NB;                            // its first icon row
+    const int nb = (int)min<int64_t>(NB, w.out_h - oy0);  // workgroup-uniform
     const bool replicate = p.border == 1;
     const int64_t last_row = w.H - 1;
     const uint8_t* img = w.src;
@@ -256,7 +256,8 @@ void haar_block_sum_kernel(LLParams p)
     }
     const uint32_t nrec = (uint32_t)((row_bytes + 15) & ~(int64_t)15);  // inside the pitch
 
-    auto issue = [&](u32x4 (&v)[U][C], int g) {
+    // loads of chunk g of the band starting at input row y0
+    auto issue = [&](u32x4 (&v)[U][C], int64_t y0, int g) {
         const int64_t ybase = y0 + g * U;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -274,14 +275,9 @@ void haar_block_sum_kernel(LLParams p)
             for (int j = 0; j < 4; ++j) { lo[k][j] = 0; hi[k][j] = 0; }
     };
 
-    auto epilogue = [&]() {
-        band_epilogue<L, C, OutT>(p, w, tid, px0, oy, y0, rows_real, valid, lo, hi, colsum, stage,
-                                  lastcol);
-    };
-
     // Reduce chunk g (its loads were issued earlier); CONSTANT rows below the
     // image are masked out (their value enters as k * pad cells).
-    auto consume = [&](u32x4 (&v)[U][C], int g) {
+    auto consume = [&](u32x4 (&v)[U][C], int g, int rows_real) {
         const int c0 = g * U;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -296,20 +292,50 @@ void haar_block_sum_kernel(LLParams p)
         }
     };
 
-    zero_acc();
-    for (int g = 0; g < CPB; ++g) {
-        u32x4 v[U][C];
-        issue(v, g);
-        consume(v, g);
-    }
 #ifdef WICCA_ABLATE_EPILOGUE  // timing-only build: stream + reduce, no LDS/store phase
+    auto epilogue = [&](int, int64_t, int) {
 #pragma unroll
-    for (int k = 0; k < C; ++k)
+        for (int k = 0; k < C; ++k)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(lo[k][j]), "v"(hi[k][j]));
-    return;
+            for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(lo[k][j]), "v"(hi[k][j]));
+    };
+#else
+    auto epilogue = [&](int oy, int64_t y0, int rows_real) {
+        band_epilogue<L, C, OutT>(p, w, tid, px0, oy, y0, rows_real, valid, lo, hi, colsum, stage,
+                                  lastcol);
+    };
 #endif
-    epilogue();
+    auto band_rows = [&](int64_t y0) { return (int)min<int64_t>(max<int64_t>(w.H - y0, 0), R); };
+
+    if constexpr (NB == 1) {
+        const int64_t y0 = (int64_t)oy0 << L;
+        const int rows_real = band_rows(y0);
+        zero_acc();
+        for (int g = 0; g < CPB; ++g) {
+            u32x4 v[U][C];
+            issue(v, y0, g);
+            consume(v, g, rows_real);
+        }
+        epilogue(oy0, y0, rows_real);
+    } else {
+        // several bands: the next band's loads stream in while this band's
+        // LDS epilogue runs (the chunk stays live across it: one-chunk bands only)
+        static_assert(CPB == 1, "multi-band units prefetch whole bands");
+        u32x4 v[U][C];
+        issue(v, (int64_t)oy0 << L, 0);
+        for (int bi = 0; bi < nb; ++bi) {
+            const int oy = oy0 + bi;
+            const int64_t y0 = (int64_t)oy << L;
+            const int rows_real = band_rows(y0);
+            zero_acc();
+            consume(v, 0, rows_real);
+            if (bi + 1 < nb) issue(v, y0 + R, 0);
+            // a staging area shared with the column sums is read by the
+            // previous band's stores: every lane must be past them
+            if (kReuse && bi > 0) __syncthreads();
+            epilogue(oy, y0, rows_real);
+        }
+    }
 }
 
 // ----------------------------------------------------------------------------
@@ -895,7 +921,7 @@ hipError_t launch_block_sum(LLParams p, int L, int C, hipStream_t stream)
     constexpr int64_t kMax = max_grid_blocks(kThreads);  // strip and segment kernels: 256 lanes
     if (p.descs == nullptr && out_al && fast_path_ok(p, L, C)) {
         p.n_seg = (int32_t)segments_for(p.out_w, L, C, false);
-        const int64_t per_image = p.out_h * p.n_seg;  // work units
+        const int64_t per_image = unit_rows(p.out_h, L, false) * p.n_seg;  // work units
         const int64_t upb = units_per_block(L, false);
         if (per_image <= 0 || p.n_images <= 0) return hipSuccess;
         if (per_image > kMax * upb) return hipErrorInvalidValue;  // one image past the grid limit
