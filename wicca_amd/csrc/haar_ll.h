@@ -85,6 +85,17 @@
 #ifndef WICCA_K1_BANDS4
 #define WICCA_K1_BANDS4 1       // the same at D=4 (2 / 4: -12 / -7 %: 192 VGPRs of loads stay live)
 #endif
+#ifndef WICCA_K1_WAVESEG1
+#define WICCA_K1_WAVESEG1 0     // K1 at D=1, uniform batches: 1 = one 1,024-px segment per wave (four
+                                // per workgroup) instead of one 4,096-px segment per workgroup
+#endif
+#ifndef WICCA_K1_WAVESEG1R
+#define WICCA_K1_WAVESEG1R 0    // the same for ragged batches (-2.5 % on ragged D=1, neutral on uniform:
+                                // idle lanes are not what holds ragged D=1 back; profiles/r02_ab_k1_waveseg.json)
+#endif
+#ifndef WICCA_K1_WAVESEG4
+#define WICCA_K1_WAVESEG4 0     // the same at D=4
+#endif
 #ifndef WICCA_XCD_REMAP
 #define WICCA_XCD_REMAP 128   // logical blocks per XCD turn: 0 = hardware order (round-robin over
                               // the 8 XCDs), K > 0 = runs of K, -1 = one contiguous run per XCD
@@ -135,6 +146,13 @@ constexpr int k1_bands(int L, bool ragged)
          : L == 1              ? (ragged ? WICCA_K1_BANDS1R : WICCA_K1_BANDS1)
          : L == 4              ? WICCA_K1_BANDS4
                                : 1;
+}
+// Lanes that share one K1 segment (16 pixels each): 256 = the workgroup, 64 = a wave.
+constexpr int k1_threads(int L, bool ragged)
+{
+    return (L == 1 ? (ragged ? WICCA_K1_WAVESEG1R : WICCA_K1_WAVESEG1) : L == 4 ? WICCA_K1_WAVESEG4 : 0)
+               ? 64
+               : 256;
 }
 // Work-unit rows of an image with out_h icon rows (groups of k1_bands bands).
 constexpr int64_t unit_rows(int64_t out_h, int L, bool ragged)

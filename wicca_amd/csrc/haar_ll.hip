@@ -41,7 +41,20 @@ namespace wicca {
 
 // Band epilogue of the segment kernel K1: column sums -> LDS -> per-icon sums
 // -> staged 16-B stores of one icon row of one segment.
-template <int L, int C, typename OutT>
+// Barrier of the NT lanes that share a segment (the workgroup, or one wave).
+template <int NT>
+__device__ __forceinline__ void seg_barrier()
+{
+    if constexpr (NT == kThreads) {
+        __syncthreads();
+    } else {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+template <int L, int C, typename OutT, int NT>
 __device__ __forceinline__ void band_epilogue(const LLParams& p, const BlockWork& w, int tid,
                                               int64_t px0, int oy, int64_t y0, int rows_real,
                                               const bool (&valid)[C], const uint32_t (&lo)[C][4],
@@ -49,8 +62,9 @@ __device__ __forceinline__ void band_epilogue(const LLParams& p, const BlockWork
                                               uint8_t* stage, uint32_t* lastcol)
 {
     constexpr int R = 1 << L;
-    constexpr int kColBytes = kSegPx * C * 2;
-    constexpr int kOutPerSeg = kSegPx >> L;
+    constexpr int SEG = NT * 16;  // pixels per segment
+    constexpr int kColBytes = SEG * C * 2;
+    constexpr int kOutPerSeg = SEG >> L;
     constexpr int kStageAligned = (kOutPerSeg * C * (int)sizeof(OutT) + 15) & ~15;
     constexpr bool kReuse = kColBytes + kStageAligned > 40 * 1024;
     const bool replicate = p.border == 1;
@@ -69,13 +83,13 @@ __device__ __forceinline__ void band_epilogue(const LLParams& p, const BlockWork
             if (j < 2) { a[2 * j] = w0; a[2 * j + 1] = w1; }
             else       { b[2 * j - 4] = w0; b[2 * j - 3] = w1; }
         }
-        u32x4* dstv = reinterpret_cast<u32x4*>(colsum + k * (kThreads * 16) + 16 * tid);
+        u32x4* dstv = reinterpret_cast<u32x4*>(colsum + k * (NT * 16) + 16 * tid);
         dstv[0] = a;
         dstv[1] = b;
     }
     // REPLICATE pad columns whose source column W-1 lies in an earlier
     // segment (only in the D > 8 pre-pass, where padding exceeds 2^L).
-    const bool tail = px0 + kSegPx > w.W;
+    const bool tail = px0 + SEG > w.W;
     bool last_elsewhere = false;
     if constexpr (sizeof(OutT) == 4 && L == 8) last_elsewhere = replicate && tail && px0 > w.W - 1;
     if (last_elsewhere && tid < C) {
@@ -86,7 +100,7 @@ __device__ __forceinline__ void band_epilogue(const LLParams& p, const BlockWork
         }
         lastcol[tid] = s;
     }
-    __syncthreads();
+    seg_barrier<NT>();
 
     constexpr int G = L <= 4 ? (1 << L) : 16;  // pixels per icon inside a lane
     constexpr int NJ = 16 / G;                  // icons per lane
@@ -142,7 +156,7 @@ __device__ __forceinline__ void band_epilogue(const LLParams& p, const BlockWork
 #pragma unroll
             for (int c = 0; c < C; ++c) s[0][c] += __shfl_xor(s[0][c], m, 64);
     }
-    if constexpr (kReuse) __syncthreads();  // colsum reads done before staging
+    if constexpr (kReuse) seg_barrier<NT>();  // colsum reads done before staging
 
     const int64_t seg_out0 = px0 >> L;
     const int n_out = (int)min<int64_t>(kOutPerSeg, w.out_w - seg_out0);
@@ -187,14 +201,14 @@ __device__ __forceinline__ void band_epilogue(const LLParams& p, const BlockWork
             }
         }
     }
-    __syncthreads();
+    seg_barrier<NT>();
 
     const int nbytes = n_out * C * (int)sizeof(OutT);
     uint8_t* drow = w.dst + (int64_t)oy * w.dst_pitch + seg_out0 * C * (int64_t)sizeof(OutT);
     // rows of the icon are 16-B aligned (launcher guarantees); the last
     // partial chunk of a row is written with 4-B / 1-B stores
     const int full = nbytes & ~15;
-    for (int i = tid * 16; i < full; i += kThreads * 16) {
+    for (int i = tid * 16; i < full; i += NT * 16) {
         store_row_b128(drow, (uint32_t)i, *reinterpret_cast<const u32x4*>(stage + i));
     }
     if (tid < nbytes - full) drow[full + tid] = stage[full + tid];
@@ -222,26 +236,44 @@ void haar_block_sum_kernel(LLParams p)
     constexpr int U = R < chunk_rows(L) ? R : chunk_rows(L);  // rows per load chunk
     constexpr int CPB = R / U;                                       // chunks per band
     static_assert(R % U == 0, "chunk rows must divide the band");
-    constexpr int kColBytes = kSegPx * C * 2;            // u16 column sums
-    constexpr int kOutPerSeg = kSegPx >> L;              // icons per segment row
+    constexpr int NT = k1_threads(L, RAGGED);            // lanes per segment
+    constexpr int NW = kThreads / NT;                    // segments per workgroup
+    constexpr int SEG = NT * 16;                         // pixels per segment
+    constexpr int kColBytes = SEG * C * 2;               // u16 column sums
+    constexpr int kOutPerSeg = SEG >> L;                 // icons per segment row
     constexpr int kStageBytes = kOutPerSeg * C * (int)sizeof(OutT);
     constexpr int kStageAligned = (kStageBytes + 15) & ~15;
 
     // Wide outputs (f32/u32 at small L) reuse the column-sum area for staging.
     constexpr bool kReuse = kColBytes + kStageAligned > 40 * 1024;
-    constexpr int kSmem = std::max((kReuse ? kColBytes : kColBytes + kStageAligned) + 16, k1_min_lds(L));
+    constexpr int kRegion = (kReuse ? kColBytes : kColBytes + kStageAligned) + 16;  // per segment
+    constexpr int kSmem = std::max(NW * kRegion, k1_min_lds(L));
     __shared__ __attribute__((aligned(16))) uint8_t smem[kSmem];
-    uint16_t* colsum = reinterpret_cast<uint16_t*>(smem);
-    uint8_t* stage = kReuse ? smem : smem + kColBytes;
-    uint32_t* lastcol = reinterpret_cast<uint32_t*>(smem + kSmem - 16);
+    const int grp = (int)threadIdx.x / NT;
+    uint8_t* region = smem + grp * kRegion;
+    uint16_t* colsum = reinterpret_cast<uint16_t*>(region);
+    uint8_t* stage = kReuse ? region : region + kColBytes;
+    uint32_t* lastcol = reinterpret_cast<uint32_t*>(region + kRegion - 16);
 
-    const BlockWork w = resolve_block<L, RAGGED>(p);
-    const int tid = threadIdx.x;
+    BlockWork w;
+    if constexpr (NW == 1) {
+        w = resolve_block<L, RAGGED>(p);
+    } else {
+        // a wave per segment: the workgroup's waves take consecutive units, so
+        // only the batch's last workgroup can hold idle waves (which leave here:
+        // the wave-scope path has no workgroup barriers)
+        const uint64_t unit = ((uint64_t)logical_block(blockIdx.x, gridDim.x) + (RAGGED ? p.block_base : 0u)) *
+                                  NW + (uint64_t)grp;
+        const int64_t n_units = RAGGED ? p.total_blocks : p.n_images * unit_rows(p.out_h, L, false) * p.n_seg;
+        if ((int64_t)unit >= n_units) return;
+        w = resolve_unit<L, RAGGED>(p, (uint32_t)unit);
+    }
+    const int tid = (int)threadIdx.x % NT;
     const int64_t row_bytes = w.W * C;
-    const int64_t px0 = (int64_t)w.seg * kSegPx;          // first pixel of segment
-    constexpr int NB = k1_bands(L, RAGGED);                       // icon rows (bands) of this unit
+    const int64_t px0 = (int64_t)w.seg * SEG;             // first pixel of segment
+    constexpr int NB = k1_bands(L, RAGGED);               // icon rows (bands) of this unit
     const int oy0 = w.oy * NB;                            // its first icon row
-    const int nb = (int)min<int64_t>(NB, w.out_h - oy0);  // workgroup-uniform
+    const int nb = (int)min<int64_t>(NB, w.out_h - oy0);  // uniform over the segment's lanes
     const bool replicate = p.border == 1;
     const int64_t last_row = w.H - 1;
     const uint8_t* img = w.src;
@@ -250,7 +282,7 @@ void haar_block_sum_kernel(LLParams p)
     bool valid[C];
 #pragma unroll
     for (int k = 0; k < C; ++k) {
-        const int64_t o = px0 * C + (int64_t)k * (kThreads * 16) + 16 * tid;  // byte in row
+        const int64_t o = px0 * C + (int64_t)k * (NT * 16) + 16 * tid;  // byte in row
         valid[k] = o < row_bytes;
         off[k] = (uint32_t)o;  // past the record count -> zeros
     }
@@ -301,7 +333,7 @@ void haar_block_sum_kernel(LLParams p)
     };
 #else
     auto epilogue = [&](int oy, int64_t y0, int rows_real) {
-        band_epilogue<L, C, OutT>(p, w, tid, px0, oy, y0, rows_real, valid, lo, hi, colsum, stage,
+        band_epilogue<L, C, OutT, NT>(p, w, tid, px0, oy, y0, rows_real, valid, lo, hi, colsum, stage,
                                   lastcol);
     };
 #endif
@@ -332,7 +364,7 @@ void haar_block_sum_kernel(LLParams p)
             if (bi + 1 < nb) issue(v, y0 + R, 0);
             // a staging area shared with the column sums is read by the
             // previous band's stores: every lane must be past them
-            if (kReuse && bi > 0) __syncthreads();
+            if (kReuse && bi > 0) seg_barrier<NT>();
             epilogue(oy, y0, rows_real);
         }
     }
@@ -898,12 +930,14 @@ int64_t segments_for(int64_t out_w, int L, int C, bool ragged)
         const int64_t strips = ((out_w << L) + strip - 1) / strip;
         return strip_flat(L, ragged) ? strips : (strips + kStripWaves - 1) / kStripWaves;
     }
-    return ((out_w << L) + kSegPx - 1) / kSegPx;  // 4,096-pixel segments
+    const int64_t seg = 16 * k1_threads(L, ragged);  // 4,096- or 1,024-pixel segments
+    return ((out_w << L) + seg - 1) / seg;
 }
 
 int units_per_block(int L, bool ragged)
 {
-    return use_strip_kernel(L) && strip_flat(L, ragged) ? kStripWaves : 1;
+    if (use_strip_kernel(L)) return strip_flat(L, ragged) ? kStripWaves : 1;
+    return kThreads / k1_threads(L, ragged);
 }
 
 bool fast_path_ok(const LLParams& p, int L, int C)
