@@ -47,7 +47,7 @@
 #define WICCA_MULTI_FW 0      // K5: level-DMIN blocks per flush window (power of 2); 0: multi_fw table
 #endif
 #ifndef WICCA_MULTI_CHUNK
-#define WICCA_MULTI_CHUNK 8   // K5 interior strips: rows per load chunk (double-buffered)
+#define WICCA_MULTI_CHUNK 0   // K5 interior strips: rows per load chunk (double-buffered); 0: multi_chunk table
 #endif
 #ifndef WICCA_STRIP_WAVES
 #define WICCA_STRIP_WAVES 4   // K1s: wave strips per workgroup
@@ -245,6 +245,9 @@ struct MultiParams {
 };
 // K5 flush window (level-DMIN blocks): 8 at DMIN = 1 (depths 1-6 +1.5 %), 16
 // otherwise (depths 2-6: 8 was -1.7 %; profiles/r02_ab_fw_*.json).
+// K5 load chunk (rows): 4 at DMIN = 2 (depths 2-6 +1.0 %; 16: -1.1 %), 8
+// otherwise (depths 1-6: 4 -12 %, 16 -40 %; profiles/r02_ab_k5_knobs.json).
+constexpr int multi_chunk(int dmin) { return WICCA_MULTI_CHUNK > 0 ? WICCA_MULTI_CHUNK : (dmin == 2 ? 4 : 8); }
 constexpr int multi_fw(int dmin) { return WICCA_MULTI_FW > 0 ? WICCA_MULTI_FW : (dmin == 1 ? 8 : 16); }
 
 bool multi_kernel_ok(const uint8_t* src, int64_t src_pitch, int64_t src_stride, int64_t W, int C,

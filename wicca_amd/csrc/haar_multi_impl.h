@@ -320,7 +320,7 @@ __device__ __forceinline__ void multi_wave_dot(const MultiParams& p, const Multi
     constexpr int NT = lane_icons<C, DMIN>() * C;  // level-DMIN targets per lane
     constexpr int SB = 1 << DMIN;                   // rows per level-DMIN block
     constexpr int R = 1 << DMAX;
-    constexpr int CH = R < WICCA_MULTI_CHUNK ? R : WICCA_MULTI_CHUNK;  // rows per load chunk
+    constexpr int CH = R < multi_chunk(DMIN) ? R : multi_chunk(DMIN);  // rows per load chunk
     constexpr int nchunks = R / CH;
     const int64_t last_row = p.H - 1;
     auto issue = [&](uint32_t (&d)[CH][NDW], int ci) {
