@@ -71,6 +71,9 @@ def parse():
                     help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-live-pmc", action="store_true",
+                    help="batch config at N=1: skip the two rocprofv3 --pmc child runs that "
+                         "measure roofline.traffic live (the committed --pmc summary is used)")
     ap.add_argument("--dry-run", action="store_true",
                     help="print each rank's (rank, world) and exit before touching the GPU")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_r02.json"),
@@ -166,6 +169,56 @@ def cpu_baseline(args, budget_s: float):
         "affinity_cpus": aff, "cgroup_cpu_quota": quota, "memory_thread_cap": mem_cap,
         "host_cpus": os.cpu_count(), "cpu_model": model,
     }
+
+
+def live_pmc(args, kernel: str, timeout_s: float = 150.0):
+    """roofline.traffic measured in this run: two child runs of this bench's
+    workload under rocprofv3, one counter per pass (FETCH_SIZE, WRITE_SIZE;
+    gfx950 TCC slots cannot hold both), corrected as tools/pmc_summary.py does
+    (KiB; FETCH_SIZE counts half of a wide coalesced read stream).  Children,
+    not exec: this process has initialised the GPU.  None when rocprofv3 is
+    absent or a pass fails (the caller falls back to the committed summary)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    child = [sys.executable, os.path.abspath(__file__), "--steps", "3", "--warmup", "1",
+             "--no-verify", "--no-cpu-baseline", "--no-live-pmc",
+             "--images", str(args.images), "--height", str(args.height), "--width", str(args.width),
+             "--channels", str(args.channels), "--depth", str(args.depth),
+             "--border", str(args.border), "--seed", str(args.seed)]
+    env = dict(os.environ, TMPDIR="/tmp")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    kib = {}
+    with tempfile.TemporaryDirectory(prefix="wicca_pmc_", dir="/tmp") as tmp:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            out_dir = os.path.join(tmp, counter)
+            try:
+                r = subprocess.run([prof, "--pmc", counter, "--output-format", "csv", "-d", out_dir,
+                                    "--"] + child, cwd="/tmp", env=env, timeout=timeout_s,
+                                   stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+            except (OSError, subprocess.TimeoutExpired):
+                return None
+            if r.returncode != 0:
+                return None
+            vals = []
+            for path in glob.glob(os.path.join(out_dir, "**", "*counter_collection.csv"), recursive=True):
+                with open(path) as f:
+                    for row in csv.DictReader(f):
+                        if row.get("Counter_Name") == counter and kernel in row.get("Kernel_Name", ""):
+                            vals.append(float(row["Counter_Value"]))
+            if not vals:
+                return None
+            kib[counter] = sum(vals) / len(vals)
+    read_b = kib["FETCH_SIZE"] * 1024 * 2
+    write_b = kib["WRITE_SIZE"] * 1024
+    return {"read_bytes": read_b, "write_bytes": write_b, "hbm_bytes_per_launch": read_b + write_b}
 
 
 def read_pmc(path: str, workload_key: str):
@@ -744,8 +797,13 @@ def main():
     alg_bytes = B * (H * W * C + oh * ow * C)  # per launch: u8 read once + u8 icon write
     achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
     workload_key = f"b{B}_{W}x{H}x{C}_d{D}"
-    pmc = read_pmc(args.pmc, workload_key)
-    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    kernel = lib.wicca_kernel_name(D, C, 0).decode()
+    pmc = live_pmc(args, kernel) if world == 1 and not args.no_live_pmc else None
+    pmc_source = "live (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child runs of this workload)" if pmc else None
+    if pmc is None:
+        pmc = read_pmc(args.pmc, workload_key)
+        pmc_source = os.path.relpath(args.pmc, REPO) if pmc else None
+    traffic = round(pmc["hbm_bytes_per_launch"]) if pmc else None
 
     out = {
         "metric": BASELINE["metric"],
@@ -774,10 +832,10 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
-            "kernel": lib.wicca_kernel_name(D, C, 0).decode(),
+            "kernel": kernel,
             "kernel_ms": round(kernel_ms, 4),
             "alg_bytes_per_launch": alg_bytes,
-            "pmc_source": os.path.relpath(args.pmc, REPO) if pmc else None,
+            "pmc_source": pmc_source,
         },
         "cpu_baseline": None,
         "verified_vs_numpy_port": verified,
