@@ -187,6 +187,11 @@ def live_pmc(args, kernel: str, timeout_s: float = 150.0):
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
         return None
+    # already under a profiler (e.g. rocprofv3 --kernel-trace around this
+    # bench): a nested rocprofv3 would inherit its preload, so use the fallback
+    if any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ) or \
+            "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return None
     child = [sys.executable, os.path.abspath(__file__), "--steps", "3", "--warmup", "1",
              "--no-verify", "--no-cpu-baseline", "--no-live-pmc",
              "--images", str(args.images), "--height", str(args.height), "--width", str(args.width),

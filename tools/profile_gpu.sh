@@ -12,7 +12,7 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-ARGS="--no-cpu-baseline $*"
+ARGS="--no-cpu-baseline --no-live-pmc $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -- \
     python3 "$R/bench.py" --steps 20 --warmup 3 $ARGS > "$OUT/bench_kt.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -- \
