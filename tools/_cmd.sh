@@ -1,4 +1,6 @@
 set -e
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_nest -- python3 -u bench.py --steps 10 --no-cpu-baseline > gpurun_out/bench_nested.json
-python3 -c "import json; j=json.load(open('gpurun_out/bench_nested.json')); print(j['roofline']['pmc_source'], j['roofline']['traffic'])"
+P="python3 -c \"import json,sys; j=json.load(sys.stdin); print(j['config']['workload'][:60], j['ms_per_step'], j['roofline']['achieved'])\""
+timeout -k 10 200 python -u bench.py --depth 1 --images 256 --height 2160 --width 3840 --no-cpu-baseline --no-live-pmc --no-verify | eval $P
+timeout -k 10 200 python -u bench.py --config ragged --depth 1 --images 256 --height 2160 --width 3840 --ragged-min 0.999 --ragged-align 128 --steps 30 --no-cpu-baseline | eval $P
+timeout -k 10 200 python -u bench.py --config ragged --depth 1 --images 256 --height 2160 --width 3840 --ragged-align 128 --steps 30 --no-cpu-baseline | eval $P
+timeout -k 10 200 python -u bench.py --depth 1 --images 128 --no-cpu-baseline --no-live-pmc --no-verify | eval $P
