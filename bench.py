@@ -178,8 +178,6 @@ def live_pmc(args, kernel: str, timeout_s: float = 150.0):
     (KiB; FETCH_SIZE counts half of a wide coalesced read stream).  Children,
     not exec: this process has initialised the GPU.  None when rocprofv3 is
     absent or a pass fails (the caller falls back to the committed summary)."""
-    import csv
-    import glob
     import shutil
     import subprocess
     import tempfile
@@ -212,17 +210,33 @@ def live_pmc(args, kernel: str, timeout_s: float = 150.0):
                 return None
             if r.returncode != 0:
                 return None
-            vals = []
-            for path in glob.glob(os.path.join(out_dir, "**", "*counter_collection.csv"), recursive=True):
-                with open(path) as f:
-                    for row in csv.DictReader(f):
-                        if row.get("Counter_Name") == counter and kernel in row.get("Kernel_Name", ""):
-                            vals.append(float(row["Counter_Value"]))
-            if not vals:
+            kib[counter] = pmc_counter_kib(out_dir, counter, kernel)
+            if kib[counter] is None:
                 return None
-            kib[counter] = sum(vals) / len(vals)
-    read_b = kib["FETCH_SIZE"] * 1024 * 2
-    write_b = kib["WRITE_SIZE"] * 1024
+    return pmc_hbm_bytes(kib["FETCH_SIZE"], kib["WRITE_SIZE"])
+
+
+def pmc_counter_kib(out_dir: str, counter: str, kernel: str):
+    """Mean per-launch value of `counter` over the launches of `kernel` (a
+    substring of rocprofv3's Kernel_Name) in a --pmc run's counter_collection
+    CSVs under out_dir; None when there are none."""
+    import csv
+    import glob
+
+    vals = []
+    for path in glob.glob(os.path.join(out_dir, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") == counter and kernel in row.get("Kernel_Name", ""):
+                    vals.append(float(row["Counter_Value"]))
+    return sum(vals) / len(vals) if vals else None
+
+
+def pmc_hbm_bytes(fetch_kib: float, write_kib: float):
+    """gfx950 corrections (MI355X_MICROARCH.md, HBM section): both counters
+    in KiB; FETCH_SIZE reports half of a wide coalesced read stream."""
+    read_b = fetch_kib * 1024 * 2
+    write_b = write_kib * 1024
     return {"read_bytes": read_b, "write_bytes": write_b, "hbm_bytes_per_launch": read_b + write_b}
 
 

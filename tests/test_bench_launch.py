@@ -48,3 +48,26 @@ def test_default_is_one_rank():
                          capture_output=True, text=True, timeout=60)
     assert out.returncode == 0, out.stderr
     assert json.loads(out.stdout.strip()) == {"rank": 0, "local_rank": 0, "world": 1}
+
+
+def test_live_pmc_parsing(tmp_path):
+    """roofline.traffic from rocprofv3 --pmc CSVs: only the named kernel's
+    launches, averaged; FETCH_SIZE doubled (gfx950), both in KiB."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    kernel = "haar_strip_kernel<5, 3, unsigned char, false>"
+    for counter, vals in (("FETCH_SIZE", (100.0, 300.0)), ("WRITE_SIZE", (7.0, 9.0))):
+        d = tmp_path / counter / "host" / "123"
+        d.mkdir(parents=True)
+        rows = ["Kernel_Name,Counter_Name,Counter_Value"]
+        rows += [f'"void wicca::{kernel}(wicca::LLParams)",{counter},{v}' for v in vals]
+        rows.append(f'"wicca::synth_u8_kernel(unsigned char*)",{counter},999999')
+        rows.append(f'"void wicca::{kernel}(wicca::LLParams)",OTHER,5')
+        (d / "123_counter_collection.csv").write_text("\n".join(rows) + "\n")
+    fetch = bench.pmc_counter_kib(str(tmp_path / "FETCH_SIZE"), "FETCH_SIZE", kernel)
+    write = bench.pmc_counter_kib(str(tmp_path / "WRITE_SIZE"), "WRITE_SIZE", kernel)
+    assert (fetch, write) == (200.0, 8.0)
+    assert bench.pmc_counter_kib(str(tmp_path / "FETCH_SIZE"), "FETCH_SIZE", "nope") is None
+    hbm = bench.pmc_hbm_bytes(fetch, write)
+    assert hbm == {"read_bytes": 409600.0, "write_bytes": 8192.0, "hbm_bytes_per_launch": 417792.0}
