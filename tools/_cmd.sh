@@ -1,6 +1,3 @@
 set -e
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_suite.log 2>&1
-tail -1 gpurun_out/gpu_suite.log
-timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()"
-timeout -k 10 500 python -u bench.py > gpurun_out/bench_default.json
-cat gpurun_out/bench_default.json
+V=tools/variants
+timeout -k 10 300 python -u tools/ab.py --libs $V/lib_base.so $V/lib_cap6.so $V/lib_cap0.so $V/lib_x64.so --depths 3 --rounds 7 --steps 30 --images 32 --height 2160 --width 3840 --out gpurun_out/ab_4k_d3.json
