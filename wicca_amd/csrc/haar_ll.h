@@ -37,7 +37,8 @@
 #define WICCA_MULTI_DOT 1     // K5: v_dot4 per-(icon, channel) sums on interior strips
 #endif
 #ifndef WICCA_MULTI_WAVES
-#define WICCA_MULTI_WAVES 4   // K5: wave strips per workgroup (8: slower, profiles/r01_ab_k5_stores.json)
+#define WICCA_MULTI_WAVES 4   // K5: wave strips per workgroup (8: slower, profiles/r01_ab_k5_stores.json;
+                              // 2: -1.7 % depths 1-6, -2.7 % depths 2-6, r02z_ab_k5_waves.json)
 #endif
 #ifndef WICCA_MULTI_D1
 #define WICCA_MULTI_D1 1      // K5 also serves depth 1: depths 1-6 in 3.3 ms vs 5.1-5.3 with a
