@@ -1,4 +1,4 @@
 set -e
-V=tools/variants
-timeout -k 10 300 python -u tools/ab.py --libs $V/lib_base.so $V/lib_mw2.so --multi 1,2,3,4,5,6 --rounds 5 --out gpurun_out/ab_k5_mw16.json
-timeout -k 10 300 python -u tools/ab.py --libs $V/lib_base.so $V/lib_mw2.so --multi 2,3,4,5,6 --rounds 5 --out gpurun_out/ab_k5_mw26.json
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_suite.log 2>&1
+tail -1 gpurun_out/gpu_suite.log
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()"
