@@ -75,3 +75,92 @@ def test_destuff_avx2_matches_scalar(tmp_path):
                    check=True, capture_output=True, timeout=120)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "bad=0" in r.stdout, r.stdout
+
+
+def _segments(data):
+    """(offset, length incl. marker, marker) of the segments before the scan."""
+    out, p = [], 2
+    while p + 4 <= len(data) and data[p] == 0xFF:
+        m = data[p + 1]
+        ln = (data[p + 2] << 8) | data[p + 3]
+        out.append((p, 2 + ln, m))
+        if m == 0xDA:
+            break
+        p += 2 + ln
+    return out
+
+
+def _seed():
+    return bytearray(_read("scene_420_q75.jpg"))
+
+
+def test_parser_rejects_oversubscribed_huffman_table():
+    """bits[1] = 3: libjpeg-turbo's 'Bogus Huffman table
+    definition'; used to write past the 512-entry lookup."""
+    for counts in ({1: 3}, {1: 2}, {1: 1, 2: 2}, {2: 4}, {9: 255}):
+        d = _seed()
+        at, _, _ = [s for s in _segments(d) if s[2] == 0xC4][0]
+        body = at + 4
+        for l in range(1, 17):
+            d[body + l] = 0
+        total = 0
+        for l, n in counts.items():
+            d[body + l] = n
+            total += n
+        # keep the segment consistent: the first table's values are reused as
+        # they are (the length field still covers them when total is small)
+        rc, *_ = _info(bytes(d))
+        assert rc in (_lib.WICCA_ERR_DECODE,), (counts, rc, _lib.last_error())
+
+
+def test_parser_rejects_dc_symbol_above_15():
+    d = _seed()
+    for at, ln, m in _segments(d):
+        if m == 0xC4 and (d[at + 4] >> 4) == 0:  # a DC table
+            d[at + 4 + 17] = 16
+            break
+    rc, *_ = _info(bytes(d))
+    assert rc == _lib.WICCA_ERR_DECODE and "Huffman" in _lib.last_error()
+
+
+def test_parser_rejects_subsampled_luma_and_duplicate_ids():
+    d = _seed()
+    at, _, _ = [s for s in _segments(d) if s[2] in (0xC0, 0xC1)][0]
+    y = at + 4 + 6
+    sub = bytearray(d)
+    sub[y + 1] = 0x11   # Y 1x1
+    sub[y + 4] = 0x22   # Cb 2x2
+    rc, *_ = _info(bytes(sub))
+    assert rc == _lib.WICCA_ERR_UNSUPPORTED and "luma" in _lib.last_error()
+    dup = bytearray(d)
+    dup[y + 3] = dup[y]  # Cb id = Y id
+    rc, *_ = _info(bytes(dup))
+    assert rc == _lib.WICCA_ERR_DECODE and "duplicate" in _lib.last_error()
+    dsos = bytearray(d)
+    at, _, _ = [s for s in _segments(d) if s[2] == 0xDA][0]
+    dsos[at + 7] = dsos[at + 5]  # second scan component = first
+    rc, *_ = _info(bytes(dsos))
+    assert rc == _lib.WICCA_ERR_DECODE and "duplicate" in _lib.last_error()
+
+
+def test_parser_short_sos_at_end_of_buffer():
+    d = _seed()
+    at, _, _ = [s for s in _segments(d) if s[2] == 0xDA][0]
+    cut = bytes(d[:at]) + b"\xff\xda\x00\x02"  # SOS with an empty payload, nothing after it
+    arr = np.frombuffer(cut, np.uint8).copy()
+    rc, *_ = _info(arr.tobytes())
+    assert rc == _lib.WICCA_ERR_DECODE
+
+
+def test_parser_fuzz_sanitized():
+    """ASan + UBSan build of jpeg_host.cpp under the marker-segment mutation
+    fuzz (tests/native/parser_fuzz.cpp; seeds: the golden JPEGs)."""
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None or not os.path.isdir("/opt/rocm/include"):
+        pytest.skip("g++ or ROCm headers missing")
+    csrc = os.path.join(os.path.dirname(__file__), "..", "wicca_amd", "csrc")
+    r = subprocess.run(["make", "-s", "-C", csrc, "sanitize", "FUZZ_ITERS=60000"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "iterations=60000" in r.stdout and "accepted=" in r.stdout

@@ -69,6 +69,13 @@ bool jpeg_timing()
     return on;
 }
 
+// Every exit after the first upload from the pinned staging waits for the
+// stream: the next call rewrites that staging (jhost, jtab) on the host.
+struct SyncOnExit {
+    hipStream_t s;
+    ~SyncOnExit() { (void)hipStreamSynchronize(s); }
+};
+
 double now_ms()
 {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -112,6 +119,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     // the copies run while the other threads are still de-stuffing)
     HIP_TRY(ws->jstream.reserve(stream_bytes));
     uint8_t* stream_d = (uint8_t*)ws->jstream.ptr;
+    SyncOnExit sync_on_exit{stream};
     HIP_TRY(hipMemcpyAsync(stream_d + img_off[(size_t)n], stream_h + img_off[(size_t)n], 64,
                            hipMemcpyHostToDevice, stream));
     std::vector<std::vector<int64_t>> seg_off((size_t)n);
@@ -136,10 +144,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         work();
         for (auto& t : th) t.join();
     }
-    if (upload_err) {
-        (void)hipStreamSynchronize(stream);  // the staging is reused by the next call
-        return fail(WICCA_ERR_HIP, "JPEG stream upload failed");
-    }
+    if (upload_err) return fail(WICCA_ERR_HIP, "JPEG stream upload failed");
     const double t_destuffed = now_ms();
     int64_t total_bits = 0;
     for (int64_t i = 0; i < n; ++i) total_bits += seg_off[(size_t)i].back() * 8;

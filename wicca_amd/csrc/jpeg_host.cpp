@@ -58,6 +58,24 @@ int exif_orientation(const uint8_t* p, size_t n)
 
 }  // namespace
 
+// jdhuff.c jpeg_make_d_derived_tbl, run on the tables a scan uses: after the
+// codes of each length the next code must stay below 2^length (the all-ones
+// code is reserved), and DC symbols (magnitude categories) are <= 15.  A table
+// that fails would otherwise write past the 9-bit lookup in build_huff_dev.
+bool huff_table_ok(const JpegHuffTable& t, bool dc)
+{
+    int64_t code = 0;
+    for (int l = 1; l <= 16; ++l) {
+        code += t.bits[l];
+        if (code >= ((int64_t)1 << l)) return false;
+        code <<= 1;
+    }
+    if (dc)
+        for (int i = 0; i < t.nvals; ++i)
+            if (t.vals[i] > 15) return false;
+    return true;
+}
+
 int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
 {
     auto bad = [&](int code, const char* m) {
@@ -98,6 +116,8 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
                 k.v = s[7 + 3 * c] & 15;
                 k.tq = s[8 + 3 * c];
                 if (k.h < 1 || k.h > 4 || k.v < 1 || k.v > 4 || k.tq > 3) return bad(-1, "bad SOF component");
+                for (int j = 0; j < c; ++j)
+                    if (info->comp[j].id == k.id) return bad(-1, "duplicate component id in SOF");
             }
             have_sof = true;
         } else if ((m >= 0xC2 && m <= 0xC3) || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
@@ -140,6 +160,7 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
             if (o != 1) info->orientation = o;
         } else if (m == 0xDA) {  // SOS
             if (!have_sof) return bad(-1, "SOS before SOF");
+            if (sl < 1) return bad(-1, "bad SOS");
             const int ns = s[0];
             if (ns != info->ncomp)
                 return bad(-2, "multi-scan (non-interleaved) JPEG is not supported");
@@ -150,6 +171,8 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
                 for (int k = 0; k < info->ncomp; ++k)
                     if (info->comp[k].id == id) c = k;
                 if (c < 0) return bad(-1, "SOS names an unknown component");
+                for (int j = 0; j < i; ++j)
+                    if (scan_ids[j] == c) return bad(-1, "duplicate component in SOS");
                 scan_ids[i] = c;
                 info->comp[c].td = s[2 + 2 * i] >> 4;
                 info->comp[c].ta = s[2 + 2 * i] & 15;
@@ -168,6 +191,8 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
         const JpegComponent& k = info->comp[c];
         if (!info->qt_present[k.tq]) return bad(-1, "missing quantisation table");
         if (!info->dc_present[k.td] || !info->ac_present[k.ta]) return bad(-1, "missing Huffman table");
+        if (!huff_table_ok(info->dc[k.td], true) || !huff_table_ok(info->ac[k.ta], false))
+            return bad(-1, "bogus Huffman table definition");
     }
     // geometry
     if (info->ncomp == 1) {
@@ -191,6 +216,9 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
         }
         info->hmax = hmax;
         info->vmax = vmax;
+        // the colour pass reads the Y plane at full resolution
+        if (info->comp[0].h != hmax || info->comp[0].v != vmax)
+            return bad(-2, "only full-resolution luma sampling is supported");
         for (int c = 0; c < 3; ++c) {
             const int fh = hmax / info->comp[c].h, fv = vmax / info->comp[c].v;
             if (hmax % info->comp[c].h || vmax % info->comp[c].v || fh > 2 || fv > 2 || (fh == 1 && fv == 2))
@@ -320,7 +348,8 @@ void build_huff_dev(const JpegHuffTable& t, HuffDev* d)
             d->valoff[l] = k - code;
             for (int i = 0; i < t.bits[l]; ++i, ++k, ++code) {
                 if (l <= kHuffLutBits) {
-                    const int lo = code << (kHuffLutBits - l), hi = (code + 1) << (kHuffLutBits - l);
+                    const int lo = code << (kHuffLutBits - l);
+                    const int hi = std::min((code + 1) << (kHuffLutBits - l), 1 << kHuffLutBits);
                     for (int e = lo; e < hi; ++e) d->lut[e] = (uint16_t)((l << 8) | t.vals[k]);
                 }
             }
