@@ -457,7 +457,7 @@ def run_stage(args, torch, rank):
     host = dev.cpu().numpy().reshape(B, H, W, C)
     del dev
     imgs = [host[i] for i in range(B)]
-    coder = HaarCoder()
+    coder = HaarCoder(device=None)  # the rank's current device
     for _ in range(args.warmup):
         coder.icon_stage(imgs, D, shape, args.interpolation)
     t0 = time.perf_counter()

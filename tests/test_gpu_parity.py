@@ -158,6 +158,35 @@ def test_concurrent_threads(coder):
     assert not errors
 
 
+def test_shared_coder_auto_devices_32_threads():
+    """ONE coder shared by a 32-worker pool, as ClassifierProcessor does
+    (classifying_tools.py:144, 414-419, call :317): device="auto" binds each
+    worker to the least-loaded device.  The device list is injected ([0] x 8
+    slots on a one-GPU box); every icon equals the oracle and the thread ->
+    slot map is balanced (4 live threads per slot)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from wicca_amd import HaarCoder
+    coder = HaarCoder(device="auto", devices=[0] * 8)
+    rng = np.random.default_rng(81)
+    imgs = [rng.integers(0, 256, (int(rng.integers(40, 500)), int(rng.integers(40, 700)), 3),
+                        dtype=np.uint8) for _ in range(32)]
+    refs = [c_oracle.ll_int_block(im, 3)[0] for im in imgs]
+    gate = threading.Barrier(32)
+
+    def work(i):
+        ok = np.array_equal(coder.get_small_copy(imgs[i], 3), refs[i])
+        gate.wait(timeout=60)  # all 32 workers bound at once
+        for _ in range(3):
+            ok = ok and np.array_equal(coder.get_small_copy(imgs[i], 3), refs[i])
+        return ok
+
+    with ThreadPoolExecutor(max_workers=32) as ex:
+        assert all(ex.map(work, range(32)))
+    slots = [s for _, s, _ in coder.binder.history]
+    assert len(slots) == 32
+    assert [slots.count(k) for k in range(8)] == [4] * 8
+
+
 def test_device_synth_matches_host(coder):
     import ctypes
     from wicca_amd import _lib

@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import ctypes
 import operator
+import threading
 from abc import ABC, abstractmethod
 from typing import Iterable, Sequence
 
@@ -93,21 +94,133 @@ def _as_hwc(image: np.ndarray) -> np.ndarray:
     return np.ascontiguousarray(img)
 
 
+class _Binding:
+    """One thread's device slot; returned to the binder when the thread ends
+    (CPython drops a thread's ``threading.local`` values at thread exit)."""
+
+    __slots__ = ("binder", "slot")
+
+    def __init__(self, binder: "DeviceBinder", slot: int):
+        self.binder = binder
+        self.slot = slot
+
+    def __del__(self):
+        try:
+            self.binder._release(self.slot)
+        except Exception:  # interpreter shutdown
+            pass
+
+
+class DeviceBinder:
+    """Thread -> device assignment for one shared coder.
+
+    ``ClassifierProcessor`` hands ONE coder to a ``ThreadPoolExecutor`` with a
+    worker per classifier (``classifying_tools.py:144, 414-419``; a new pool per
+    depth, ``:546-551``), and every worker calls ``get_small_copy``
+    (``:317``).  The first call on a thread binds it to the slot of
+    ``devices`` with the fewest live threads (ties: the slot bound least often,
+    then the lowest); the binding lasts for the thread's life, and its slot is
+    released when the thread ends, so each new pool spreads over every GPU
+    again.  ``devices`` may repeat an id (e.g. ``[0] * 8`` to exercise the
+    assignment on a one-GPU box).
+    """
+
+    def __init__(self, devices: Sequence[int] | None = None):
+        self._given = None if devices is None else [int(d) for d in devices]
+        if self._given is not None and not self._given:
+            raise ValueError("devices must not be empty")
+        self._devices: list[int] | None = self._given
+        self._lock = threading.Lock()
+        self._local = threading.local()
+        self._live: list[int] = []
+        self._total: list[int] = []
+        self.history: list[tuple[int, int, int]] = []  # (thread ident, slot, device)
+
+    @property
+    def devices(self) -> list[int]:
+        if self._devices is None:
+            with self._lock:
+                if self._devices is None:
+                    self._devices = self._default_devices()
+        return self._devices
+
+    @staticmethod
+    def _default_devices() -> list[int]:
+        # One rank of a multi-process launch (torch.distributed.run sets
+        # LOCAL_WORLD_SIZE) owns the device it made current: -1 follows it.
+        # No device visible: -1 too, so the C call raises NODEVICE.
+        import os
+        if int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1) > 1:
+            return [-1]
+        n = _lib.device_count()
+        return list(range(n)) if n > 0 else [-1]
+
+    def device(self) -> int:
+        b = getattr(self._local, "binding", None)
+        if b is None:
+            devs = self.devices
+            with self._lock:
+                if len(self._live) != len(devs):
+                    self._live = [0] * len(devs)
+                    self._total = [0] * len(devs)
+                slot = min(range(len(devs)), key=lambda i: (self._live[i], self._total[i], i))
+                self._live[slot] += 1
+                self._total[slot] += 1
+                self.history.append((threading.get_ident(), slot, devs[slot]))
+            b = _Binding(self, slot)
+            self._local.binding = b
+        return self._devices[b.slot]  # type: ignore[index]
+
+    def _release(self, slot: int) -> None:
+        with self._lock:
+            if slot < len(self._live) and self._live[slot] > 0:
+                self._live[slot] -= 1
+
+    def live_counts(self) -> list[int]:
+        """Live threads bound to each slot."""
+        with self._lock:
+            return list(self._live)
+
+
 class HaarCoder(WaveletCoder):
     """The simplified image compressor based on the Haar wavelet, on MI355X.
 
     Reference: ``wicca/wavelet_coder.py:41-67``.
 
     Args:
-        device: HIP device ordinal, or ``None`` for the calling thread's
-            current device.
+        device: ``"auto"`` (default): every calling thread is bound, on its
+            first call, to the least-loaded of ``devices`` (all visible GPUs
+            unless given) — one shared coder spreads ``ClassifierProcessor``'s
+            worker threads over the node (:class:`DeviceBinder`).  An int: that
+            HIP device for every call.  ``None``: the calling thread's current
+            HIP device.
+        devices: the device ids ``"auto"`` binds threads to.
     """
 
-    def __init__(self, device: int | None = None):
+    def __init__(self, device: int | str | None = "auto", devices: Sequence[int] | None = None):
         super().__init__()
         self._ONE_STEP_RATIO = 2
-        self.device = -1 if device is None else int(device)
+        self._binder: DeviceBinder | None = None
+        if isinstance(device, str):
+            if device != "auto":
+                raise ValueError(f"device must be an int, None or 'auto', not {device!r}")
+            self._binder = DeviceBinder(devices)
+            self.device = -1
+        else:
+            if devices is not None:
+                raise ValueError("devices= is only used with device='auto'")
+            self.device = -1 if device is None else int(device)
         self._lib = _lib.load()
+
+    @property
+    def binder(self) -> DeviceBinder | None:
+        """The thread -> device assignment (``device="auto"``), else None."""
+        return getattr(self, "_binder", None)
+
+    def _dev(self) -> int:
+        """The device of this call: the thread's binding, or the fixed id."""
+        b = getattr(self, "_binder", None)
+        return b.device() if b is not None else self.device
 
     # ------------------------------------------------------------------ #
     # reference interface
@@ -130,7 +243,7 @@ class HaarCoder(WaveletCoder):
         out = np.empty((oh, ow, C), np.uint8)
         _lib.check(self._lib.wicca_haar_ll_u8(
             img.ctypes.data, H, W, C, img.strides[0], depth, border, k,
-            out.ctypes.data, ow * C, 0, 0, self.device, None))
+            out.ctypes.data, ow * C, 0, 0, self._dev(), None))
         return out
 
     # ------------------------------------------------------------------ #
@@ -151,7 +264,7 @@ class HaarCoder(WaveletCoder):
         out = np.empty((oh, ow, C), np.float32)
         _lib.check(self._lib.wicca_haar_ll_f32(
             img.ctypes.data, H, W, C, img.strides[0], depth, border, k,
-            out.ctypes.data, ow * C * 4, 0, 0, self.device, None))
+            out.ctypes.data, ow * C * 4, 0, 0, self._dev(), None))
         return out[:, :, 0] if image.ndim == 2 else out
 
     def get_small_copies(self, images: Sequence[np.ndarray], transform_depth: int,
@@ -196,7 +309,7 @@ class HaarCoder(WaveletCoder):
                 _lib.check(self._lib.wicca_haar_ll_u8_batch_multi_gpu(
                     descs, len(idx), C, depth, border, k, devs, len(devices)))
             else:
-                dev = devices[0] if devices else self.device
+                dev = devices[0] if devices else self._dev()
                 _lib.check(self._lib.wicca_haar_ll_u8_batch(descs, len(idx), C, depth, border, k,
                                                             0, 0, dev, None))
             del keep
@@ -236,7 +349,7 @@ class HaarCoder(WaveletCoder):
         icons = np.empty((n, out_h, out_w, C), np.uint8)
         _lib.check(self._lib.wicca_icon_stage_u8(descs, n, C, depth, border, k, out_w, out_h,
                                                  int(interpolation), resized.ctypes.data,
-                                                 icons.ctypes.data, self.device))
+                                                 icons.ctypes.data, self._dev()))
         del keep
         if C == 1:  # cv2.resize returns single-channel images as 2-D arrays
             return resized[..., 0].copy(), icons[..., 0].copy()
@@ -273,7 +386,7 @@ class HaarCoder(WaveletCoder):
             c_pitch = (ctypes.c_int64 * n)(*[o.shape[1] * C for o in outs])
             _lib.check(self._lib.wicca_haar_ll_u8_multi(
                 img.ctypes.data, H, W, C, img.strides[0], c_depths, n, border, k,
-                c_dsts, c_pitch, 0, 0, self.device, None))
+                c_dsts, c_pitch, 0, 0, self._dev(), None))
             for d, o in zip(dev_depths, outs):
                 result[d] = o
         return result
@@ -326,5 +439,5 @@ class HaarCoder(WaveletCoder):
         out = np.empty((H, W, C), np.uint8)
         _lib.check(self._lib.wicca_haar_ll_u8(
             img.ctypes.data, H, W, C, img.strides[0], 0, BORDER_REPLICATE, 0,
-            out.ctypes.data, W * C, 0, 0, self.device, None))
+            out.ctypes.data, W * C, 0, 0, self._dev(), None))
         return out[:, :, 0].copy() if ndim == 2 else out
