@@ -33,6 +33,17 @@ def main(root):
     res["trace"] = {k: {"launches": len(v), "avg_ns": statistics.mean(v),
                         "median_ns": statistics.median(v), "min_ns": min(v)}
                     for k, v in durs.items()}
+    # the same per (kernel, grid): bench.py's one-image verification launch
+    # (and any other differently sized launch) gets a row of its own instead
+    # of pulling the timed launches' average down
+    shapes = {}
+    for r in rows(os.path.join(root, "kt", "**", "*kernel_trace.csv")):
+        grid = "x".join(r[c] for c in sorted(r) if c.startswith("Grid_Size") and r[c])
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        shapes.setdefault(f'{r["Kernel_Name"]} [grid {grid}]', []).append(d)
+    res["trace_by_grid"] = {k: {"launches": len(v), "avg_ns": statistics.mean(v),
+                                "median_ns": statistics.median(v), "min_ns": min(v)}
+                            for k, v in shapes.items()}
     for name, counter in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         per = {}
         for r in rows(os.path.join(root, name, "**", "*counter_collection.csv")):
