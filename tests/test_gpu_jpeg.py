@@ -186,3 +186,79 @@ def test_six_table_write_kernel_subprocess():
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+STAGE = [(1, (224, 224), 3, 1, 0), (6, (224, 224), 3, 0, 77), (8, (331, 331), 3, 1, 0),
+         (4, (240, 240), 1, 0, 9), (3, (299, 299), 0, 1, 0), (7, (224, 224), 3, 0, 255)]
+
+
+@pytest.mark.parametrize("depth,shape,interp,border,k", STAGE,
+                         ids=[f"d{d}-{s[0]}-i{i}-b{b}-k{k}" for d, s, i, b, k in STAGE])
+def test_file_caller_stage_fused_cases(tmp_path, depth, shape, interp, border, k):
+    """The fused stage (each decoded image read once for its INTER_AREA row
+    sums and its icon, stage.hip) against cv2.resize restated (oracle) and the
+    C oracle's icon: every depth class, both borders, the non-AREA
+    interpolations (separate source resize), images smaller than the
+    classifier input (upscaled: no row sums) and odd sizes."""
+    sizes = [(480, 640), (1081, 1919), (133, 517), (77, 61), (300, 2050), (600, 401)]
+    paths, refs = [], []
+    for i, (h, w) in enumerate(sizes):
+        data = J.encode(J.test_image("scene" if i % 2 else "noise", h, w, 7 * i + depth), 85, i % 3)
+        p = tmp_path / f"s{i}.jpg"
+        p.write_bytes(data)
+        paths.append(str(p))
+        refs.append(J.decode_rgb(data))
+    imgs, icons = wicca_amd.get_img_batch(paths, shape, depth, interp, border, k)
+    for i, rgb in enumerate(refs):
+        assert np.array_equal(imgs[i], R.resize(rgb, shape, interp)), i
+        icon = c_oracle.ll_int_block(rgb, depth, border, k)[0]
+        assert np.array_equal(icons[i], R.resize(icon, shape, interp)), i
+
+
+def test_file_caller_stage_fused_equals_unfused(tmp_path):
+    """WICCA_STAGE_FUSED=0 (per-image resize, icon and icon-resize launches)
+    in a child process gives the same bytes as the fused stage."""
+    import subprocess
+    import sys
+    paths = []
+    for i, (h, w) in enumerate([(720, 1280), (1001, 999), (64, 4000), (2160, 3840)]):
+        p = tmp_path / f"u{i}.jpg"
+        p.write_bytes(J.encode(J.test_image("scene", h, w, 90 + i), 88, 2))
+        paths.append(str(p))
+    code = ("import sys, numpy as np, wicca_amd\n"
+            f"paths = {paths!r}\n"
+            "a, b = wicca_amd.get_img_batch(paths, (224, 224), 5, 3, 0, 31)\n"
+            "np.save(sys.argv[1], np.concatenate([a.ravel(), b.ravel()]))\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = []
+    for fused in ("1", "0"):
+        f = str(tmp_path / f"o{fused}.npy")
+        env = dict(os.environ, WICCA_STAGE_FUSED=fused)
+        r = subprocess.run([sys.executable, "-c", code, f], env=env, capture_output=True, text=True,
+                           timeout=240, cwd=root)
+        assert r.returncode == 0, r.stdout + r.stderr
+        outs.append(np.load(f))
+    assert np.array_equal(outs[0], outs[1])
+
+
+def test_fused_backend_equals_separate_launches():
+    """WICCA_JPEG_FUSED=0 (IDCT and colour as separate launches, the luma
+    plane through HBM) gives the same pixels as the fused back end on the
+    golden files, in a child process."""
+    import subprocess
+    import sys
+    code = (
+        "import hashlib, json, os, sys\n"
+        "from wicca_amd import jpeg as WJ\n"
+        f"gold = {GOLD!r}\n"
+        "cases = json.load(open(os.path.join(gold, 'cases.json')))['cases']\n"
+        "data = [open(os.path.join(gold, c['file']), 'rb').read() for c in cases]\n"
+        "outs = WJ.decode_batch(data)\n"
+        "bad = [c['name'] for c, o in zip(cases, outs)\n"
+        "       if hashlib.sha256(o.tobytes()).hexdigest() != c['sha256_rgb']]\n"
+        "print('BAD', bad)\n"
+        "sys.exit(1 if bad else 0)\n")
+    env = dict(os.environ, WICCA_JPEG_FUSED="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stdout + r.stderr

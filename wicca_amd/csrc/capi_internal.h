@@ -111,13 +111,15 @@ struct Workspace {
     // JPEG decode (wicca_jpeg_*): stream + tables, coefficients, planes, scratch, RGB images
     DevBuf jstream, jmeta, jcoef, jplanes, jscratch, jrgb, jtmp;
     DevBuf rscratch;  // two-pass INTER_AREA row sums (float)
+    DevBuf smeta;     // fused caller stage: image descriptors + icon resize parameters
+    HostBuf spin;     // their pinned host staging
     HostBuf jhost;  // pinned host staging of the de-stuffed JPEG streams
     HostBuf jtab;   // pinned host staging of the decode tables
     size_t bytes() const
     {
         return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
                slot[0].cap + slot[1].cap + icon[0].cap + icon[1].cap + jstream.cap + jmeta.cap + jcoef.cap +
-               jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap + rscratch.cap;
+               jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap + rscratch.cap + smeta.cap;
     }
     hipError_t ensure_pipeline()
     {
@@ -150,6 +152,8 @@ struct Workspace {
         }
         jstream.release();
         rscratch.release();
+        smeta.release();
+        spin.release();
         jmeta.release();
         jcoef.release();
         jplanes.release();

@@ -15,6 +15,7 @@
 
 #include "capi_internal.h"
 #include "jpeg.h"
+#include "stage.h"
 
 using namespace wicca_capi;
 
@@ -194,8 +195,10 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
             im.ac_tab[c] = tab_ac[k.ta];
             im.comp_block0[c] = coef_blocks;
             coef_blocks += (int64_t)k.bw * k.bh;
-            im.comp_plane0[c] = plane_bytes;
-            plane_bytes += round_up((int64_t)k.bw * 8 * k.bh * 8, 256);
+            if (c > 0 || !wicca::jpeg_fused()) {  // the fused back end keeps luma in LDS
+                im.comp_plane0[c] = plane_bytes;
+                plane_bytes += round_up((int64_t)k.bw * 8 * k.bh * 8, 256);
+            }
             memcpy(im.qt[c], f.qt[k.tq], sizeof(im.qt[c]));
         }
         if (orient && f.orientation != 1) {  // decode into a temporary, then orient
@@ -211,10 +214,14 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         const std::vector<int64_t>& off = seg_off[(size_t)i];
         const int64_t mcus = (int64_t)f.mcux * f.mcuy;
         const int64_t ri = f.restart_interval > 0 ? f.restart_interval : mcus;
-        const int64_t nseg = std::max<int64_t>(1, std::min<int64_t>((mcus + ri - 1) / ri, (int64_t)off.size() - 1));
+        // every expected restart segment gets an entry: one the (truncated)
+        // data lacks is empty, and its lane zeroes its blocks (the write pass
+        // writes every coefficient; nothing clears the buffer beforehand)
+        const int64_t nseg = std::max<int64_t>(1, (mcus + ri - 1) / ri);
+        const int64_t have = (int64_t)off.size() - 1;
         for (int64_t sgi = 0; sgi < nseg; ++sgi) {
             wicca::JpegSegDev sg;
-            const int64_t b0 = off[(size_t)sgi], b1 = off[(size_t)sgi + 1];
+            const int64_t b0 = off[(size_t)std::min(sgi, have)], b1 = off[(size_t)std::min(sgi + 1, have)];
             sg.bit0 = (img_off[(size_t)i] + b0) * 8;
             sg.bits = (b1 - b0) * 8;
             sg.block0 = sgi * ri * f.bpm;
@@ -238,7 +245,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     const size_t meta_bytes = o_huf + huff.size() * sizeof(wicca::HuffDev);
     HIP_TRY(ws->jmeta.reserve(meta_bytes));
     HIP_TRY(ws->jcoef.reserve((size_t)coef_blocks * 128));
-    HIP_TRY(ws->jplanes.reserve((size_t)plane_bytes));
+    HIP_TRY(ws->jplanes.reserve((size_t)std::max<int64_t>(plane_bytes, 256)));
     HIP_TRY(ws->jscratch.reserve(wicca::jpeg_scratch_bytes((int64_t)sub_seg.size(), (int64_t)segs.size())));
     if (tmp_bytes) HIP_TRY(ws->jtmp.reserve((size_t)tmp_bytes));
     for (int64_t i = 0; i < n; ++i)
@@ -255,7 +262,6 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     memcpy(packed + o_img, ims.data(), ims.size() * sizeof(wicca::JpegImageDev));
     memcpy(packed + o_huf, huff.data(), huff.size() * sizeof(wicca::HuffDev));
     HIP_TRY(hipMemcpyAsync(m, packed, meta_bytes, hipMemcpyHostToDevice, stream));
-    HIP_TRY(hipMemsetAsync(ws->jcoef.ptr, 0, (size_t)coef_blocks * 128, stream));
     wicca::JpegPlan P{};
     P.stream = stream_d;
     P.segs = (const wicca::JpegSegDev*)(m + o_seg);
@@ -297,6 +303,111 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
 }
 
 thread_local int t_jpeg_rounds = 0;
+
+// WICCA_STAGE_FUSED=0: the per-image resize / icon / icon-resize launches
+// (each decoded image read twice) instead of the fused stage.
+bool stage_fused()
+{
+    static const bool on = [] {
+        const char* e = getenv("WICCA_STAGE_FUSED");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+// The caller stage over n device-resident RGB images (img[i], pitch[i]):
+// one stage_rows launch reads every image once for its icon and, when its
+// source resize is the two-pass INTER_AREA, that resize's row sums; then the
+// row sums' vertical pass, any other source resize per image, and one launch
+// resizing every icon.  Outputs are dense (out_h, out_w, 3) per image.
+int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, const int64_t* pitch,
+                const int64_t* H, const int64_t* W, const int64_t* ih, const int64_t* iw, int depth, int border,
+                int k, int64_t out_w, int64_t out_h, int interpolation, uint8_t* dres, uint8_t* dico)
+{
+    const int64_t out_bytes = out_w * out_h * 3;
+    std::vector<wicca::StageImageDev> sd((size_t)n);
+    std::vector<wicca::ResizeParams> src_rp((size_t)n), icon_rp((size_t)n);
+    int64_t icon_total = 0, hsum_total = 0;
+    int max_oh = 0;
+    const bool hs_ok = wicca::stage_hsum_ok(out_w, 3);
+    auto wants_hsum = [&](int64_t i) { return hs_ok && src_rp[(size_t)i].mode == wicca::RS_AREA; };
+    for (int64_t i = 0; i < n; ++i) {
+        wicca::plan_resize((int)H[i], (int)W[i], (int)out_h, (int)out_w, 3, interpolation, &src_rp[(size_t)i]);
+        wicca::plan_resize((int)ih[i], (int)iw[i], (int)out_h, (int)out_w, 3, interpolation, &icon_rp[(size_t)i]);
+        icon_total += round_up(iw[i] * 3, 16) * ih[i];
+        if (wants_hsum(i)) hsum_total += H[i] * out_w * 3 * (int64_t)sizeof(float);
+        max_oh = std::max(max_oh, (int)ih[i]);
+    }
+    HIP_TRY(ws->icon[0].reserve((size_t)icon_total));
+    if (hsum_total) HIP_TRY(ws->rscratch.reserve((size_t)hsum_total));
+    int64_t ioff = 0, hoff = 0;
+    bool any_hsum = false, any_copy = false;
+    for (int64_t i = 0; i < n; ++i) {
+        wicca::StageImageDev& e = sd[(size_t)i];
+        memset(&e, 0, sizeof(e));
+        e.src = img[i];
+        e.src_pitch = pitch[i];
+        e.icon = (uint8_t*)ws->icon[0].ptr + ioff;
+        e.icon_pitch = round_up(iw[i] * 3, 16);
+        ioff += e.icon_pitch * ih[i];
+        e.H = (int32_t)H[i];
+        e.W = (int32_t)W[i];
+        e.oh = (int32_t)ih[i];
+        e.ow = (int32_t)iw[i];
+        e.dst = dres + i * out_bytes;
+        if (wants_hsum(i)) {
+            e.hsum = (float*)((uint8_t*)ws->rscratch.ptr + hoff);
+            hoff += H[i] * out_w * 3 * (int64_t)sizeof(float);
+            e.scale_x = src_rp[(size_t)i].scale_x;
+            e.scale_y = src_rp[(size_t)i].scale_y;
+            any_hsum = true;
+        }
+        wicca::ResizeParams& q = icon_rp[(size_t)i];
+        q.src = e.icon;
+        q.src_pitch = e.icon_pitch;
+        q.src_stride = 0;
+        q.dst = dico + i * out_bytes;
+        q.dst_pitch = out_w * 3;
+        q.dst_stride = 0;
+        any_copy = any_copy || q.mode == wicca::RS_COPY;
+    }
+    // descriptors: [StageImageDev x n | ResizeParams x n], pinned, one upload
+    // (the call synchronises before it returns, so the staging is free again)
+    const size_t o_rp = (size_t)round_up((int64_t)(sizeof(wicca::StageImageDev) * (size_t)n), 256);
+    const size_t bytes = o_rp + sizeof(wicca::ResizeParams) * (size_t)n;
+    HIP_TRY(ws->spin.reserve(bytes, 64 << 10));
+    HIP_TRY(ws->smeta.reserve(bytes));
+    memcpy(ws->spin.ptr, sd.data(), sizeof(wicca::StageImageDev) * (size_t)n);
+    memcpy(ws->spin.ptr + o_rp, icon_rp.data(), sizeof(wicca::ResizeParams) * (size_t)n);
+    HIP_TRY(hipMemcpyAsync(ws->smeta.ptr, ws->spin.ptr, bytes, hipMemcpyHostToDevice, cs));
+    wicca::StageParams sp{};
+    sp.imgs = (const wicca::StageImageDev*)ws->smeta.ptr;
+    sp.C = 3;
+    sp.depth = depth;
+    sp.border = border;
+    sp.k = (int32_t)saturate_k(k);
+    sp.dw = (int32_t)out_w;
+    sp.dh = (int32_t)out_h;
+    HIP_TRY(wicca::launch_stage_rows(sp, n, max_oh, cs));
+    if (any_hsum) HIP_TRY(wicca::launch_stage_vsum(sp, n, cs));
+    for (int64_t i = 0; i < n; ++i) {  // source resizes the row kernel did not prepare
+        if (sd[(size_t)i].hsum) continue;
+        int rc = run_resize(src_rp[(size_t)i], img[i], pitch[i], 0, dres + i * out_bytes, out_w * 3, 0, 1, cs, ws);
+        if (rc) return rc;
+    }
+    // icons -> (out_w, out_h) in one launch (a same-size icon is a copy: then per image)
+    if (!any_copy) {
+        HIP_TRY(wicca::launch_resize_desc((const wicca::ResizeParams*)((uint8_t*)ws->smeta.ptr + o_rp), n, (int)out_h,
+                                          (int)(out_w * 3), cs));
+    } else {
+        for (int64_t i = 0; i < n; ++i) {
+            int rc = run_resize(icon_rp[(size_t)i], sd[(size_t)i].icon, sd[(size_t)i].icon_pitch, 0,
+                                dico + i * out_bytes, out_w * 3, 0, 1, cs, ws);
+            if (rc) return rc;
+        }
+    }
+    return WICCA_OK;
+}
 
 }  // namespace
 
@@ -434,8 +545,18 @@ int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, i
     if ((rc = jpeg_decode_to_device(ws, data, sizes, n, d.data(), p.data(), true, cs, &t_jpeg_rounds))) return rc;
     uint8_t* dres = (uint8_t*)ws->out.ptr;
     uint8_t* dico = dres + n * out_bytes;
+    // classifying_tools.py:315-318 for the whole batch, each decoded image read
+    // once (stage.hip) when the depth is 1..8 and every row fits the LDS stage;
+    // otherwise per image: resize, icon, icon resize
+    bool fused = stage_fused() && depth >= 1 && depth <= 8 && n <= 65535 && out_h <= 65535;
+    for (int64_t i = 0; i < n && fused; ++i) fused = wicca::stage_row_ok(W[i], 3);
+    if (fused) {
+        rc = fused_stage(ws, cs, n, d.data(), p.data(), H.data(), W.data(), ih.data(), iw.data(), depth, border_type,
+                         border_constant, out_w, out_h, interpolation, dres, dico);
+        if (rc) return rc;
+    }
     uint8_t* ico = (uint8_t*)ws->icon[0].ptr;
-    for (int64_t i = 0; i < n; ++i) {
+    for (int64_t i = 0; i < n && !fused; ++i) {
         // classifying_tools.py:315, :317, :318
         wicca::ResizeParams rp{};
         wicca::plan_resize((int)H[i], (int)W[i], (int)out_h, (int)out_w, 3, interpolation, &rp);

@@ -131,4 +131,9 @@ hipError_t launch_orient(const uint8_t* src, int64_t sp, int W, int H, int orien
 
 void build_huff_dev(const JpegHuffTable& t, HuffDev* d);
 
+// Fused luma IDCT + upsampling + colour (default) or the separate launches
+// (WICCA_JPEG_FUSED=0).  With the fused back end only the chroma components
+// need sample planes.
+bool jpeg_fused();
+
 }  // namespace wicca

@@ -267,20 +267,36 @@ __device__ __forceinline__ void flush_blocks(bool done, int64_t blk, uint64_t nz
     wave_lds_sync();  // the owners reuse their blocks and the list next iteration
 }
 
+// Zigzag positions [from, to) of block `blk` set to zero (2-B stores).
+__device__ __forceinline__ void zero_zig(int16_t* coef, int64_t blk, int from, int to)
+{
+    for (int z = from; z < to; ++z) coef[blk * 64 + kNatural[z]] = 0;
+}
+
+// Every coefficient of every block [block_lo, block_end) is written exactly
+// once by exactly one lane, zeros included, so the coefficient buffer needs
+// no clearing pass: a block decoded whole by one lane leaves as a full 128-B
+// block; a block split between two lanes is written position by position,
+// each lane covering its own zigzag range [k at its start, k at its end); the
+// last lane of a segment zeroes what the segment's data never reached (a
+// truncated or corrupt stream: libjpeg-turbo substitutes zeros there too).
 template <bool WRITE>
 __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br, int64_t stop,
                            DecState& st, int64_t& started, int32_t (&dc)[kJpegMaxComp], int64_t g,
-                           int64_t block_lo, int64_t block_end, int16_t* coef, const WaveStage* ws = nullptr)
+                           int64_t block_lo, int64_t block_end, int16_t* coef, const WaveStage* ws = nullptr,
+                           bool seg_last = false)
 {
     int64_t blk = -1;
     bool staged = false;
     uint64_t nz = 0;
+    int zk = 0;  // next zigzag position of a block written position by position (not staged)
     BlockPos pos;
     int16_t* lb = nullptr;
     if (WRITE) {
         if (WICCA_JPEG_STAGE) lb = ws->blocks + (threadIdx.x & 63) * kLaneBlock;
         pos.init(im, g < 0 ? 0 : g);
         if (g >= block_lo && g < block_end) blk = pos.index(im);
+        zk = st.k;  // the block in progress at the start: this lane owns [st.k, ...)
     }
     while (br.p < stop) {
         const int c = im.slot_comp[st.slot];
@@ -302,6 +318,7 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
                         staged = true;
                     } else {
                         coef[blk * 64] = (int16_t)dc[c];
+                        zk = 1;
                     }
                 }
             }
@@ -317,7 +334,9 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
                         lb[n] = (int16_t)v;
                         nz |= 1ull << n;
                     } else {
+                        zero_zig(coef, blk, zk, st.k);
                         coef[blk * 64 + n] = (int16_t)v;
+                        zk = st.k + 1;
                     }
                 }
                 ++st.k;
@@ -330,17 +349,33 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
         bool done = false;
         if (st.k >= 64) {
             done = WRITE && staged;  // a whole block of this lane
+            if (WRITE && !staged && blk >= 0) zero_zig(coef, blk, zk, 64);
             staged = false;
             st.slot = st.slot + 1 == im.bpm ? 0 : st.slot + 1;
             st.k = 0;
         }
         if (WRITE && WICCA_JPEG_STAGE) flush_blocks(done, blk, nz, *ws, coef);
     }
-    if (WRITE && staged) {  // the range ends inside this block: its nonzero coefficients only
-        while (nz) {
-            const int n = __builtin_ctzll(nz);
-            nz &= nz - 1;
-            coef[blk * 64 + n] = lb[n];
+    if (WRITE && blk >= 0 && st.k > 0) {  // the range ends inside block blk: this lane's part [.., st.k)
+        const int kend = min(st.k, 64);
+        if (staged) {
+            for (int z = 0; z < kend; ++z) {
+                const int n = kNatural[z];
+                coef[blk * 64 + n] = ((nz >> n) & 1) ? lb[n] : (int16_t)0;
+            }
+        } else {
+            zero_zig(coef, blk, zk, kend);
+        }
+        if (seg_last) zero_zig(coef, blk, kend, 64);  // nobody decodes the rest
+    }
+    if (WRITE && seg_last) {  // blocks the segment's data never started
+        if (g >= 0) pos.next(im);
+        for (int64_t h = g + 1; h < block_end; ++h) {
+            if (h >= block_lo) {
+                uint4* d = reinterpret_cast<uint4*>(coef + pos.index(im) * 64);
+                for (int q = 0; q < 8; ++q) d[q] = uint4{0, 0, 0, 0};
+            }
+            pos.next(im);
         }
     }
     st.p = br.p;
@@ -565,7 +600,7 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 4 : 1) void jpeg_write_kernel(
 #endif
     // the block in progress at the start was started by an earlier lane
     decode_run<true>(im, tabs.t, br, b1, st, started, dc, sg.block0 + b.block - 1, sg.block0,
-                     sg.block_end, P.coef, &ws);
+                     sg.block_end, P.coef, &ws, j == sg.n_sub - 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -658,15 +693,16 @@ __device__ __forceinline__ void islow_1d(const T (&v)[8], T (&o)[8])
 // they are not needed for bit-exactness.
 constexpr int kIdctBlocksPerWg = 32;
 
-__device__ __forceinline__ void idct_group(const JpegPlan& P, const IdctJob& jb, int64_t group, int32_t* tr)
+// Lane r of the 8 lanes of one block: dequantised row r in, row r of the
+// block's samples out (px).  `t` is the block's 64-int LDS transpose area;
+// every lane of the wave must call this (wave barriers), `live` is uniform
+// over the block's 8 lanes.
+__device__ __forceinline__ void idct8_lane(const int16_t* blk, const uint16_t* qt, int r, bool live, int32_t* t,
+                                           uint8_t (&px)[8])
 {
-    const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;  // block of the group, row / column
-    const int64_t b = group * kIdctBlocksPerWg + lb;
-    const bool live = b < (int64_t)jb.bw * jb.bh;  // uniform over the block's 8 lanes
-    int32_t* t = tr + lb * 64;
     if (live) {
-        const uint4 v = *reinterpret_cast<const uint4*>(P.coef + (jb.block0 + b) * 64 + r * 8);
-        const uint4 qv = *reinterpret_cast<const uint4*>(P.imgs[jb.img].qt[jb.comp] + r * 8);
+        const uint4 v = *reinterpret_cast<const uint4*>(blk + r * 8);
+        const uint4 qv = *reinterpret_cast<const uint4*>(qt + r * 8);
         const uint32_t cw[4] = {v.x, v.y, v.z, v.w}, qw[4] = {qv.x, qv.y, qv.z, qv.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {  // dequantised row r (coefficient * quantiser fits in int32)
@@ -695,15 +731,29 @@ __device__ __forceinline__ void idct_group(const JpegPlan& P, const IdctJob& jb,
     for (int k = 0; k < 8; ++k) row[k] = t[r * 8 + k];
     islow_1d<int64_t>(row, o);
     constexpr int sh = kConstBits + kPass1Bits + 3;
-    uint8_t px[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) px[k] = idct_limit(descale(o[k], sh));
-    const int by = (int)(b / jb.bw), bx = (int)(b - (int64_t)by * jb.bw);
-    const int64_t pitch = (int64_t)jb.bw * 8;
+}
+
+__device__ __forceinline__ uint2 pack8(const uint8_t (&px)[8])
+{
     uint2 pk;
     pk.x = (uint32_t)px[0] | ((uint32_t)px[1] << 8) | ((uint32_t)px[2] << 16) | ((uint32_t)px[3] << 24);
     pk.y = (uint32_t)px[4] | ((uint32_t)px[5] << 8) | ((uint32_t)px[6] << 16) | ((uint32_t)px[7] << 24);
-    *reinterpret_cast<uint2*>(P.planes + jb.plane0 + ((int64_t)by * 8 + r) * pitch + (int64_t)bx * 8) = pk;
+    return pk;
+}
+
+__device__ __forceinline__ void idct_group(const JpegPlan& P, const IdctJob& jb, int64_t group, int32_t* tr)
+{
+    const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;  // block of the group, row / column
+    const int64_t b = group * kIdctBlocksPerWg + lb;
+    const bool live = b < (int64_t)jb.bw * jb.bh;  // uniform over the block's 8 lanes
+    uint8_t px[8];
+    idct8_lane(P.coef + (jb.block0 + b) * 64, P.imgs[jb.img].qt[jb.comp], r, live, tr + lb * 64, px);
+    if (!live) return;
+    const int by = (int)(b / jb.bw), bx = (int)(b - (int64_t)by * jb.bw);
+    const int64_t pitch = (int64_t)jb.bw * 8;
+    *reinterpret_cast<uint2*>(P.planes + jb.plane0 + ((int64_t)by * 8 + r) * pitch + (int64_t)bx * 8) = pack8(px);
 }
 
 // kIdctGroups groups of 32 blocks per workgroup: one-group workgroups were
@@ -897,6 +947,153 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(JpegPlan P)
     }
 }
 
+// ---------------------------------------------------------------------------
+// Fused back end: luma IDCT + fancy upsampling + YCbCr -> RGB in one kernel.
+// A workgroup owns a 256 x 8 pixel tile (32 luma blocks of one block row):
+// the 8 lanes of each block run the ISLOW IDCT (idct8_lane) into an LDS luma
+// tile, then every lane colours 8 pixels of one row — chroma from the chroma
+// planes the chroma IDCT wrote (a quarter of the plane bytes at 4:2:0, read
+// back through L2 with their neighbour rows) — and the tile's RGB leaves from
+// LDS as 16-B stores.  The luma plane (2/3 of the plane bytes at 4:2:0) never
+// touches HBM: against separate IDCT and colour launches this drops its write
+// and re-read.
+// ---------------------------------------------------------------------------
+constexpr int kFuseBlocks = 32;               // luma blocks per tile row
+constexpr int kFuseW = kFuseBlocks * 8;       // 256 pixels
+constexpr int kFuseRowBytes = kFuseW * 3;     // 768 RGB bytes per tile row
+
+// 8 chroma samples (output pixels x .. x+7, x even) of row y by h2v2 fancy
+// upsampling: chroma columns c-1 .. c+4 (c = x/2) of the nearest and the
+// next-nearest chroma row (jdsample.c h2v2_fancy_upsample; edge columns and
+// rows as chroma_sample).
+__device__ __forceinline__ void chroma8_h2v2(const uint8_t* plane, int64_t pitch, int dw, int dh, int x, int y,
+                                             int (&out)[8])
+{
+    const int c = x >> 1, iy = y >> 1;
+    const int oy = (y & 1) ? min(iy + 1, dh - 1) : max(iy - 1, 0);
+    const uint8_t* r0 = plane + (int64_t)iy * pitch;
+    const uint8_t* r1 = plane + (int64_t)oy * pitch;
+    int t[6];
+    if (c >= 1 && c + 4 <= dw - 1 && ((c + 3) & ~3) + 8 <= pitch) {
+        const uint32_t a0 = load4_unaligned(r0, c - 1), a1 = load4_unaligned(r0, c + 3);
+        const uint32_t b0 = load4_unaligned(r1, c - 1), b1 = load4_unaligned(r1, c + 3);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = (int)((a0 >> (8 * k)) & 255) * 3 + (int)((b0 >> (8 * k)) & 255);
+#pragma unroll
+        for (int k = 4; k < 6; ++k) t[k] = (int)((a1 >> (8 * (k - 4))) & 255) * 3 + (int)((b1 >> (8 * (k - 4))) & 255);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const int cc = min(max(c - 1 + k, 0), dw - 1);
+            t[k] = r0[cc] * 3 + r1[cc];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        out[2 * j] = c + j == 0 ? (t[j + 1] * 4 + 8) >> 4 : (t[j + 1] * 3 + t[j] + 8) >> 4;
+        out[2 * j + 1] = c + j >= dw - 1 ? (t[j + 1] * 4 + 7) >> 4 : (t[j + 1] * 3 + t[j + 2] + 7) >> 4;
+    }
+}
+
+__device__ __forceinline__ void ycc8_to_rgb(uint32_t ylo, uint32_t yhi, const int (&cbv)[8], const int (&crv)[8],
+                                            uint8_t (&o)[24])
+{
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int Y = (int)(((q < 4 ? ylo : yhi) >> (8 * (q & 3))) & 255);
+        const int cb = cbv[q] - 128, cr = crv[q] - 128;
+        const int crr = (91881 * cr + 32768) >> 16;
+        const int cbb = (116130 * cb + 32768) >> 16;
+        const int g = (-46802 * cr + (-22554 * cb + 32768)) >> 16;
+        o[3 * q] = clamp255(Y + crr);
+        o[3 * q + 1] = clamp255(Y + g);
+        o[3 * q + 2] = clamp255(Y + cbb);
+    }
+}
+
+__global__ __launch_bounds__(256) void jpeg_luma_color_kernel(JpegPlan P)
+{
+    __shared__ int32_t tr[kFuseBlocks * 64];
+    __shared__ __attribute__((aligned(16))) uint8_t ytile[8 * kFuseW];
+    __shared__ __attribute__((aligned(16))) uint32_t stage[8 * kFuseRowBytes / 4];
+    const JpegImageDev& im = P.imgs[blockIdx.z];
+    const int x0 = blockIdx.x * kFuseW, y0 = blockIdx.y * 8;
+    if (x0 >= im.W || y0 >= im.H) return;  // uniform: the grid is sized for the batch's largest image
+    // 1. luma IDCT: block (blockIdx.x * 32 + lb, blockIdx.y), lane r = row r
+    {
+        const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;
+        const int bx = blockIdx.x * kFuseBlocks + lb;
+        const bool live = bx < im.comp_bw[0];
+        uint8_t px[8];
+        idct8_lane(P.coef + (im.comp_block0[0] + (int64_t)blockIdx.y * im.comp_bw[0] + bx) * 64, im.qt[0], r, live,
+                   tr + lb * 64, px);
+        if (live) *reinterpret_cast<uint2*>(ytile + r * kFuseW + lb * 8) = pack8(px);
+    }
+    __syncthreads();
+    // 2. colour: lane -> tile row rr, pixels cx .. cx+7
+    const int rr = threadIdx.x >> 5, cx = (threadIdx.x & 31) * 8;
+    const int y = y0 + rr, x = x0 + cx;
+    uint8_t o[24];
+#pragma unroll
+    for (int i = 0; i < 24; ++i) o[i] = 0;
+    if (y < im.H && x < im.W) {
+        const uint2 yv = *reinterpret_cast<const uint2*>(ytile + rr * kFuseW + cx);
+        if (im.ncomp == 1) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) o[3 * q] = o[3 * q + 1] = o[3 * q + 2] = (uint8_t)(((q < 4 ? yv.x : yv.y) >> (8 * (q & 3))) & 255);
+        } else {
+            const int fh1 = im.hmax / im.comp_h[1], fv1 = im.vmax / im.comp_v[1];
+            const int fh2 = im.hmax / im.comp_h[2], fv2 = im.vmax / im.comp_v[2];
+            const uint8_t* pb = P.planes + im.comp_plane0[1];
+            const uint8_t* pr = P.planes + im.comp_plane0[2];
+            const int64_t sb = (int64_t)im.comp_bw[1] * 8, sr = (int64_t)im.comp_bw[2] * 8;
+            int cbv[8], crv[8];
+            if (fh1 == 2 && fv1 == 2 && fh2 == 2 && fv2 == 2 && im.comp_dw[1] > 2 && im.comp_dw[2] > 2) {
+                chroma8_h2v2(pb, sb, im.comp_dw[1], im.comp_dh[1], x, y, cbv);
+                chroma8_h2v2(pr, sr, im.comp_dw[2], im.comp_dh[2], x, y, crv);
+            } else if (fh1 == 1 && fv1 == 1 && fh2 == 1 && fv2 == 1) {  // 4:4:4: x is 8-aligned in 8-B rows
+                const uint2 b8 = *reinterpret_cast<const uint2*>(pb + (int64_t)y * sb + x);
+                const uint2 r8 = *reinterpret_cast<const uint2*>(pr + (int64_t)y * sr + x);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    cbv[q] = (int)(((q < 4 ? b8.x : b8.y) >> (8 * (q & 3))) & 255);
+                    crv[q] = (int)(((q < 4 ? r8.x : r8.y) >> (8 * (q & 3))) & 255);
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int xx = min(x + q, im.W - 1);
+                    cbv[q] = chroma_sample(pb, sb, im.comp_dw[1], im.comp_dh[1], fh1, fv1, xx, y);
+                    crv[q] = chroma_sample(pr, sr, im.comp_dw[2], im.comp_dh[2], fh2, fv2, xx, y);
+                }
+            }
+            ycc8_to_rgb(yv.x, yv.y, cbv, crv, o);
+        }
+    }
+    uint32_t* srow = stage + rr * (kFuseRowBytes / 4) + (cx * 3) / 4;  // 24 B = 6 dwords per lane
+#pragma unroll
+    for (int w = 0; w < 6; ++w)
+        srow[w] = (uint32_t)o[4 * w] | ((uint32_t)o[4 * w + 1] << 8) | ((uint32_t)o[4 * w + 2] << 16) |
+                  ((uint32_t)o[4 * w + 3] << 24);
+    __syncthreads();
+    // 3. the tile's rows leave from LDS
+    const int rows = min(8, im.H - y0);
+    const int nbytes = min(kFuseW, im.W - x0) * 3;
+    const bool al16 = (((uintptr_t)im.dst | (uintptr_t)im.dst_pitch) & 15) == 0;  // uniform
+    const uint8_t* s8 = reinterpret_cast<const uint8_t*>(stage);
+    for (int q = threadIdx.x; q < 8 * (kFuseRowBytes / 16); q += 256) {
+        const int row = q / (kFuseRowBytes / 16), off = (q - row * (kFuseRowBytes / 16)) * 16;
+        if (row >= rows || off >= nbytes) continue;
+        uint8_t* d = im.dst + (int64_t)(y0 + row) * im.dst_pitch + (int64_t)x0 * 3 + off;
+        const uint8_t* sp = s8 + row * kFuseRowBytes + off;
+        if (al16 && off + 16 <= nbytes) {
+            *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(sp);
+        } else {
+            for (int i = 0; i < 16 && off + i < nbytes; ++i) d[i] = sp[i];
+        }
+    }
+}
+
 // EXIF orientation (tag 0x0112), as cv2.imread applies it for IMREAD_COLOR:
 // output pixel (x, y) of the W' x H' result reads input pixel (sx, sy).
 __global__ __launch_bounds__(256) void orient_kernel(const uint8_t* src, int64_t sp, int W, int H, int orient,
@@ -938,6 +1135,15 @@ hipError_t launch_orient(const uint8_t* src, int64_t sp, int W, int H, int orien
     return hipGetLastError();
 }
 
+bool jpeg_fused()
+{
+    static const bool on = [] {
+        const char* e = getenv("WICCA_JPEG_FUSED");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
 size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg)
 {
     (void)n_seg;
@@ -956,10 +1162,13 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     IdctJob* jobs = (IdctJob*)((uint8_t*)changed + 64);
     // IDCT jobs: every (image, component); uploaded first, while the stream
     // still waits for the entropy-coded data
+    // fused back end (default; WICCA_JPEG_FUSED=0: separate IDCT and colour
+    // launches, the luma plane through HBM): only the chroma planes are IDCT jobs
+    const bool fused = jpeg_fused();
     std::vector<IdctJob> hj;
     int64_t max_blocks = 0;
     for (int64_t i = 0; i < n_images; ++i)
-        for (int c = 0; c < ims[(size_t)i].ncomp; ++c) {
+        for (int c = fused ? 1 : 0; c < ims[(size_t)i].ncomp; ++c) {
             IdctJob j;
             j.block0 = ims[(size_t)i].comp_block0[c];
             j.plane0 = ims[(size_t)i].comp_plane0[c];
@@ -971,7 +1180,8 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             max_blocks = std::max<int64_t>(max_blocks, (int64_t)j.bw * j.bh);
         }
     if (hj.size() > (size_t)kJpegMaxJobs) return hipErrorInvalidValue;
-    hipError_t e = hipMemcpyAsync(jobs, hj.data(), sizeof(IdctJob) * hj.size(), hipMemcpyHostToDevice, s);
+    hipError_t e = hj.empty() ? hipSuccess
+                              : hipMemcpyAsync(jobs, hj.data(), sizeof(IdctJob) * hj.size(), hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return e;
     const uint32_t grid = (uint32_t)((P.n_sub + kJThreads - 1) / kJThreads);
     // round 0 + rounds until no end state changes; results rotate through
@@ -1014,9 +1224,34 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
         hipLaunchKernelGGL(jpeg_write_kernel<2 * kJpegMaxComp>, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const int64_t per_wg = (int64_t)kIdctBlocksPerWg * kIdctGroups;
-    hipLaunchKernelGGL(jpeg_idct_kernel, dim3((uint32_t)((max_blocks + per_wg - 1) / per_wg), (uint32_t)hj.size()),
-                       dim3(256), 0, s, P, jobs);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (!hj.empty()) {
+        hipLaunchKernelGGL(jpeg_idct_kernel, dim3((uint32_t)((max_blocks + per_wg - 1) / per_wg), (uint32_t)hj.size()),
+                           dim3(256), 0, s, P, jobs);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (fused) {
+        int max_w = 0, max_h = 0;
+        int64_t real_wg = 0;
+        for (int64_t i = 0; i < n_images; ++i) {
+            max_w = std::max(max_w, ims[(size_t)i].W);
+            max_h = std::max(max_h, ims[(size_t)i].H);
+            real_wg += (int64_t)((ims[(size_t)i].W + kFuseW - 1) / kFuseW) * ((ims[(size_t)i].H + 7) / 8);
+        }
+        const int64_t gx = (max_w + kFuseW - 1) / kFuseW, gy = (max_h + 7) / 8;
+        const bool batched = gx * gy * n_images <= 2 * real_wg + 65536;
+        const int64_t per_launch = batched ? 65535 : 1;  // grid.z limit
+        for (int64_t i0 = 0; i0 < n_images; i0 += per_launch) {
+            JpegPlan Q = P;
+            Q.imgs = P.imgs + i0;
+            const JpegImageDev& im = ims[(size_t)i0];
+            const uint32_t x = (uint32_t)(batched ? gx : (im.W + kFuseW - 1) / kFuseW);
+            const uint32_t y = (uint32_t)(batched ? gy : (im.H + 7) / 8);
+            hipLaunchKernelGGL(jpeg_luma_color_kernel,
+                               dim3(x, y, (uint32_t)std::min<int64_t>(per_launch, n_images - i0)), dim3(256), 0, s, Q);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
     // one launch over the batch unless the images differ so much in size that
     // the padded grid would be mostly empty workgroups
     int max_w = 0, max_h = 0;

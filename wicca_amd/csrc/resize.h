@@ -84,5 +84,9 @@ inline bool plan_resize(int H, int W, int dh, int dw, int C, int interpolation, 
 size_t resize_scratch_bytes(const ResizeParams& p, int64_t n_images);
 hipError_t launch_resize(const ResizeParams& p, int64_t n_images, hipStream_t s, void* scratch = nullptr,
                          size_t scratch_bytes = 0);
+// n images with their own parameters (a device array; src / dst per entry,
+// strides unused), one lane per output byte; grid sized for the largest output
+// (max_dh rows of max_row bytes).
+hipError_t launch_resize_desc(const ResizeParams* params, int64_t n, int max_dh, int max_row, hipStream_t s);
 
 }  // namespace wicca

@@ -29,6 +29,7 @@
 #include <stdint.h>
 
 #include "resize.h"
+#include "resize_device.h"
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -37,141 +38,24 @@ namespace wicca {
 namespace {
 
 constexpr int kRsThreads = 256;
-constexpr int kCoefScale = 2048;  // 1 << INTER_RESIZE_COEF_BITS
-
-__device__ __forceinline__ int round_f32(float v) { return (int)rintf(v); }  // cvRound(float)
-__device__ __forceinline__ uint8_t sat_u8(int v) { return (uint8_t)min(255, max(0, v)); }
-
-// Fixed-point bilinear coefficients of one destination index (the x rule of
-// resize.cpp; `fold_edge` applies its clamps at the right/bottom edge).
-struct LinCoef {
-    int s, a0, a1;
-    bool edge;  // past xmax: the source sample times ONE
-};
-
-__device__ __forceinline__ LinCoef lin_coef(int d, int ssize, double scale, double inv_scale,
-                                            bool area_rule, bool fold_edge)
-{
-    int s;
-    float f;
-    if (area_rule) {
-        s = (int)floor(d * scale);
-        f = (float)((double)(d + 1) - (double)(s + 1) * inv_scale);
-        f = f <= 0.f ? 0.f : f - (float)(int)floorf(f);
-    } else {
-        f = (float)((d + 0.5) * scale - 0.5);
-        s = (int)floorf(f);
-        f -= (float)s;
-    }
-    LinCoef c;
-    c.edge = false;
-    if (fold_edge) {
-        if (s < 0) {
-            f = 0.f;
-            s = 0;
-        }
-        c.edge = s + 1 >= ssize;
-        if (s >= ssize - 1) {
-            f = 0.f;
-            s = ssize - 1;
-        }
-    }
-    c.s = s;
-    c.a0 = round_f32((1.f - f) * (float)kCoefScale);
-    c.a1 = round_f32(f * (float)kCoefScale);
-    return c;
-}
-
-// computeResizeAreaTab entries of one destination index: [first partial
-// cell] + full cells [s1, s2) + [last partial cell].
-struct AreaTab {
-    int s1, s2;
-    bool has_a, has_b;
-    float wa, wm, wb;
-};
-
-__device__ __forceinline__ AreaTab area_tab(int d, int ssize, double scale)
-{
-    const double f1 = d * scale;
-    const double f2 = f1 + scale;
-    const double cell = fmin(scale, (double)ssize - f1);
-    int s1 = (int)ceil(f1), s2 = (int)floor(f2);
-    s2 = min(s2, ssize - 1);
-    s1 = min(s1, s2);
-    AreaTab t;
-    t.s1 = s1;
-    t.s2 = s2;
-    t.has_a = (double)s1 - f1 > 1e-3;
-    t.wa = (float)(((double)s1 - f1) / cell);
-    t.wm = (float)(1.0 / cell);
-    t.has_b = f2 - (double)s2 > 1e-3;
-    t.wb = (float)(fmin(fmin(f2 - (double)s2, 1.0), cell) / cell);
-    return t;
-}
+using namespace rs;
 
 __global__ __launch_bounds__(kRsThreads) void resize_u8_kernel(ResizeParams p)
 {
     const int64_t e = (int64_t)blockIdx.x * kRsThreads + threadIdx.x;  // dx * C + c
-    const int dy = blockIdx.y;
-    const int C = p.C;
-    if (e >= (int64_t)p.dw * C) return;
-    const int dx = (int)(e / C), c = (int)(e - (int64_t)dx * C);
+    if (e >= (int64_t)p.dw * p.C) return;
     const uint8_t* img = p.src + (int64_t)blockIdx.z * p.src_stride;
-    uint8_t* out = p.dst + (int64_t)blockIdx.z * p.dst_stride + (int64_t)dy * p.dst_pitch;
-    uint8_t v;
-    switch (p.mode) {
-    case RS_NEAREST: {
-        const int sx = min((int)floor(dx * p.ifx), p.W - 1);
-        const int sy = min((int)floor(dy * p.ify), p.H - 1);
-        v = img[(int64_t)sy * p.src_pitch + (int64_t)sx * C + c];
-        break;
-    }
-    case RS_AREA_FAST: {
-        const int kx = p.kx, ky = p.ky;
-        int s = 0;
-        for (int yy = 0; yy < ky; ++yy) {
-            const uint8_t* row = img + (int64_t)(dy * ky + yy) * p.src_pitch + (int64_t)dx * kx * C + c;
-            for (int xx = 0; xx < kx; ++xx) s += row[xx * C];
-        }
-        if (kx == 2 && ky == 2 && C != 2) v = (uint8_t)((s + 2) >> 2);
-        else v = sat_u8(round_f32((float)s * p.area_scale));
-        break;
-    }
-    case RS_AREA: {
-        const AreaTab tx = area_tab(dx, p.W, p.scale_x);
-        const AreaTab ty = area_tab(dy, p.H, p.scale_y);
-        float sum = 0.f;
-        bool first = true;
-        auto row_term = [&](int sy, float beta) {
-            const uint8_t* row = img + (int64_t)sy * p.src_pitch + c;
-            float buf = 0.f;
-            if (tx.has_a) buf = buf + (float)row[(int64_t)(tx.s1 - 1) * C] * tx.wa;
-            for (int sx = tx.s1; sx < tx.s2; ++sx) buf = buf + (float)row[(int64_t)sx * C] * tx.wm;
-            if (tx.has_b) buf = buf + (float)row[(int64_t)tx.s2 * C] * tx.wb;
-            const float t = beta * buf;
-            sum = first ? t : sum + t;
-            first = false;
-        };
-        if (ty.has_a) row_term(ty.s1 - 1, ty.wa);
-        for (int sy = ty.s1; sy < ty.s2; ++sy) row_term(sy, ty.wm);
-        if (ty.has_b) row_term(ty.s2, ty.wb);
-        v = sat_u8(round_f32(sum));
-        break;
-    }
-    default: {  // RS_LINEAR
-        const LinCoef cx = lin_coef(dx, p.W, p.scale_x, p.inv_x, p.area_rule, true);
-        const LinCoef cy = lin_coef(dy, p.H, p.scale_y, p.inv_y, p.area_rule, false);
-        const int r0 = min(max(cy.s, 0), p.H - 1), r1 = min(max(cy.s + 1, 0), p.H - 1);
-        auto hres = [&](int r) -> int {
-            const uint8_t* row = img + (int64_t)r * p.src_pitch + (int64_t)cx.s * C + c;
-            return cx.edge ? (int)row[0] * kCoefScale : (int)row[0] * cx.a0 + (int)row[C] * cx.a1;
-        };
-        const int h0 = hres(r0), h1 = hres(r1);
-        v = (uint8_t)((((cy.a0 * (h0 >> 4)) >> 16) + ((cy.a1 * (h1 >> 4)) >> 16) + 2) >> 2);
-        break;
-    }
-    }
-    out[e] = v;
+    uint8_t* out = p.dst + (int64_t)blockIdx.z * p.dst_stride + (int64_t)blockIdx.y * p.dst_pitch;
+    out[e] = resize_byte(p, img, e, blockIdx.y);
+}
+
+// A ragged batch: image z has its own ResizeParams (grid sized for the largest).
+__global__ __launch_bounds__(kRsThreads) void resize_desc_kernel(const ResizeParams* ps)
+{
+    const ResizeParams& p = ps[blockIdx.z];
+    const int64_t e = (int64_t)blockIdx.x * kRsThreads + threadIdx.x;
+    if (e >= (int64_t)p.dw * p.C || (int)blockIdx.y >= p.dh) return;
+    p.dst[(int64_t)blockIdx.y * p.dst_pitch + e] = resize_byte(p, p.src, e, blockIdx.y);
 }
 
 // RS_AREA in two passes with a float scratch plane (H rows x dw*C per image):
@@ -239,6 +123,16 @@ size_t resize_scratch_bytes(const ResizeParams& p, int64_t n_images)
 {
     const bool two_pass = p.mode == RS_AREA && (int64_t)p.W * p.C <= kAreaRowMax;
     return two_pass ? (size_t)n_images * (size_t)p.H * (size_t)p.dw * (size_t)p.C * sizeof(float) : 0;
+}
+
+hipError_t launch_resize_desc(const ResizeParams* params, int64_t n, int max_dh, int max_row, hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    if (n > 65535 || max_dh > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(resize_desc_kernel, dim3((uint32_t)((max_row + kRsThreads - 1) / kRsThreads), (uint32_t)max_dh,
+                                                (uint32_t)n),
+                       dim3(kRsThreads), 0, s, params);
+    return hipGetLastError();
 }
 
 hipError_t launch_resize(const ResizeParams& p, int64_t n_images, hipStream_t s, void* scratch,

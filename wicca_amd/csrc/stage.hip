@@ -1,0 +1,202 @@
+// stage.hip — the caller stage of ClassifierProcessor._get_img_batch
+// (wicca/classifying_tools.py:297-323) reading each decoded image ONCE.
+//
+// The reference reads every image twice: cv2.resize(image, shape, INTER_AREA)
+// (:315) and get_small_copy(image, depth) (:317).  Here one workgroup owns a
+// band of 2^D rows of one image (a row of its icon) and streams the band's
+// rows once:
+//   * every 16-B chunk of a row is added into the lane's packed u16 column
+//     sums (255 * 2^8 < 2^16, so D <= 8 never carries between the halves);
+//   * the row also goes to LDS (two buffers, the next row's loads in flight
+//     meanwhile), where each lane forms the INTER_AREA horizontal sums of its
+//     output elements for that row exactly as resize.hip's area_hsum_kernel
+//     does (computeResizeAreaTab weights, OpenCV's float order) and writes them
+//     to the row-sum plane;
+//   * after the band the column sums go to LDS (the two row buffers), and the
+//     lanes reduce them to the icon row: S = sum of the 2^D x 2^D padded block,
+//     icon = S >> 2D (bit-exact for D <= 8), REPLICATE
+//     padding by row clamping and column W-1, CONSTANT as k per padded cell.
+// area_vsum then finishes the source resize from the row sums (a 16-rows-per-
+// output-row reduction over a plane 1/34 of the image's size), and the icons
+// are resized by the per-image resize kernel (resize.hip).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "resize_device.h"
+#include "stage.h"
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+namespace wicca {
+
+namespace {
+
+using namespace rs;
+
+constexpr int kStThreads = 256;
+constexpr int kStChunks = kStageRowMax / 16 / kStThreads;  // 16-B chunks of a row per lane (6)
+
+__global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t buf[2][kStageRowMax];
+    const StageImageDev& im = P.imgs[blockIdx.y];
+    const int band = blockIdx.x;
+    if (band >= im.oh) return;  // uniform: the grid is sized for the largest icon
+    const int C = P.C, D = P.depth, R = 1 << D;
+    const int H = im.H, W = im.W;
+    const int y0 = band * R;
+    const int nq = (W * C + 15) >> 4;  // 16-B chunks of a row (the pitch covers them)
+    const bool replicate = P.border == 1;
+    const bool hs = im.hsum != nullptr;  // uniform
+    const int n_el = P.dw * C;
+    const int t = threadIdx.x;
+
+    // this lane's INTER_AREA output elements and their column tables
+    AreaTab tab[kStageMaxEl];
+    if (hs) {
+#pragma unroll
+        for (int i = 0; i < kStageMaxEl; ++i) {
+            const int e = t + i * kStThreads;
+            if (e < n_el) tab[i] = area_tab(e / C, W, im.scale_x);
+        }
+    }
+    uint32_t lo[kStChunks][4], hi[kStChunks][4];
+#pragma unroll
+    for (int m = 0; m < kStChunks; ++m)
+#pragma unroll
+        for (int w = 0; w < 4; ++w) lo[m][w] = hi[m][w] = 0;
+    u32x4 v[kStChunks];
+    auto load_row = [&](int y) {
+        const u32x4* row = reinterpret_cast<const u32x4*>(im.src + (int64_t)min(y, H - 1) * im.src_pitch);
+#pragma unroll
+        for (int m = 0; m < kStChunks; ++m) {
+            const int q = t + m * kStThreads;
+            v[m] = q < nq ? __builtin_nontemporal_load(row + q) : u32x4{0, 0, 0, 0};
+        }
+    };
+    // rows the block sums take: real rows, and under REPLICATE the clamped
+    // copies of row H-1 below the image
+    const int rows_in = replicate ? R : max(0, min(R, H - y0));
+    if (rows_in > 0) load_row(y0);
+    for (int r = 0; r < rows_in; ++r) {
+        const int y = y0 + r;
+#pragma unroll
+        for (int m = 0; m < kStChunks; ++m) {
+            const u32x4 a = v[m];
+            lo[m][0] += a.x & 0x00FF00FFu;
+            hi[m][0] += (a.x >> 8) & 0x00FF00FFu;
+            lo[m][1] += a.y & 0x00FF00FFu;
+            hi[m][1] += (a.y >> 8) & 0x00FF00FFu;
+            lo[m][2] += a.z & 0x00FF00FFu;
+            hi[m][2] += (a.z >> 8) & 0x00FF00FFu;
+            lo[m][3] += a.w & 0x00FF00FFu;
+            hi[m][3] += (a.w >> 8) & 0x00FF00FFu;
+        }
+        const bool hrow = hs && y < H;  // uniform
+        uint8_t* b = buf[r & 1];
+        if (hrow) {
+#pragma unroll
+            for (int m = 0; m < kStChunks; ++m) {
+                const int q = t + m * kStThreads;
+                if (q < nq) reinterpret_cast<u32x4*>(b)[q] = v[m];
+            }
+        }
+        if (r + 1 < rows_in) load_row(y + 1);  // in flight during the row sums below
+        if (hrow) {
+            __syncthreads();  // row y is in buf[r & 1]; buf[(r + 1) & 1] was last read before this
+            float* out = im.hsum + (int64_t)y * n_el;
+#pragma unroll
+            for (int i = 0; i < kStageMaxEl; ++i) {
+                const int e = t + i * kStThreads;
+                if (e >= n_el) break;
+                const int c = e - (e / C) * C;
+                const AreaTab& tx = tab[i];
+                const uint8_t* rr = b + c;
+                float s = 0.f;
+                if (tx.has_a) s = s + (float)rr[(tx.s1 - 1) * C] * tx.wa;
+                for (int sx = tx.s1; sx < tx.s2; ++sx) s = s + (float)rr[sx * C] * tx.wm;
+                if (tx.has_b) s = s + (float)rr[tx.s2 * C] * tx.wb;
+                out[e] = s;
+            }
+        }
+    }
+    __syncthreads();  // the row buffers are free: they take the column sums
+    // column sums as u16 per row byte (2 * W * C <= 48 KiB)
+    uint16_t* cs = reinterpret_cast<uint16_t*>(&buf[0][0]);
+#pragma unroll
+    for (int m = 0; m < kStChunks; ++m) {
+        const int q = t + m * kStThreads;
+        if (q < nq) {
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                uint2 d;
+                d.x = (lo[m][w] & 0xFFFFu) | (hi[m][w] << 16);
+                d.y = (lo[m][w] >> 16) | (hi[m][w] & 0xFFFF0000u);
+                *reinterpret_cast<uint2*>(cs + q * 16 + 4 * w) = d;
+            }
+        }
+    }
+    __syncthreads();
+    // icon row `band`: (ow, C) block sums over 2^D columns of the column sums
+    const uint32_t kpad = replicate ? 0u : (uint32_t)P.k * (uint32_t)max(0, y0 + R - H);  // CONSTANT rows below
+    uint8_t* icon = im.icon + (int64_t)band * im.icon_pitch;
+    for (int e = t; e < im.ow * C; e += kStThreads) {
+        const int ox = e / C, c = e - ox * C;
+        const int col0 = ox << D;
+        const int ncol = min(R, W - col0);  // real columns of the block
+        uint32_t S = 0;
+        for (int j = 0; j < ncol; ++j) S += cs[(col0 + j) * C + c];
+        S += kpad * (uint32_t)ncol;
+        if (ncol < R)  // right padding
+            S += replicate ? (uint32_t)(R - ncol) * cs[(W - 1) * C + c] : (uint32_t)(R - ncol) * (uint32_t)P.k * R;
+        icon[e] = (uint8_t)(S >> (2 * D));
+    }
+}
+
+// sum = beta * rowsum over the rows of each output row's window (resize.hip's
+// area_vsum_kernel), per image of the batch.
+__global__ __launch_bounds__(kStThreads) void stage_vsum_kernel(StageParams P)
+{
+    const StageImageDev& im = P.imgs[blockIdx.z];
+    if (im.hsum == nullptr) return;
+    const int n_el = P.dw * P.C;
+    const int e = blockIdx.x * kStThreads + threadIdx.x;
+    if (e >= n_el) return;
+    const int dy = blockIdx.y;
+    const AreaTab ty = area_tab(dy, im.H, im.scale_y);
+    const float* col = im.hsum + e;
+    float sum = 0.f;
+    bool first = true;
+    auto term = [&](int sy, float beta) {
+        const float v = beta * col[(int64_t)sy * n_el];
+        sum = first ? v : sum + v;
+        first = false;
+    };
+    if (ty.has_a) term(ty.s1 - 1, ty.wa);
+    for (int sy = ty.s1; sy < ty.s2; ++sy) term(sy, ty.wm);
+    if (ty.has_b) term(ty.s2, ty.wb);
+    im.dst[(int64_t)dy * n_el + e] = sat_u8(round_f32(sum));
+}
+
+}  // namespace
+
+hipError_t launch_stage_rows(const StageParams& p, int64_t n, int max_oh, hipStream_t s)
+{
+    if (n <= 0 || max_oh <= 0) return hipSuccess;
+    if (n > 65535 || p.depth < 1 || p.depth > 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(stage_rows_kernel, dim3((uint32_t)max_oh, (uint32_t)n), dim3(kStThreads), 0, s, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_stage_vsum(const StageParams& p, int64_t n, hipStream_t s)
+{
+    if (n <= 0) return hipSuccess;
+    if (n > 65535 || p.dh > 65535) return hipErrorInvalidValue;
+    const int n_el = p.dw * p.C;
+    hipLaunchKernelGGL(stage_vsum_kernel, dim3((uint32_t)((n_el + kStThreads - 1) / kStThreads), (uint32_t)p.dh,
+                                               (uint32_t)n),
+                       dim3(kStThreads), 0, s, p);
+    return hipGetLastError();
+}
+
+}  // namespace wicca
