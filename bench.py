@@ -522,7 +522,7 @@ def run_jpeg(args, torch, rank):
     sh = ctypes.c_void_p(stream.cuda_stream)
 
     def decode():
-        _lib.check(lib.wicca_jpeg_decode_u8(ptrs, sizes, B, dsts, pitches, 1, 1, -1, sh))
+        _lib.check(lib.wicca_jpeg_decode_u8(ptrs, sizes, B, dsts, pitches, 1, 1, -1, sh, None))
         stream.synchronize()
 
     for _ in range(args.warmup):
@@ -544,7 +544,7 @@ def run_jpeg(args, torch, rank):
 
     def stage():
         _lib.check(lib.wicca_jpeg_icon_stage_u8(ptrs, sizes, B, D, 1, 0, shape[0], shape[1],
-                                                args.interpolation, res.ctypes.data, ico.ctypes.data, -1))
+                                                args.interpolation, res.ctypes.data, ico.ctypes.data, -1, None))
 
     stage()
     t0 = time.perf_counter()

@@ -260,10 +260,14 @@ int wicca_jpeg_info(const uint8_t* data, int64_t size, int apply_orientation,
 
 /* Decode n JPEG files (data[i], sizes[i] bytes, host memory) into RGB images
  * dsts[i] (row pitch dst_pitches[i] >= width*3, host or device per the flag),
- * all in one device pass. */
+ * all in one device pass.  status: NULL (any file that fails to parse fails
+ * the call) or n ints receiving each file's code (0 or WICCA_ERR_*): a file
+ * that fails leaves its dst untouched and the others decode — the reference's
+ * load_image returns None for that file alone (data_loader.py:61-63). */
 int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n,
                          uint8_t* const* dsts, const int64_t* dst_pitches,
-                         int apply_orientation, int dst_is_device, int device, void* stream);
+                         int apply_orientation, int dst_is_device, int device, void* stream,
+                         int* status);
 
 /* Synchronisation passes of the calling thread's last JPEG decode (diagnostic). */
 int wicca_jpeg_last_sync_rounds(void);
@@ -273,12 +277,13 @@ int wicca_jpeg_last_sync_rounds(void);
  * the FILE bytes: GPU decode (load_image, :313) + cv2.resize of the image
  * (:315) + icon (:317) + cv2.resize of the icon (:318); only the compressed
  * files cross PCIe.  resized / resized_icons: dense host arrays (n, out_h,
- * out_w, 3), the np.stack of :323.
+ * out_w, 3), the np.stack of :323.  status: as wicca_jpeg_decode_u8; a file
+ * that fails gets zero outputs and the batch's other files are processed.
  */
 int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n,
                              int depth, int border_type, int border_constant,
                              int64_t out_w, int64_t out_h, int interpolation,
-                             uint8_t* resized, uint8_t* resized_icons, int device);
+                             uint8_t* resized, uint8_t* resized_icons, int device, int* status);
 
 /* wicca_jpeg_icon_stage_u8 over several GPUs of one process: contiguous file
  * ranges balanced by file size, one host thread per device (devices NULL /
@@ -287,7 +292,7 @@ int wicca_jpeg_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* s
                                     int depth, int border_type, int border_constant,
                                     int64_t out_w, int64_t out_h, int interpolation,
                                     uint8_t* resized, uint8_t* resized_icons,
-                                    const int* devices, int n_devices);
+                                    const int* devices, int n_devices, int* status);
 
 /*
  * Deterministic synthetic images on device (no PCIe in timed regions):

@@ -262,3 +262,41 @@ def test_fused_backend_equals_separate_launches():
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_batch_with_unreadable_files_fails_per_slot(tmp_path, capsys):
+    """One file the decoder cannot read (PNG bytes, a progressive JPEG, a
+    header cut short) fails its own slot only: errors="zero" / "none" give
+    the other files' exact results; errors="raise" (the default) raises."""
+    good = [J.encode(J.test_image("scene", h, w, 60 + i), 85, 2) for i, (h, w) in
+            enumerate([(240, 320), (333, 517), (100, 90)])]
+    bad = [b"\x89PNG\r\n\x1a\n" + b"\x00" * 64,
+           J.encode(J.test_image("scene", 64, 64, 3), 80, 2, progressive=True),
+           good[0][:30]]
+    blobs = [good[0], bad[0], good[1], bad[1], bad[2], good[2]]
+    outs = WJ.decode_batch(blobs, errors="none")
+    assert [o is None for o in outs] == [False, True, False, True, True, False]
+    for b, o in zip(blobs, outs):
+        if o is not None:
+            assert np.array_equal(o, J.decode_rgb(b))
+    with pytest.raises((ValueError, NotImplementedError)):
+        WJ.decode_batch(blobs)
+    paths = []
+    for i, b in enumerate(blobs):
+        p = tmp_path / f"f{i}.jpg"
+        p.write_bytes(b)
+        paths.append(str(p))
+    imgs, icons = wicca_amd.get_img_batch(paths, (224, 224), 4, errors="zero")
+    printed = capsys.readouterr().out
+    for i, b in enumerate(blobs):
+        if outs[i] is None:
+            assert not imgs[i].any() and not icons[i].any()
+            assert f"Error loading image {paths[i]}" in printed
+        else:
+            rgb = J.decode_rgb(b)
+            assert np.array_equal(imgs[i], R.resize(rgb, (224, 224), R.INTER_AREA))
+            assert np.array_equal(icons[i], R.resize(c_oracle.ll_int_block(rgb, 4)[0], (224, 224), R.INTER_AREA))
+    with pytest.raises((ValueError, NotImplementedError)):
+        wicca_amd.get_img_batch(paths, (224, 224), 4)
+    two = wicca_amd.get_img_batch(paths, (224, 224), 4, devices=[0, 0], errors="zero")
+    assert np.array_equal(two[0], imgs) and np.array_equal(two[1], icons)

@@ -164,3 +164,24 @@ def test_parser_fuzz_sanitized():
                        text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "iterations=60000" in r.stdout and "accepted=" in r.stdout
+
+
+def test_all_slots_unreadable_needs_no_device(tmp_path, capsys):
+    """Per-slot failure without a GPU: when no file of a batch parses, every
+    slot fails on its own (None / zero outputs) and nothing reaches the device."""
+    from wicca_amd import jpeg as WJ
+    import wicca_amd
+    bad = [b"\x89PNG\r\n\x1a\n" + b"\x00" * 64, b"\xff\xd8\xff\xdb\x00", b""]
+    bad[2] = b"not a jpeg at all"
+    assert WJ.decode_batch(bad, errors="none") == [None, None, None]
+    paths = []
+    for i, b in enumerate(bad):
+        p = tmp_path / f"b{i}.jpg"
+        p.write_bytes(b)
+        paths.append(str(p))
+    imgs, icons = wicca_amd.get_img_batch(paths, (32, 32), 3, errors="zero")
+    assert imgs.shape == (3, 32, 32, 3) and not imgs.any() and not icons.any()
+    out = capsys.readouterr().out
+    assert all(f"Error loading image {p}" in out for p in paths)
+    with pytest.raises(ValueError):
+        WJ.decode_batch(bad)

@@ -54,6 +54,29 @@ int parse_one(const uint8_t* data, int64_t size, wicca::JpegInfo* info, int64_t 
     return WICCA_OK;
 }
 
+// Parse every file; status[i] = 0 or its error code (the first failure's
+// message stays in the thread's last error).  good: the files that parse.
+// Without a status array nothing is screened: every index is "good" and the
+// first bad file fails the whole call, as before.
+int screen_files(const uint8_t* const* data, const int64_t* sizes, int64_t n, int* status, std::vector<int64_t>* good)
+{
+    good->clear();
+    std::string first;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!status) {
+            good->push_back(i);
+            continue;
+        }
+        wicca::JpegInfo f;
+        const int rc = parse_one(data[i], sizes[i], &f, i);
+        status[i] = rc;
+        if (rc == WICCA_OK) good->push_back(i);
+        else if (first.empty()) first = t_last_error;
+    }
+    t_last_error = first;
+    return WICCA_OK;
+}
+
 void oriented_dims(const wicca::JpegInfo& in, bool apply, int64_t* h, int64_t* w)
 {
     const bool swap = apply && in.orientation >= 5;
@@ -427,20 +450,41 @@ int wicca_jpeg_info(const uint8_t* data, int64_t size, int apply_orientation, in
 
 int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, uint8_t* const* dsts,
                          const int64_t* dst_pitches, int apply_orientation, int dst_is_device, int device,
-                         void* stream_in)
+                         void* stream_in, int* status)
 {
     if (n < 0 || (n > 0 && (!data || !sizes || !dsts || !dst_pitches))) return fail(WICCA_ERR_ARG, "bad arrays");
     if (n == 0) return WICCA_OK;
+    // per-slot statuses: a file that does not parse fails its own slot only
+    std::vector<int64_t> good;
+    int rc = screen_files(data, sizes, n, status, &good);
+    if (rc) return rc;
+    if (good.size() < (size_t)n) {
+        const int64_t m = (int64_t)good.size();
+        if (m == 0) return WICCA_OK;
+        std::vector<const uint8_t*> gd((size_t)m);
+        std::vector<int64_t> gs((size_t)m), gp((size_t)m);
+        std::vector<uint8_t*> gdst((size_t)m);
+        for (int64_t j = 0; j < m; ++j) {
+            gd[(size_t)j] = data[good[(size_t)j]];
+            gs[(size_t)j] = sizes[good[(size_t)j]];
+            gdst[(size_t)j] = dsts[good[(size_t)j]];
+            gp[(size_t)j] = dst_pitches[good[(size_t)j]];
+        }
+        std::string first_err = t_last_error;
+        rc = wicca_jpeg_decode_u8(gd.data(), gs.data(), m, gdst.data(), gp.data(), apply_orientation, dst_is_device,
+                                  device, stream_in, nullptr);
+        if (rc == WICCA_OK) t_last_error = first_err;  // the failed slots' first message
+        return rc;
+    }
     std::vector<int64_t> oh((size_t)n), ow((size_t)n);
     for (int64_t i = 0; i < n; ++i) {
         wicca::JpegInfo f;
-        int rc = parse_one(data[i], sizes[i], &f, i);
-        if (rc) return rc;
+        if ((rc = parse_one(data[i], sizes[i], &f, i))) return rc;
         oriented_dims(f, apply_orientation != 0, &oh[i], &ow[i]);
         if (!dsts[i] || dst_pitches[i] < ow[i] * 3) return fail(WICCA_ERR_ARG, "bad output %lld", (long long)i);
     }
     DeviceGuard dg;
-    int dev, rc;
+    int dev;
     if ((rc = select_device(device, &dev, dg))) return rc;
     WorkspaceLease lease;
     if ((rc = acquire(dev, lease))) return rc;
@@ -480,12 +524,12 @@ int wicca_jpeg_last_sync_rounds(void) { return t_jpeg_rounds; }
 
 int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
                              int border_type, int border_constant, int64_t out_w, int64_t out_h,
-                             int interpolation, uint8_t* resized, uint8_t* resized_icons, int device);
+                             int interpolation, uint8_t* resized, uint8_t* resized_icons, int device, int* status);
 
 int wicca_jpeg_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
                                     int border_type, int border_constant, int64_t out_w, int64_t out_h,
                                     int interpolation, uint8_t* resized, uint8_t* resized_icons,
-                                    const int* devices, int n_devices)
+                                    const int* devices, int n_devices, int* status)
 {
     if (n < 0 || (n > 0 && (!data || !sizes))) return fail(WICCA_ERR_ARG, "bad arrays");
     if (n == 0) return WICCA_OK;
@@ -496,17 +540,50 @@ int wicca_jpeg_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* s
     std::vector<int64_t> w(sizes, sizes + n);
     return split_over_devices(w, devices, n_devices, [&](int64_t a, int64_t b, int dev) {
         return wicca_jpeg_icon_stage_u8(data + a, sizes + a, b - a, depth, border_type, border_constant, out_w,
-                                        out_h, interpolation, resized + a * ob, resized_icons + a * ob, dev);
+                                        out_h, interpolation, resized + a * ob, resized_icons + a * ob, dev,
+                                        status ? status + a : nullptr);
     });
 }
 
 int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
                              int border_type, int border_constant, int64_t out_w, int64_t out_h,
-                             int interpolation, uint8_t* resized, uint8_t* resized_icons, int device)
+                             int interpolation, uint8_t* resized, uint8_t* resized_icons, int device, int* status)
 {
     if (n < 0 || (n > 0 && (!data || !sizes))) return fail(WICCA_ERR_ARG, "bad arrays");
     if (n == 0) return WICCA_OK;
     if (!resized || !resized_icons) return fail(WICCA_ERR_ARG, "output buffer is NULL");
+    if (status) {  // a file that does not parse fails its own slot (zero outputs) only
+        if (out_w <= 0 || out_h <= 0 || out_w > 65535 || out_h > 65535) return fail(WICCA_ERR_ARG, "bad output size");
+        std::vector<int64_t> good;
+        int rc = screen_files(data, sizes, n, status, &good);
+        if (rc) return rc;
+        if (good.size() < (size_t)n) {
+            const int64_t ob = out_w * out_h * 3, m = (int64_t)good.size();
+            for (int64_t i = 0; i < n; ++i)
+                if (status[i]) {
+                    memset(resized + i * ob, 0, (size_t)ob);
+                    memset(resized_icons + i * ob, 0, (size_t)ob);
+                }
+            if (m == 0) return WICCA_OK;
+            std::vector<const uint8_t*> gd((size_t)m);
+            std::vector<int64_t> gs((size_t)m);
+            for (int64_t j = 0; j < m; ++j) {
+                gd[(size_t)j] = data[good[(size_t)j]];
+                gs[(size_t)j] = sizes[good[(size_t)j]];
+            }
+            std::vector<uint8_t> r((size_t)(m * ob)), c((size_t)(m * ob));
+            std::string first_err = t_last_error;
+            rc = wicca_jpeg_icon_stage_u8(gd.data(), gs.data(), m, depth, border_type, border_constant, out_w, out_h,
+                                          interpolation, r.data(), c.data(), device, nullptr);
+            if (rc) return rc;
+            for (int64_t j = 0; j < m; ++j) {
+                memcpy(resized + good[(size_t)j] * ob, r.data() + j * ob, (size_t)ob);
+                memcpy(resized_icons + good[(size_t)j] * ob, c.data() + j * ob, (size_t)ob);
+            }
+            t_last_error = first_err;
+            return WICCA_OK;
+        }
+    }
     std::vector<int64_t> H((size_t)n), W((size_t)n), ih((size_t)n), iw((size_t)n);
     int64_t max_icon = 0, rgb_total = 0;
     for (int64_t i = 0; i < n; ++i) {

@@ -697,11 +697,10 @@ constexpr int kIdctBlocksPerWg = 32;
 // block's samples out (px).  `t` is the block's 64-int LDS transpose area;
 // every lane of the wave must call this (wave barriers), `live` is uniform
 // over the block's 8 lanes.
-__device__ __forceinline__ void idct8_lane(const int16_t* blk, const uint16_t* qt, int r, bool live, int32_t* t,
-                                           uint8_t (&px)[8])
+__device__ __forceinline__ void idct8_lane_v(uint4 v, const uint16_t* qt, int r, bool live, int32_t* t,
+                                             uint8_t (&px)[8])
 {
     if (live) {
-        const uint4 v = *reinterpret_cast<const uint4*>(blk + r * 8);
         const uint4 qv = *reinterpret_cast<const uint4*>(qt + r * 8);
         const uint32_t cw[4] = {v.x, v.y, v.z, v.w}, qw[4] = {qv.x, qv.y, qv.z, qv.w};
 #pragma unroll
@@ -733,6 +732,13 @@ __device__ __forceinline__ void idct8_lane(const int16_t* blk, const uint16_t* q
     constexpr int sh = kConstBits + kPass1Bits + 3;
 #pragma unroll
     for (int k = 0; k < 8; ++k) px[k] = idct_limit(descale(o[k], sh));
+}
+
+__device__ __forceinline__ void idct8_lane(const int16_t* blk, const uint16_t* qt, int r, bool live, int32_t* t,
+                                           uint8_t (&px)[8])
+{
+    const uint4 v = live ? *reinterpret_cast<const uint4*>(blk + r * 8) : uint4{0, 0, 0, 0};
+    idct8_lane_v(v, qt, r, live, t, px);
 }
 
 __device__ __forceinline__ uint2 pack8(const uint8_t (&px)[8])
@@ -1011,85 +1017,105 @@ __device__ __forceinline__ void ycc8_to_rgb(uint32_t ylo, uint32_t yhi, const in
     }
 }
 
+// A workgroup walks kFuseRows tiles down one 256-pixel column strip: the next
+// tile's coefficients are loaded while the current one is transformed and
+// coloured, and each tile's chroma loads are issued before its IDCT.
+constexpr int kFuseRows = 4;
+
+__device__ __forceinline__ void chroma8(const JpegPlan& P, const JpegImageDev& im, int x, int y, int (&cbv)[8],
+                                        int (&crv)[8])
+{
+    const int fh1 = im.hmax / im.comp_h[1], fv1 = im.vmax / im.comp_v[1];
+    const int fh2 = im.hmax / im.comp_h[2], fv2 = im.vmax / im.comp_v[2];
+    const uint8_t* pb = P.planes + im.comp_plane0[1];
+    const uint8_t* pr = P.planes + im.comp_plane0[2];
+    const int64_t sb = (int64_t)im.comp_bw[1] * 8, sr = (int64_t)im.comp_bw[2] * 8;
+    if (fh1 == 2 && fv1 == 2 && fh2 == 2 && fv2 == 2 && im.comp_dw[1] > 2 && im.comp_dw[2] > 2) {
+        chroma8_h2v2(pb, sb, im.comp_dw[1], im.comp_dh[1], x, y, cbv);
+        chroma8_h2v2(pr, sr, im.comp_dw[2], im.comp_dh[2], x, y, crv);
+    } else if (fh1 == 1 && fv1 == 1 && fh2 == 1 && fv2 == 1) {  // 4:4:4: x is 8-aligned in 8-B rows
+        const uint2 b8 = *reinterpret_cast<const uint2*>(pb + (int64_t)y * sb + x);
+        const uint2 r8 = *reinterpret_cast<const uint2*>(pr + (int64_t)y * sr + x);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            cbv[q] = (int)(((q < 4 ? b8.x : b8.y) >> (8 * (q & 3))) & 255);
+            crv[q] = (int)(((q < 4 ? r8.x : r8.y) >> (8 * (q & 3))) & 255);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int xx = min(x + q, im.W - 1);
+            cbv[q] = chroma_sample(pb, sb, im.comp_dw[1], im.comp_dh[1], fh1, fv1, xx, y);
+            crv[q] = chroma_sample(pr, sr, im.comp_dw[2], im.comp_dh[2], fh2, fv2, xx, y);
+        }
+    }
+}
+
 __global__ __launch_bounds__(256) void jpeg_luma_color_kernel(JpegPlan P)
 {
     __shared__ int32_t tr[kFuseBlocks * 64];
     __shared__ __attribute__((aligned(16))) uint8_t ytile[8 * kFuseW];
     __shared__ __attribute__((aligned(16))) uint32_t stage[8 * kFuseRowBytes / 4];
     const JpegImageDev& im = P.imgs[blockIdx.z];
-    const int x0 = blockIdx.x * kFuseW, y0 = blockIdx.y * 8;
-    if (x0 >= im.W || y0 >= im.H) return;  // uniform: the grid is sized for the batch's largest image
-    // 1. luma IDCT: block (blockIdx.x * 32 + lb, blockIdx.y), lane r = row r
-    {
-        const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;
-        const int bx = blockIdx.x * kFuseBlocks + lb;
-        const bool live = bx < im.comp_bw[0];
-        uint8_t px[8];
-        idct8_lane(P.coef + (im.comp_block0[0] + (int64_t)blockIdx.y * im.comp_bw[0] + bx) * 64, im.qt[0], r, live,
-                   tr + lb * 64, px);
-        if (live) *reinterpret_cast<uint2*>(ytile + r * kFuseW + lb * 8) = pack8(px);
-    }
-    __syncthreads();
-    // 2. colour: lane -> tile row rr, pixels cx .. cx+7
+    const int x0 = blockIdx.x * kFuseW, by0 = blockIdx.y * kFuseRows;
+    if (x0 >= im.W || by0 * 8 >= im.H) return;  // uniform: the grid is sized for the batch's largest image
+    const int nby = min(kFuseRows, (im.H + 7) / 8 - by0);  // tiles of this workgroup
+    // IDCT lanes: block (blockIdx.x * 32 + lb, row), lane r = row r of the block
+    const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;
+    const int bx = blockIdx.x * kFuseBlocks + lb;
+    const bool blive = bx < im.comp_bw[0];
+    const int16_t* cbase = P.coef + (im.comp_block0[0] + bx) * 64 + r * 8;
+    const int64_t crow = (int64_t)im.comp_bw[0] * 64;  // coefficients per block row
+    // colour lanes: tile row rr, pixels cx .. cx+7
     const int rr = threadIdx.x >> 5, cx = (threadIdx.x & 31) * 8;
-    const int y = y0 + rr, x = x0 + cx;
-    uint8_t o[24];
-#pragma unroll
-    for (int i = 0; i < 24; ++i) o[i] = 0;
-    if (y < im.H && x < im.W) {
-        const uint2 yv = *reinterpret_cast<const uint2*>(ytile + rr * kFuseW + cx);
-        if (im.ncomp == 1) {
-#pragma unroll
-            for (int q = 0; q < 8; ++q) o[3 * q] = o[3 * q + 1] = o[3 * q + 2] = (uint8_t)(((q < 4 ? yv.x : yv.y) >> (8 * (q & 3))) & 255);
-        } else {
-            const int fh1 = im.hmax / im.comp_h[1], fv1 = im.vmax / im.comp_v[1];
-            const int fh2 = im.hmax / im.comp_h[2], fv2 = im.vmax / im.comp_v[2];
-            const uint8_t* pb = P.planes + im.comp_plane0[1];
-            const uint8_t* pr = P.planes + im.comp_plane0[2];
-            const int64_t sb = (int64_t)im.comp_bw[1] * 8, sr = (int64_t)im.comp_bw[2] * 8;
-            int cbv[8], crv[8];
-            if (fh1 == 2 && fv1 == 2 && fh2 == 2 && fv2 == 2 && im.comp_dw[1] > 2 && im.comp_dw[2] > 2) {
-                chroma8_h2v2(pb, sb, im.comp_dw[1], im.comp_dh[1], x, y, cbv);
-                chroma8_h2v2(pr, sr, im.comp_dw[2], im.comp_dh[2], x, y, crv);
-            } else if (fh1 == 1 && fv1 == 1 && fh2 == 1 && fv2 == 1) {  // 4:4:4: x is 8-aligned in 8-B rows
-                const uint2 b8 = *reinterpret_cast<const uint2*>(pb + (int64_t)y * sb + x);
-                const uint2 r8 = *reinterpret_cast<const uint2*>(pr + (int64_t)y * sr + x);
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    cbv[q] = (int)(((q < 4 ? b8.x : b8.y) >> (8 * (q & 3))) & 255);
-                    crv[q] = (int)(((q < 4 ? r8.x : r8.y) >> (8 * (q & 3))) & 255);
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const int xx = min(x + q, im.W - 1);
-                    cbv[q] = chroma_sample(pb, sb, im.comp_dw[1], im.comp_dh[1], fh1, fv1, xx, y);
-                    crv[q] = chroma_sample(pr, sr, im.comp_dw[2], im.comp_dh[2], fh2, fv2, xx, y);
-                }
-            }
-            ycc8_to_rgb(yv.x, yv.y, cbv, crv, o);
-        }
-    }
-    uint32_t* srow = stage + rr * (kFuseRowBytes / 4) + (cx * 3) / 4;  // 24 B = 6 dwords per lane
-#pragma unroll
-    for (int w = 0; w < 6; ++w)
-        srow[w] = (uint32_t)o[4 * w] | ((uint32_t)o[4 * w + 1] << 8) | ((uint32_t)o[4 * w + 2] << 16) |
-                  ((uint32_t)o[4 * w + 3] << 24);
-    __syncthreads();
-    // 3. the tile's rows leave from LDS
-    const int rows = min(8, im.H - y0);
-    const int nbytes = min(kFuseW, im.W - x0) * 3;
+    const int x = x0 + cx;
+    const int rows_out = min(kFuseW, im.W - x0);
+    const int nbytes = rows_out * 3;
     const bool al16 = (((uintptr_t)im.dst | (uintptr_t)im.dst_pitch) & 15) == 0;  // uniform
-    const uint8_t* s8 = reinterpret_cast<const uint8_t*>(stage);
-    for (int q = threadIdx.x; q < 8 * (kFuseRowBytes / 16); q += 256) {
-        const int row = q / (kFuseRowBytes / 16), off = (q - row * (kFuseRowBytes / 16)) * 16;
-        if (row >= rows || off >= nbytes) continue;
-        uint8_t* d = im.dst + (int64_t)(y0 + row) * im.dst_pitch + (int64_t)x0 * 3 + off;
-        const uint8_t* sp = s8 + row * kFuseRowBytes + off;
-        if (al16 && off + 16 <= nbytes) {
-            *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(sp);
-        } else {
-            for (int i = 0; i < 16 && off + i < nbytes; ++i) d[i] = sp[i];
+    uint4 cnext = blive ? *reinterpret_cast<const uint4*>(cbase + by0 * crow) : uint4{0, 0, 0, 0};
+#pragma unroll 1
+    for (int g = 0; g < nby; ++g) {
+        const int y0 = (by0 + g) * 8, y = y0 + rr;
+        const bool px_live = y < im.H && x < im.W;
+        const uint4 ccur = cnext;
+        if (g + 1 < nby && blive) cnext = *reinterpret_cast<const uint4*>(cbase + (by0 + g + 1) * crow);
+        int cbv[8], crv[8];
+        if (px_live && im.ncomp == 3) chroma8(P, im, x, y, cbv, crv);
+        uint8_t px[8];
+        idct8_lane_v(ccur, im.qt[0], r, blive, tr + lb * 64, px);
+        if (blive) *reinterpret_cast<uint2*>(ytile + r * kFuseW + lb * 8) = pack8(px);
+        __syncthreads();  // ytile complete; the previous tile's stage has been stored
+        uint8_t o[24];
+#pragma unroll
+        for (int i = 0; i < 24; ++i) o[i] = 0;
+        if (px_live) {
+            const uint2 yv = *reinterpret_cast<const uint2*>(ytile + rr * kFuseW + cx);
+            if (im.ncomp == 1) {
+#pragma unroll
+                for (int q = 0; q < 8; ++q)
+                    o[3 * q] = o[3 * q + 1] = o[3 * q + 2] = (uint8_t)(((q < 4 ? yv.x : yv.y) >> (8 * (q & 3))) & 255);
+            } else {
+                ycc8_to_rgb(yv.x, yv.y, cbv, crv, o);
+            }
+        }
+        uint32_t* srow = stage + rr * (kFuseRowBytes / 4) + (cx * 3) / 4;  // 24 B = 6 dwords per lane
+#pragma unroll
+        for (int w = 0; w < 6; ++w)
+            srow[w] = (uint32_t)o[4 * w] | ((uint32_t)o[4 * w + 1] << 8) | ((uint32_t)o[4 * w + 2] << 16) |
+                      ((uint32_t)o[4 * w + 3] << 24);
+        __syncthreads();  // stage complete; ytile free for the next tile
+        const int rows = min(8, im.H - y0);
+        const uint8_t* s8 = reinterpret_cast<const uint8_t*>(stage);
+        for (int q = threadIdx.x; q < 8 * (kFuseRowBytes / 16); q += 256) {
+            const int row = q / (kFuseRowBytes / 16), off = (q - row * (kFuseRowBytes / 16)) * 16;
+            if (row >= rows || off >= nbytes) continue;
+            uint8_t* d = im.dst + (int64_t)(y0 + row) * im.dst_pitch + (int64_t)x0 * 3 + off;
+            const uint8_t* sp = s8 + row * kFuseRowBytes + off;
+            if (al16 && off + 16 <= nbytes) {
+                *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(sp);
+            } else {
+                for (int i = 0; i < 16 && off + i < nbytes; ++i) d[i] = sp[i];
+            }
         }
     }
 }
@@ -1235,9 +1261,9 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
         for (int64_t i = 0; i < n_images; ++i) {
             max_w = std::max(max_w, ims[(size_t)i].W);
             max_h = std::max(max_h, ims[(size_t)i].H);
-            real_wg += (int64_t)((ims[(size_t)i].W + kFuseW - 1) / kFuseW) * ((ims[(size_t)i].H + 7) / 8);
+            real_wg += (int64_t)((ims[(size_t)i].W + kFuseW - 1) / kFuseW) * ((ims[(size_t)i].H + 8 * kFuseRows - 1) / (8 * kFuseRows));
         }
-        const int64_t gx = (max_w + kFuseW - 1) / kFuseW, gy = (max_h + 7) / 8;
+        const int64_t gx = (max_w + kFuseW - 1) / kFuseW, gy = (max_h + 8 * kFuseRows - 1) / (8 * kFuseRows);
         const bool batched = gx * gy * n_images <= 2 * real_wg + 65536;
         const int64_t per_launch = batched ? 65535 : 1;  // grid.z limit
         for (int64_t i0 = 0; i0 < n_images; i0 += per_launch) {
@@ -1245,7 +1271,7 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             Q.imgs = P.imgs + i0;
             const JpegImageDev& im = ims[(size_t)i0];
             const uint32_t x = (uint32_t)(batched ? gx : (im.W + kFuseW - 1) / kFuseW);
-            const uint32_t y = (uint32_t)(batched ? gy : (im.H + 7) / 8);
+            const uint32_t y = (uint32_t)(batched ? gy : (im.H + 8 * kFuseRows - 1) / (8 * kFuseRows));
             hipLaunchKernelGGL(jpeg_luma_color_kernel,
                                dim3(x, y, (uint32_t)std::min<int64_t>(per_launch, n_images - i0)), dim3(256), 0, s, Q);
             if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -36,6 +36,8 @@ using namespace rs;
 constexpr int kStThreads = 256;
 constexpr int kStChunks = kStageRowMax / 16 / kStThreads;  // 16-B chunks of a row per lane (6)
 
+// NE = the row-sum elements per lane, ceil(dw * C / 256) (1..4; 3 for 224 x 224 RGB)
+template <int NE>
 __global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
 {
     __shared__ __attribute__((aligned(16))) uint8_t buf[2][kStageRowMax];
@@ -52,10 +54,10 @@ __global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
     const int t = threadIdx.x;
 
     // this lane's INTER_AREA output elements and their column tables
-    AreaTab tab[kStageMaxEl];
+    AreaTab tab[NE] = {};
     if (hs) {
 #pragma unroll
-        for (int i = 0; i < kStageMaxEl; ++i) {
+        for (int i = 0; i < NE; ++i) {
             const int e = t + i * kStThreads;
             if (e < n_el) tab[i] = area_tab(e / C, W, im.scale_x);
         }
@@ -104,19 +106,58 @@ __global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
         if (r + 1 < rows_in) load_row(y + 1);  // in flight during the row sums below
         if (hrow) {
             __syncthreads();  // row y is in buf[r & 1]; buf[(r + 1) & 1] was last read before this
+            // the lane's elements are independent float chains: one loop over
+            // the longest window advances all of them, branch-free (a term
+            // past an element's window reads a valid LDS byte and is not
+            // added), so their LDS reads overlap; each chain keeps OpenCV's
+            // order: first partial cell, full cells left to right, last cell
             float* out = im.hsum + (int64_t)y * n_el;
+            float acc[NE];
+            int len[NE], base[NE];
+            int maxlen = 0;
+            const int last = nq * 16 - 1;  // the staged row's last byte
 #pragma unroll
-            for (int i = 0; i < kStageMaxEl; ++i) {
+            for (int i = 0; i < NE; ++i) {
                 const int e = t + i * kStThreads;
-                if (e >= n_el) break;
-                const int c = e - (e / C) * C;
                 const AreaTab& tx = tab[i];
-                const uint8_t* rr = b + c;
-                float s = 0.f;
-                if (tx.has_a) s = s + (float)rr[(tx.s1 - 1) * C] * tx.wa;
-                for (int sx = tx.s1; sx < tx.s2; ++sx) s = s + (float)rr[sx * C] * tx.wm;
-                if (tx.has_b) s = s + (float)rr[tx.s2 * C] * tx.wb;
-                out[e] = s;
+                const bool live = e < n_el;
+                const int c = e - (e / C) * C;
+                base[i] = live ? tx.s1 * C + c : 0;
+                len[i] = live ? tx.s2 - tx.s1 : 0;
+                maxlen = max(maxlen, len[i]);
+                const float a = (float)b[live && tx.has_a ? base[i] - C : 0] * tx.wa;
+                acc[i] = live && tx.has_a ? 0.f + a : 0.f;
+            }
+            int j = 0;
+            for (; j + 2 <= maxlen; j += 2) {
+                float v0[NE], v1[NE];
+#pragma unroll
+                for (int i = 0; i < NE; ++i) {
+                    v0[i] = (float)b[min(base[i] + j * C, last)];
+                    v1[i] = (float)b[min(base[i] + (j + 1) * C, last)];
+                }
+#pragma unroll
+                for (int i = 0; i < NE; ++i) {
+                    const float s0 = acc[i] + v0[i] * tab[i].wm;
+                    acc[i] = j < len[i] ? s0 : acc[i];
+                    const float s1 = acc[i] + v1[i] * tab[i].wm;
+                    acc[i] = j + 1 < len[i] ? s1 : acc[i];
+                }
+            }
+            if (j < maxlen) {
+#pragma unroll
+                for (int i = 0; i < NE; ++i) {
+                    const float v = (float)b[min(base[i] + j * C, last)];
+                    const float s0 = acc[i] + v * tab[i].wm;
+                    acc[i] = j < len[i] ? s0 : acc[i];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < NE; ++i) {
+                const int e = t + i * kStThreads;
+                if (e >= n_el) continue;
+                if (tab[i].has_b) acc[i] = acc[i] + (float)b[base[i] + len[i] * C] * tab[i].wb;
+                out[e] = acc[i];
             }
         }
     }
@@ -184,7 +225,13 @@ hipError_t launch_stage_rows(const StageParams& p, int64_t n, int max_oh, hipStr
 {
     if (n <= 0 || max_oh <= 0) return hipSuccess;
     if (n > 65535 || p.depth < 1 || p.depth > 8) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(stage_rows_kernel, dim3((uint32_t)max_oh, (uint32_t)n), dim3(kStThreads), 0, s, p);
+    const int ne = (p.dw * p.C + kStThreads - 1) / kStThreads;
+    const dim3 grid((uint32_t)max_oh, (uint32_t)n);
+    if (ne <= 1) hipLaunchKernelGGL(stage_rows_kernel<1>, grid, dim3(kStThreads), 0, s, p);
+    else if (ne == 2) hipLaunchKernelGGL(stage_rows_kernel<2>, grid, dim3(kStThreads), 0, s, p);
+    else if (ne == 3) hipLaunchKernelGGL(stage_rows_kernel<3>, grid, dim3(kStThreads), 0, s, p);
+    else if (ne == 4) hipLaunchKernelGGL(stage_rows_kernel<4>, grid, dim3(kStThreads), 0, s, p);
+    else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -42,22 +42,51 @@ def info(data: bytes, apply_orientation: bool = True) -> tuple[int, int, int, in
     return h.value, w.value, c.value, o.value
 
 
+def _slot_error(data: bytes) -> str:
+    """The parser's message for one file (re-parsed; host only)."""
+    try:
+        info(data)
+    except Exception as e:  # the message of the C ABI's failure
+        return str(e)
+    return "decode failed"
+
+
 def decode_batch(blobs: Sequence[bytes], apply_orientation: bool = True,
-                 device: int | None = None) -> list[np.ndarray]:
-    """RGB (H, W, 3) uint8 arrays of JPEG files, decoded in one GPU pass."""
+                 device: int | None = None, errors: str = "raise") -> list[np.ndarray | None]:
+    """RGB (H, W, 3) uint8 arrays of JPEG files, decoded in one GPU pass.
+
+    errors="raise": the first file that does not parse raises (nothing is
+    decoded); errors="none": such a file gives None in its slot and the others
+    decode (load_image's per-file contract, data_loader.py:61-63).
+    """
+    if errors not in ("raise", "none"):
+        raise ValueError("errors must be 'raise' or 'none'")
     if not blobs:
         return []
-    outs = []
+    n = len(blobs)
+    outs: list[np.ndarray | None] = []
     for b in blobs:
-        h, w, _, _ = info(b, apply_orientation)
+        try:
+            h, w, _, _ = info(b, apply_orientation)
+        except (ValueError, NotImplementedError):
+            if errors == "raise":
+                raise
+            outs.append(None)
+            continue
         outs.append(np.empty((h, w, 3), np.uint8))
     keep, ptrs, sizes = _buffers(blobs)
-    n = len(blobs)
-    dsts = (ctypes.c_void_p * n)(*[o.ctypes.data for o in outs])
-    pitches = (ctypes.c_int64 * n)(*[o.shape[1] * 3 for o in outs])
+    # slots that failed to parse get a 1-pixel placeholder (never written)
+    holder = np.empty(3, np.uint8)
+    dsts = (ctypes.c_void_p * n)(*[o.ctypes.data if o is not None else holder.ctypes.data for o in outs])
+    pitches = (ctypes.c_int64 * n)(*[o.shape[1] * 3 if o is not None else 3 for o in outs])
+    status = (ctypes.c_int * n)() if errors == "none" else None
     _lib.check(_lib.load().wicca_jpeg_decode_u8(ptrs, sizes, n, dsts, pitches, int(apply_orientation),
-                                                0, -1 if device is None else int(device), None))
+                                                0, -1 if device is None else int(device), None, status))
     del keep
+    if status is not None:
+        for i in range(n):
+            if status[i] != 0:
+                outs[i] = None
     return outs
 
 
@@ -81,12 +110,18 @@ def load_image(file_path: str) -> np.ndarray | None:
 
 def get_img_batch(file_paths: Sequence[str], shape, transform_depth: int, interpolation: int = 3,
                   border_type: int = 1, border_constant: int = 0, device: int | None = None,
-                  devices: Sequence[int] | None = None) -> tuple[np.ndarray, np.ndarray]:
+                  devices: Sequence[int] | None = None, errors: str = "raise") -> tuple[np.ndarray, np.ndarray]:
     """``ClassifierProcessor._get_img_batch`` (classifying_tools.py:297-323)
     from file paths: GPU decode + resize + icon + icon resize; only the
     compressed files cross PCIe.  Returns ``(batch_images, batch_icons)``.
     With ``devices`` (several ids) the files are split over those GPUs,
-    balanced by file size, one host thread each."""
+    balanced by file size, one host thread each.
+
+    errors="raise" (the reference: an unreadable file makes load_image return
+    None and cv2.resize then raises, aborting the batch): the first file that
+    does not parse raises.  errors="zero": that file alone fails — its slots
+    are zero images, the error is printed as load_image prints it, and the
+    batch's other files are processed."""
     from .coder import _border_value, _depth_index
     blobs = []
     for p in file_paths:
@@ -100,18 +135,25 @@ def get_img_batch(file_paths: Sequence[str], shape, transform_depth: int, interp
     n = len(blobs)
     resized = np.empty((n, out_h, out_w, 3), np.uint8)
     icons = np.empty((n, out_h, out_w, 3), np.uint8)
+    if errors not in ("raise", "zero"):
+        raise ValueError("errors must be 'raise' or 'zero'")
     keep, ptrs, sizes = _buffers(blobs)
     k = _border_value(border_constant) if int(border_type) == 0 else 0
     lib = _lib.load()
+    status = (ctypes.c_int * n)() if errors == "zero" else None
     if devices is not None and len(devices) > 1:
         devs = (ctypes.c_int * len(devices))(*devices)
         _lib.check(lib.wicca_jpeg_icon_stage_multi_gpu(
             ptrs, sizes, n, _depth_index(transform_depth), int(border_type), k, out_w, out_h,
-            int(interpolation), resized.ctypes.data, icons.ctypes.data, devs, len(devices)))
+            int(interpolation), resized.ctypes.data, icons.ctypes.data, devs, len(devices), status))
     else:
         dev = devices[0] if devices else (-1 if device is None else int(device))
         _lib.check(lib.wicca_jpeg_icon_stage_u8(
             ptrs, sizes, n, _depth_index(transform_depth), int(border_type), k, out_w, out_h,
-            int(interpolation), resized.ctypes.data, icons.ctypes.data, dev))
+            int(interpolation), resized.ctypes.data, icons.ctypes.data, dev, status))
     del keep
+    if status is not None:
+        for i in range(n):
+            if status[i] != 0:  # as load_image reports it (data_loader.py:61-63)
+                print(f"Error loading image {file_paths[i]}: {_slot_error(blobs[i])}")
     return resized, icons
