@@ -207,8 +207,11 @@ int wicca_haar_ll_u8_multi_uniform(const uint8_t* src, int64_t n, int64_t H,
  * (C = 1..4): the resizes of the reference's caller stage,
  * wicca/classifying_tools.py:315 (source image) and :318 (icon), which run
  * with interpolation=cv2.INTER_AREA in the demo.  interpolation uses OpenCV's
- * codes: 0 INTER_NEAREST, 1 INTER_LINEAR, 3 INTER_AREA (others ->
- * WICCA_ERR_ARG).  The arithmetic restates OpenCV's resize.cpp (see
+ * codes: 0 INTER_NEAREST, 1 INTER_LINEAR, 2 INTER_CUBIC, 3 INTER_AREA,
+ * 4 INTER_LANCZOS4, 5 INTER_LINEAR_EXACT, 6 INTER_NEAREST_EXACT — every code
+ * ClassifierProcessor accepts (classifying_tools.py:168-176); others ->
+ * WICCA_ERR_ARG.  INTER_CUBIC / INTER_LANCZOS4 synchronise the stream (their
+ * coefficient tables are uploaded through the call's workspace).  The arithmetic restates OpenCV's resize.cpp (see
  * oracle/resize_cv.py; parity against an OpenCV binary is unpinned here).
  * Note OpenCV's argument order: width first.  Buffers host or device per the
  * flags, as in wicca_haar_ll_u8.
@@ -224,6 +227,14 @@ int wicca_resize_u8_uniform(const uint8_t* src, int64_t n, int64_t H, int64_t W,
                             uint8_t* dst, int64_t out_w, int64_t out_h,
                             int64_t dst_pitch, int64_t dst_image_stride,
                             int interpolation, int device, void* stream);
+
+/* The INTER_CUBIC (2) / INTER_LANCZOS4 (4) coefficient tables of an (H, W) ->
+ * (out_h, out_w) resize as the engine builds them on the host (OpenCV's
+ * interpolateCubic / interpolateLanczos4, resize.cpp): int32 [xofs out_w |
+ * alpha out_w*K | yofs out_h | beta out_h*K], K = 4 or 8.  Writes at most cap
+ * entries to tab (may be NULL) and the full count to *needed.  No device. */
+int wicca_resize_kernel_tables(int64_t H, int64_t W, int64_t out_w, int64_t out_h, int interpolation,
+                               int32_t* tab, int64_t cap, int64_t* needed);
 
 /*
  * The per-image work of ClassifierProcessor._get_img_batch

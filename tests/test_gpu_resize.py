@@ -60,8 +60,8 @@ def test_resize_strided_view():
 
 
 def test_resize_rejects_unimplemented_interpolation():
-    with pytest.raises(ValueError, match="interpolation 2"):
-        wicca_amd.resize(np.zeros((8, 8, 3), np.uint8), (4, 4), 2)
+    with pytest.raises(ValueError, match="interpolation 7"):
+        wicca_amd.resize(np.zeros((8, 8, 3), np.uint8), (4, 4), 7)
 
 
 def test_resize_uniform_device_batch():

@@ -111,5 +111,125 @@ def test_nearest_picks_floor_sources():
 
 
 def test_unsupported_interpolation_raises():
+    # cv2.INTER_MAX (7) and the WARP_* flags are not interpolations of cv2.resize
     with pytest.raises(NotImplementedError):
-        R.resize(np.zeros((4, 4, 3), np.uint8), (2, 2), 2)
+        R.resize(np.zeros((4, 4, 3), np.uint8), (2, 2), 7)
+
+
+# ---- INTER_CUBIC / INTER_LANCZOS4 / INTER_LINEAR_EXACT / INTER_NEAREST_EXACT ----
+# (the interpolations ClassifierProcessor accepts beyond the demo's,
+# /root/reference/wicca/classifying_tools.py:168-176; parity-unpinned like the rest)
+
+def _ref_separable(img, dw, dh, kern, K):
+    """float64 separable filter with half-pixel centres and replicated borders."""
+    H, W, C = img.shape
+    src = img.astype(np.float64)
+
+    def axis_w(n, m):
+        sc = n / m
+        Wm = np.zeros((m, n))
+        for d in range(m):
+            f = (d + 0.5) * sc - 0.5
+            s = int(np.floor(f))
+            t = f - s
+            w = np.array([kern(t + (K // 2 - 1) - j) for j in range(K)])
+            w /= w.sum()
+            for j in range(K):
+                Wm[d, min(max(s - (K // 2 - 1) + j, 0), n - 1)] += w[j]
+        return Wm
+
+    Wx, Wy = axis_w(W, dw), axis_w(H, dh)
+    tmp = np.einsum("hwc,xw->hxc", src, Wx, optimize=True)
+    return np.einsum("yh,hxc->yxc", Wy, tmp, optimize=True)
+
+
+def _cubic_k(t, A=-0.75):
+    t = abs(t)
+    if t <= 1:
+        return (A + 2) * t ** 3 - (A + 3) * t ** 2 + 1
+    if t < 2:
+        return A * t ** 3 - 5 * A * t ** 2 + 8 * A * t - 4 * A
+    return 0.0
+
+
+def _lanczos_k(t, a=4):
+    return 1.0 if t == 0 else (a * np.sin(np.pi * t) * np.sin(np.pi * t / a) / (np.pi * t) ** 2 if abs(t) < a else 0.0)
+
+
+@pytest.mark.parametrize("dsize", [(224, 224), (53, 37), (300, 410)])
+def test_cubic_close_to_float_bicubic(dsize):
+    img = rng.integers(0, 256, (120, 170, 3), dtype=np.uint8)
+    ref = np.clip(_ref_separable(img, dsize[0], dsize[1], _cubic_k, 4), 0, 255)
+    out = R.resize(img, dsize, R.INTER_CUBIC).astype(np.float64)
+    assert np.abs(out - ref).max() <= 1.5
+
+
+@pytest.mark.parametrize("dsize", [(224, 224), (53, 37), (300, 410)])
+def test_lanczos4_close_to_float_lanczos(dsize):
+    img = rng.integers(0, 256, (120, 170, 3), dtype=np.uint8)
+    ref = np.clip(_ref_separable(img, dsize[0], dsize[1], _lanczos_k, 8), 0, 255)
+    out = R.resize(img, dsize, R.INTER_LANCZOS4).astype(np.float64)
+    assert np.abs(out - ref).max() <= 2.0
+
+
+def test_cubic_coefficients_partition_unity():
+    for x in np.linspace(0, 0.999, 37, dtype=np.float32):
+        c = R.cubic_coeffs(x)
+        assert abs(float(sum(np.float64(v) for v in c)) - 1.0) < 1e-6
+        l = R.lanczos4_coeffs(x)
+        assert abs(float(sum(np.float64(v) for v in l)) - 1.0) < 1e-5
+    assert R.lanczos4_coeffs(0.0)[3] == np.float32(1.0)
+
+
+def test_cubic_simd_and_scalar_paths_agree_closely():
+    """OpenCV's float (SIMD) and integer (tail) vertical cubic paths may differ
+    in the last bit only: a 1-channel 13-wide output has 8 SIMD + 5 tail bytes."""
+    img = rng.integers(0, 256, (40, 29), dtype=np.uint8)
+    a = R.resize(img, (13, 50), R.INTER_CUBIC).astype(int)
+    b = R.resize(img.T.copy(), (50, 13), R.INTER_CUBIC).T.astype(int)
+    assert np.abs(a - b).max() <= 1
+
+
+@pytest.mark.parametrize("dsize", [(224, 224), (53, 37), (300, 410), (131, 97)])
+def test_linear_exact_close_to_float_bilinear(dsize):
+    img = rng.integers(0, 256, (97, 131, 3), dtype=np.uint8)
+    ref = _ref_separable(img, dsize[0], dsize[1], lambda t: max(0.0, 1 - abs(t)), 2)
+    out = R.resize(img, dsize, R.INTER_LINEAR_EXACT).astype(np.float64)
+    # 8-bit weights (1/512 each way) plus the final rounding
+    assert np.abs(out - ref).max() <= 1.25
+
+
+def test_linear_exact_half_size_is_area():
+    img = rng.integers(0, 256, (64, 96, 3), dtype=np.uint8)
+    assert np.array_equal(R.resize(img, (48, 32), R.INTER_LINEAR_EXACT), R.resize(img, (48, 32), R.INTER_AREA))
+
+
+@pytest.mark.parametrize("src,dst", [(100, 50), (99, 33), (224, 224 * 3), (480, 224), (7, 300)])
+def test_nearest_exact_picks_pixel_centres(src, dst):
+    """resizeNN_bitexact: the source pixel under each destination pixel centre
+    (floor((d + 0.5) * src / dst)), within the 16-bit fixed point's reach."""
+    idx = R.nearest_exact_index(src, dst)
+    exact = np.minimum(np.floor((np.arange(dst) + 0.5) * src / dst).astype(int), src - 1)
+    assert np.abs(idx - exact).max() <= 1 and (idx == exact).mean() > 0.98
+
+
+@pytest.mark.parametrize("interp,K", [(R.INTER_CUBIC, 4), (R.INTER_LANCZOS4, 8)])
+@pytest.mark.parametrize("src,dst", [((135, 240), (224, 224)), ((4320, 7680), (331, 331)), ((7, 5), (299, 240)),
+                                     ((224, 224), (448, 112)), ((1, 1), (3, 2)), ((68, 120), (240, 240))])
+def test_engine_coefficient_tables_match_oracle(interp, K, src, dst):
+    """The C++ host tables the GPU kernel reads (wicca_resize_kernel_tables,
+    no device needed) equal the oracle's restatement of OpenCV's
+    interpolateCubic / interpolateLanczos4 entry for entry."""
+    import ctypes
+    from wicca_amd import _lib
+    lib = _lib.load()
+    (H, W), (dh, dw) = src, dst
+    need = ctypes.c_int64()
+    assert lib.wicca_resize_kernel_tables(H, W, dw, dh, interp, None, 0, ctypes.byref(need)) == 0
+    tab = (ctypes.c_int32 * need.value)()
+    assert lib.wicca_resize_kernel_tables(H, W, dw, dh, interp, tab, need.value, ctypes.byref(need)) == 0
+    t = np.frombuffer(tab, np.int32).astype(np.int64)
+    xo, xa = R.kernel_tables(W, dw, W / dw if False else 1.0 / (dw / W), K)
+    yo, yb = R.kernel_tables(H, dh, 1.0 / (dh / H), K)
+    ref = np.concatenate([xo, xa.ravel(), yo, yb.ravel()])
+    assert t.shape == ref.shape and np.array_equal(t, ref)

@@ -70,6 +70,8 @@ SIGNATURES = {
                                _int, _int, _p]),
     "wicca_resize_u8_uniform": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, _p, _i64, _i64,
                                        _i64, _i64, _int, _int, _p]),
+    "wicca_resize_kernel_tables": (_int, [_i64, _i64, _i64, _i64, _int, ctypes.POINTER(ctypes.c_int32), _i64,
+                                          ctypes.POINTER(_i64)]),
     "wicca_icon_stage_u8": (_int, [ctypes.POINTER(ImageDesc), _i64, _i64, _int, _int, _int, _i64,
                                    _i64, _int, _p, _p, _int]),
     "wicca_jpeg_info": (_int, [_p, _i64, _int, ctypes.POINTER(_i64), ctypes.POINTER(_i64),

@@ -112,6 +112,8 @@ struct Workspace {
     DevBuf jstream, jmeta, jcoef, jplanes, jscratch, jrgb, jtmp;
     DevBuf rscratch;  // two-pass INTER_AREA row sums (float)
     DevBuf smeta;     // fused caller stage: image descriptors + icon resize parameters
+    DevBuf rtab;      // INTER_CUBIC / INTER_LANCZOS4 coefficient tables
+    HostBuf rtab_pin; // their pinned host staging
     HostBuf spin;     // their pinned host staging
     HostBuf jhost;  // pinned host staging of the de-stuffed JPEG streams
     HostBuf jtab;   // pinned host staging of the decode tables
@@ -119,7 +121,7 @@ struct Workspace {
     {
         return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
                slot[0].cap + slot[1].cap + icon[0].cap + icon[1].cap + jstream.cap + jmeta.cap + jcoef.cap +
-               jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap + rscratch.cap + smeta.cap;
+               jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap + rscratch.cap + smeta.cap + rtab.cap;
     }
     hipError_t ensure_pipeline()
     {
@@ -154,6 +156,8 @@ struct Workspace {
         rscratch.release();
         smeta.release();
         spin.release();
+        rtab.release();
+        rtab_pin.release();
         jmeta.release();
         jcoef.release();
         jplanes.release();
@@ -241,6 +245,6 @@ int check_resize(int64_t H, int64_t W, int64_t C, int64_t out_w, int64_t out_h, 
                  wicca::ResizeParams* rp);
 int run_resize(wicca::ResizeParams rp, const uint8_t* src, int64_t src_pitch, int64_t src_stride,
                uint8_t* dst, int64_t dst_pitch, int64_t dst_stride, int64_t n, hipStream_t stream,
-               Workspace* ws);
+               Workspace* ws, bool scratch_ok = true);
 
 }  // namespace wicca_capi

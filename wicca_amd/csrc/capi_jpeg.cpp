@@ -392,7 +392,8 @@ int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, c
         q.dst = dico + i * out_bytes;
         q.dst_pitch = out_w * 3;
         q.dst_stride = 0;
-        any_copy = any_copy || q.mode == wicca::RS_COPY;
+        // copies and cubic / Lanczos-4 (host tables per image) take the per-image path
+        any_copy = any_copy || q.mode == wicca::RS_COPY || q.mode == wicca::RS_KERNEL;
     }
     // descriptors: [StageImageDev x n | ResizeParams x n], pinned, one upload
     // (the call synchronises before it returns, so the staging is free again)

@@ -20,6 +20,79 @@ using namespace wicca_capi;
 // ---------------------------------------------------------------------------
 // cv2.resize and the caller stage of _get_img_batch
 // ---------------------------------------------------------------------------
+namespace wicca {
+
+namespace {
+
+// interpolateCubic (resize.cpp), float in the source's order (the library is
+// built with -ffp-contract=off and x86-64 float math is SSE: no excess precision)
+void cubic_coeffs(float x, float* c)
+{
+    const float A = -0.75f;
+    c[0] = ((A * (x + 1) - 5 * A) * (x + 1) + 8 * A) * (x + 1) - 4 * A;
+    c[1] = ((A + 2) * x - (A + 3)) * x * x + 1;
+    c[2] = ((A + 2) * (1 - x) - (A + 3)) * (1 - x) * (1 - x) + 1;
+    c[3] = 1.f - c[0] - c[1] - c[2];
+}
+
+// interpolateLanczos4 (resize.cpp): glibc's double sin / cos, float sums, the
+// 1e30 tap where x + 3 - i is zero
+void lanczos4_coeffs(float x, float* c)
+{
+    static const double s45 = 0.70710678118654752440084436210485;
+    static const double cs[][2] = {{1, 0}, {-s45, -s45}, {0, 1}, {s45, -s45}, {-1, 0}, {s45, s45}, {0, -1}, {-s45, s45}};
+    const double pi = 3.1415926535897932384626433832795;
+    float sum = 0;
+    const double y0 = -(x + 3) * pi * 0.25, s0 = std::sin(y0), c0 = std::cos(y0);
+    for (int i = 0; i < 8; ++i) {
+        const float yi = (x + 3 - i);
+        if (std::fabs(yi) >= 1e-6f) {
+            const double y = -yi * pi * 0.25;
+            c[i] = (float)((cs[i][0] * s0 + cs[i][1] * c0) / (y * y));
+        } else {
+            c[i] = 1e30f;
+        }
+        sum += c[i];
+    }
+    sum = 1.f / sum;
+    for (int i = 0; i < 8; ++i) c[i] *= sum;
+}
+
+int16_t short_coef(float c)  // saturate_cast<short>(c * INTER_RESIZE_COEF_SCALE)
+{
+    const float v = c * 2048;
+    const long r = std::lrint(v);
+    return (int16_t)std::min<long>(32767, std::max<long>(-32768, r));
+}
+
+void axis_tables(int dsize, double scale, int K, int32_t* ofs, int32_t* co)
+{
+    float cb[8];
+    for (int d = 0; d < dsize; ++d) {
+        float f = (float)((d + 0.5) * scale - 0.5);
+        const int s = (int)std::floor(f);
+        f -= (float)s;
+        if (K == 4) cubic_coeffs(f, cb);
+        else lanczos4_coeffs(f, cb);
+        ofs[d] = s;
+        for (int k = 0; k < K; ++k) co[(int64_t)d * K + k] = short_coef(cb[k]);
+    }
+}
+
+}  // namespace
+
+void resize_kernel_tables(const ResizeParams& p, std::vector<int32_t>& tab)
+{
+    const int K = p.ksize;
+    tab.assign((size_t)(p.dw + (int64_t)p.dw * K + p.dh + (int64_t)p.dh * K), 0);
+    int32_t* x = tab.data();
+    axis_tables(p.dw, p.scale_x, K, x, x + p.dw);
+    int32_t* y = x + p.dw + (int64_t)p.dw * K;
+    axis_tables(p.dh, p.scale_y, K, y, y + p.dh);
+}
+
+}  // namespace wicca
+
 namespace wicca_capi {
 
 int check_resize(int64_t H, int64_t W, int64_t C, int64_t out_w, int64_t out_h, int interpolation,
@@ -32,15 +105,15 @@ int check_resize(int64_t H, int64_t W, int64_t C, int64_t out_w, int64_t out_h, 
     if (H >= ((int64_t)1 << 31) || W * C >= ((int64_t)1 << 31))
         return fail(WICCA_ERR_ARG, "image too large to resize");
     if (!wicca::plan_resize((int)H, (int)W, (int)out_h, (int)out_w, (int)C, interpolation, rp))
-        return fail(WICCA_ERR_ARG, "interpolation %d is not implemented (INTER_NEAREST, "
-                    "INTER_LINEAR and INTER_AREA are)", interpolation);
+        return fail(WICCA_ERR_ARG, "interpolation %d is not implemented (cv2.INTER_NEAREST .. "
+                    "INTER_NEAREST_EXACT, 0-6, are)", interpolation);
     return WICCA_OK;
 }
 
 // Device-resident resize of n images (uniform shape) on `stream`.
 int run_resize(wicca::ResizeParams rp, const uint8_t* src, int64_t src_pitch, int64_t src_stride,
                uint8_t* dst, int64_t dst_pitch, int64_t dst_stride, int64_t n, hipStream_t stream,
-               Workspace* ws)
+               Workspace* ws, bool scratch_ok)
 {
     if (rp.mode == wicca::RS_COPY) {
         for (int64_t i = 0; i < n; ++i)
@@ -54,6 +127,28 @@ int run_resize(wicca::ResizeParams rp, const uint8_t* src, int64_t src_pitch, in
     rp.dst = dst;
     rp.dst_pitch = dst_pitch;
     rp.dst_stride = dst_stride;
+    if (rp.mode == wicca::RS_KERNEL) {
+        // cubic / Lanczos-4 coefficient tables, built on the host as OpenCV
+        // builds them (glibc sin / cos), uploaded through the workspace; the
+        // stream is synchronised before return so the pinned staging is free
+        if (!ws) return fail(WICCA_ERR_ARG, "internal: INTER_CUBIC / INTER_LANCZOS4 need a workspace");
+        std::vector<int32_t> tab;
+        wicca::resize_kernel_tables(rp, tab);
+        const size_t tb = tab.size() * sizeof(int32_t);
+        HIP_TRY(ws->rtab_pin.reserve(tb, 64 << 10));
+        HIP_TRY(ws->rtab.reserve(tb));
+        memcpy(ws->rtab_pin.ptr, tab.data(), tb);
+        HIP_TRY(hipMemcpyAsync(ws->rtab.ptr, ws->rtab_pin.ptr, tb, hipMemcpyHostToDevice, stream));
+        rp.tab = (const int32_t*)ws->rtab.ptr;
+        for (int64_t i0 = 0; i0 < n; i0 += 65535) {
+            wicca::ResizeParams q = rp;
+            q.src = src + i0 * src_stride;
+            q.dst = dst + i0 * dst_stride;
+            HIP_TRY(wicca::launch_resize(q, std::min<int64_t>(65535, n - i0), stream));
+        }
+        HIP_TRY(hipStreamSynchronize(stream));
+        return WICCA_OK;
+    }
     // the two-pass INTER_AREA path: at most ~256 MiB of row sums per launch
     // (an 8K RGB source to 224 x 224: 11.6 MB per image); without scratch the
     // one-pass kernel runs
@@ -62,7 +157,7 @@ int run_resize(wicca::ResizeParams rp, const uint8_t* src, int64_t src_pitch, in
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
     constexpr size_t kScratchCap = (size_t)256 << 20;
-    if (per_image > 0 && per_image <= kScratchCap && ws) {
+    if (per_image > 0 && per_image <= kScratchCap && ws && scratch_ok) {
         step = std::min<int64_t>(step, (int64_t)(kScratchCap / per_image));
         const size_t want = per_image * (size_t)std::min<int64_t>(step, n);
         if (ws->rscratch.reserve(want) == hipSuccess) {
@@ -85,6 +180,20 @@ int run_resize(wicca::ResizeParams rp, const uint8_t* src, int64_t src_pitch, in
 }  // namespace wicca_capi
 
 extern "C" {
+
+int wicca_resize_kernel_tables(int64_t H, int64_t W, int64_t out_w, int64_t out_h, int interpolation, int32_t* tab,
+                               int64_t cap, int64_t* needed)
+{
+    wicca::ResizeParams rp{};
+    int rc = check_resize(H, W, 1, out_w, out_h, interpolation, &rp);
+    if (rc) return rc;
+    if (rp.mode != wicca::RS_KERNEL) return fail(WICCA_ERR_ARG, "interpolation %d has no coefficient tables", interpolation);
+    std::vector<int32_t> t;
+    wicca::resize_kernel_tables(rp, t);
+    if (needed) *needed = (int64_t)t.size();
+    if (tab && cap > 0) memcpy(tab, t.data(), sizeof(int32_t) * (size_t)std::min<int64_t>(cap, (int64_t)t.size()));
+    return WICCA_OK;
+}
 
 int wicca_resize_u8(const uint8_t* src, int64_t H, int64_t W, int64_t C, int64_t src_pitch,
                     uint8_t* dst, int64_t out_w, int64_t out_h, int64_t dst_pitch, int interpolation,
@@ -148,9 +257,10 @@ int wicca_resize_u8_uniform(const uint8_t* src, int64_t n, int64_t H, int64_t W,
     if ((rc = acquire(dev, lease))) return rc;
     hipStream_t stream = stream_in ? (hipStream_t)stream_in : lease.ws->stream;
     // on a caller's stream the call returns before the kernels finish: no
-    // workspace scratch then (one-pass INTER_AREA kernel)
+    // workspace scratch then (one-pass INTER_AREA kernel); cubic / Lanczos-4
+    // tables synchronise the stream themselves
     if ((rc = run_resize(rp, src, src_pitch, src_image_stride, dst, dst_pitch, dst_image_stride, n,
-                         stream, stream_in ? nullptr : lease.ws)))
+                         stream, lease.ws, !stream_in)))
         return rc;
     if (!stream_in) HIP_TRY(hipStreamSynchronize(stream));
     return WICCA_OK;

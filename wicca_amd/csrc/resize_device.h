@@ -126,6 +126,64 @@ __device__ __forceinline__ uint8_t resize_byte(const ResizeParams& p, const uint
         if (ty.has_b) row_term(ty.s2, ty.wb);
         return sat_u8(round_f32(sum));
     }
+    case RS_NEAREST_EXACT: {  // resizeNN_bitexact
+        const int sx = min(max((p.nfx * dx + p.nfx0) >> 16, 0), p.W - 1);
+        const int sy = min(max((p.nfy * dy + p.nfy0) >> 16, 0), p.H - 1);
+        return img[(int64_t)sy * p.src_pitch + (int64_t)sx * C + c];
+    }
+    case RS_LINEAR_EXACT: {  // resize_bitExact<uchar, interpolationLinear>: 8.8 fixed point
+        auto hres = [&](int r) -> uint32_t {  // ufixedpoint16 of the horizontal pass
+            const uint8_t* row = img + (int64_t)r * p.src_pitch + c;
+            if (dx < p.min_x) return (uint32_t)row[0] << 8;
+            if (dx >= p.max_x) return (uint32_t)row[(int64_t)(p.W - 1) * C] << 8;
+            const double f = p.scale_x * ((double)dx + 0.5) - 0.5;
+            const int i = (int)floor(f);
+            const uint32_t c1 = (uint32_t)rint((f - (double)i) * 256.0), c0 = 256u - c1;
+            return c0 * row[(int64_t)i * C] + c1 * row[(int64_t)(i + 1) * C];
+        };
+        if (dy < p.min_y) return (uint8_t)min(255u, (hres(0) + 128u) >> 8);
+        if (dy >= p.max_y) return (uint8_t)min(255u, (hres(p.H - 1) + 128u) >> 8);
+        const double f = p.scale_y * ((double)dy + 0.5) - 0.5;
+        const int i = (int)floor(f);
+        const uint32_t c1 = (uint32_t)rint((f - (double)i) * 256.0), c0 = 256u - c1;
+        return (uint8_t)min(255u, (hres(i) * c0 + hres(i + 1) * c1 + 32768u) >> 16);
+    }
+    case RS_KERNEL: {  // resizeGeneric_: HResizeCubic/Lanczos4 + VResizeCubic/Lanczos4 (uchar)
+        const int K = p.ksize, half = K / 2 - 1;
+        const int32_t* xofs = p.tab;
+        const int32_t* alpha = xofs + p.dw + (int64_t)dx * K;
+        const int32_t* yofs = xofs + p.dw + (int64_t)p.dw * K;
+        const int32_t* beta = yofs + p.dh + (int64_t)dy * K;
+        const int sx = xofs[dx], sy = yofs[dy];
+        int h[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k >= K) break;
+            const uint8_t* row = img + (int64_t)min(max(sy - half + k, 0), p.H - 1) * p.src_pitch + c;
+            int v = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                if (j >= K) break;
+                v += alpha[j] * (int)row[(int64_t)min(max(sx - half + j, 0), p.W - 1) * C];
+            }
+            h[k] = v;
+        }
+        if (e < p.vec_end) {  // VResizeCubicVec_32s8u: float32, S0*b0 + (S1*b1 + (S2*b2 + S3*b3))
+            const float sc = 1.f / (2048.f * 2048.f);
+            float t = (float)h[3] * ((float)beta[3] * sc);
+            t = (float)h[2] * ((float)beta[2] * sc) + t;
+            t = (float)h[1] * ((float)beta[1] * sc) + t;
+            t = (float)h[0] * ((float)beta[0] * sc) + t;
+            return sat_u8((int)rintf(t));
+        }
+        int sum = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (k >= K) break;
+            sum += h[k] * beta[k];
+        }
+        return sat_u8((sum + (1 << 21)) >> 22);
+    }
     default: {  // RS_LINEAR
         const LinCoef cx = lin_coef(dx, p.W, p.scale_x, p.inv_x, p.area_rule, true);
         const LinCoef cy = lin_coef(dy, p.H, p.scale_y, p.inv_y, p.area_rule, false);

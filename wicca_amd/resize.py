@@ -6,8 +6,10 @@ classifier's input shape (``/root/reference/wicca/classifying_tools.py:315,
 the same arguments as ``cv2.resize(src, dsize, interpolation=...)`` — ``dsize``
 is ``(width, height)`` — for uint8 (H, W) / (H, W, C <= 4) arrays and computes
 on the GPU (``wicca_resize_u8``, ``wicca_amd/csrc/resize.hip``).  The
-arithmetic restates OpenCV's resize.cpp (INTER_NEAREST, INTER_LINEAR,
-INTER_AREA); parity against an OpenCV binary is unpinned (cv2 is absent here,
+arithmetic restates OpenCV's resize.cpp (every interpolation
+``ClassifierProcessor`` accepts, ``classifying_tools.py:168-176``:
+INTER_NEAREST, INTER_LINEAR, INTER_CUBIC, INTER_AREA, INTER_LANCZOS4,
+INTER_LINEAR_EXACT, INTER_NEAREST_EXACT); parity against an OpenCV binary is unpinned (cv2 is absent here,
 see ``oracle/resize_cv.py``).  Like OpenCV's binding, single-channel results
 are 2-D.
 """
@@ -19,7 +21,11 @@ from . import _lib
 
 INTER_NEAREST = 0
 INTER_LINEAR = 1
+INTER_CUBIC = 2
 INTER_AREA = 3
+INTER_LANCZOS4 = 4
+INTER_LINEAR_EXACT = 5
+INTER_NEAREST_EXACT = 6
 
 
 def _hwc(image: np.ndarray) -> np.ndarray:
