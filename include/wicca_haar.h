@@ -260,8 +260,11 @@ int wicca_icon_stage_u8(const wicca_image_desc* images, int64_t n, int64_t C, in
  * restart markers allowed): libjpeg-turbo's default arithmetic (ISLOW IDCT,
  * fancy upsampling, integer YCbCr->RGB) restated on the device, output RGB
  * HWC uint8 (grayscale replicated to 3 channels, as IMREAD_COLOR does).
- * Progressive / arithmetic / 12-bit / CMYK files return WICCA_ERR_UNSUPPORTED,
- * corrupt ones WICCA_ERR_DECODE.
+ * Progressive (SOF2) and multi-scan sequential files are entropy-decoded on
+ * host threads (AC refinement scans depend on every earlier scan's result per
+ * block, which defeats the device's self-synchronising decode) and share the
+ * device back end.  Lossless / hierarchical / arithmetic / 12-bit / CMYK files
+ * return WICCA_ERR_UNSUPPORTED, corrupt ones WICCA_ERR_DECODE.
  */
 
 /* Dimensions of a JPEG file (after EXIF orientation when apply_orientation;
@@ -282,6 +285,16 @@ int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64
 
 /* Synchronisation passes of the calling thread's last JPEG decode (diagnostic). */
 int wicca_jpeg_last_sync_rounds(void);
+
+/* The quantised DCT coefficients of a JPEG file as the host entropy decoder
+ * produces them for multi-scan files (progressive SOF2, or sequential with a
+ * scan per component; jdhuff.c / jdphuff.c semantics): components back to
+ * back, each bw x bh blocks (whole MCUs) of 64 int16 in natural order.
+ * force_host also runs a single-scan sequential file through it (otherwise
+ * those decode on the device).  *blocks receives the block count; out may be
+ * NULL to query it.  No device is used (diagnostic / parity tests). */
+int wicca_jpeg_host_coefficients(const uint8_t* data, int64_t size, int force_host, int16_t* out,
+                                 int64_t cap_blocks, int64_t* blocks);
 
 /*
  * ClassifierProcessor._get_img_batch (wicca/classifying_tools.py:297-323) from

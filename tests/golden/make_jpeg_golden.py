@@ -27,15 +27,23 @@ CASES = [
     ("scene_420_orient3", "scene", 50, 66, 75, 2, 0, 0, False, 3),
     ("tiny_3x5", "scene", 3, 5, 90, 2, 0, 0, False, 1),
 ]
+# progressive (SOF2: libjpeg's default progression, DC and AC first and
+# refinement scans) - decoded by the host entropy decoder + device back end
+PROGRESSIVE = [
+    ("prog_scene_420_q80", "scene", 90, 122, 80, 2, 0, 0, False, 1),
+    ("prog_scene_444_rst2", "scene", 57, 75, 90, 0, 2, 0, False, 1),
+    ("prog_gray_q70", "gray", 41, 66, 70, 0, 0, 0, False, 1),
+    ("prog_smooth_422_orient8", "smooth", 64, 40, 85, 1, 0, 0, True, 8),
+]
 
 
 def main():
     out = os.path.join(HERE, "jpeg")
     os.makedirs(out, exist_ok=True)
     meta = {"libjpeg_turbo": J.libjpeg_version(), "cases": []}
-    for i, (name, kind, H, W, q, sub, rb, rr, opt, orient) in enumerate(CASES):
+    for i, (name, kind, H, W, q, sub, rb, rr, opt, orient) in enumerate(CASES + PROGRESSIVE):
         img = J.test_image(kind, H, W, 1000 + i)
-        data = J.encode(img, q, sub, rb, rr, opt, orientation=orient)
+        data = J.encode(img, q, sub, rb, rr, opt, orientation=orient, progressive=i >= len(CASES))
         with open(os.path.join(out, name + ".jpg"), "wb") as f:
             f.write(data)
         rgb = J.decode_rgb(data)
@@ -44,7 +52,7 @@ def main():
                               "sha256_rgb": hashlib.sha256(rgb.tobytes()).hexdigest()})
     with open(os.path.join(out, "cases.json"), "w") as f:
         json.dump(meta, f, indent=1)
-    print(f"{len(CASES)} cases, libjpeg-turbo {meta['libjpeg_turbo']}")
+    print(f"{len(CASES) + len(PROGRESSIVE)} cases, libjpeg-turbo {meta['libjpeg_turbo']}")
 
 
 if __name__ == "__main__":

@@ -4,12 +4,13 @@
 //
 // Seeds: the JPEG files named on the command line (tests/golden/jpeg/*.jpg).
 // Each iteration picks one marker segment of a seed — SOF, DHT, DQT, DRI, SOS
-// or APP1 — and mutates it: flipped / random bytes inside the segment, a new
+// or APP1, the later scans' segments of progressive seeds included — and mutates it: flipped / random bytes inside the segment, a new
 // length field, Huffman counts pushed past the code space, a truncation inside
 // the segment, or a duplicated / dropped segment.  The mutant goes through
 // jpeg_parse and, when accepted, through what the decode call runs on the host
 // for it: de-stuffing into a buffer of exactly scan_len bytes and the device
-// Huffman tables of every table a component uses.  Any out-of-bounds access
+// Huffman tables of every table a component uses, or (multi-scan and
+// progressive files) the host entropy decoder into an exact-size buffer.  Any out-of-bounds access
 // or undefined behaviour aborts the run under the sanitizers.
 #include "../../wicca_amd/csrc/jpeg_host.cpp"
 
@@ -47,9 +48,24 @@ bool wanted(int m)
     return m == 0xC0 || m == 0xC1 || m == 0xC2 || m == 0xC4 || m == 0xDB || m == 0xDD || m == 0xDA || m == 0xE1;
 }
 
+// every marker segment of a file, the later scans of a progressive one included
+std::vector<Seg> all_segments(const std::vector<uint8_t>& f)
+{
+    std::vector<Seg> out;
+    for (size_t p = 2; p + 4 <= f.size(); ++p) {
+        if (f[p] != 0xFF) continue;
+        const int m = f[p + 1];
+        if (m == 0x00 || m == 0xFF || (m >= 0xD0 && m <= 0xD9)) continue;
+        const size_t l = ((size_t)f[p + 2] << 8) | f[p + 3];
+        if (l < 2 || p + 2 + l > f.size()) continue;
+        out.push_back({p, 2 + l, m});
+    }
+    return out;
+}
+
 std::vector<uint8_t> mutate(const std::vector<uint8_t>& f, std::mt19937& rng)
 {
-    std::vector<Seg> segs = segments(f);
+    std::vector<Seg> segs = rng() % 2 ? segments(f) : all_segments(f);
     std::vector<Seg> pick;
     for (const Seg& s : segs)
         if (wanted(s.marker)) pick.push_back(s);
@@ -130,6 +146,18 @@ int main(int argc, char** argv)
         if (got > info.scan_len || seg_off.back() != (int64_t)got) {
             fprintf(stderr, "de-stuffed length %zu beyond the scan (%zu)\n", got, info.scan_len);
             return 1;
+        }
+        if (info.host_scans) {  // multi-scan / progressive: the host entropy decoder, exact-size buffer
+            int64_t rel[wicca::kJpegMaxComp] = {0, 0, 0}, blocks = 0;
+            for (int c = 0; c < info.ncomp; ++c) {
+                rel[c] = blocks;
+                blocks += (int64_t)info.comp[c].bw * info.comp[c].bh;
+            }
+            if (blocks <= ((int64_t)1 << 22)) {
+                std::unique_ptr<int16_t[]> coef(new int16_t[(size_t)blocks * 64]());
+                wicca::jpeg_host_decode(info, coef.get(), rel);
+            }
+            continue;
         }
         for (int c = 0; c < info.ncomp; ++c) {
             wicca::build_huff_dev(info.dc[info.comp[c].td], &hd[0]);

@@ -80,10 +80,52 @@ def test_batch_decode_mixed():
         assert np.array_equal(g, J.decode_rgb(b))
 
 
-def test_progressive_is_unsupported():
-    data = J.encode(J.test_image("scene", 40, 40, 1), progressive=True)
-    with pytest.raises(NotImplementedError, match="progressive"):
-        WJ.decode(data)
+PROG = [(k, h, w, s, q, rb) for k, (h, w) in (("scene", (333, 517)), ("smooth", (64, 80)), ("gray", (97, 55)))
+        for s in (0, 1, 2) for q, rb in ((50, 0), (90, 0), (85, 4))]
+PROG += [("scene", 1080, 1920, 2, 90, 0), ("noise", 200, 300, 2, 60, 1), ("scene", 4320, 7680, 2, 85, 0)]
+
+
+@pytest.mark.parametrize("kind,H,W,sub,q,rb", PROG, ids=[f"{k}-{h}x{w}-s{s}-q{q}-r{r}" for k, h, w, s, q, r in PROG])
+def test_progressive_matches_libjpeg(kind, H, W, sub, q, rb):
+    """Progressive JPEG (SOF2, libjpeg's default progression: DC / AC first
+    and refinement scans): host entropy decode + the device back end, bit for
+    bit against libjpeg-turbo."""
+    img = J.test_image(kind, H, W, H * 3 + W + sub)
+    data = J.encode(img, q, sub, rb, progressive=True)
+    assert np.array_equal(WJ.decode(data), J.decode_rgb(data))
+
+
+def test_mixed_progressive_and_baseline_batch(tmp_path):
+    """One decode call over baseline (device Huffman decode) and progressive
+    (host entropy decode) files, and the file-based caller stage over them."""
+    blobs = []
+    for i, (h, w, prog) in enumerate([(240, 320, True), (333, 517, False), (100, 90, True), (77, 61, False),
+                                      (480, 640, True)]):
+        blobs.append(J.encode(J.test_image("scene", h, w, 70 + i), 85, 2, progressive=prog))
+    got = WJ.decode_batch(blobs)
+    for b, g in zip(blobs, got):
+        assert np.array_equal(g, J.decode_rgb(b))
+    only_prog = WJ.decode_batch([blobs[0], blobs[2]])
+    assert np.array_equal(only_prog[0], got[0]) and np.array_equal(only_prog[1], got[2])
+    paths = []
+    for i, b in enumerate(blobs):
+        p = tmp_path / f"m{i}.jpg"
+        p.write_bytes(b)
+        paths.append(str(p))
+    imgs, icons = wicca_amd.get_img_batch(paths, (224, 224), 3)
+    for i, b in enumerate(blobs):
+        rgb = J.decode_rgb(b)
+        assert np.array_equal(imgs[i], R.resize(rgb, (224, 224), R.INTER_AREA))
+        assert np.array_equal(icons[i], R.resize(c_oracle.ll_int_block(rgb, 3)[0], (224, 224), R.INTER_AREA))
+
+
+def test_truncated_progressive_decodes_without_fault():
+    """A progressive file cut inside a scan: the scans before the cut stand,
+    the rest reads as missing data (no fault, the right shape)."""
+    data = J.encode(J.test_image("scene", 256, 384, 21), 90, 2, progressive=True)
+    for cut in (0.3, 0.6, 0.9):
+        got = WJ.decode(data[:int(len(data) * cut)])
+        assert got.shape == (256, 384, 3)
 
 
 def test_load_image_contract(tmp_path, capsys):
@@ -265,13 +307,14 @@ def test_fused_backend_equals_separate_launches():
 
 
 def test_batch_with_unreadable_files_fails_per_slot(tmp_path, capsys):
-    """One file the decoder cannot read (PNG bytes, a progressive JPEG, a
-    header cut short) fails its own slot only: errors="zero" / "none" give
+    """One file the decoder cannot read (PNG bytes, an arithmetic-coded JPEG,
+    a header cut short) fails its own slot only: errors="zero" / "none" give
     the other files' exact results; errors="raise" (the default) raises."""
     good = [J.encode(J.test_image("scene", h, w, 60 + i), 85, 2) for i, (h, w) in
             enumerate([(240, 320), (333, 517), (100, 90)])]
+    sof = good[1].index(b"\xff\xc0")
     bad = [b"\x89PNG\r\n\x1a\n" + b"\x00" * 64,
-           J.encode(J.test_image("scene", 64, 64, 3), 80, 2, progressive=True),
+           good[1][:sof + 1] + b"\xc9" + good[1][sof + 2:],  # arithmetic-coded: unsupported
            good[0][:30]]
     blobs = [good[0], bad[0], good[1], bad[1], bad[2], good[2]]
     outs = WJ.decode_batch(blobs, errors="none")

@@ -117,6 +117,7 @@ struct Workspace {
     HostBuf spin;     // their pinned host staging
     HostBuf jhost;  // pinned host staging of the de-stuffed JPEG streams
     HostBuf jtab;   // pinned host staging of the decode tables
+    HostBuf jhcoef; // pinned coefficients of host-decoded (multi-scan / progressive) JPEG files
     size_t bytes() const
     {
         return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
@@ -166,6 +167,7 @@ struct Workspace {
         jtmp.release();
         jhost.release();
         jtab.release();
+        jhcoef.release();
     }
     void destroy()
     {

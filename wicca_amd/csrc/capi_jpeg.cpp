@@ -126,6 +126,25 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         int rc = parse_one(data[i], sizes[i], &info[(size_t)i], i);
         if (rc) return rc;
     }
+    // coefficient layout: image i's components back to back from coef0[i]
+    // blocks (component c: bw x bh blocks); multi-scan files (progressive,
+    // scan per component) are entropy-decoded on the host into a pinned copy
+    // of their region (hoff) and uploaded, the others on the device
+    std::vector<int64_t> coef0((size_t)n + 1, 0), hoff((size_t)n, -1);
+    int64_t host_blocks = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const wicca::JpegInfo& f = info[(size_t)i];
+        int64_t b = 0;
+        for (int c = 0; c < f.ncomp; ++c) b += (int64_t)f.comp[c].bw * f.comp[c].bh;
+        coef0[(size_t)i + 1] = coef0[(size_t)i] + b;
+        if (f.host_scans) {
+            hoff[(size_t)i] = host_blocks;
+            host_blocks += b;
+        }
+    }
+    HIP_TRY(ws->jcoef.reserve((size_t)coef0[(size_t)n] * 128));
+    if (host_blocks && ws->jhcoef.reserve((size_t)host_blocks * 128, 16 << 20) != hipSuccess)
+        return fail(WICCA_ERR_NOMEM, "pinned staging of %lld coefficient blocks", (long long)host_blocks);
     // de-stuff every image's scan in parallel into its own region of one buffer
     std::vector<int64_t> img_off((size_t)n + 1, 0);
     for (int64_t i = 0; i < n; ++i)
@@ -154,6 +173,20 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         auto work = [&] {
             for (int64_t i; (i = next.fetch_add(1)) < n;)
             {
+                if (info[(size_t)i].host_scans) {
+                    const wicca::JpegInfo& f = info[(size_t)i];
+                    int16_t* hc = (int16_t*)ws->jhcoef.ptr + hoff[(size_t)i] * 64;
+                    const int64_t blocks = coef0[(size_t)i + 1] - coef0[(size_t)i];
+                    memset(hc, 0, (size_t)blocks * 128);
+                    int64_t rel[wicca::kJpegMaxComp] = {0, 0, 0};
+                    for (int c = 1; c < f.ncomp; ++c) rel[c] = rel[c - 1] + (int64_t)f.comp[c - 1].bw * f.comp[c - 1].bh;
+                    wicca::jpeg_host_decode(f, hc, rel);
+                    seg_off[(size_t)i].assign(1, 0);
+                    if (hipMemcpyAsync((int16_t*)ws->jcoef.ptr + coef0[(size_t)i] * 64, hc, (size_t)blocks * 128,
+                                       hipMemcpyHostToDevice, stream) != hipSuccess)
+                        upload_err = 1;
+                    continue;
+                }
                 const size_t got = wicca::jpeg_destuff_into(info[(size_t)i], stream_h + img_off[(size_t)i],
                                                             seg_off[(size_t)i]);
                 memset(stream_h + img_off[(size_t)i] + got, 0, info[(size_t)i].scan_len - got);
@@ -204,20 +237,24 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
             im.comp_bh[c] = k.bh;
             im.comp_dw[c] = k.dw;
             im.comp_dh[c] = k.dh;
-            if (tab_dc[k.td] < 0) {
-                tab_dc[k.td] = (int)huff.size();
-                huff.emplace_back();
-                wicca::build_huff_dev(f.dc[k.td], &huff.back());
+            if (f.host_scans) {  // no device Huffman decode: no tables
+                im.dc_tab[c] = im.ac_tab[c] = 0;
+            } else {
+                if (tab_dc[k.td] < 0) {
+                    tab_dc[k.td] = (int)huff.size();
+                    huff.emplace_back();
+                    wicca::build_huff_dev(f.dc[k.td], &huff.back());
+                }
+                if (tab_ac[k.ta] < 0) {
+                    tab_ac[k.ta] = (int)huff.size();
+                    huff.emplace_back();
+                    wicca::build_huff_dev(f.ac[k.ta], &huff.back());
+                }
+                im.dc_tab[c] = tab_dc[k.td];
+                im.ac_tab[c] = tab_ac[k.ta];
             }
-            if (tab_ac[k.ta] < 0) {
-                tab_ac[k.ta] = (int)huff.size();
-                huff.emplace_back();
-                wicca::build_huff_dev(f.ac[k.ta], &huff.back());
-            }
-            im.dc_tab[c] = tab_dc[k.td];
-            im.ac_tab[c] = tab_ac[k.ta];
             im.comp_block0[c] = coef_blocks;
-            coef_blocks += (int64_t)k.bw * k.bh;
+            coef_blocks += (int64_t)k.bw * k.bh;  // == coef0[i] + the earlier components
             if (c > 0 || !wicca::jpeg_fused()) {  // the fused back end keeps luma in LDS
                 im.comp_plane0[c] = plane_bytes;
                 plane_bytes += round_up((int64_t)k.bw * 8 * k.bh * 8, 256);
@@ -232,6 +269,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
             im.dst = dst[i];
             im.dst_pitch = dpitch[i];
         }
+        if (f.host_scans) continue;  // coefficients come from the host decode
         // restart segments and their subsequences; the image's subsequences
         // are padded to whole workgroups (padding lanes: segment -1)
         const std::vector<int64_t>& off = seg_off[(size_t)i];
@@ -267,7 +305,6 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     const size_t o_huf = o_img + (size_t)round_up((int64_t)(ims.size() * sizeof(wicca::JpegImageDev)), 256);
     const size_t meta_bytes = o_huf + huff.size() * sizeof(wicca::HuffDev);
     HIP_TRY(ws->jmeta.reserve(meta_bytes));
-    HIP_TRY(ws->jcoef.reserve((size_t)coef_blocks * 128));
     HIP_TRY(ws->jplanes.reserve((size_t)std::max<int64_t>(plane_bytes, 256)));
     HIP_TRY(ws->jscratch.reserve(wicca::jpeg_scratch_bytes((int64_t)sub_seg.size(), (int64_t)segs.size())));
     if (tmp_bytes) HIP_TRY(ws->jtmp.reserve((size_t)tmp_bytes));
@@ -299,7 +336,9 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     P.sub_bits = (int32_t)S;
     // an image's tables are consecutive in `huff`: its count is max - min + 1
     P.max_tabs = 1;
-    for (const auto& im : ims) {
+    for (int64_t i = 0; i < n; ++i) {
+        if (info[(size_t)i].host_scans) continue;
+        const wicca::JpegImageDev& im = ims[(size_t)i];
         int lo = INT32_MAX, hi = -1;
         for (int c = 0; c < im.ncomp; ++c) {
             lo = std::min({lo, im.dc_tab[c], im.ac_tab[c]});
@@ -522,6 +561,44 @@ int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64
 }
 
 int wicca_jpeg_last_sync_rounds(void) { return t_jpeg_rounds; }
+
+int wicca_jpeg_host_coefficients(const uint8_t* data, int64_t size, int force_host, int16_t* out, int64_t cap_blocks,
+                                 int64_t* blocks)
+{
+    wicca::JpegInfo f;
+    int rc = parse_one(data, size, &f, 0);
+    if (rc) return rc;
+    int64_t b = 0;
+    for (int c = 0; c < f.ncomp; ++c) b += (int64_t)f.comp[c].bw * f.comp[c].bh;
+    if (blocks) *blocks = b;
+    if (!out) return WICCA_OK;
+    if (cap_blocks < b) return fail(WICCA_ERR_ARG, "coefficient buffer holds %lld of %lld blocks", (long long)cap_blocks,
+                                    (long long)b);
+    if (!f.host_scans) {
+        if (!force_host) return fail(WICCA_ERR_ARG, "a single-scan sequential file is decoded on the device");
+        // the file's one interleaved scan as a host scan
+        wicca::JpegScan sc;
+        sc.ns = f.ncomp;
+        // the scan's component order is the order of the MCU slots
+        int order = 0;
+        for (int k = 0; k < f.bpm && order < f.ncomp; ++k)
+            if (k == 0 || f.slot_comp[k] != f.slot_comp[k - 1]) sc.comp[order++] = f.slot_comp[k];
+        for (int i = 0; i < sc.ns; ++i) {
+            sc.dc[i] = f.dc[f.comp[sc.comp[i]].td];
+            sc.ac[i] = f.ac[f.comp[sc.comp[i]].ta];
+        }
+        sc.restart_interval = f.restart_interval;
+        sc.data = f.scan;
+        sc.len = wicca::scan_data_end(f.scan, f.scan_len, 0);
+        f.scans.push_back(sc);
+        f.host_scans = true;
+    }
+    memset(out, 0, (size_t)b * 128);
+    int64_t rel[wicca::kJpegMaxComp] = {0, 0, 0};
+    for (int c = 1; c < f.ncomp; ++c) rel[c] = rel[c - 1] + (int64_t)f.comp[c - 1].bw * f.comp[c - 1].bh;
+    wicca::jpeg_host_decode(f, out, rel);
+    return WICCA_OK;
+}
 
 int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
                              int border_type, int border_constant, int64_t out_w, int64_t out_h,

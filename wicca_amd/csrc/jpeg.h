@@ -36,8 +36,23 @@ struct JpegComponent {
     int dw, dh;          // downsampled (real) sample width / height
 };
 
+// One scan of a multi-scan file (progressive, or sequential with a scan per
+// component): decoded on the host (jpeg_host_decode).
+struct JpegScan {
+    int ns = 0;
+    int comp[kJpegMaxComp];            // SOF component index of each scan component
+    int Ss = 0, Se = 63, Ah = 0, Al = 0;
+    int restart_interval = 0;          // DRI in effect when the scan starts
+    JpegHuffTable dc[kJpegMaxComp], ac[kJpegMaxComp];  // the tables in effect, per scan component
+    const uint8_t* data = nullptr;     // entropy-coded data (stuffed, with RST markers)
+    size_t len = 0;                    // up to the marker that ends the scan
+};
+
 struct JpegInfo {
     int W = 0, H = 0, ncomp = 0;
+    bool progressive = false;           // SOF2
+    bool host_scans = false;            // multi-scan file: entropy decode on the host (scans below)
+    std::vector<JpegScan> scans;
     JpegComponent comp[kJpegMaxComp];
     int hmax = 1, vmax = 1, mcux = 0, mcuy = 0, bpm = 0;
     int slot_comp[kJpegMaxSlots], slot_h[kJpegMaxSlots], slot_v[kJpegMaxSlots];
@@ -52,10 +67,24 @@ struct JpegInfo {
     int64_t total_blocks() const { return (int64_t)mcux * mcuy * bpm; }
 };
 
-// Parse up to the first SOS.  Returns 0 or a negative code with *err set:
-// -1 not a JPEG / truncated, -2 unsupported (progressive, arithmetic coding,
-// 12-bit, CMYK, non-interleaved multi-scan, unusual sampling).
+// Parse the file.  A single-scan sequential file stops at its SOS (the GPU
+// Huffman path takes scan / scan_len); a progressive (SOF2) or multi-scan
+// sequential file is parsed to its end and its scans listed (host_scans).
+// Returns 0 or a negative code with *err set: -1 not a JPEG / corrupt /
+// truncated headers, -2 unsupported (lossless, hierarchical, arithmetic
+// coding, 12-bit, CMYK, unusual sampling).
 int jpeg_parse(const uint8_t* data, size_t size, JpegInfo* info, std::string* err);
+
+// Entropy-decode every scan of a host_scans file into coef (the image's
+// blocks, component c at comp_block0[c] blocks, comp bw x bh blocks, 64
+// int16 in natural order each; zeroed by the caller), following libjpeg-
+// turbo's jdhuff.c (sequential) and jdphuff.c (progressive DC / AC, first and
+// refinement scans, EOB runs, restart markers; missing data reads as zeros).
+void jpeg_host_decode(const JpegInfo& info, int16_t* coef, const int64_t* comp_block0);
+
+// End of entropy-coded data starting at d[pos]: the first marker other than
+// stuffing, fill bytes or RSTn (its 0xFF), or n.
+size_t scan_data_end(const uint8_t* d, size_t n, size_t pos);
 
 // Remove byte stuffing (FF 00 -> FF) and split at RSTn markers: `out` gets the
 // de-stuffed bytes of every restart segment back to back; seg_off[s] is the

@@ -124,18 +124,16 @@ __device__ __forceinline__ int huff_decode(const HuffDev& t, BitReader& br)
         br.skip((int)(e >> 8));
         return (int)(e & 255);
     }
-    int l = kHuffLutBits + 1;
-    int32_t code = (int32_t)(look >> (16 - l));
-    while (l <= 16 && code > t.maxcode[l]) {
-        ++l;
-        code = (int32_t)(look >> (16 - l));
+    for (int l = kHuffLutBits + 1; l <= 16; ++l) {
+        const int32_t code = (int32_t)(look >> (16 - l));
+        if (code <= t.maxcode[l]) {
+            br.skip(l);
+            return t.vals[(t.valoff[l] + code) & 255];
+        }
     }
-    if (l > 16) {  // not a code (only off the true decode path): jdhuff returns 0
-        br.skip(16);
-        return 0;
-    }
-    br.skip(l);
-    return t.vals[(t.valoff[l] + code) & 255];
+    // not a code (only off the true decode path): jdhuff returns 0
+    br.skip(16);
+    return 0;
 }
 
 // HUFF_EXTEND (jdhuff.h)
@@ -626,6 +624,12 @@ struct IdctJob {
 constexpr int kConstBits = 13, kPass1Bits = 2;
 
 __device__ __forceinline__ int64_t descale(int64_t x, int n) { return (x + ((int64_t)1 << (n - 1))) >> n; }
+__device__ __forceinline__ int32_t descale32(int32_t x, int n) { return (x + (1 << (n - 1))) >> n; }
+
+#ifndef WICCA_IDCT32
+#define WICCA_IDCT32 1  // 0: every IDCT pass in 64-bit arithmetic
+#endif
+constexpr int32_t kIdct32Max = 12600;  // 32-bit IDCT pass exact for inputs within +-kIdct32Max (with the descale rounding term)
 
 // idct_sample_range_limit[x & 1023] of jdmaster.c's prepare_range_limit_table
 __device__ __forceinline__ uint8_t idct_limit(int64_t v)
@@ -710,28 +714,64 @@ __device__ __forceinline__ void idct8_lane_v(uint4 v, const uint16_t* qt, int r,
         }
     }
     wave_lds_sync();
-    int64_t col[8], o[8];
+    // each pass in 32-bit arithmetic when every input of the wave is at most
+    // kIdct32Max (jidctint.c's butterfly grows a value by < 169,352 = 2^17.4:
+    // 12,600 * 169,352 + 2^17 < 2^31, so the products and sums equal the JLONG ones);
+    // otherwise in 64-bit (JLONG) as libjpeg-turbo computes on LP64
+    int32_t in[8];
+    bool big = false;
     if (live) {  // pass 1: column r
 #pragma unroll
-        for (int k = 0; k < 8; ++k) col[k] = t[k * 8 + r];
-        islow_1d<int64_t>(col, o);
+        for (int k = 0; k < 8; ++k) {
+            in[k] = t[k * 8 + r];
+            big |= in[k] > kIdct32Max || in[k] < -kIdct32Max;
+        }
+    }
+    int32_t p1[8];
+    if (WICCA_IDCT32 && !__any(big)) {
+        int32_t o[8];
+        if (live) islow_1d<int32_t>(in, o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p1[k] = (int32_t)descale32(o[k], kConstBits - kPass1Bits);
+    } else {
+        int64_t c64[8], o[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) c64[k] = in[k];
+        if (live) islow_1d<int64_t>(c64, o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p1[k] = (int32_t)descale(o[k], kConstBits - kPass1Bits);
     }
     wave_lds_sync();
     if (live) {
-        constexpr int sh = kConstBits - kPass1Bits;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) t[k * 8 + r] = (int32_t)descale(o[k], sh);
+        for (int k = 0; k < 8; ++k) t[k * 8 + r] = p1[k];
     }
     wave_lds_sync();
-    if (!live) return;
     // pass 2: row r -> samples
-    int64_t row[8];
+    big = false;
+    if (live) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) row[k] = t[r * 8 + k];
-    islow_1d<int64_t>(row, o);
+        for (int k = 0; k < 8; ++k) {
+            in[k] = t[r * 8 + k];
+            big |= in[k] > kIdct32Max || in[k] < -kIdct32Max;
+        }
+    }
     constexpr int sh = kConstBits + kPass1Bits + 3;
+    if (WICCA_IDCT32 && !__any(big)) {
+        int32_t o[8];
+        if (!live) return;
+        islow_1d<int32_t>(in, o);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) px[k] = idct_limit(descale(o[k], sh));
+        for (int k = 0; k < 8; ++k) px[k] = idct_limit(descale32(o[k], sh));
+    } else {
+        int64_t r64[8], o[8];
+        if (!live) return;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r64[k] = in[k];
+        islow_1d<int64_t>(r64, o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) px[k] = idct_limit(descale(o[k], sh));
+    }
 }
 
 __device__ __forceinline__ void idct8_lane(const int16_t* blk, const uint16_t* qt, int r, bool live, int32_t* t,
@@ -1020,7 +1060,10 @@ __device__ __forceinline__ void ycc8_to_rgb(uint32_t ylo, uint32_t yhi, const in
 // A workgroup walks kFuseRows tiles down one 256-pixel column strip: the next
 // tile's coefficients are loaded while the current one is transformed and
 // coloured, and each tile's chroma loads are issued before its IDCT.
-constexpr int kFuseRows = 4;
+#ifndef WICCA_FUSE_ROWS
+#define WICCA_FUSE_ROWS 1
+#endif
+constexpr int kFuseRows = WICCA_FUSE_ROWS;
 
 __device__ __forceinline__ void chroma8(const JpegPlan& P, const JpegImageDev& im, int x, int y, int (&cbv)[8],
                                         int (&crv)[8])
@@ -1209,46 +1252,51 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     hipError_t e = hj.empty() ? hipSuccess
                               : hipMemcpyAsync(jobs, hj.data(), sizeof(IdctJob) * hj.size(), hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return e;
-    const uint32_t grid = (uint32_t)((P.n_sub + kJThreads - 1) / kJThreads);
-    // round 0 + rounds until no end state changes; results rotate through
-    // three buffers (older = round - 2, cur = round - 1, nxt = this round)
-    hipLaunchKernelGGL(jpeg_sync_kernel, dim3(grid), dim3(kJThreads), 0, s, P, ra, ra, 0, changed,
-                       (const SubResult*)nullptr);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    SubResult* older = rc;
-    SubResult* cur = ra;
-    SubResult* nxt = rb;
-    int rounds = 0;
-    for (;;) {
-        int h_changed = 0;
-        e = hipMemsetAsync(changed, 0, sizeof(int), s);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(jpeg_sync_kernel, dim3(grid), dim3(kJThreads), 0, s, P, cur, nxt, rounds + 1, changed,
-                           (const SubResult*)older);
+    // the device Huffman decode (every image not decoded on the host)
+    if (P.n_sub > 0) {
+        const uint32_t grid = (uint32_t)((P.n_sub + kJThreads - 1) / kJThreads);
+        // round 0 + rounds until no end state changes; results rotate through
+        // three buffers (older = round - 2, cur = round - 1, nxt = this round)
+        hipLaunchKernelGGL(jpeg_sync_kernel, dim3(grid), dim3(kJThreads), 0, s, P, ra, ra, 0, changed,
+                           (const SubResult*)nullptr);
         e = hipGetLastError();
-        if (e == hipSuccess) e = hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return e;
-        SubResult* t = older;
-        older = cur;
-        cur = nxt;
-        nxt = t;
-        ++rounds;
-        if (!h_changed || rounds > P.n_sub) break;
+        SubResult* older = rc;
+        SubResult* cur = ra;
+        SubResult* nxt = rb;
+        int rounds = 0;
+        for (;;) {
+            int h_changed = 0;
+            e = hipMemsetAsync(changed, 0, sizeof(int), s);
+            if (e != hipSuccess) return e;
+            hipLaunchKernelGGL(jpeg_sync_kernel, dim3(grid), dim3(kJThreads), 0, s, P, cur, nxt, rounds + 1, changed,
+                               (const SubResult*)older);
+            e = hipGetLastError();
+            if (e == hipSuccess) e = hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e != hipSuccess) return e;
+            SubResult* t = older;
+            older = cur;
+            cur = nxt;
+            nxt = t;
+            ++rounds;
+            if (!h_changed || rounds > P.n_sub) break;
+        }
+        if (sync_rounds) *sync_rounds = rounds;
+        hipLaunchKernelGGL(jpeg_scan_kernel, dim3((uint32_t)P.n_seg), dim3(256), 0, s, P, cur, sb);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        static const bool force6 = [] {  // WICCA_JPEG_WRITE_SLOTS=6: the 6-table kernel for every batch (tests)
+            const char* e = getenv("WICCA_JPEG_WRITE_SLOTS");
+            return e && atoi(e) == 6;
+        }();
+        if (P.max_tabs <= 4 && !force6)
+            hipLaunchKernelGGL(jpeg_write_kernel<4>, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
+        else
+            hipLaunchKernelGGL(jpeg_write_kernel<2 * kJpegMaxComp>, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    } else if (sync_rounds) {
+        *sync_rounds = 0;
     }
-    if (sync_rounds) *sync_rounds = rounds;
-    hipLaunchKernelGGL(jpeg_scan_kernel, dim3((uint32_t)P.n_seg), dim3(256), 0, s, P, cur, sb);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    static const bool force6 = [] {  // WICCA_JPEG_WRITE_SLOTS=6: the 6-table kernel for every batch (tests)
-        const char* e = getenv("WICCA_JPEG_WRITE_SLOTS");
-        return e && atoi(e) == 6;
-    }();
-    if (P.max_tabs <= 4 && !force6)
-        hipLaunchKernelGGL(jpeg_write_kernel<4>, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
-    else
-        hipLaunchKernelGGL(jpeg_write_kernel<2 * kJpegMaxComp>, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
     const int64_t per_wg = (int64_t)kIdctBlocksPerWg * kIdctGroups;
     if (!hj.empty()) {
         hipLaunchKernelGGL(jpeg_idct_kernel, dim3((uint32_t)((max_blocks + per_wg - 1) / per_wg), (uint32_t)hj.size()),

@@ -76,6 +76,25 @@ bool huff_table_ok(const JpegHuffTable& t, bool dc)
     return true;
 }
 
+// End of the entropy-coded data that starts at d[pos]: the first marker other
+// than a stuffed 0xFF00, fill bytes or RSTn (the position of its 0xFF), or n.
+size_t scan_data_end(const uint8_t* d, size_t n, size_t pos)
+{
+    for (size_t i = pos; i + 1 < n; ++i) {
+        if (d[i] != 0xFF) continue;
+        size_t j = i + 1;
+        while (j < n && d[j] == 0xFF) ++j;  // fill bytes
+        if (j >= n) return n;
+        const uint8_t m = d[j];
+        if (m == 0x00 || (m >= 0xD0 && m <= 0xD7)) {
+            i = j;
+            continue;
+        }
+        return i;
+    }
+    return n;
+}
+
 int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
 {
     auto bad = [&](int code, const char* m) {
@@ -85,23 +104,37 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
     if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return bad(-1, "not a JPEG file (no SOI marker)");
     size_t pos = 2;
     bool have_sof = false;
-    int scan_ids[kJpegMaxComp] = {0, 0, 0};
+    int scan_ids[kJpegMaxComp] = {0, 1, 2};
     for (;;) {
         while (pos < n && d[pos] != 0xFF) ++pos;  // tolerate garbage between segments
         while (pos < n && d[pos] == 0xFF) ++pos;  // fill bytes
-        if (pos >= n) return bad(-1, "truncated JPEG (no SOS)");
+        if (pos >= n) {
+            if (info->host_scans && !info->scans.empty()) break;  // truncated after a scan: decode what is there
+            return bad(-1, "truncated JPEG (no SOS)");
+        }
         const int m = d[pos++];
         if (m == 0xD8 || (m >= 0xD0 && m <= 0xD7) || m == 0x01) continue;  // no length
-        if (m == 0xD9) return bad(-1, "EOI before SOS");
-        if (pos + 2 > n) return bad(-1, "truncated marker segment");
+        if (m == 0xD9) {
+            if (info->host_scans && !info->scans.empty()) break;  // EOI after the last scan
+            return bad(-1, "EOI before SOS");
+        }
+        if (pos + 2 > n) {
+            if (info->host_scans && !info->scans.empty()) break;
+            return bad(-1, "truncated marker segment");
+        }
         const int len = u16be(d + pos);
-        if (len < 2 || pos + (size_t)len > n) return bad(-1, "truncated marker segment");
+        if (len < 2 || pos + (size_t)len > n) {
+            if (info->host_scans && !info->scans.empty()) break;
+            return bad(-1, "truncated marker segment");
+        }
         const uint8_t* s = d + pos + 2;
         const int sl = len - 2;
         pos += (size_t)len;
-        if (m == 0xC0 || m == 0xC1) {  // baseline / extended sequential, Huffman
+        if (m == 0xC0 || m == 0xC1 || m == 0xC2) {  // baseline / extended sequential / progressive, Huffman
+            if (have_sof) return bad(-1, "duplicate SOF");
             if (sl < 6) return bad(-1, "bad SOF");
             if (s[0] != 8) return bad(-2, "only 8-bit JPEG is supported");
+            info->progressive = m == 0xC2;
             info->H = u16be(s + 1);
             info->W = u16be(s + 3);
             info->ncomp = s[5];
@@ -120,9 +153,8 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
                     if (info->comp[j].id == k.id) return bad(-1, "duplicate component id in SOF");
             }
             have_sof = true;
-        } else if ((m >= 0xC2 && m <= 0xC3) || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) ||
-                   (m >= 0xCD && m <= 0xCF)) {
-            return bad(-2, "progressive, lossless, hierarchical and arithmetic-coded JPEG are not supported");
+        } else if (m == 0xC3 || (m >= 0xC5 && m <= 0xC7) || (m >= 0xC9 && m <= 0xCB) || (m >= 0xCD && m <= 0xCF)) {
+            return bad(-2, "lossless, hierarchical and arithmetic-coded JPEG are not supported");
         } else if (m == 0xC4) {  // DHT
             int o = 0;
             while (o < sl) {
@@ -162,9 +194,9 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
             if (!have_sof) return bad(-1, "SOS before SOF");
             if (sl < 1) return bad(-1, "bad SOS");
             const int ns = s[0];
-            if (ns != info->ncomp)
-                return bad(-2, "multi-scan (non-interleaved) JPEG is not supported");
-            if (sl < 1 + 2 * ns + 3) return bad(-1, "bad SOS");
+            if (ns < 1 || ns > info->ncomp || sl < 1 + 2 * ns + 3) return bad(-1, "bad SOS");
+            JpegScan sc;
+            sc.ns = ns;
             for (int i = 0; i < ns; ++i) {
                 const int id = s[1 + 2 * i];
                 int c = -1;
@@ -172,27 +204,74 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
                     if (info->comp[k].id == id) c = k;
                 if (c < 0) return bad(-1, "SOS names an unknown component");
                 for (int j = 0; j < i; ++j)
-                    if (scan_ids[j] == c) return bad(-1, "duplicate component in SOS");
-                scan_ids[i] = c;
-                info->comp[c].td = s[2 + 2 * i] >> 4;
-                info->comp[c].ta = s[2 + 2 * i] & 15;
-                if (info->comp[c].td > 3 || info->comp[c].ta > 3) return bad(-1, "bad SOS table id");
+                    if (sc.comp[j] == c) return bad(-1, "duplicate component in SOS");
+                sc.comp[i] = c;
+                const int td = s[2 + 2 * i] >> 4, ta = s[2 + 2 * i] & 15;
+                if (td > 3 || ta > 3) return bad(-1, "bad SOS table id");
+                info->comp[c].td = td;
+                info->comp[c].ta = ta;
             }
-            const int ss = s[1 + 2 * ns], se = s[2 + 2 * ns], ahl = s[3 + 2 * ns];
-            if (ss != 0 || se != 63 || ahl != 0) return bad(-2, "spectral selection / successive approximation");
-            info->scan = d + pos;
-            info->scan_len = n - pos;
-            break;
+            sc.Ss = s[1 + 2 * ns];
+            sc.Se = s[2 + 2 * ns];
+            sc.Ah = s[3 + 2 * ns] >> 4;
+            sc.Al = s[3 + 2 * ns] & 15;
+            if (!info->progressive && ns == info->ncomp && info->scans.empty()) {
+                // one interleaved sequential scan: the GPU Huffman path
+                if (sc.Ss != 0 || sc.Se != 63 || sc.Ah != 0 || sc.Al != 0)
+                    return bad(-1, "bad sequential scan parameters");
+                for (int i = 0; i < ns; ++i) scan_ids[i] = sc.comp[i];
+                info->scan = d + pos;
+                info->scan_len = n - pos;
+                break;
+            }
+            // a scan of a multi-scan file (jdphuff.c start_pass_phuff_decoder's checks)
+            info->host_scans = true;
+            if (info->progressive) {
+                const bool dc = sc.Ss == 0;
+                if (dc ? sc.Se != 0 : (sc.Se < sc.Ss || sc.Se > 63 || ns != 1))
+                    return bad(-1, "invalid progressive scan parameters");
+                if ((sc.Ah != 0 && sc.Al != sc.Ah - 1) || sc.Al > 13)
+                    return bad(-1, "invalid progressive scan parameters");
+            } else if (sc.Ss != 0 || sc.Se != 63 || sc.Ah != 0 || sc.Al != 0) {
+                return bad(-1, "bad sequential scan parameters");
+            }
+            for (int i = 0; i < ns; ++i) {
+                const JpegComponent& k = info->comp[sc.comp[i]];
+                const bool need_dc = sc.Ss == 0 && sc.Ah == 0, need_ac = sc.Se > 0 || !info->progressive;
+                if (need_dc) {
+                    if (!info->dc_present[k.td] || !huff_table_ok(info->dc[k.td], true))
+                        return bad(-1, "missing or bogus Huffman table");
+                    sc.dc[i] = info->dc[k.td];
+                }
+                if (need_ac) {
+                    if (!info->ac_present[k.ta] || !huff_table_ok(info->ac[k.ta], false))
+                        return bad(-1, "missing or bogus Huffman table");
+                    sc.ac[i] = info->ac[k.ta];
+                }
+                if (!info->qt_present[k.tq]) return bad(-1, "missing quantisation table");
+            }
+            sc.restart_interval = info->restart_interval;
+            sc.data = d + pos;
+            const size_t end = scan_data_end(d, n, pos);
+            sc.len = end - pos;
+            info->scans.push_back(sc);
+            pos = end;
+            continue;
         }
         // other APPn, COM, ...: skipped
     }
-    // tables present?
-    for (int c = 0; c < info->ncomp; ++c) {
-        const JpegComponent& k = info->comp[c];
-        if (!info->qt_present[k.tq]) return bad(-1, "missing quantisation table");
-        if (!info->dc_present[k.td] || !info->ac_present[k.ta]) return bad(-1, "missing Huffman table");
-        if (!huff_table_ok(info->dc[k.td], true) || !huff_table_ok(info->ac[k.ta], false))
-            return bad(-1, "bogus Huffman table definition");
+    if (!info->host_scans) {
+        // tables present?
+        for (int c = 0; c < info->ncomp; ++c) {
+            const JpegComponent& k = info->comp[c];
+            if (!info->qt_present[k.tq]) return bad(-1, "missing quantisation table");
+            if (!info->dc_present[k.td] || !info->ac_present[k.ta]) return bad(-1, "missing Huffman table");
+            if (!huff_table_ok(info->dc[k.td], true) || !huff_table_ok(info->ac[k.ta], false))
+                return bad(-1, "bogus Huffman table definition");
+        }
+    } else {
+        for (int c = 0; c < info->ncomp; ++c)
+            if (!info->qt_present[info->comp[c].tq]) return bad(-1, "missing quantisation table");
     }
     // geometry
     if (info->ncomp == 1) {
@@ -244,6 +323,14 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
                 }
         }
         info->bpm = slot;
+    }
+    if (info->host_scans) {  // an interleaved scan may hold at most 10 blocks per MCU (jdinput.c)
+        for (const JpegScan& sc : info->scans) {
+            if (sc.ns <= 1) continue;
+            int blocks = 0;
+            for (int i = 0; i < sc.ns; ++i) blocks += info->comp[sc.comp[i]].h * info->comp[sc.comp[i]].v;
+            if (blocks > kJpegMaxSlots) return bad(-1, "too many blocks per MCU");
+        }
     }
     return 0;
 }
@@ -360,6 +447,287 @@ void build_huff_dev(const JpegHuffTable& t, HuffDev* d)
     d->maxcode[0] = -1;
     d->maxcode[17] = INT_MAX;  // sentinel
     memcpy(d->vals, t.vals, 256);
+}
+
+}  // namespace wicca
+
+// ---------------------------------------------------------------------------
+// Host entropy decode of multi-scan files (progressive, or sequential with a
+// scan per component).  Progressive AC refinement scans read one correction
+// bit per coefficient that is already nonzero in the block, so where a symbol
+// starts depends on every earlier scan's result for that exact block: the
+// self-synchronising subsequence decode of the GPU path (which must guess
+// the block a lane starts in) does not apply, and these files are decoded
+// here, one host thread per file, into the same coefficient layout; the
+// device runs the same IDCT / upsampling / colour back end on them.
+// ---------------------------------------------------------------------------
+namespace wicca {
+
+namespace {
+
+// jpeg_natural_order with libjpeg's 16 guard entries (corrupt run lengths)
+constexpr int kNaturalX[80] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,
+                               12, 19, 26, 33, 40, 48, 41, 34, 27, 20, 13, 6,  7,  14, 21, 28,
+                               35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23, 30, 37, 44, 51,
+                               58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63,
+                               63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63, 63};
+
+// jdhuff.c's bit buffer: bytes in, 0xFF00 -> 0xFF, fill bytes skipped; at a
+// marker nothing more is read and zero bits follow.  Like libjpeg-turbo, only
+// bits the decoder actually consumes past the data count as running out
+// (insufficient): a Huffman lookahead into the zeros does not.
+struct HostBits {
+    const uint8_t* d = nullptr;
+    size_t n = 0, pos = 0;
+    uint64_t buf = 0;  // cnt valid bits, right-aligned; the lowest `zeros` of them are padding
+    int cnt = 0, zeros = 0;
+    bool at_marker = false;
+    bool insufficient = false;
+
+    void reset(const uint8_t* data, size_t len)
+    {
+        d = data;
+        n = len;
+        pos = 0;
+        buf = 0;
+        cnt = zeros = 0;
+        at_marker = false;
+    }
+    void fill()
+    {
+        while (cnt <= 56) {
+            if (!at_marker && zeros == 0 && pos < n) {
+                const uint8_t b = d[pos];
+                if (b == 0xFF) {
+                    size_t j = pos + 1;
+                    while (j < n && d[j] == 0xFF) ++j;
+                    if (j < n && d[j] == 0x00) {
+                        pos = j + 1;
+                    } else {  // a marker (RSTn or the end of the scan): stop in front of it
+                        pos = j - 1;
+                        at_marker = true;
+                        continue;
+                    }
+                } else {
+                    ++pos;
+                }
+                buf = (buf << 8) | b;
+                cnt += 8;
+            } else {
+                buf <<= 8;
+                cnt += 8;
+                zeros += 8;
+            }
+        }
+    }
+    uint32_t peek(int k)
+    {
+        if (cnt < k) fill();
+        return (uint32_t)(buf >> (cnt - k)) & ((1u << k) - 1);
+    }
+    void skip(int k)
+    {
+        cnt -= k;
+        if (cnt < zeros) {  // consumed padding: the data ran out
+            insufficient = true;
+            zeros = cnt;
+        }
+    }
+    uint32_t get(int k)
+    {
+        if (k == 0) return 0;
+        const uint32_t v = peek(k);
+        skip(k);
+        return v;
+    }
+    // process_restart: drop the bits left, consume the RSTn marker
+    void restart()
+    {
+        buf = 0;
+        cnt = zeros = 0;
+        size_t j = pos;
+        while (j < n && d[j] != 0xFF) ++j;  // bytes the encoder left before the marker (corrupt streams)
+        while (j < n && d[j] == 0xFF) ++j;
+        if (j < n && d[j] >= 0xD0 && d[j] <= 0xD7) {
+            pos = j + 1;
+            at_marker = false;
+            insufficient = false;
+        } else {
+            pos = j > 0 ? j - 1 : j;
+            at_marker = true;  // no restart marker where one was due: the segment reads as empty
+        }
+    }
+};
+
+int host_huff(const HuffDev& t, HostBits& br)
+{
+    const uint32_t look = br.peek(16);
+    const uint16_t e = t.lut[look >> (16 - kHuffLutBits)];
+    if (e) {
+        br.skip(e >> 8);
+        return e & 255;
+    }
+    for (int l = kHuffLutBits + 1; l <= 16; ++l) {
+        const int32_t code = (int32_t)(look >> (16 - l));
+        if (code <= t.maxcode[l]) {
+            br.skip(l);
+            return t.vals[(t.valoff[l] + code) & 255];
+        }
+    }
+    // jdhuff.c: not a code; 17 bits consumed, a zero returned
+    br.skip(16);
+    br.get(1);
+    return 0;
+}
+
+inline int host_extend(uint32_t v, int s) { return (int)v < (1 << (s - 1)) ? (int)v - (1 << s) + 1 : (int)v; }
+
+}  // namespace
+
+void jpeg_host_decode(const JpegInfo& info, int16_t* coef, const int64_t* comp_block0)
+{
+    HostBits br;
+    std::vector<HuffDev> dct(kJpegMaxComp), act(kJpegMaxComp);
+    for (const JpegScan& sc : info.scans) {
+        const bool prog = info.progressive;
+        const bool dc_scan = sc.Ss == 0, first = sc.Ah == 0;
+        for (int i = 0; i < sc.ns; ++i) {
+            if (!prog || (dc_scan && first)) build_huff_dev(sc.dc[i], &dct[(size_t)i]);
+            if (!prog || !dc_scan) build_huff_dev(sc.ac[i], &act[(size_t)i]);
+        }
+        br.reset(sc.data, sc.len);
+        br.insufficient = false;
+        int last_dc[kJpegMaxComp] = {0, 0, 0};
+        uint32_t eobrun = 0;
+        const int p1 = 1 << sc.Al, m1 = -(1 << sc.Al);
+        auto block_of = [&](int c, int64_t bx, int64_t by) {
+            return coef + (comp_block0[c] + by * info.comp[c].bw + bx) * 64;
+        };
+        auto decode_block = [&](int i, int16_t* blk) {
+            const int c = sc.comp[i];
+            if (!prog) {  // jdhuff.c decode_mcu (sequential)
+                const int s = host_huff(dct[(size_t)i], br);
+                if (s) last_dc[c] += host_extend(br.get(s), s);
+                blk[0] = (int16_t)last_dc[c];
+                for (int k = 1; k < 64; ++k) {
+                    const int rs = host_huff(act[(size_t)i], br);
+                    const int r = rs >> 4, sz = rs & 15;
+                    if (sz) {
+                        k += r;
+                        blk[kNaturalX[k]] = (int16_t)host_extend(br.get(sz), sz);
+                    } else {
+                        if (r != 15) break;
+                        k += 15;
+                    }
+                }
+                return;
+            }
+            if (dc_scan) {
+                if (first) {  // decode_mcu_DC_first
+                    const int s = host_huff(dct[(size_t)i], br);
+                    if (s) last_dc[c] += host_extend(br.get(s), s);
+                    blk[0] = (int16_t)((uint32_t)last_dc[c] << sc.Al);
+                } else if (br.get(1)) {  // decode_mcu_DC_refine
+                    blk[0] = (int16_t)(blk[0] | p1);
+                }
+                return;
+            }
+            if (first) {  // decode_mcu_AC_first
+                if (eobrun > 0) {
+                    --eobrun;
+                    return;
+                }
+                for (int k = sc.Ss; k <= sc.Se; ++k) {
+                    const int rs = host_huff(act[(size_t)i], br);
+                    int r = rs >> 4;
+                    const int sz = rs & 15;
+                    if (sz) {
+                        k += r;
+                        blk[kNaturalX[k]] = (int16_t)((uint32_t)host_extend(br.get(sz), sz) << sc.Al);
+                    } else if (r == 15) {
+                        k += 15;
+                    } else {
+                        eobrun = 1u << r;
+                        if (r) eobrun += br.get(r);
+                        --eobrun;
+                        break;
+                    }
+                }
+                return;
+            }
+            // decode_mcu_AC_refine
+            int k = sc.Ss;
+            auto correct = [&](int16_t& v) {
+                if (br.get(1) && (v & p1) == 0) v = (int16_t)(v >= 0 ? v + p1 : v + m1);
+            };
+            if (eobrun == 0) {
+                for (; k <= sc.Se; ++k) {
+                    const int rs = host_huff(act[(size_t)i], br);
+                    int r = rs >> 4, sz = rs & 15;
+                    int val = 0;
+                    if (sz) {  // sz is 1 in a valid stream
+                        val = br.get(1) ? p1 : m1;
+                    } else if (r != 15) {
+                        eobrun = 1u << r;
+                        if (r) eobrun += br.get(r);
+                        break;
+                    }
+                    do {
+                        int16_t& t = blk[kNaturalX[k]];
+                        if (t != 0) {
+                            correct(t);
+                        } else {
+                            if (--r < 0) break;
+                        }
+                        ++k;
+                    } while (k <= sc.Se);
+                    if (sz) blk[kNaturalX[k]] = (int16_t)val;
+                }
+            }
+            if (eobrun > 0) {
+                for (; k <= sc.Se; ++k) {
+                    int16_t& t = blk[kNaturalX[k]];
+                    if (t != 0) correct(t);
+                }
+                --eobrun;
+            }
+        };
+        int restarts_to_go = sc.restart_interval;
+        auto before_mcu = [&]() {
+            if (sc.restart_interval) {
+                if (restarts_to_go == 0) {  // process_restart
+                    br.restart();
+                    for (int c = 0; c < kJpegMaxComp; ++c) last_dc[c] = 0;
+                    eobrun = 0;
+                    restarts_to_go = sc.restart_interval;
+                }
+                --restarts_to_go;
+            }
+        };
+        if (sc.ns > 1) {  // interleaved: MCUs of the frame
+            for (int64_t my = 0; my < info.mcuy; ++my)
+                for (int64_t mx = 0; mx < info.mcux; ++mx) {
+                    before_mcu();
+                    if (br.insufficient) continue;  // jdhuff / jdphuff: MCUs past the data are skipped
+                    for (int i = 0; i < sc.ns; ++i) {
+                        const JpegComponent& k = info.comp[sc.comp[i]];
+                        for (int v = 0; v < k.v; ++v)
+                            for (int h = 0; h < k.h; ++h)
+                                decode_block(i, block_of(sc.comp[i], mx * k.h + h, my * k.v + v));
+                    }
+                }
+        } else {  // one component: its own blocks, one per MCU
+            const int c = sc.comp[0];
+            const JpegComponent& k = info.comp[c];
+            const int64_t wb = (k.dw + 7) / 8, hb = (k.dh + 7) / 8;
+            for (int64_t by = 0; by < hb; ++by)
+                for (int64_t bx = 0; bx < wb; ++bx) {
+                    before_mcu();
+                    if (br.insufficient) continue;
+                    decode_block(0, block_of(c, bx, by));
+                }
+        }
+    }
 }
 
 }  // namespace wicca
