@@ -701,16 +701,32 @@ constexpr int kIdctBlocksPerWg = 32;
 // block's samples out (px).  `t` is the block's 64-int LDS transpose area;
 // every lane of the wave must call this (wave barriers), `live` is uniform
 // over the block's 8 lanes.
+// Position of element (row i, column j) of a block's 8x8 LDS transpose area:
+// column-major with each column rotated by its index, and the whole area
+// rotated by 8 words per block of the wave (rot).  Writing a row (lane = row,
+// one column per instruction) and reading a column (lane = column, one row
+// per instruction) then touch 64 different banks across the wave's 8 blocks;
+// the plain row-major layout put every block's lanes on the same 8 banks
+// (8-way conflicts on every transpose access).
+__device__ __forceinline__ int tix(int rot, int i, int j) { return (8 * j + ((i + j) & 7) + rot) & 63; }
+
+// SWZ: the rotated transpose layout (tix) instead of row-major; I32: 32-bit
+// passes where exact.  The chroma IDCT kernel is faster with both (346 vs
+// 394 us per 25 x 8K call), the VALU-bound fused luma kernel without them
+// (1.97 vs 2.11 ms: the index arithmetic costs more than the conflicts).
+template <bool SWZ, bool I32>
 __device__ __forceinline__ void idct8_lane_v(uint4 v, const uint16_t* qt, int r, bool live, int32_t* t,
                                              uint8_t (&px)[8])
 {
+    const int rot = 8 * ((threadIdx.x >> 3) & 7);  // the block's place in its wave
+    auto at = [&](int i, int j) { return SWZ ? tix(rot, i, j) : i * 8 + j; };
     if (live) {
         const uint4 qv = *reinterpret_cast<const uint4*>(qt + r * 8);
         const uint32_t cw[4] = {v.x, v.y, v.z, v.w}, qw[4] = {qv.x, qv.y, qv.z, qv.w};
 #pragma unroll
         for (int k = 0; k < 4; ++k) {  // dequantised row r (coefficient * quantiser fits in int32)
-            t[r * 8 + 2 * k] = (int32_t)(int16_t)(cw[k] & 0xFFFF) * (int32_t)(qw[k] & 0xFFFF);
-            t[r * 8 + 2 * k + 1] = (int32_t)(int16_t)(cw[k] >> 16) * (int32_t)(qw[k] >> 16);
+            t[at(r, 2 * k)] = (int32_t)(int16_t)(cw[k] & 0xFFFF) * (int32_t)(qw[k] & 0xFFFF);
+            t[at(r, 2 * k + 1)] = (int32_t)(int16_t)(cw[k] >> 16) * (int32_t)(qw[k] >> 16);
         }
     }
     wave_lds_sync();
@@ -723,12 +739,12 @@ __device__ __forceinline__ void idct8_lane_v(uint4 v, const uint16_t* qt, int r,
     if (live) {  // pass 1: column r
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            in[k] = t[k * 8 + r];
+            in[k] = t[at(k, r)];
             big |= in[k] > kIdct32Max || in[k] < -kIdct32Max;
         }
     }
     int32_t p1[8];
-    if (WICCA_IDCT32 && !__any(big)) {
+    if (I32 && !__any(big)) {
         int32_t o[8];
         if (live) islow_1d<int32_t>(in, o);
 #pragma unroll
@@ -744,7 +760,7 @@ __device__ __forceinline__ void idct8_lane_v(uint4 v, const uint16_t* qt, int r,
     wave_lds_sync();
     if (live) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) t[k * 8 + r] = p1[k];
+        for (int k = 0; k < 8; ++k) t[at(k, r)] = p1[k];
     }
     wave_lds_sync();
     // pass 2: row r -> samples
@@ -752,12 +768,12 @@ __device__ __forceinline__ void idct8_lane_v(uint4 v, const uint16_t* qt, int r,
     if (live) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            in[k] = t[r * 8 + k];
+            in[k] = t[at(r, k)];
             big |= in[k] > kIdct32Max || in[k] < -kIdct32Max;
         }
     }
     constexpr int sh = kConstBits + kPass1Bits + 3;
-    if (WICCA_IDCT32 && !__any(big)) {
+    if (I32 && !__any(big)) {
         int32_t o[8];
         if (!live) return;
         islow_1d<int32_t>(in, o);
@@ -778,7 +794,7 @@ __device__ __forceinline__ void idct8_lane(const int16_t* blk, const uint16_t* q
                                            uint8_t (&px)[8])
 {
     const uint4 v = live ? *reinterpret_cast<const uint4*>(blk + r * 8) : uint4{0, 0, 0, 0};
-    idct8_lane_v(v, qt, r, live, t, px);
+    idct8_lane_v<true, WICCA_IDCT32 != 0>(v, qt, r, live, t, px);
 }
 
 __device__ __forceinline__ uint2 pack8(const uint8_t (&px)[8])
@@ -1007,6 +1023,8 @@ __global__ __launch_bounds__(256) void jpeg_color_kernel(JpegPlan P)
 constexpr int kFuseBlocks = 32;               // luma blocks per tile row
 constexpr int kFuseW = kFuseBlocks * 8;       // 256 pixels
 constexpr int kFuseRowBytes = kFuseW * 3;     // 768 RGB bytes per tile row
+constexpr int kYPitch = kFuseW + 32;          // luma tile row pitch: 72 words, so the IDCT lanes'
+                                              // row stores (8 rows x 8 blocks) meet at most 2 per bank
 
 // 8 chroma samples (output pixels x .. x+7, x even) of row y by h2v2 fancy
 // upsampling: chroma columns c-1 .. c+4 (c = x/2) of the nearest and the
@@ -1097,7 +1115,7 @@ __device__ __forceinline__ void chroma8(const JpegPlan& P, const JpegImageDev& i
 __global__ __launch_bounds__(256) void jpeg_luma_color_kernel(JpegPlan P)
 {
     __shared__ int32_t tr[kFuseBlocks * 64];
-    __shared__ __attribute__((aligned(16))) uint8_t ytile[8 * kFuseW];
+    __shared__ __attribute__((aligned(16))) uint8_t ytile[8 * kYPitch];
     __shared__ __attribute__((aligned(16))) uint32_t stage[8 * kFuseRowBytes / 4];
     const JpegImageDev& im = P.imgs[blockIdx.z];
     const int x0 = blockIdx.x * kFuseW, by0 = blockIdx.y * kFuseRows;
@@ -1125,14 +1143,14 @@ __global__ __launch_bounds__(256) void jpeg_luma_color_kernel(JpegPlan P)
         int cbv[8], crv[8];
         if (px_live && im.ncomp == 3) chroma8(P, im, x, y, cbv, crv);
         uint8_t px[8];
-        idct8_lane_v(ccur, im.qt[0], r, blive, tr + lb * 64, px);
-        if (blive) *reinterpret_cast<uint2*>(ytile + r * kFuseW + lb * 8) = pack8(px);
+        idct8_lane_v<false, false>(ccur, im.qt[0], r, blive, tr + lb * 64, px);
+        if (blive) *reinterpret_cast<uint2*>(ytile + r * kYPitch + lb * 8) = pack8(px);
         __syncthreads();  // ytile complete; the previous tile's stage has been stored
         uint8_t o[24];
 #pragma unroll
         for (int i = 0; i < 24; ++i) o[i] = 0;
         if (px_live) {
-            const uint2 yv = *reinterpret_cast<const uint2*>(ytile + rr * kFuseW + cx);
+            const uint2 yv = *reinterpret_cast<const uint2*>(ytile + rr * kYPitch + cx);
             if (im.ncomp == 1) {
 #pragma unroll
                 for (int q = 0; q < 8; ++q)

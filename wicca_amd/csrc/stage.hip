@@ -114,7 +114,7 @@ __global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
             float* out = im.hsum + (int64_t)y * n_el;
             float acc[NE];
             int len[NE], base[NE];
-            int maxlen = 0;
+            int minlen = 1 << 30, maxlen = 0;
             const int last = nq * 16 - 1;  // the staged row's last byte
 #pragma unroll
             for (int i = 0; i < NE; ++i) {
@@ -124,27 +124,22 @@ __global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
                 const int c = e - (e / C) * C;
                 base[i] = live ? tx.s1 * C + c : 0;
                 len[i] = live ? tx.s2 - tx.s1 : 0;
+                if (live) minlen = min(minlen, len[i]);
                 maxlen = max(maxlen, len[i]);
                 const float a = (float)b[live && tx.has_a ? base[i] - C : 0] * tx.wa;
                 acc[i] = live && tx.has_a ? 0.f + a : 0.f;
             }
+            if (minlen > maxlen) minlen = 0;  // no live element
+            // the windows of a lane's elements differ by at most one full cell
+            // (floor / ceil of the scale): the common part runs unpredicated
+            // (dead elements read a valid byte into a chain that is never stored)
             int j = 0;
-            for (; j + 2 <= maxlen; j += 2) {
-                float v0[NE], v1[NE];
+#pragma unroll 4
+            for (; j < minlen; ++j) {
 #pragma unroll
-                for (int i = 0; i < NE; ++i) {
-                    v0[i] = (float)b[min(base[i] + j * C, last)];
-                    v1[i] = (float)b[min(base[i] + (j + 1) * C, last)];
-                }
-#pragma unroll
-                for (int i = 0; i < NE; ++i) {
-                    const float s0 = acc[i] + v0[i] * tab[i].wm;
-                    acc[i] = j < len[i] ? s0 : acc[i];
-                    const float s1 = acc[i] + v1[i] * tab[i].wm;
-                    acc[i] = j + 1 < len[i] ? s1 : acc[i];
-                }
+                for (int i = 0; i < NE; ++i) acc[i] = acc[i] + (float)b[base[i] + j * C] * tab[i].wm;
             }
-            if (j < maxlen) {
+            for (; j < maxlen; ++j) {
 #pragma unroll
                 for (int i = 0; i < NE; ++i) {
                     const float v = (float)b[min(base[i] + j * C, last)];
