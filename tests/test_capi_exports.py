@@ -84,3 +84,11 @@ def test_multi_gpu_batch_host_checks():
                                                    4, 4, 12, 6))
         rc = lib.wicca_haar_ll_u8_batch_multi_gpu(desc, 1, 3, 1, 1, 0, None, 0)
         assert rc == _lib.WICCA_ERR_NODEVICE
+
+
+def test_library_built_from_this_tree():
+    """The source stamp compiled into libwicca_hip.so (wicca_version) equals
+    the SHA-256 of this tree's library sources: the tested binary is the one
+    these sources build."""
+    from wicca_amd import _lib
+    assert _lib.built_source_hash() == _lib.source_hash()

@@ -167,5 +167,28 @@ def check(rc: int) -> None:
     raise WiccaHipError(f"wicca_hip status {rc}: {msg}")
 
 
+def source_hash() -> str:
+    """SHA-256 (16 hex digits) of the library's sources in this tree, as the
+    Makefile stamps it into ``wicca_version()`` (sorted csrc/*.hip, *.cpp,
+    *.h, then include/wicca_haar.h)."""
+    import glob
+    import hashlib
+    csrc = os.path.join(_HERE, "csrc")
+    files = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")) +
+                   glob.glob(os.path.join(csrc, "*.h")))
+    files.append(os.path.abspath(os.path.join(_HERE, "..", "include", "wicca_haar.h")))
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def built_source_hash() -> str:
+    """The source stamp compiled into the loaded library."""
+    v = load().wicca_version().decode()
+    return v.rsplit("src:", 1)[-1] if "src:" in v else ""
+
+
 def device_count() -> int:
     return int(load().wicca_device_count())

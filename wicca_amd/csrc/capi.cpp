@@ -549,7 +549,10 @@ int wicca_device_count(void)
 
 const char* wicca_last_error(void) { return t_last_error.c_str(); }
 
-const char* wicca_version(void) { return "wicca_hip 0.2 gfx950"; }
+#ifndef WICCA_SRC_HASH
+#define WICCA_SRC_HASH "unknown"
+#endif
+const char* wicca_version(void) { return "wicca_hip 0.3 gfx950 src:" WICCA_SRC_HASH; }
 
 const char* wicca_kernel_name(int depth, int64_t C, int ragged)
 {
