@@ -1141,9 +1141,16 @@ __global__ __launch_bounds__(256) void jpeg_luma_color_kernel(JpegPlan P)
         const uint4 ccur = cnext;
         if (g + 1 < nby && blive) cnext = *reinterpret_cast<const uint4*>(cbase + (by0 + g + 1) * crow);
         int cbv[8], crv[8];
+#ifndef WICCA_ABL_NOCOLOR
         if (px_live && im.ncomp == 3) chroma8(P, im, x, y, cbv, crv);
+#endif
         uint8_t px[8];
+#ifndef WICCA_ABL_NOIDCT
         idct8_lane_v<false, false>(ccur, im.qt[0], r, blive, tr + lb * 64, px);
+#else  // ablation (timing only): the coefficients' low bytes instead of the IDCT
+        px[0] = ccur.x; px[1] = ccur.x >> 8; px[2] = ccur.y; px[3] = ccur.y >> 8;
+        px[4] = ccur.z; px[5] = ccur.z >> 8; px[6] = ccur.w; px[7] = ccur.w >> 8;
+#endif
         if (blive) *reinterpret_cast<uint2*>(ytile + r * kYPitch + lb * 8) = pack8(px);
         __syncthreads();  // ytile complete; the previous tile's stage has been stored
         uint8_t o[24];
@@ -1151,7 +1158,11 @@ __global__ __launch_bounds__(256) void jpeg_luma_color_kernel(JpegPlan P)
         for (int i = 0; i < 24; ++i) o[i] = 0;
         if (px_live) {
             const uint2 yv = *reinterpret_cast<const uint2*>(ytile + rr * kYPitch + cx);
+#ifdef WICCA_ABL_NOCOLOR  // ablation (timing only): every image coloured as grayscale
+            if (true) {
+#else
             if (im.ncomp == 1) {
+#endif
 #pragma unroll
                 for (int q = 0; q < 8; ++q)
                     o[3 * q] = o[3 * q + 1] = o[3 * q + 2] = (uint8_t)(((q < 4 ? yv.x : yv.y) >> (8 * (q & 3))) & 255);
