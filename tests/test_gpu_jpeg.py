@@ -95,6 +95,28 @@ def test_progressive_matches_libjpeg(kind, H, W, sub, q, rb):
     assert np.array_equal(WJ.decode(data), J.decode_rgb(data))
 
 
+SPLIT = [("scene", 333, 517, 2, 85, (0, 1, 2), 0), ("noise", 135, 241, 0, 70, (2, 0, 1), 0),
+         ("smooth", 64, 80, 1, 50, (1, 2, 0), 3), ("scene", 1080, 1920, 2, 90, (0, 2, 1), 0),
+         ("scene", 17, 9, 2, 95, (2, 1, 0), 1), ("noise", 240, 320, 2, 75, (0, 1, 2), 100)]
+
+
+@pytest.mark.parametrize("kind,H,W,sub,q,order,ri", SPLIT,
+                         ids=[f"{k}-{h}x{w}-s{s}-o{''.join(map(str, o))}-r{r}" for k, h, w, s, q, o, r in SPLIT])
+def test_multiscan_sequential_matches_libjpeg(kind, H, W, sub, q, order, ri):
+    """A sequential file with one non-interleaved scan per component (T.81
+    A.2.2; re-coded from a baseline file by tests/jpeg_scans.py): host entropy
+    decode + the device back end, bit for bit against libjpeg-turbo, and in a
+    batch with the device-decoded original."""
+    from jpeg_scans import coefficients, split_scans
+    img = J.test_image(kind, H, W, H * 5 + W + sub)
+    base = J.encode(img, q, sub)
+    split = split_scans(base, coefficients(base, 1), order, ri)
+    ref = J.decode_rgb(split)
+    assert np.array_equal(WJ.decode(split), ref)
+    got = WJ.decode_batch([base, split])
+    assert np.array_equal(got[1], ref) and np.array_equal(got[0], J.decode_rgb(base))
+
+
 def test_mixed_progressive_and_baseline_batch(tmp_path):
     """One decode call over baseline (device Huffman decode) and progressive
     (host entropy decode) files, and the file-based caller stage over them."""

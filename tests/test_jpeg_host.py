@@ -73,15 +73,8 @@ def test_progressive_parses():
 
 
 def _host_coefs(data, force):
-    arr = np.frombuffer(data, np.uint8)
-    lib = _lib.load()
-    nb = ctypes.c_int64()
-    assert lib.wicca_jpeg_host_coefficients(arr.ctypes.data, arr.size, force, None, 0, ctypes.byref(nb)) == 0
-    out = np.empty(nb.value * 64, np.int16)
-    rc = lib.wicca_jpeg_host_coefficients(arr.ctypes.data, arr.size, force, out.ctypes.data, nb.value,
-                                          ctypes.byref(nb))
-    assert rc == 0, _lib.last_error()
-    return out
+    from jpeg_scans import coefficients
+    return coefficients(data, force)
 
 
 PROG = [("scene", 64, 80, 2, 75, 0), ("noise", 135, 241, 0, 70, 0), ("smooth", 333, 517, 1, 50, 0),
@@ -99,6 +92,54 @@ def test_progressive_coefficients_equal_baseline(kind, H, W, sub, q, rb):
     base = J.encode(img, q, sub, rb)
     prog = J.encode(img, q, sub, rb, progressive=True)
     assert np.array_equal(_host_coefs(base, 1), _host_coefs(prog, 0))
+
+
+SPLIT = [("scene", 64, 80, 2, 75, (0, 1, 2), 0), ("noise", 135, 241, 0, 70, (2, 0, 1), 0),
+         ("smooth", 333, 517, 1, 50, (1, 2, 0), 0), ("gray", 50, 77, 0, 80, (0,), 0),
+         ("scene", 17, 9, 2, 95, (0, 1, 2), 0), ("noise", 201, 299, 2, 60, (0, 2, 1), 0),
+         ("scene", 120, 200, 2, 80, (0, 1, 2), 7), ("gray", 64, 64, 0, 90, (0,), 1),
+         ("smooth", 99, 161, 1, 60, (2, 1, 0), 40)]
+
+
+def _real_blocks(data, coefs):
+    """Mask of the coded blocks: a non-interleaved scan covers only the
+    component's ceil(dw/8) x ceil(dh/8) blocks, not the MCU padding."""
+    from jpeg_scans import _segments
+    sof = next(p for m, p in _segments(data) if m in (0xC0, 0xC1))
+    H, W, nc = (sof[1] << 8) | sof[2], (sof[3] << 8) | sof[4], sof[5]
+    hv = [(sof[7 + 3 * c] >> 4, sof[7 + 3 * c] & 15) if nc > 1 else (1, 1) for c in range(nc)]
+    hmax, vmax = max(h for h, _ in hv), max(v for _, v in hv)
+    mask = []
+    for h, v in hv:
+        bw, bh = -(-W // (8 * hmax)) * h, -(-H // (8 * vmax)) * v
+        wb, hb = -(-(-(-W * h // hmax)) // 8), -(-(-(-H * v // vmax)) // 8)
+        m = np.zeros((bh, bw), bool)
+        m[:hb, :wb] = True
+        mask.append(m.ravel())
+    mask = np.concatenate(mask)
+    assert mask.size * 64 == coefs.size
+    return mask
+
+
+@pytest.mark.parametrize("kind,H,W,sub,q,order,ri", SPLIT,
+                         ids=[f"{k}-{h}x{w}-s{s}-o{''.join(map(str, o))}-r{r}" for k, h, w, s, q, o, r in SPLIT])
+def test_multiscan_sequential_coefficients(kind, H, W, sub, q, order, ri):
+    """A baseline file re-coded as one non-interleaved scan per component (in
+    any component order, own Huffman tables): Pillow decodes it to the same
+    pixels as the original (the writer is right), and the host sequential
+    multi-scan decoder recovers the original's coefficients, with and without
+    restart intervals.  No GPU."""
+    from jpeg_scans import split_scans
+    img = J.test_image(kind, H, W, H * W + sub)
+    base = J.encode(img, q, sub)
+    ref = _host_coefs(base, 1)
+    split = split_scans(base, ref, order, ri)
+    assert split.count(b"\xff\xda") == len(order)
+    assert np.array_equal(J.decode_rgb(split), J.decode_rgb(base))
+    got = _host_coefs(split, int(len(order) == 1))  # one gray scan is a single-scan (device) file
+    mask = np.repeat(_real_blocks(base, ref), 64)
+    assert np.array_equal(got[mask], ref[mask])
+    assert not got[~mask].any()
 
 
 def test_destuff_avx2_matches_scalar(tmp_path):
