@@ -229,10 +229,13 @@ def test_batch_larger_than_one_device_pass():
         assert np.array_equal(got[i], J.decode_rgb(blobs[i])), i
 
 
-def test_six_table_write_kernel_subprocess():
+@pytest.mark.parametrize("env", [{"WICCA_JPEG_WRITE_SLOTS": "6"}, {"WICCA_JPEG_SYNC_CK": "0"}],
+                         ids=["slots6", "no-checkpoints"])
+def test_write_and_sync_variants_subprocess(env):
     """The write pass has a 4-table build (every baseline file) and a 6-table
-    one (extended-sequential files with separate tables per component); force
-    the 6-table kernel in a child process and check the golden files."""
+    one (extended-sequential files with separate tables per component); the
+    sync passes run with or without checkpoints.  Each variant in a child
+    process on the golden files."""
     import subprocess
     import sys
     code = (
@@ -246,7 +249,7 @@ def test_six_table_write_kernel_subprocess():
         "       if hashlib.sha256(o.tobytes()).hexdigest() != c['sha256_rgb']]\n"
         "print('BAD', bad)\n"
         "sys.exit(1 if bad else 0)\n")
-    env = dict(os.environ, WICCA_JPEG_WRITE_SLOTS="6")
+    env = dict(os.environ, **env)
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240,
                        cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert r.returncode == 0, r.stdout + r.stderr

@@ -12,5 +12,5 @@ export TMPDIR=/tmp
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -- \
     python3 "$R/bench.py" --config jpeg --steps 5 --warmup 1 "$@" > "$OUT/bench.log" 2>&1
-python3 "$R/tools/kstats.py" "$OUT/kt" > "$OUT/kstats.txt"
+python3 "$R/tools/kstats.py" "$OUT/kt" --seq jpeg_sync > "$OUT/kstats.txt"
 echo "profile $TAG done"

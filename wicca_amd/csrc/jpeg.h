@@ -129,7 +129,7 @@ struct JpegSegDev {
 };
 
 struct JpegPlan {
-    const uint8_t* stream;   // de-stuffed bytes of every segment (+ 8 zero bytes)
+    const uint8_t* stream;   // de-stuffed bytes of every segment (+ 64 zero bytes)
     const JpegSegDev* segs;
     const int32_t* sub_seg;  // subsequence -> segment
     const JpegImageDev* imgs;

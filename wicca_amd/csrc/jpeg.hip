@@ -30,6 +30,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -56,84 +57,89 @@ struct SubResult {
     DecState end;
     int64_t started;  // blocks whose DC codeword starts in the lane's range
     int32_t dc[kJpegMaxComp];
+    int32_t n_ck;     // round 0: checkpoints recorded (SyncCk)
+};
+
+// Round 0 records, at the first kSyncCk block starts of every lane's guessed
+// decode, the decoder state there and the lane's DC sums so far.  The decode
+// from a state is a function of that state alone, so when a round-1 decode
+// (from the predecessor's end state) reaches one of these states, the rest of
+// it is the round-0 decode from there: the lane stops and takes round 0's end
+// state and counts, minus the checkpoint's prefix.  Huffman codes resynchronise
+// within a few codewords, so round 1 (which had decoded every subsequence in
+// full) costs a few blocks per lane.
+constexpr int kSyncCk = 8;
+struct SyncCk {
+    uint32_t pos_slot;  // (p - lane start) | slot << 24
+    int32_t started;    // blocks started before it
+    int32_t dc[kJpegMaxComp];
     int32_t pad_;
 };
 
-// MSB-first bit reader over the de-stuffed stream: aligned 32-bit loads (one
-// per 32 bits consumed) issued two words ahead of use, so the load latency
-// overlaps the decode of the bits already buffered.  The host pads the stream
-// with zero bytes past its end.
+// MSB-first bit reader over the de-stuffed stream: a 64-bit window refilled
+// 32 bits at a time.  The next word is loaded one refill ahead and kept raw
+// (little-endian), byte-swapped when appended: swapping it on arrival made
+// every refill wait for the load it had just issued, a full memory latency on
+// the serial decode chain.  Positions inside the loop are 32-bit, relative to
+// `base` (the lane's first word).  The host pads the stream with 64 zero bytes
+// past its end (the reader looks at most 12 bytes ahead of its position).
 struct BitReader {
-    const uint32_t* w;
-    int64_t p;     // absolute position of the next unconsumed bit
-    int64_t wi;    // index of the word in n0
-    uint64_t buf;  // n valid bits, MSB-aligned
+    const uint32_t* w;  // stream words from base
+    int64_t base;       // absolute bit position of w[0]
+    int32_t pr;         // next unconsumed bit, relative to base
+    int32_t wi;         // index of the word in nx
+    uint64_t buf;       // n valid bits, MSB-aligned
     int n;
-    uint32_t n0, n1;
+    uint32_t nx;
     __device__ __forceinline__ static uint32_t be(uint32_t x) { return __builtin_bswap32(x); }
     __device__ void reset(const uint8_t* stream, int64_t bitpos)
     {
-        w = reinterpret_cast<const uint32_t*>(stream);
-        p = bitpos;
-        const int64_t word = bitpos >> 5;
-        buf = ((uint64_t)be(w[word]) << 32) | be(w[word + 1]);
-        n = 64;
-        wi = word + 2;
-        n0 = be(w[wi]);
-        n1 = be(w[wi + 1]);
-        const int skip = (int)(bitpos & 31);
-        buf <<= skip;
-        n -= skip;
+        base = bitpos & ~(int64_t)31;
+        w = reinterpret_cast<const uint32_t*>(stream) + (base >> 5);
+        pr = (int32_t)(bitpos - base);
+        buf = ((uint64_t)be(w[0]) << 32) | be(w[1]);
+        wi = 2;
+        nx = w[2];
+        buf <<= pr;
+        n = 64 - pr;
     }
+    __device__ __forceinline__ int64_t p() const { return base + pr; }
     __device__ __forceinline__ void refill()
     {
         if (n <= 32) {
-            buf |= (uint64_t)n0 << (32 - n);
+            buf |= (uint64_t)be(nx) << (32 - n);
             n += 32;
-            n0 = n1;
-            ++wi;
-            n1 = be(w[wi + 1]);
+            nx = w[++wi];
         }
-    }
-    __device__ __forceinline__ uint32_t peek16()
-    {
-        refill();
-        return (uint32_t)(buf >> 48);
     }
     __device__ __forceinline__ void skip(int k)
     {
         buf <<= k;
         n -= k;
-        p += k;
-    }
-    __device__ __forceinline__ uint32_t get(int k)
-    {
-        if (k == 0) return 0;
-        refill();
-        const uint32_t v = (uint32_t)(buf >> (64 - k));
-        skip(k);
-        return v;
+        pr += k;
     }
 };
 
-__device__ __forceinline__ int huff_decode(const HuffDev& t, BitReader& br)
+// (code length << 8) | symbol of the codeword at the top of `look` (the next
+// 32 bits); a bit string that is no code (only off the true decode path)
+// reads as symbol 0 after 16 bits, as in jdhuff.
+__device__ __forceinline__ uint32_t huff_lookup(const HuffDev& t, uint32_t look)
 {
-    const uint32_t look = br.peek16();
-    const uint32_t e = t.lut[look >> (16 - kHuffLutBits)];
-    if (e) {
-        br.skip((int)(e >> 8));
-        return (int)(e & 255);
-    }
-    for (int l = kHuffLutBits + 1; l <= 16; ++l) {
-        const int32_t code = (int32_t)(look >> (16 - l));
-        if (code <= t.maxcode[l]) {
-            br.skip(l);
-            return t.vals[(t.valoff[l] + code) & 255];
+    uint32_t e = t.lut[look >> (32 - kHuffLutBits)];
+    if (e == 0) {
+        // a code longer than the lookup: every length's maxcode / valoff read
+        // at once and the shortest match selected, so the slow path costs two
+        // LDS round trips rather than one per length
+        int l = 0, vo = 0;
+#pragma unroll
+        for (int L = 16; L > kHuffLutBits; --L) {
+            const bool m = (int32_t)(look >> (32 - L)) <= t.maxcode[L];
+            l = m ? L : l;
+            vo = m ? t.valoff[L] : vo;
         }
+        e = l ? ((uint32_t)l << 8) | t.vals[(vo + (int32_t)(look >> (32 - l))) & 255] : 16u << 8;
     }
-    // not a code (only off the true decode path): jdhuff returns 0
-    br.skip(16);
-    return 0;
+    return e;
 }
 
 // HUFF_EXTEND (jdhuff.h)
@@ -150,6 +156,7 @@ struct DecGeom {
     int32_t slot_comp[kJpegMaxSlots], slot_h[kJpegMaxSlots], slot_v[kJpegMaxSlots];
     int32_t comp_h[kJpegMaxComp], comp_v[kJpegMaxComp], comp_bw[kJpegMaxComp];
     int32_t dc_tab[kJpegMaxComp], ac_tab[kJpegMaxComp];  // LDS table slots
+    uint32_t slot_tab[kJpegMaxSlots];  // per MCU slot: dc_tab | ac_tab << 8 | component << 16
 };
 
 // Position of a decode-order block: MCU column / row and slot, advanced
@@ -198,10 +205,14 @@ constexpr int kLaneBlock = 64;  // int16 per lane in LDS: one block
 #endif
 
 // Per-wave LDS of the write pass: every lane's block under assembly, and the
-// owner lanes of the blocks completed in the current iteration.
+// owner lanes of the blocks completed in the current iteration; and the
+// workgroup's zigzag -> natural table (a __constant__ array indexed by a
+// per-lane k compiles to a global load, and waiting for it also waited for
+// the bit reader's prefetch on every AC coefficient).
 struct WaveStage {
-    int16_t* blocks;  // 64 * kLaneBlock
-    uint8_t* owner;   // 64
+    int16_t* blocks;     // 64 * kLaneBlock
+    uint8_t* owner;      // 64
+    const uint8_t* nat;  // 80
 };
 
 __device__ __forceinline__ void wave_lds_sync()
@@ -266,9 +277,9 @@ __device__ __forceinline__ void flush_blocks(bool done, int64_t blk, uint64_t nz
 }
 
 // Zigzag positions [from, to) of block `blk` set to zero (2-B stores).
-__device__ __forceinline__ void zero_zig(int16_t* coef, int64_t blk, int from, int to)
+__device__ __forceinline__ void zero_zig(int16_t* coef, const uint8_t* nat, int64_t blk, int from, int to)
 {
-    for (int z = from; z < to; ++z) coef[blk * 64 + kNatural[z]] = 0;
+    for (int z = from; z < to; ++z) coef[blk * 64 + nat[z]] = 0;
 }
 
 // Every coefficient of every block [block_lo, block_end) is written exactly
@@ -278,12 +289,22 @@ __device__ __forceinline__ void zero_zig(int16_t* coef, int64_t blk, int from, i
 // each lane covering its own zigzag range [k at its start, k at its end); the
 // last lane of a segment zeroes what the segment's data never reached (a
 // truncated or corrupt stream: libjpeg-turbo substitutes zeros there too).
-template <bool WRITE>
-__device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br, int64_t stop,
-                           DecState& st, int64_t& started, int32_t (&dc)[kJpegMaxComp], int64_t g,
-                           int64_t block_lo, int64_t block_end, int16_t* coef, const WaveStage* ws = nullptr,
-                           bool seg_last = false)
+//
+// CK (sync passes only): 1 records checkpoints into ck (returns their count),
+// at the first block start at or after every ck_step bits from ck_base;
+// 2 stops at the first of the n_ck checkpoints in ck the decode reaches
+// (returns its index, -1 if none; *hit_ck gets it).  ck_base = the lane's
+// start bit.
+template <bool WRITE, int CK = 0>
+__device__ int decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br, int64_t stop,
+                          DecState& st, int64_t& started, int32_t (&dc)[kJpegMaxComp], int64_t g,
+                          int64_t block_lo, int64_t block_end, int16_t* coef, const WaveStage* ws = nullptr,
+                          bool seg_last = false, SyncCk* ck = nullptr, int n_ck = 0, int64_t ck_base = 0,
+                          SyncCk* hit_ck = nullptr, int ck_step = 0)
 {
+    int nck = 0, hit = -1;
+    uint32_t cur = 0;  // CK 2: pos_slot of checkpoint nck
+    if (CK == 2 && n_ck > 0) cur = ck[0].pos_slot;
     int64_t blk = -1;
     bool staged = false;
     uint64_t nz = 0;
@@ -296,15 +317,51 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
         if (g >= block_lo && g < block_end) blk = pos.index(im);
         zk = st.k;  // the block in progress at the start: this lane owns [st.k, ...)
     }
-    while (br.p < stop) {
-        const int c = im.slot_comp[st.slot];
-        // one table lookup for both symbol kinds keeps the lanes of a wave together
-        const int sym = huff_decode(tabs[st.k == 0 ? im.dc_tab[c] : im.ac_tab[c]], br);
-        if (st.k == 0) {
-            const int s = min(sym, 16);  // > 11 only in corrupt streams
-            const int diff = s ? extend(br.get(s), s) : 0;
-            ++started;
-            dc[c] += diff;
+    // the current slot's component and tables, re-read when the slot advances
+    // (one LDS read per block, not two dependent ones per codeword)
+    uint32_t sti = im.slot_tab[st.slot];
+    int c = (int)(sti >> 16);
+    const HuffDev* tdc = &tabs[sti & 255];
+    const HuffDev* tac = &tabs[(sti >> 8) & 255];
+    // 32-bit positions relative to the reader's base inside the loop
+    const int32_t stop_r = (int32_t)(stop - br.base);
+    const int32_t ck_off = (int32_t)(br.base - ck_base);  // reader-relative -> checkpoint-relative
+    int32_t nstart = 0;  // blocks started in this run
+    while (br.pr < stop_r) {
+        if (CK == 1 && st.k == 0 && nck < kSyncCk && br.pr + ck_off >= nck * ck_step) {
+            SyncCk e;
+            e.pos_slot = (uint32_t)(br.pr + ck_off) | ((uint32_t)st.slot << 24);
+            e.started = (int32_t)started + nstart;
+            for (int q = 0; q < kJpegMaxComp; ++q) e.dc[q] = dc[q];
+            e.pad_ = 0;
+            ck[nck++] = e;
+        }
+        if (CK == 2 && st.k == 0 && nck < n_ck) {
+            const uint32_t here = (uint32_t)(br.pr + ck_off);
+            while ((cur & 0xFFFFFFu) < here) {  // checkpoints are in increasing bit order
+                if (++nck == n_ck) break;
+                cur = ck[nck].pos_slot;
+            }
+            if (nck < n_ck && cur == (here | ((uint32_t)st.slot << 24))) {
+                hit = nck;
+                *hit_ck = ck[nck];
+                break;
+            }
+        }
+        // the codeword and its value bits in one step: after the refill the
+        // window holds >= 33 bits, the longest code (16) plus the longest value
+        // (16); one table lookup for both symbol kinds keeps a wave together
+        br.refill();
+        const uint32_t look = (uint32_t)(br.buf >> 32);
+        const bool isdc = st.k == 0;
+        const uint32_t e = huff_lookup(*(isdc ? tdc : tac), look);
+        const int len = (int)(e >> 8), sym = (int)(e & 255);
+        const int s = isdc ? min(sym, 16) : (sym & 15);  // a DC size > 11 only in corrupt streams
+        const int v = s ? extend((look << len) >> (32 - s), s) : 0;
+        br.skip(len + s);
+        if (isdc) {
+            ++nstart;
+            dc[c] += v;
             if (WRITE) {
                 if (g >= 0) pos.next(im);
                 ++g;
@@ -322,17 +379,16 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
             }
             st.k = 1;
         } else {
-            const int r = sym >> 4, s = sym & 15;
+            const int r = sym >> 4;
             if (s) {
                 st.k += r;
-                const int v = extend(br.get(s), s);
                 if (WRITE && blk >= 0 && st.k < 64) {
-                    const int n = kNatural[st.k];
+                    const int n = ws->nat[st.k];
                     if (staged) {
                         lb[n] = (int16_t)v;
                         nz |= 1ull << n;
                     } else {
-                        zero_zig(coef, blk, zk, st.k);
+                        zero_zig(coef, ws->nat, blk, zk, st.k);
                         coef[blk * 64 + n] = (int16_t)v;
                         zk = st.k + 1;
                     }
@@ -347,24 +403,31 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
         bool done = false;
         if (st.k >= 64) {
             done = WRITE && staged;  // a whole block of this lane
-            if (WRITE && !staged && blk >= 0) zero_zig(coef, blk, zk, 64);
+            if (WRITE && !staged && blk >= 0) zero_zig(coef, ws->nat, blk, zk, 64);
             staged = false;
             st.slot = st.slot + 1 == im.bpm ? 0 : st.slot + 1;
             st.k = 0;
+            sti = im.slot_tab[st.slot];
+            c = (int)(sti >> 16);
+            tdc = &tabs[sti & 255];
+            tac = &tabs[(sti >> 8) & 255];
         }
+        // every codeword: deferring the flush until 4 / 8 / 16 blocks wait (the
+        // finished lanes idle meanwhile) measured 6.1 / 7.4 / 7.5 ms per 25 x 8K
+        // call against 3.0 ms
         if (WRITE && WICCA_JPEG_STAGE) flush_blocks(done, blk, nz, *ws, coef);
     }
     if (WRITE && blk >= 0 && st.k > 0) {  // the range ends inside block blk: this lane's part [.., st.k)
         const int kend = min(st.k, 64);
         if (staged) {
             for (int z = 0; z < kend; ++z) {
-                const int n = kNatural[z];
+                const int n = ws->nat[z];
                 coef[blk * 64 + n] = ((nz >> n) & 1) ? lb[n] : (int16_t)0;
             }
         } else {
-            zero_zig(coef, blk, zk, kend);
+            zero_zig(coef, ws->nat, blk, zk, kend);
         }
-        if (seg_last) zero_zig(coef, blk, kend, 64);  // nobody decodes the rest
+        if (seg_last) zero_zig(coef, ws->nat, blk, kend, 64);  // nobody decodes the rest
     }
     if (WRITE && seg_last) {  // blocks the segment's data never started
         if (g >= 0) pos.next(im);
@@ -376,7 +439,9 @@ __device__ void decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br
             pos.next(im);
         }
     }
-    st.p = br.p;
+    st.p = br.p();
+    started += nstart;
+    return CK == 1 ? nck : hit;
 }
 
 // The image's Huffman tables, staged in LDS: the host stores an image's
@@ -421,6 +486,10 @@ __device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageD
             g.dc_tab[c] = c < ncomp ? imp->dc_tab[c] - first : 0;
             g.ac_tab[c] = c < ncomp ? imp->ac_tab[c] - first : 0;
         }
+        for (int k = 0; k < kJpegMaxSlots; ++k) {
+            const int c = min(max(g.slot_comp[k], 0), kJpegMaxComp - 1);
+            g.slot_tab[k] = (uint32_t)g.dc_tab[c] | ((uint32_t)g.ac_tab[c] << 8) | ((uint32_t)c << 16);
+        }
     }
     __syncthreads();
 }
@@ -438,9 +507,15 @@ __device__ __forceinline__ bool same_state(const DecState& a, const DecState& b)
     return a.p == b.p && a.slot == b.slot && a.k == b.k;
 }
 
-__global__ __launch_bounds__(kJThreads) void jpeg_sync_kernel(JpegPlan P, const SubResult* prev,
+// Keep every instantiation at <= 64 VGPRs (8 waves per SIMD): jpeg_sub_bits
+// sizes the subsequences so that one generation of lanes at that occupancy
+// covers a large batch (256 CUs x 4 SIMDs x 8 waves x 64 lanes = 524288); more
+// registers leave part of the grid to a second, serial generation of the
+// latency-bound decode (66 VGPRs cost round 0 a third of its time).
+template <int CK>  // 0 plain decode, 1 round 0 recording checkpoints, 2 round 1 stopping at one
+__global__ __launch_bounds__(kJThreads, 8) void jpeg_sync_kernel(JpegPlan P, const SubResult* prev,
                                                              SubResult* next, int round, int* changed,
-                                                             const SubResult* older)
+                                                             const SubResult* older, SyncCk* cks, int* stats)
 {
     const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
     __shared__ ImgTabs<2 * kJpegMaxComp> tabs;
@@ -479,17 +554,41 @@ __global__ __launch_bounds__(kJThreads) void jpeg_sync_kernel(JpegPlan P, const 
             }
         }
     }
+    if (stats) {  // WICCA_JPEG_TIMING: lanes decoding in this round (one atomic per wave)
+        const uint64_t m = __ballot(decode);
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(stats, (int)__popcll(m));
+    }
     if (!__syncthreads_or(decode)) return;  // uniform: nothing to decode in this workgroup
     stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);
     if (!decode) return;
     const DecGeom& im = tabs.g;
     SubResult r;
     r.started = 0;
-    r.pad_ = 0;
+    r.n_ck = 0;
     int32_t dc[kJpegMaxComp] = {0, 0, 0};
     BitReader br;
     br.reset(P.stream, st.p);
-    decode_run<false>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr);
+    SyncCk* ck = cks + i * kSyncCk;
+    if (CK == 1) {
+        r.n_ck = decode_run<false, 1>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr, nullptr, false, ck,
+                                      0, b0, nullptr, P.sub_bits / kSyncCk);
+    } else if (CK == 2) {
+        const SubResult& o = prev[i];  // this lane's round-0 result and checkpoints
+        SyncCk h;
+        const int hit = decode_run<false, 2>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr, nullptr,
+                                             false, ck, o.n_ck, b0, &h);
+        if (hit >= 0) {  // the rest is round 0's decode from checkpoint `hit`
+            if (stats) {
+                const uint64_t m = __ballot(true);
+                if (__ffsll((long long)m) - 1 == (int)(threadIdx.x & 63)) atomicAdd(stats + 1, (int)__popcll(m));
+            }
+            st = o.end;
+            r.started += o.started - h.started;
+            for (int c = 0; c < kJpegMaxComp; ++c) dc[c] += o.dc[c] - h.dc[c];
+        }
+    } else {
+        decode_run<false>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr);
+    }
     r.end = st;
     for (int c = 0; c < kJpegMaxComp; ++c) r.dc[c] = dc[c];
     if (round > 0 && !same_state(prev[i].end, st)) *changed = 1;
@@ -559,8 +658,13 @@ __global__ __launch_bounds__(256) void jpeg_scan_kernel(JpegPlan P, const SubRes
 }
 
 // Final pass: scatter coefficients (converged start states, scanned bases).
-// NS table slots: 4 (every baseline image: 2 DC + 2 AC tables) keeps the
-// workgroup's LDS under 40 KB, i.e. 4 workgroups per CU instead of 3.
+// Whole blocks leave through 32 KB of LDS staging per workgroup (4 waves per
+// SIMD).  Storing only the nonzero coefficients straight from the decode into
+// a pre-zeroed buffer (8 waves per SIMD, no staging) measured 7.58 ms against
+// 2.99 ms per 25 x 8K call: 2-B stores from 64 lanes to 64 different blocks
+// cost far more than the occupancy gains.  NS table slots: 4 (every baseline
+// image: 2 DC + 2 AC tables) keeps the workgroup's LDS under 40 KB, i.e. 4
+// workgroups per CU instead of 3.
 template <int NS>
 __global__ __launch_bounds__(kJThreads, NS <= 4 ? 4 : 1) void jpeg_write_kernel(JpegPlan P, const SubResult* res,
                                                                  const SubBase* base)
@@ -571,7 +675,9 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 4 : 1) void jpeg_write_kernel(
     __shared__ __attribute__((aligned(16))) int16_t lanes[kJThreads * kLaneBlock];
     __shared__ uint8_t s_owner[kJThreads];
 #endif
-    stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);
+    __shared__ uint8_t s_nat[80];
+    if (threadIdx.x < 80) s_nat[threadIdx.x] = (uint8_t)kNatural[threadIdx.x];
+    stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);  // its barrier covers s_nat
     const DecGeom& im = tabs.g;
     if (i >= P.n_sub || P.sub_seg[i] < 0) return;  // padding lane
     const JpegSegDev sg = P.segs[P.sub_seg[i]];
@@ -592,9 +698,9 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 4 : 1) void jpeg_write_kernel(
     br.reset(P.stream, st.p);
 #if WICCA_JPEG_STAGE
     const int w0 = (int)(threadIdx.x & ~63u);  // the wave's first lane
-    const WaveStage ws{lanes + w0 * kLaneBlock, s_owner + w0};
+    const WaveStage ws{lanes + w0 * kLaneBlock, s_owner + w0, s_nat};
 #else
-    const WaveStage ws{nullptr, nullptr};
+    const WaveStage ws{nullptr, nullptr, s_nat};
 #endif
     // the block in progress at the start was started by an earlier lane
     decode_run<true>(im, tabs.t, br, b1, st, started, dc, sg.block0 + b.block - 1, sg.block0,
@@ -1245,7 +1351,8 @@ bool jpeg_fused()
 size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg)
 {
     (void)n_seg;
-    return (size_t)n_sub * (3 * sizeof(SubResult) + sizeof(SubBase)) + 64 + kJpegMaxJobs * sizeof(IdctJob);
+    return (size_t)n_sub * (3 * sizeof(SubResult) + sizeof(SubBase) + kSyncCk * sizeof(SyncCk)) + 64 +
+           kJpegMaxJobs * sizeof(IdctJob);
 }
 
 hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* scratch, int64_t n_images,
@@ -1258,6 +1365,7 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     SubBase* sb = (SubBase*)(rc + P.n_sub);
     int* changed = (int*)(sb + P.n_sub);
     IdctJob* jobs = (IdctJob*)((uint8_t*)changed + 64);
+    SyncCk* cks = (SyncCk*)(jobs + kJpegMaxJobs);
     // IDCT jobs: every (image, component); uploaded first, while the stream
     // still waits for the entropy-coded data
     // fused back end (default; WICCA_JPEG_FUSED=0: separate IDCT and colour
@@ -1286,8 +1394,22 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
         const uint32_t grid = (uint32_t)((P.n_sub + kJThreads - 1) / kJThreads);
         // round 0 + rounds until no end state changes; results rotate through
         // three buffers (older = round - 2, cur = round - 1, nxt = this round)
-        hipLaunchKernelGGL(jpeg_sync_kernel, dim3(grid), dim3(kJThreads), 0, s, P, ra, ra, 0, changed,
-                           (const SubResult*)nullptr);
+        // WICCA_JPEG_SYNC_CK=0: no checkpoints (every round-1 lane decodes its whole subsequence);
+        // WICCA_JPEG_TIMING: per-round counts of decoding lanes and checkpoint hits to stderr
+        static const int ck_mode = [] {
+            const char* e = getenv("WICCA_JPEG_SYNC_CK");
+            return e ? atoi(e) : 1;
+        }();
+        static const bool stats_on = getenv("WICCA_JPEG_TIMING") != nullptr;
+        constexpr int kStatRounds = 6;
+        int* stats = changed + 4;  // [round][decoding lanes, checkpoint hits]
+        if (stats_on && (e = hipMemsetAsync(stats, 0, 2 * kStatRounds * sizeof(int), s)) != hipSuccess) return e;
+        if (ck_mode)
+            hipLaunchKernelGGL(jpeg_sync_kernel<1>, dim3(grid), dim3(kJThreads), 0, s, P, ra, ra, 0, changed,
+                               (const SubResult*)nullptr, cks, stats_on ? stats : nullptr);
+        else
+            hipLaunchKernelGGL(jpeg_sync_kernel<0>, dim3(grid), dim3(kJThreads), 0, s, P, ra, ra, 0, changed,
+                               (const SubResult*)nullptr, cks, stats_on ? stats : nullptr);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
         SubResult* older = rc;
@@ -1298,8 +1420,13 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             int h_changed = 0;
             e = hipMemsetAsync(changed, 0, sizeof(int), s);
             if (e != hipSuccess) return e;
-            hipLaunchKernelGGL(jpeg_sync_kernel, dim3(grid), dim3(kJThreads), 0, s, P, cur, nxt, rounds + 1, changed,
-                               (const SubResult*)older);
+            int* st_r = stats_on && rounds + 1 < kStatRounds ? stats + 2 * (rounds + 1) : nullptr;
+            if (ck_mode && rounds == 0)
+                hipLaunchKernelGGL(jpeg_sync_kernel<2>, dim3(grid), dim3(kJThreads), 0, s, P, cur, nxt, rounds + 1,
+                                   changed, (const SubResult*)older, cks, st_r);
+            else
+                hipLaunchKernelGGL(jpeg_sync_kernel<0>, dim3(grid), dim3(kJThreads), 0, s, P, cur, nxt, rounds + 1,
+                                   changed, (const SubResult*)older, cks, st_r);
             e = hipGetLastError();
             if (e == hipSuccess) e = hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
@@ -1312,6 +1439,14 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             if (!h_changed || rounds > P.n_sub) break;
         }
         if (sync_rounds) *sync_rounds = rounds;
+        if (stats_on) {
+            int h[2 * kStatRounds];
+            if ((e = hipMemcpy(h, stats, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess) return e;
+            fprintf(stderr, "[wicca jpeg] %lld subsequences; decoding lanes / checkpoint hits per round:",
+                    (long long)P.n_sub);
+            for (int r = 0; r <= std::min(rounds, kStatRounds - 1); ++r) fprintf(stderr, " %d/%d", h[2 * r], h[2 * r + 1]);
+            fprintf(stderr, "\n");
+        }
         hipLaunchKernelGGL(jpeg_scan_kernel, dim3((uint32_t)P.n_seg), dim3(256), 0, s, P, cur, sb);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         static const bool force6 = [] {  // WICCA_JPEG_WRITE_SLOTS=6: the 6-table kernel for every batch (tests)
