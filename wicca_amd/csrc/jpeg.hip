@@ -733,7 +733,10 @@ __device__ __forceinline__ int64_t descale(int64_t x, int n) { return (x + ((int
 __device__ __forceinline__ int32_t descale32(int32_t x, int n) { return (x + (1 << (n - 1))) >> n; }
 
 #ifndef WICCA_IDCT32
-#define WICCA_IDCT32 1  // 0: every IDCT pass in 64-bit arithmetic
+#define WICCA_IDCT32 1  // 0: every chroma IDCT pass in 64-bit arithmetic
+#endif
+#ifndef WICCA_LUMA_IDCT32
+#define WICCA_LUMA_IDCT32 1  // 0: the fused luma IDCT always in 64-bit passes
 #endif
 constexpr int32_t kIdct32Max = 12600;  // 32-bit IDCT pass exact for inputs within +-kIdct32Max (with the descale rounding term)
 
@@ -750,13 +753,24 @@ __device__ __forceinline__ uint8_t idct_limit(int64_t v)
 // variant, exact while every input is below 2^13.5 — intermediates stay under
 // 2^17.45 times the input bound — ran slower: 1.81 vs 1.43 ms per 25 x 8K,
 // both paths taken within waves.)
+// x * c for the butterfly's constants: in the 32-bit passes both factors are
+// below 2^23 in magnitude (inputs <= kIdct32Max, sums of a few of them,
+// constants < 2^15), so the full-rate 24-bit multiply v_mul_i32_i24 gives the
+// exact product; a plain int32 multiply is the quarter-rate v_mul_lo_u32.
+template <typename T>
+__device__ __forceinline__ T mulk(T x, int64_t c);
+template <>
+__device__ __forceinline__ int32_t mulk<int32_t>(int32_t x, int64_t c) { return __mul24(x, (int)c); }
+template <>
+__device__ __forceinline__ int64_t mulk<int64_t>(int64_t x, int64_t c) { return x * c; }
+
 template <typename T>
 __device__ __forceinline__ void islow_1d(const T (&v)[8], T (&o)[8])
 {
     T z2 = v[2], z3 = v[6];
-    T z1 = (z2 + z3) * (T)FIX_0_541196100;
-    T tmp2 = z1 + z3 * (T)(-FIX_1_847759065);
-    T tmp3 = z1 + z2 * (T)FIX_0_765366865;
+    T z1 = mulk<T>(z2 + z3, FIX_0_541196100);
+    T tmp2 = z1 + mulk<T>(z3, (-FIX_1_847759065));
+    T tmp3 = z1 + mulk<T>(z2, FIX_0_765366865);
     z2 = v[0];
     z3 = v[4];
     T tmp0 = (z2 + z3) * ((T)1 << kConstBits);
@@ -770,15 +784,15 @@ __device__ __forceinline__ void islow_1d(const T (&v)[8], T (&o)[8])
     z2 = tmp1 + tmp2;
     z3 = tmp0 + tmp2;
     T z4 = tmp1 + tmp3;
-    const T z5 = (z3 + z4) * (T)FIX_1_175875602;
-    tmp0 = tmp0 * (T)FIX_0_298631336;
-    tmp1 = tmp1 * (T)FIX_2_053119869;
-    tmp2 = tmp2 * (T)FIX_3_072711026;
-    tmp3 = tmp3 * (T)FIX_1_501321110;
-    z1 = z1 * (T)(-FIX_0_899976223);
-    z2 = z2 * (T)(-FIX_2_562915447);
-    z3 = z3 * (T)(-FIX_1_961570560);
-    z4 = z4 * (T)(-FIX_0_390180644);
+    const T z5 = mulk<T>(z3 + z4, FIX_1_175875602);
+    tmp0 = mulk<T>(tmp0, FIX_0_298631336);
+    tmp1 = mulk<T>(tmp1, FIX_2_053119869);
+    tmp2 = mulk<T>(tmp2, FIX_3_072711026);
+    tmp3 = mulk<T>(tmp3, FIX_1_501321110);
+    z1 = mulk<T>(z1, (-FIX_0_899976223));
+    z2 = mulk<T>(z2, (-FIX_2_562915447));
+    z3 = mulk<T>(z3, (-FIX_1_961570560));
+    z4 = mulk<T>(z4, (-FIX_0_390180644));
     z3 += z5;
     z4 += z5;
     tmp0 += z1 + z3;
@@ -804,28 +818,24 @@ __device__ __forceinline__ void islow_1d(const T (&v)[8], T (&o)[8])
 constexpr int kIdctBlocksPerWg = 32;
 
 // Lane r of the 8 lanes of one block: dequantised row r in, row r of the
-// block's samples out (px).  `t` is the block's 64-int LDS transpose area;
-// every lane of the wave must call this (wave barriers), `live` is uniform
-// over the block's 8 lanes.
-// Position of element (row i, column j) of a block's 8x8 LDS transpose area:
-// column-major with each column rotated by its index, and the whole area
-// rotated by 8 words per block of the wave (rot).  Writing a row (lane = row,
-// one column per instruction) and reading a column (lane = column, one row
-// per instruction) then touch 64 different banks across the wave's 8 blocks;
-// the plain row-major layout put every block's lanes on the same 8 banks
-// (8-way conflicts on every transpose access).
-__device__ __forceinline__ int tix(int rot, int i, int j) { return (8 * j + ((i + j) & 7) + rot) & 63; }
+// block's samples out (px).  `t` is the block's LDS transpose area
+// (kTrBlock ints); every lane of the wave must call this (wave barriers),
+// `live` is uniform over the block's 8 lanes.
+// The transpose area is row-major with a 9-word row pitch, kTrBlock = 72 words
+// per block.  The b32 accesses are banked (word mod 32) per 32-lane half wave
+// (4 blocks x 8 lanes): a row write or read (lane = row: words 9r + 72b + j)
+// and a column read (lane = column: 9i + 72b + r) then hit 32 distinct banks,
+// with every address a base plus a constant offset.  The 8-word pitch put
+// each half wave on 4 banks (8-way conflicts on the row accesses); a rotated
+// swizzle removed them at the price of per-access index arithmetic.
+constexpr int kTrPitch = 9, kTrBlock = 8 * kTrPitch;
 
-// SWZ: the rotated transpose layout (tix) instead of row-major; I32: 32-bit
-// passes where exact.  The chroma IDCT kernel is faster with both (346 vs
-// 394 us per 25 x 8K call), the VALU-bound fused luma kernel without them
-// (1.97 vs 2.11 ms: the index arithmetic costs more than the conflicts).
-template <bool SWZ, bool I32>
+// I32: 32-bit passes where exact (else always 64-bit, as JLONG).
+template <bool I32>
 __device__ __forceinline__ void idct8_lane_v(uint4 v, const uint16_t* qt, int r, bool live, int32_t* t,
                                              uint8_t (&px)[8])
 {
-    const int rot = 8 * ((threadIdx.x >> 3) & 7);  // the block's place in its wave
-    auto at = [&](int i, int j) { return SWZ ? tix(rot, i, j) : i * 8 + j; };
+    auto at = [&](int i, int j) { return i * kTrPitch + j; };
     if (live) {
         const uint4 qv = *reinterpret_cast<const uint4*>(qt + r * 8);
         const uint32_t cw[4] = {v.x, v.y, v.z, v.w}, qw[4] = {qv.x, qv.y, qv.z, qv.w};
@@ -900,7 +910,7 @@ __device__ __forceinline__ void idct8_lane(const int16_t* blk, const uint16_t* q
                                            uint8_t (&px)[8])
 {
     const uint4 v = live ? *reinterpret_cast<const uint4*>(blk + r * 8) : uint4{0, 0, 0, 0};
-    idct8_lane_v<true, WICCA_IDCT32 != 0>(v, qt, r, live, t, px);
+    idct8_lane_v<WICCA_IDCT32 != 0>(v, qt, r, live, t, px);
 }
 
 __device__ __forceinline__ uint2 pack8(const uint8_t (&px)[8])
@@ -917,7 +927,7 @@ __device__ __forceinline__ void idct_group(const JpegPlan& P, const IdctJob& jb,
     const int64_t b = group * kIdctBlocksPerWg + lb;
     const bool live = b < (int64_t)jb.bw * jb.bh;  // uniform over the block's 8 lanes
     uint8_t px[8];
-    idct8_lane(P.coef + (jb.block0 + b) * 64, P.imgs[jb.img].qt[jb.comp], r, live, tr + lb * 64, px);
+    idct8_lane(P.coef + (jb.block0 + b) * 64, P.imgs[jb.img].qt[jb.comp], r, live, tr + lb * kTrBlock, px);
     if (!live) return;
     const int by = (int)(b / jb.bw), bx = (int)(b - (int64_t)by * jb.bw);
     const int64_t pitch = (int64_t)jb.bw * 8;
@@ -931,7 +941,7 @@ constexpr int kIdctGroups = 8;
 
 __global__ __launch_bounds__(256) void jpeg_idct_kernel(JpegPlan P, const IdctJob* jobs)
 {
-    __shared__ int32_t tr[kIdctBlocksPerWg * 64];
+    __shared__ int32_t tr[kIdctBlocksPerWg * kTrBlock];
     const IdctJob jb = jobs[blockIdx.y];
     const int64_t n_groups = ((int64_t)jb.bw * jb.bh + kIdctBlocksPerWg - 1) / kIdctBlocksPerWg;
 #pragma unroll 1
@@ -1056,9 +1066,9 @@ __device__ __forceinline__ void color_row(const JpegPlan& P, const JpegImageDev&
             for (int q = 0; q < 4; ++q) {
                 const int Y = (int)((y4 >> (8 * q)) & 255);
                 const int cb = cbv[q] - 128, cr = crv[q] - 128;
-                const int crr = (91881 * cr + 32768) >> 16;
-                const int cbb = (116130 * cb + 32768) >> 16;
-                const int g = (-46802 * cr + (-22554 * cb + 32768)) >> 16;
+                const int crr = (__mul24(91881, cr) + 32768) >> 16;
+                const int cbb = (__mul24(116130, cb) + 32768) >> 16;
+                const int g = (__mul24(-46802, cr) + (__mul24(-22554, cb) + 32768)) >> 16;
                 o[3 * q] = clamp255(Y + crr);
                 o[3 * q + 1] = clamp255(Y + g);
                 o[3 * q + 2] = clamp255(Y + cbb);
@@ -1165,6 +1175,41 @@ __device__ __forceinline__ void chroma8_h2v2(const uint8_t* plane, int64_t pitch
     }
 }
 
+// The same for the fused kernel's lanes (c = x/2 a multiple of 4) away from
+// the plane's edges, two samples per 32-bit operation: the bytes of a chroma
+// row word split into even and odd 16-bit halves, 3 * near + far of two
+// columns in one integer multiply-add (each half <= 1020), then each pair of
+// outputs (3 * t[j+1] + t[j or j+2] + 8 or 7) >> 4 in one more (<= 4088 per
+// half, no carry between them).  One 12-byte load per chroma row (columns
+// c-4 .. c+7) instead of four unaligned 4-byte windows.  False: use chroma8_h2v2.
+__device__ __forceinline__ bool chroma8_h2v2_pair(const uint8_t* plane, int64_t pitch, int dw, int dh, int x, int y,
+                                                  int (&out)[8])
+{
+    const int c = x >> 1, iy = y >> 1;
+    if (c < 4 || c + 4 > dw - 1 || c + 8 > pitch) return false;
+    const int oy = (y & 1) ? min(iy + 1, dh - 1) : max(iy - 1, 0);
+    const uint3 a = *reinterpret_cast<const uint3*>(plane + (int64_t)iy * pitch + c - 4);
+    const uint3 b = *reinterpret_cast<const uint3*>(plane + (int64_t)oy * pitch + c - 4);
+    constexpr uint32_t kM = 0x00FF00FFu;
+    const uint32_t te = 3u * (a.y & kM) + (b.y & kM);                // (t3, t1): columns c+2, c
+    const uint32_t to = 3u * ((a.y >> 8) & kM) + ((b.y >> 8) & kM);  // (t4, t2): columns c+3, c+1
+    const uint32_t t0 = 3u * (a.x >> 24) + (b.x >> 24);              // column c-1
+    const uint32_t t5 = 3u * (a.z & 255u) + (b.z & 255u);            // column c+4
+    const uint32_t p04 = ((3u * te + ((to << 16) | t0) + 0x00080008u) >> 4) & kM;
+    const uint32_t p15 = ((3u * te + to + 0x00070007u) >> 4) & kM;
+    const uint32_t p26 = ((3u * to + te + 0x00080008u) >> 4) & kM;
+    const uint32_t p37 = ((3u * to + ((t5 << 16) | (te >> 16)) + 0x00070007u) >> 4) & kM;
+    out[0] = (int)(p04 & 255u);
+    out[4] = (int)(p04 >> 16);
+    out[1] = (int)(p15 & 255u);
+    out[5] = (int)(p15 >> 16);
+    out[2] = (int)(p26 & 255u);
+    out[6] = (int)(p26 >> 16);
+    out[3] = (int)(p37 & 255u);
+    out[7] = (int)(p37 >> 16);
+    return true;
+}
+
 __device__ __forceinline__ void ycc8_to_rgb(uint32_t ylo, uint32_t yhi, const int (&cbv)[8], const int (&crv)[8],
                                             uint8_t (&o)[24])
 {
@@ -1172,9 +1217,10 @@ __device__ __forceinline__ void ycc8_to_rgb(uint32_t ylo, uint32_t yhi, const in
     for (int q = 0; q < 8; ++q) {
         const int Y = (int)(((q < 4 ? ylo : yhi) >> (8 * (q & 3))) & 255);
         const int cb = cbv[q] - 128, cr = crv[q] - 128;
-        const int crr = (91881 * cr + 32768) >> 16;
-        const int cbb = (116130 * cb + 32768) >> 16;
-        const int g = (-46802 * cr + (-22554 * cb + 32768)) >> 16;
+        // 24-bit multiplies (full rate): |cb|, |cr| <= 128, the constants < 2^17
+        const int crr = (__mul24(91881, cr) + 32768) >> 16;
+        const int cbb = (__mul24(116130, cb) + 32768) >> 16;
+        const int g = (__mul24(-46802, cr) + (__mul24(-22554, cb) + 32768)) >> 16;
         o[3 * q] = clamp255(Y + crr);
         o[3 * q + 1] = clamp255(Y + g);
         o[3 * q + 2] = clamp255(Y + cbb);
@@ -1198,8 +1244,10 @@ __device__ __forceinline__ void chroma8(const JpegPlan& P, const JpegImageDev& i
     const uint8_t* pr = P.planes + im.comp_plane0[2];
     const int64_t sb = (int64_t)im.comp_bw[1] * 8, sr = (int64_t)im.comp_bw[2] * 8;
     if (fh1 == 2 && fv1 == 2 && fh2 == 2 && fv2 == 2 && im.comp_dw[1] > 2 && im.comp_dw[2] > 2) {
-        chroma8_h2v2(pb, sb, im.comp_dw[1], im.comp_dh[1], x, y, cbv);
-        chroma8_h2v2(pr, sr, im.comp_dw[2], im.comp_dh[2], x, y, crv);
+        if (!chroma8_h2v2_pair(pb, sb, im.comp_dw[1], im.comp_dh[1], x, y, cbv))
+            chroma8_h2v2(pb, sb, im.comp_dw[1], im.comp_dh[1], x, y, cbv);
+        if (!chroma8_h2v2_pair(pr, sr, im.comp_dw[2], im.comp_dh[2], x, y, crv))
+            chroma8_h2v2(pr, sr, im.comp_dw[2], im.comp_dh[2], x, y, crv);
     } else if (fh1 == 1 && fv1 == 1 && fh2 == 1 && fv2 == 1) {  // 4:4:4: x is 8-aligned in 8-B rows
         const uint2 b8 = *reinterpret_cast<const uint2*>(pb + (int64_t)y * sb + x);
         const uint2 r8 = *reinterpret_cast<const uint2*>(pr + (int64_t)y * sr + x);
@@ -1220,7 +1268,7 @@ __device__ __forceinline__ void chroma8(const JpegPlan& P, const JpegImageDev& i
 
 __global__ __launch_bounds__(256) void jpeg_luma_color_kernel(JpegPlan P)
 {
-    __shared__ int32_t tr[kFuseBlocks * 64];
+    __shared__ int32_t tr[kFuseBlocks * kTrBlock];
     __shared__ __attribute__((aligned(16))) uint8_t ytile[8 * kYPitch];
     __shared__ __attribute__((aligned(16))) uint32_t stage[8 * kFuseRowBytes / 4];
     const JpegImageDev& im = P.imgs[blockIdx.z];
@@ -1252,7 +1300,7 @@ __global__ __launch_bounds__(256) void jpeg_luma_color_kernel(JpegPlan P)
 #endif
         uint8_t px[8];
 #ifndef WICCA_ABL_NOIDCT
-        idct8_lane_v<false, false>(ccur, im.qt[0], r, blive, tr + lb * 64, px);
+        idct8_lane_v<WICCA_LUMA_IDCT32 != 0>(ccur, im.qt[0], r, blive, tr + lb * kTrBlock, px);
 #else  // ablation (timing only): the coefficients' low bytes instead of the IDCT
         px[0] = ccur.x; px[1] = ccur.x >> 8; px[2] = ccur.y; px[3] = ccur.y >> 8;
         px[4] = ccur.z; px[5] = ccur.z >> 8; px[6] = ccur.w; px[7] = ccur.w >> 8;
