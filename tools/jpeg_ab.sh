@@ -2,6 +2,7 @@
 # A/B of JPEG decode variants on the GPU box: for each spec NAME[:ENV=VAL,...]
 # (NAME = a tools/variants/lib_NAME.so or "cur" for the in-tree library) one
 # stats run (WICCA_JPEG_TIMING) and one rocprofv3 kernel trace of the jpeg bench.
+# AB_ARGS: extra bench.py arguments (e.g. --no-verify for timing-only ablations).
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 for spec in "$@"; do
@@ -13,9 +14,9 @@ for spec in "$@"; do
   (
     export WICCA_HIP_LIB=$lib
     for kv in ${envs//,/ }; do export "$kv"; done
-    WICCA_JPEG_TIMING=1 timeout -k 10 200 python3 "$R/bench.py" --config jpeg --steps 2 --warmup 1 \
+    WICCA_JPEG_TIMING=1 timeout -k 10 200 python3 "$R/bench.py" --config jpeg --steps 2 --warmup 1 ${AB_ARGS:-} \
       > "$R/gpurun_out/ab_$tag.out" 2> "$R/gpurun_out/ab_$tag.err"
-    bash "$R/tools/profile_jpeg.sh" "ab_$tag" > /dev/null 2>&1
+    bash "$R/tools/profile_jpeg.sh" "ab_$tag" ${AB_ARGS:-} > /dev/null 2>&1
   )
   echo "$spec done"
 done

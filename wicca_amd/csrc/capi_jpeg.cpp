@@ -7,6 +7,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -105,9 +108,17 @@ double now_ms()
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Upload ordering hooks for the two-group pipeline (jpeg_decode_groups):
+// the stream waits for `wait` before this call's first upload, records `done`
+// after its last, then `issued()` runs on the calling thread.
+struct UploadOrder {
+    hipEvent_t wait = nullptr, done = nullptr;
+    std::function<void()> issued;
+};
+
 int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
                           uint8_t* const* dst, const int64_t* dpitch, bool orient, hipStream_t stream,
-                          int* rounds_out)
+                          int* rounds_out, const UploadOrder* order = nullptr)
 {
     // at most kJpegMaxJobs (image, component) IDCT jobs per device pass
     constexpr int64_t kChunk = wicca::kJpegMaxJobs / wicca::kJpegMaxComp;
@@ -115,7 +126,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         for (int64_t a = 0; a < n; a += kChunk) {
             const int64_t m = std::min(kChunk, n - a);
             int rc = jpeg_decode_to_device(ws, data + a, sizes + a, m, dst + a, dpitch + a, orient, stream,
-                                           rounds_out);
+                                           rounds_out, a == 0 ? order : nullptr);
             if (rc) return rc;
         }
         return WICCA_OK;
@@ -163,6 +174,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     HIP_TRY(ws->jstream.reserve(stream_bytes));
     uint8_t* stream_d = (uint8_t*)ws->jstream.ptr;
     SyncOnExit sync_on_exit{stream};
+    if (order && order->wait) HIP_TRY(hipStreamWaitEvent(stream, order->wait, 0));
     HIP_TRY(hipMemcpyAsync(stream_d + img_off[(size_t)n], stream_h + img_off[(size_t)n], 64,
                            hipMemcpyHostToDevice, stream));
     std::vector<std::vector<int64_t>> seg_off((size_t)n);
@@ -202,6 +214,10 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         for (auto& t : th) t.join();
     }
     if (upload_err) return fail(WICCA_ERR_HIP, "JPEG stream upload failed");
+    if (order) {
+        if (order->done) HIP_TRY(hipEventRecord(order->done, stream));
+        if (order->issued) order->issued();
+    }
     const double t_destuffed = now_ms();
     int64_t total_bits = 0;
     for (int64_t i = 0; i < n; ++i) total_bits += seg_off[(size_t)i].back() * 8;
@@ -209,6 +225,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     std::vector<wicca::JpegSegDev> segs;
     std::vector<int32_t> sub_seg, sub_img;
     std::vector<wicca::HuffDev> huff;
+    std::vector<wicca::HuffDevSync> huff_sync;  // the same tables, 11-bit lookups (sync passes)
     std::vector<wicca::JpegImageDev> ims((size_t)n);
     int64_t coef_blocks = 0, plane_bytes = 0, tmp_bytes = 0;
     std::vector<int64_t> tmp_off((size_t)n, -1);
@@ -244,11 +261,15 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
                     tab_dc[k.td] = (int)huff.size();
                     huff.emplace_back();
                     wicca::build_huff_dev(f.dc[k.td], &huff.back());
+                    huff_sync.emplace_back();
+                    wicca::build_huff_dev(f.dc[k.td], &huff_sync.back());
                 }
                 if (tab_ac[k.ta] < 0) {
                     tab_ac[k.ta] = (int)huff.size();
                     huff.emplace_back();
                     wicca::build_huff_dev(f.ac[k.ta], &huff.back());
+                    huff_sync.emplace_back();
+                    wicca::build_huff_dev(f.ac[k.ta], &huff_sync.back());
                 }
                 im.dc_tab[c] = tab_dc[k.td];
                 im.ac_tab[c] = tab_ac[k.ta];
@@ -303,7 +324,8 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     const size_t o_sim = o_sub + (size_t)round_up((int64_t)(sub_seg.size() * sizeof(int32_t)), 256);
     const size_t o_img = o_sim + (size_t)round_up((int64_t)(sub_img.size() * sizeof(int32_t)), 256);
     const size_t o_huf = o_img + (size_t)round_up((int64_t)(ims.size() * sizeof(wicca::JpegImageDev)), 256);
-    const size_t meta_bytes = o_huf + huff.size() * sizeof(wicca::HuffDev);
+    const size_t o_hsy = o_huf + (size_t)round_up((int64_t)(huff.size() * sizeof(wicca::HuffDev)), 256);
+    const size_t meta_bytes = o_hsy + huff_sync.size() * sizeof(wicca::HuffDevSync);
     HIP_TRY(ws->jmeta.reserve(meta_bytes));
     HIP_TRY(ws->jplanes.reserve((size_t)std::max<int64_t>(plane_bytes, 256)));
     HIP_TRY(ws->jscratch.reserve(wicca::jpeg_scratch_bytes((int64_t)sub_seg.size(), (int64_t)segs.size())));
@@ -321,6 +343,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     memcpy(packed + o_sim, sub_img.data(), sub_img.size() * sizeof(int32_t));
     memcpy(packed + o_img, ims.data(), ims.size() * sizeof(wicca::JpegImageDev));
     memcpy(packed + o_huf, huff.data(), huff.size() * sizeof(wicca::HuffDev));
+    memcpy(packed + o_hsy, huff_sync.data(), huff_sync.size() * sizeof(wicca::HuffDevSync));
     HIP_TRY(hipMemcpyAsync(m, packed, meta_bytes, hipMemcpyHostToDevice, stream));
     wicca::JpegPlan P{};
     P.stream = stream_d;
@@ -329,6 +352,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     P.sub_img = (const int32_t*)(m + o_sim);
     P.imgs = (const wicca::JpegImageDev*)(m + o_img);
     P.huff = (const wicca::HuffDev*)(m + o_huf);
+    P.huff_sync = (const wicca::HuffDevSync*)(m + o_hsy);
     P.coef = (int16_t*)ws->jcoef.ptr;
     P.planes = (uint8_t*)ws->jplanes.ptr;
     P.n_sub = (int64_t)sub_seg.size();
@@ -361,6 +385,77 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         fprintf(stderr, "[wicca jpeg] %lld files: parse+destuff %.2f ms, tables+upload issue %.2f ms, "
                 "device decode %.2f ms (%d sync passes), sub_bits %lld\n", (long long)n, t_destuffed - t_start,
                 t_upload - t_destuffed, now_ms() - t_upload, rounds, (long long)S);
+    return WICCA_OK;
+}
+
+// Two-group pipeline (WICCA_JPEG_GROUPS=2): the batch splits at its
+// compressed-size midpoint; the second group runs on a second workspace and
+// stream from a second host thread, starting its host work once the first
+// group's uploads are issued and its uploads once they have landed, so the
+// first group's device decode runs while the second group's bytes cross PCIe.
+int jpeg_groups()
+{
+    static const int g = [] {
+        const char* e = getenv("WICCA_JPEG_GROUPS");
+        return e ? std::max(1, std::min(2, atoi(e))) : 1;
+    }();
+    return g;
+}
+
+int jpeg_decode_groups(int dev, Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                       uint8_t* const* dst, const int64_t* dpitch, bool orient, hipStream_t stream, int* rounds_out)
+{
+    if (jpeg_groups() < 2 || n < 2)
+        return jpeg_decode_to_device(ws, data, sizes, n, dst, dpitch, orient, stream, rounds_out);
+    int64_t total = 0, acc = 0, k = 0;
+    for (int64_t i = 0; i < n; ++i) total += sizes[i];
+    while (k < n - 1 && acc + sizes[k] <= total / 2) acc += sizes[k++];
+    k = std::max<int64_t>(k, 1);
+    WorkspaceLease lease2;
+    int rc = acquire(dev, lease2);
+    if (rc) return rc;
+    Workspace* ws2 = lease2.ws;
+    hipEvent_t landed = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&landed, hipEventDisableTiming));
+    std::mutex mu;
+    std::condition_variable cv;
+    bool go = false;
+    UploadOrder first;
+    first.done = landed;
+    first.issued = [&] {
+        std::lock_guard<std::mutex> g(mu);
+        go = true;
+        cv.notify_all();
+    };
+    int rc2 = WICCA_OK, rounds2 = 0;
+    std::string err2;
+    std::thread second([&] {
+        (void)hipSetDevice(dev);
+        {
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return go; });
+        }
+        UploadOrder o2;
+        o2.wait = landed;
+        rc2 = jpeg_decode_to_device(ws2, data + k, sizes + k, n - k, dst + k, dpitch + k, orient, ws2->stream,
+                                    &rounds2, &o2);
+        if (rc2) err2 = t_last_error;
+    });
+    int rounds1 = 0;
+    rc = jpeg_decode_to_device(ws, data, sizes, k, dst, dpitch, orient, stream, &rounds1, &first);
+    {  // a first group that failed before its uploads must still release the second
+        std::lock_guard<std::mutex> g(mu);
+        go = true;
+        cv.notify_all();
+    }
+    second.join();
+    (void)hipEventDestroy(landed);
+    if (rounds_out) *rounds_out = std::max(rounds1, rounds2);
+    if (rc) return rc;
+    if (rc2) {
+        t_last_error = err2;
+        return rc2;
+    }
     return WICCA_OK;
 }
 
@@ -548,8 +643,8 @@ int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64
             off += p[(size_t)i] * oh[i];
         }
     }
-    if ((rc = jpeg_decode_to_device(ws, data, sizes, n, d.data(), p.data(), apply_orientation != 0, stream,
-                                    &t_jpeg_rounds)))
+    if ((rc = jpeg_decode_groups(dev, ws, data, sizes, n, d.data(), p.data(), apply_orientation != 0, stream,
+                                 &t_jpeg_rounds)))
         return rc;
     if (!dst_is_device) {
         for (int64_t i = 0; i < n; ++i)

@@ -97,14 +97,20 @@ size_t jpeg_destuff_into(const JpegInfo& info, uint8_t* out, std::vector<int64_t
 // ---------------------------------------------------------------------------
 // Device plan (built on the host, uploaded once per decode call).
 // ---------------------------------------------------------------------------
-constexpr int kHuffLutBits = 9;
+constexpr int kHuffLutBits = 9;       // the write pass's tables (LDS shared with its block staging)
+constexpr int kHuffLutBitsSync = 11;  // the sync passes' tables: codes > 9 bits are ~1.6 % of AC
+                                      // codewords at q90, i.e. in most wave iterations of some lane
 
-struct HuffDev {
-    uint16_t lut[1 << kHuffLutBits];  // (len << 8) | symbol for codes <= 9 bits, 0 = longer
-    int32_t maxcode[18];              // largest code of length l, -1 if none (maxcode[17] sentinel)
-    int32_t valoff[18];               // vals index of the first code of length l, minus that code
+template <int B>
+struct HuffDevT {
+    static constexpr int kBits = B;
+    uint16_t lut[1 << B];  // (len << 8) | symbol for codes <= B bits, 0 = longer
+    int32_t maxcode[18];   // largest code of length l, -1 if none (maxcode[17] sentinel)
+    int32_t valoff[18];    // vals index of the first code of length l, minus that code
     uint8_t vals[256];
 };
+using HuffDev = HuffDevT<kHuffLutBits>;
+using HuffDevSync = HuffDevT<kHuffLutBitsSync>;
 
 struct JpegImageDev {
     int32_t W, H, ncomp, bpm, mcux, hmax, vmax;
@@ -134,6 +140,7 @@ struct JpegPlan {
     const int32_t* sub_seg;  // subsequence -> segment
     const JpegImageDev* imgs;
     const HuffDev* huff;
+    const HuffDevSync* huff_sync;  // the same tables with an 11-bit lookup, same indices
     int16_t* coef;           // (total blocks) x 64, natural order
     uint8_t* planes;         // component sample planes
     int64_t n_sub, n_seg;
@@ -159,6 +166,7 @@ hipError_t launch_orient(const uint8_t* src, int64_t sp, int W, int H, int orien
                          hipStream_t s);
 
 void build_huff_dev(const JpegHuffTable& t, HuffDev* d);
+void build_huff_dev(const JpegHuffTable& t, HuffDevSync* d);
 
 // Fused luma IDCT + upsampling + colour (default) or the separate launches
 // (WICCA_JPEG_FUSED=0).  With the fused back end only the chroma components

@@ -123,8 +123,10 @@ struct BitReader {
 // (code length << 8) | symbol of the codeword at the top of `look` (the next
 // 32 bits); a bit string that is no code (only off the true decode path)
 // reads as symbol 0 after 16 bits, as in jdhuff.
-__device__ __forceinline__ uint32_t huff_lookup(const HuffDev& t, uint32_t look)
+template <typename HT>
+__device__ __forceinline__ uint32_t huff_lookup(const HT& t, uint32_t look)
 {
+    constexpr int kHuffLutBits = HT::kBits;
     uint32_t e = t.lut[look >> (32 - kHuffLutBits)];
     if (e == 0) {
         // a code longer than the lookup: every length's maxcode / valoff read
@@ -193,16 +195,22 @@ struct BlockPos {
 // coefficients of blocks [block_lo, block_end) (g = decode-order block index of
 // the block in progress), absolute DC values from the running predictors.
 // Blocks that start AND end inside the lane's range are assembled in the
-// lane's LDS block `lb` (only the coefficients it sets, tracked in the 64-bit
-// mask `nz`: no zeroing) and leave through the wave's cooperative flush; the
+// lane's LDS block `lb`, which is all zeros whenever no block is under
+// assembly (zeroed at the start, and by the flush as it reads each chunk), so
+// only the coefficients the block sets are written; they leave through the
+// wave's cooperative flush; the
 // block in progress at the start (begun by the previous lane) is written
 // coefficient by coefficient, and so is the nonzero part of a block the range
 // ends inside (the next lane writes its other coefficients): no two lanes ever
 // write the same bytes.
-constexpr int kLaneBlock = 64;  // int16 per lane in LDS: one block
+constexpr int kLaneBlock = 64;  // coefficients per lane in LDS: one block
 #ifndef WICCA_JPEG_STAGE
-#define WICCA_JPEG_STAGE 1  // 0: every coefficient leaves as its own 2-B store (no LDS staging)
+// 0: every coefficient leaves as its own 2-B store (no LDS staging);
+// 1: int16 staging (128 B per lane); 2: int8 staging (64 B per lane: the DC
+//    in a register, |v| >= 128 as a -128 marker plus a per-lane list)
+#define WICCA_JPEG_STAGE 1
 #endif
+constexpr int kEsc = 3;  // STAGE 2: large AC coefficients per block before it spills to direct stores
 
 // Per-wave LDS of the write pass: every lane's block under assembly, and the
 // owner lanes of the blocks completed in the current iteration; and the
@@ -210,10 +218,52 @@ constexpr int kLaneBlock = 64;  // int16 per lane in LDS: one block
 // per-lane k compiles to a global load, and waiting for it also waited for
 // the bit reader's prefetch on every AC coefficient).
 struct WaveStage {
-    int16_t* blocks;     // 64 * kLaneBlock
+    int16_t* blocks;     // 64 * kLaneBlock (STAGE 1)
     uint8_t* owner;      // 64
     const uint8_t* nat;  // 80
+    int8_t* blocks8;     // 64 * kLaneBlock (STAGE 2)
+    uint32_t* esc;       // 64 * kEsc (STAGE 2): (natural index << 16) | value
 };
+
+// STAGE 2: chunk q (natural positions 8q .. 8q+7) of a lane's int8 block as 8
+// int16: bytes sign-extended two per 16-bit lane, the DC from the register
+// copy, -128 markers from the escape list.
+__device__ __forceinline__ uint4 expand_chunk(uint2 raw, int q, int dcv, const uint32_t* esc, int nesc)
+{
+    typedef short s16x2 __attribute__((ext_vector_type(2)));
+    auto sx = [](uint32_t x, uint32_t sel) -> uint32_t {  // two bytes of x -> two sign-extended int16
+        const uint32_t t = __builtin_amdgcn_perm(0u, x, sel) ^ 0x00800080u;
+        s16x2 v = __builtin_bit_cast(s16x2, t) - s16x2{128, 128};
+        return __builtin_bit_cast(uint32_t, v);
+    };
+    uint4 w;
+    w.x = sx(raw.x, 0x0c010c00u);
+    w.y = sx(raw.x, 0x0c030c02u);
+    w.z = sx(raw.y, 0x0c010c00u);
+    w.w = sx(raw.y, 0x0c030c02u);
+    if (q == 0) w.x = (w.x & 0xFFFF0000u) | ((uint32_t)dcv & 0xFFFFu);
+    const auto marked = [](uint32_t x) {  // any byte == 0x80
+        const uint32_t t = x ^ 0x80808080u;
+        return ((t - 0x01010101u) & ~t & 0x80808080u) != 0;
+    };
+    if (nesc > 0 && (marked(raw.x) || marked(raw.y))) {
+        for (int e = 0; e < nesc; ++e) {
+            const uint32_t ent = esc[e];
+            const int n = (int)(ent >> 16);
+            if ((n >> 3) != q) continue;
+            const int j = n & 7;
+            const bool hi = j & 1;
+            auto patch = [&](uint32_t d) {
+                return hi ? ((d & 0xFFFFu) | (ent << 16)) : ((d & 0xFFFF0000u) | (ent & 0xFFFFu));
+            };
+            if ((j >> 1) == 0) w.x = patch(w.x);
+            else if ((j >> 1) == 1) w.y = patch(w.y);
+            else if ((j >> 1) == 2) w.z = patch(w.z);
+            else w.w = patch(w.w);
+        }
+    }
+    return w;
+}
 
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -232,11 +282,13 @@ __device__ __forceinline__ int64_t shfl64(int64_t v, int src)
 // 128-B blocks: the wave's active lanes deal the 8 16-B chunks of every such
 // block among themselves, so one store instruction writes up to 8 blocks
 // (a lane storing its own block issued 8 mostly-empty instructions per block,
-// on nearly every iteration of every wave).  Coefficients the block did not
-// set come out as zeros (mask `nz`).  Block index and mask come from the owner
-// lane by shuffle; every active lane runs every round of the loop (owners are
-// active), only the stores are predicated.
-__device__ __forceinline__ void flush_blocks(bool done, int64_t blk, uint64_t nz, const WaveStage& ws,
+// on nearly every iteration of every wave).  Each chunk is zeroed in LDS as it
+// is read, so the owner's next block starts from zeros (a 64-bit mask of the
+// coefficients set, kept per coefficient and applied per chunk, cost more
+// VALU).  The block index comes from the owner lane by shuffle; every active
+// lane runs every round of the loop (owners are active), only the stores are
+// predicated.
+__device__ __forceinline__ void flush_blocks(bool done, int64_t blk, int dcv, int nesc, const WaveStage& ws,
                                              int16_t* coef)
 {
     const uint64_t pend = __ballot(done);
@@ -255,17 +307,23 @@ __device__ __forceinline__ void flush_blocks(bool done, int64_t blk, uint64_t nz
         const int bi = valid ? c >> 3 : 0, q = c & 7;
         const int o = ws.owner[bi];
         const int64_t ob = shfl64(blk, o);
-        const uint64_t onz = (uint64_t)shfl64((int64_t)nz, o);
+        int od = 0, on = 0;
+        if (WICCA_JPEG_STAGE == 2) {
+            od = __shfl(dcv, o, 64);
+            on = __shfl(nesc, o, 64);
+        }
         if (valid) {
-            uint4 v = *reinterpret_cast<const uint4*>(ws.blocks + o * kLaneBlock + q * 8);
-            const uint32_t m = (uint32_t)(onz >> (q * 8)) & 0xFFu;
-            auto keep = [&](uint32_t w, int d) -> uint32_t {
-                return w & (((m >> (2 * d)) & 1u ? 0x0000FFFFu : 0u) | ((m >> (2 * d + 1)) & 1u ? 0xFFFF0000u : 0u));
-            };
-            v.x = keep(v.x, 0);
-            v.y = keep(v.y, 1);
-            v.z = keep(v.z, 2);
-            v.w = keep(v.w, 3);
+            uint4 v;
+            if (WICCA_JPEG_STAGE == 2) {
+                uint2* chunk = reinterpret_cast<uint2*>(ws.blocks8 + o * kLaneBlock + q * 8);
+                const uint2 raw = *chunk;
+                *chunk = uint2{0, 0};
+                v = expand_chunk(raw, q, od, ws.esc + o * kEsc, on);
+            } else {
+                uint4* chunk = reinterpret_cast<uint4*>(ws.blocks + o * kLaneBlock + q * 8);
+                v = *chunk;
+                *chunk = uint4{0, 0, 0, 0};
+            }
 #ifndef WICCA_JPEG_ABLATE_STORES
             *reinterpret_cast<uint4*>(coef + ob * 64 + q * 8) = v;
 #else
@@ -295,8 +353,8 @@ __device__ __forceinline__ void zero_zig(int16_t* coef, const uint8_t* nat, int6
 // 2 stops at the first of the n_ck checkpoints in ck the decode reaches
 // (returns its index, -1 if none; *hit_ck gets it).  ck_base = the lane's
 // start bit.
-template <bool WRITE, int CK = 0>
-__device__ int decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br, int64_t stop,
+template <bool WRITE, int CK = 0, typename HT = HuffDev>
+__device__ int decode_run(const DecGeom& im, const HT* tabs, BitReader& br, int64_t stop,
                           DecState& st, int64_t& started, int32_t (&dc)[kJpegMaxComp], int64_t g,
                           int64_t block_lo, int64_t block_end, int16_t* coef, const WaveStage* ws = nullptr,
                           bool seg_last = false, SyncCk* ck = nullptr, int n_ck = 0, int64_t ck_base = 0,
@@ -307,12 +365,18 @@ __device__ int decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br,
     if (CK == 2 && n_ck > 0) cur = ck[0].pos_slot;
     int64_t blk = -1;
     bool staged = false;
-    uint64_t nz = 0;
     int zk = 0;  // next zigzag position of a block written position by position (not staged)
     BlockPos pos;
     int16_t* lb = nullptr;
+    int8_t* lb8 = nullptr;    // STAGE 2: the lane's int8 block,
+    uint32_t* lesc = nullptr; // its escape list,
+    int dcv = 0, nesc = 0;    // the block's DC and escape count
     if (WRITE) {
-        if (WICCA_JPEG_STAGE) lb = ws->blocks + (threadIdx.x & 63) * kLaneBlock;
+        if (WICCA_JPEG_STAGE == 1) lb = ws->blocks + (threadIdx.x & 63) * kLaneBlock;
+        if (WICCA_JPEG_STAGE == 2) {
+            lb8 = ws->blocks8 + (threadIdx.x & 63) * kLaneBlock;
+            lesc = ws->esc + (threadIdx.x & 63) * kEsc;
+        }
         pos.init(im, g < 0 ? 0 : g);
         if (g >= block_lo && g < block_end) blk = pos.index(im);
         zk = st.k;  // the block in progress at the start: this lane owns [st.k, ...)
@@ -321,8 +385,8 @@ __device__ int decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br,
     // (one LDS read per block, not two dependent ones per codeword)
     uint32_t sti = im.slot_tab[st.slot];
     int c = (int)(sti >> 16);
-    const HuffDev* tdc = &tabs[sti & 255];
-    const HuffDev* tac = &tabs[(sti >> 8) & 255];
+    const HT* tdc = &tabs[sti & 255];
+    const HT* tac = &tabs[(sti >> 8) & 255];
     // 32-bit positions relative to the reader's base inside the loop
     const int32_t stop_r = (int32_t)(stop - br.base);
     const int32_t ck_off = (int32_t)(br.base - ck_base);  // reader-relative -> checkpoint-relative
@@ -367,9 +431,12 @@ __device__ int decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br,
                 ++g;
                 blk = (g >= block_lo && g < block_end) ? pos.index(im) : -1;
                 if (blk >= 0) {
-                    if (WICCA_JPEG_STAGE) {
+                    if (WICCA_JPEG_STAGE == 2) {
+                        dcv = dc[c];
+                        nesc = 0;
+                        staged = true;
+                    } else if (WICCA_JPEG_STAGE) {
                         lb[0] = (int16_t)dc[c];
-                        nz = 1;
                         staged = true;
                     } else {
                         coef[blk * 64] = (int16_t)dc[c];
@@ -384,9 +451,25 @@ __device__ int decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br,
                 st.k += r;
                 if (WRITE && blk >= 0 && st.k < 64) {
                     const int n = ws->nat[st.k];
-                    if (staged) {
+                    if (staged && WICCA_JPEG_STAGE == 2 && (unsigned)(v + 127) > 254u) {
+                        if (nesc < kEsc) {  // |v| >= 128: a marker and the escape list
+                            lesc[nesc++] = ((uint32_t)n << 16) | ((uint32_t)v & 0xFFFFu);
+                            lb8[n] = (int8_t)-128;
+                        } else {  // spill (rare): the block so far straight to HBM, then unstaged
+                            uint2* ch = reinterpret_cast<uint2*>(lb8);
+                            uint4* d = reinterpret_cast<uint4*>(coef + blk * 64);
+                            for (int q = 0; q < 8; ++q) {
+                                d[q] = expand_chunk(ch[q], q, dcv, lesc, nesc);
+                                ch[q] = uint2{0, 0};
+                            }
+                            staged = false;
+                            coef[blk * 64 + n] = (int16_t)v;
+                            zk = st.k + 1;
+                        }
+                    } else if (staged && WICCA_JPEG_STAGE == 2) {
+                        lb8[n] = (int8_t)v;
+                    } else if (staged) {
                         lb[n] = (int16_t)v;
-                        nz |= 1ull << n;
                     } else {
                         zero_zig(coef, ws->nat, blk, zk, st.k);
                         coef[blk * 64 + n] = (int16_t)v;
@@ -415,14 +498,22 @@ __device__ int decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br,
         // every codeword: deferring the flush until 4 / 8 / 16 blocks wait (the
         // finished lanes idle meanwhile) measured 6.1 / 7.4 / 7.5 ms per 25 x 8K
         // call against 3.0 ms
-        if (WRITE && WICCA_JPEG_STAGE) flush_blocks(done, blk, nz, *ws, coef);
+        if (WRITE && WICCA_JPEG_STAGE) flush_blocks(done, blk, dcv, nesc, *ws, coef);
     }
     if (WRITE && blk >= 0 && st.k > 0) {  // the range ends inside block blk: this lane's part [.., st.k)
         const int kend = min(st.k, 64);
-        if (staged) {
+        if (staged && WICCA_JPEG_STAGE == 2) {
+            const uint2* ch = reinterpret_cast<const uint2*>(lb8);
             for (int z = 0; z < kend; ++z) {
                 const int n = ws->nat[z];
-                coef[blk * 64 + n] = ((nz >> n) & 1) ? lb[n] : (int16_t)0;
+                const uint4 w = expand_chunk(ch[n >> 3], n >> 3, dcv, lesc, nesc);
+                const uint32_t d = (n & 7) < 2 ? w.x : (n & 7) < 4 ? w.y : (n & 7) < 6 ? w.z : w.w;
+                coef[blk * 64 + n] = (int16_t)((n & 1) ? d >> 16 : d & 0xFFFFu);
+            }
+        } else if (staged) {
+            for (int z = 0; z < kend; ++z) {
+                const int n = ws->nat[z];
+                coef[blk * 64 + n] = lb[n];  // zeros where the block set nothing
             }
         } else {
             zero_zig(coef, ws->nat, blk, zk, kend);
@@ -448,17 +539,17 @@ __device__ int decode_run(const DecGeom& im, const HuffDev* tabs, BitReader& br,
 // distinct tables consecutively in P.huff (at most NS of them here), slot s =
 // table first + s.  Every workgroup serves one image (the host pads each
 // image's subsequences to whole workgroups).
-template <int NS>
+template <int NS, typename HT = HuffDev>
 struct ImgTabs {
-    HuffDev t[NS];
+    HT t[NS];
     DecGeom g;
 };
 
-template <int NS>
-__device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageDev* imp, ImgTabs<NS>& lds)
+template <int NS, typename HT>
+__device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageDev* imp, ImgTabs<NS, HT>& lds)
 {
-    constexpr int kWords = sizeof(HuffDev) / 4;
-    static_assert(sizeof(HuffDev) % 4 == 0, "word copy");
+    constexpr int kWords = sizeof(HT) / 4;
+    static_assert(sizeof(HT) % 4 == 0, "word copy");
     const int ncomp = imp->ncomp;
     int first = imp->dc_tab[0], last = imp->dc_tab[0];
     for (int c = 0; c < ncomp; ++c) {
@@ -466,7 +557,10 @@ __device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageD
         last = max(last, max(imp->dc_tab[c], imp->ac_tab[c]));
     }
     const int n = min(last - first + 1, NS);  // the launcher picked NS >= every image's count
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(P.huff + first);
+    const HT* tables;
+    if constexpr (HT::kBits == kHuffLutBitsSync) tables = P.huff_sync;
+    else tables = P.huff;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(tables + first);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&lds.t[0]);
     for (int w = threadIdx.x; w < n * kWords; w += kJThreads) dst[w] = src[w];
     if (threadIdx.x == 0) {
@@ -512,13 +606,16 @@ __device__ __forceinline__ bool same_state(const DecState& a, const DecState& b)
 // covers a large batch (256 CUs x 4 SIMDs x 8 waves x 64 lanes = 524288); more
 // registers leave part of the grid to a second, serial generation of the
 // latency-bound decode (66 VGPRs cost round 0 a third of its time).
-template <int CK>  // 0 plain decode, 1 round 0 recording checkpoints, 2 round 1 stopping at one
-__global__ __launch_bounds__(kJThreads, 8) void jpeg_sync_kernel(JpegPlan P, const SubResult* prev,
+// CK: 0 plain decode, 1 round 0 recording checkpoints, 2 later rounds stopping
+// at one; NS table slots in LDS (4: every baseline image), 11-bit lookups.
+template <int CK, int NS>
+__global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(JpegPlan P, const SubResult* prev,
                                                              SubResult* next, int round, int* changed,
-                                                             const SubResult* older, SyncCk* cks, int* stats)
+                                                             const SubResult* older, SyncCk* cks, int* stats,
+                                                             const SubResult* r0res)
 {
     const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
-    __shared__ ImgTabs<2 * kJpegMaxComp> tabs;
+    __shared__ ImgTabs<NS, HuffDevSync> tabs;
     // this lane's start state, and whether it has to decode at all (every
     // lane of a workgroup that repeats its result skips the table staging too)
     const bool lane_live = i < P.n_sub && P.sub_seg[i] >= 0;  // else a padding lane
@@ -570,12 +667,12 @@ __global__ __launch_bounds__(kJThreads, 8) void jpeg_sync_kernel(JpegPlan P, con
     br.reset(P.stream, st.p);
     SyncCk* ck = cks + i * kSyncCk;
     if (CK == 1) {
-        r.n_ck = decode_run<false, 1>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr, nullptr, false, ck,
+        r.n_ck = decode_run<false, 1, HuffDevSync>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr, nullptr, false, ck,
                                       0, b0, nullptr, P.sub_bits / kSyncCk);
     } else if (CK == 2) {
-        const SubResult& o = prev[i];  // this lane's round-0 result and checkpoints
+        const SubResult& o = r0res[i];  // this lane's round-0 result and checkpoints
         SyncCk h;
-        const int hit = decode_run<false, 2>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr, nullptr,
+        const int hit = decode_run<false, 2, HuffDevSync>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr, nullptr,
                                              false, ck, o.n_ck, b0, &h);
         if (hit >= 0) {  // the rest is round 0's decode from checkpoint `hit`
             if (stats) {
@@ -587,7 +684,7 @@ __global__ __launch_bounds__(kJThreads, 8) void jpeg_sync_kernel(JpegPlan P, con
             for (int c = 0; c < kJpegMaxComp; ++c) dc[c] += o.dc[c] - h.dc[c];
         }
     } else {
-        decode_run<false>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr);
+        decode_run<false, 0, HuffDevSync>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr);
     }
     r.end = st;
     for (int c = 0; c < kJpegMaxComp; ++c) r.dc[c] = dc[c];
@@ -666,18 +763,35 @@ __global__ __launch_bounds__(256) void jpeg_scan_kernel(JpegPlan P, const SubRes
 // image: 2 DC + 2 AC tables) keeps the workgroup's LDS under 40 KB, i.e. 4
 // workgroups per CU instead of 3.
 template <int NS>
-__global__ __launch_bounds__(kJThreads, NS <= 4 ? 4 : 1) void jpeg_write_kernel(JpegPlan P, const SubResult* res,
+__global__ __launch_bounds__(kJThreads, NS > 4 ? 1 : WICCA_JPEG_STAGE == 2 ? 6 : 4) void jpeg_write_kernel(JpegPlan P, const SubResult* res,
                                                                  const SubBase* base)
 {
     const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
     __shared__ ImgTabs<NS> tabs;
-#if WICCA_JPEG_STAGE
+#if WICCA_JPEG_STAGE == 1
     __shared__ __attribute__((aligned(16))) int16_t lanes[kJThreads * kLaneBlock];
+    __shared__ uint8_t s_owner[kJThreads];
+#elif WICCA_JPEG_STAGE == 2
+    __shared__ __attribute__((aligned(16))) int8_t lanes8[kJThreads * kLaneBlock];
+    __shared__ uint32_t s_esc[kJThreads * kEsc];
     __shared__ uint8_t s_owner[kJThreads];
 #endif
     __shared__ uint8_t s_nat[80];
     if (threadIdx.x < 80) s_nat[threadIdx.x] = (uint8_t)kNatural[threadIdx.x];
-    stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);  // its barrier covers s_nat
+#if WICCA_JPEG_STAGE == 1
+    {  // every lane block starts zeroed (decode_run writes only what a block sets)
+        uint4* z = reinterpret_cast<uint4*>(lanes + threadIdx.x * kLaneBlock);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) z[q] = uint4{0, 0, 0, 0};
+    }
+#elif WICCA_JPEG_STAGE == 2
+    {
+        uint4* z = reinterpret_cast<uint4*>(lanes8 + threadIdx.x * kLaneBlock);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) z[q] = uint4{0, 0, 0, 0};
+    }
+#endif
+    stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);  // its barrier covers s_nat and the zeroing
     const DecGeom& im = tabs.g;
     if (i >= P.n_sub || P.sub_seg[i] < 0) return;  // padding lane
     const JpegSegDev sg = P.segs[P.sub_seg[i]];
@@ -696,11 +810,13 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 4 : 1) void jpeg_write_kernel(
     int64_t started = 0;
     BitReader br;
     br.reset(P.stream, st.p);
-#if WICCA_JPEG_STAGE
     const int w0 = (int)(threadIdx.x & ~63u);  // the wave's first lane
-    const WaveStage ws{lanes + w0 * kLaneBlock, s_owner + w0, s_nat};
+#if WICCA_JPEG_STAGE == 1
+    const WaveStage ws{lanes + w0 * kLaneBlock, s_owner + w0, s_nat, nullptr, nullptr};
+#elif WICCA_JPEG_STAGE == 2
+    const WaveStage ws{nullptr, s_owner + w0, s_nat, lanes8 + w0 * kLaneBlock, s_esc + w0 * kEsc};
 #else
-    const WaveStage ws{nullptr, nullptr, s_nat};
+    const WaveStage ws{nullptr, nullptr, s_nat, nullptr, nullptr};
 #endif
     // the block in progress at the start was started by an earlier lane
     decode_run<true>(im, tabs.t, br, b1, st, started, dc, sg.block0 + b.block - 1, sg.block0,
@@ -739,6 +855,18 @@ __device__ __forceinline__ int32_t descale32(int32_t x, int n) { return (x + (1 
 #define WICCA_LUMA_IDCT32 1  // 0: the fused luma IDCT always in 64-bit passes
 #endif
 constexpr int32_t kIdct32Max = 12600;  // 32-bit IDCT pass exact for inputs within +-kIdct32Max (with the descale rounding term)
+
+// The last pass's descale by 2^18 and idct_limit in one: bits 18..27 of the
+// rounded sum plus 512 << 18 (a 32-bit wrap does not touch them) are
+// (x + 512) & 1023 for x = the descaled value, and the table's four ranges
+// (x' < 128 -> x' + 128, < 512 -> 255, < 896 -> 0, else x' - 896, x' = x & 1023)
+// are clamp(((x + 512) & 1023) - 384, 0, 255).
+__device__ __forceinline__ uint8_t idct_limit_descale32(int32_t o)
+{
+    constexpr int sh = kConstBits + kPass1Bits + 3;
+    const uint32_t w = ((uint32_t)o + (1u << (sh - 1)) + (512u << sh)) >> sh;
+    return (uint8_t)min(255, max(0, (int)(w & 1023u) - 384));
+}
 
 // idct_sample_range_limit[x & 1023] of jdmaster.c's prepare_range_limit_table
 __device__ __forceinline__ uint8_t idct_limit(int64_t v)
@@ -894,7 +1022,7 @@ __device__ __forceinline__ void idct8_lane_v(uint4 v, const uint16_t* qt, int r,
         if (!live) return;
         islow_1d<int32_t>(in, o);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) px[k] = idct_limit(descale32(o[k], sh));
+        for (int k = 0; k < 8; ++k) px[k] = idct_limit_descale32(o[k]);
     } else {
         int64_t r64[8], o[8];
         if (!live) return;
@@ -1210,20 +1338,22 @@ __device__ __forceinline__ bool chroma8_h2v2_pair(const uint8_t* plane, int64_t 
     return true;
 }
 
+// jdcolor.c: R = Y + ((91881 (Cr - 128) + 2^15) >> 16), B likewise with
+// 116130 Cb, G = Y + ((-46802 (Cr - 128) - 22554 (Cb - 128) + 2^15) >> 16),
+// each clamped.  Y << 16 and the -128 offsets fold into the addend of one
+// full-rate 24-bit multiply-add per product (the sums stay within +-2^26, and
+// adding a multiple of 2^16 before the arithmetic shift adds Y after it).
 __device__ __forceinline__ void ycc8_to_rgb(uint32_t ylo, uint32_t yhi, const int (&cbv)[8], const int (&crv)[8],
                                             uint8_t (&o)[24])
 {
+    constexpr int kR = 32768 - 91881 * 128, kB = 32768 - 116130 * 128, kG = 32768 + (46802 + 22554) * 128;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
         const int Y = (int)(((q < 4 ? ylo : yhi) >> (8 * (q & 3))) & 255);
-        const int cb = cbv[q] - 128, cr = crv[q] - 128;
-        // 24-bit multiplies (full rate): |cb|, |cr| <= 128, the constants < 2^17
-        const int crr = (__mul24(91881, cr) + 32768) >> 16;
-        const int cbb = (__mul24(116130, cb) + 32768) >> 16;
-        const int g = (__mul24(-46802, cr) + (__mul24(-22554, cb) + 32768)) >> 16;
-        o[3 * q] = clamp255(Y + crr);
-        o[3 * q + 1] = clamp255(Y + g);
-        o[3 * q + 2] = clamp255(Y + cbb);
+        const int y16 = Y << 16;
+        o[3 * q] = clamp255((__mul24(91881, crv[q]) + (y16 + kR)) >> 16);
+        o[3 * q + 1] = clamp255((__mul24(-46802, crv[q]) + (__mul24(-22554, cbv[q]) + (y16 + kG))) >> 16);
+        o[3 * q + 2] = clamp255((__mul24(116130, cbv[q]) + (y16 + kB)) >> 16);
     }
 }
 
@@ -1399,7 +1529,7 @@ bool jpeg_fused()
 size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg)
 {
     (void)n_seg;
-    return (size_t)n_sub * (3 * sizeof(SubResult) + sizeof(SubBase) + kSyncCk * sizeof(SyncCk)) + 64 +
+    return (size_t)n_sub * (4 * sizeof(SubResult) + sizeof(SubBase) + kSyncCk * sizeof(SyncCk)) + 64 +
            kJpegMaxJobs * sizeof(IdctJob);
 }
 
@@ -1410,7 +1540,8 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     SubResult* ra = (SubResult*)base;
     SubResult* rb = ra + P.n_sub;
     SubResult* rc = rb + P.n_sub;
-    SubBase* sb = (SubBase*)(rc + P.n_sub);
+    SubResult* r0 = rc + P.n_sub;  // round 0's results: kept for every later round's checkpoint hits
+    SubBase* sb = (SubBase*)(r0 + P.n_sub);
     int* changed = (int*)(sb + P.n_sub);
     IdctJob* jobs = (IdctJob*)((uint8_t*)changed + 64);
     SyncCk* cks = (SyncCk*)(jobs + kJpegMaxJobs);
@@ -1440,8 +1571,12 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     // the device Huffman decode (every image not decoded on the host)
     if (P.n_sub > 0) {
         const uint32_t grid = (uint32_t)((P.n_sub + kJThreads - 1) / kJThreads);
-        // round 0 + rounds until no end state changes; results rotate through
-        // three buffers (older = round - 2, cur = round - 1, nxt = this round)
+        // round 0 (into r0, kept) + rounds until no end state changes; later
+        // results rotate through three buffers (older = round - 2, cur =
+        // round - 1, nxt = this round).  Every later round stops a lane at the
+        // first round-0 checkpoint its decode reaches: a lane re-decoded in
+        // round 2 or 3 (its predecessor's end moved) usually meets its own
+        // round-0 decode within a few blocks.
         // WICCA_JPEG_SYNC_CK=0: no checkpoints (every round-1 lane decodes its whole subsequence);
         // WICCA_JPEG_TIMING: per-round counts of decoding lanes and checkpoint hits to stderr
         static const int ck_mode = [] {
@@ -1452,37 +1587,49 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
         constexpr int kStatRounds = 6;
         int* stats = changed + 4;  // [round][decoding lanes, checkpoint hits]
         if (stats_on && (e = hipMemsetAsync(stats, 0, 2 * kStatRounds * sizeof(int), s)) != hipSuccess) return e;
-        if (ck_mode)
-            hipLaunchKernelGGL(jpeg_sync_kernel<1>, dim3(grid), dim3(kJThreads), 0, s, P, ra, ra, 0, changed,
-                               (const SubResult*)nullptr, cks, stats_on ? stats : nullptr);
-        else
-            hipLaunchKernelGGL(jpeg_sync_kernel<0>, dim3(grid), dim3(kJThreads), 0, s, P, ra, ra, 0, changed,
-                               (const SubResult*)nullptr, cks, stats_on ? stats : nullptr);
-        e = hipGetLastError();
+        // the 4-slot kernels (18 KB of 11-bit tables: 8 workgroups per CU)
+        // serve every baseline image; 6 slots only for extended-sequential
+        // files with a table pair per component
+        static const bool force6 = [] {  // WICCA_JPEG_WRITE_SLOTS=6: the 6-table kernels for every batch (tests)
+            const char* e = getenv("WICCA_JPEG_WRITE_SLOTS");
+            return e && atoi(e) == 6;
+        }();
+        const bool ns4 = P.max_tabs <= 4 && !force6;
+        auto sync = [&](int ck, const SubResult* prev, SubResult* next, int round, const SubResult* older,
+                        int* st) {
+#define WICCA_SYNC_LAUNCH(CKV, NSV)                                                                        \
+    hipLaunchKernelGGL((jpeg_sync_kernel<CKV, NSV>), dim3(grid), dim3(kJThreads), 0, s, P, prev, next, round, \
+                       changed, older, cks, st, (const SubResult*)r0)
+            if (ns4) {
+                if (ck == 1) WICCA_SYNC_LAUNCH(1, 4);
+                else if (ck == 2) WICCA_SYNC_LAUNCH(2, 4);
+                else WICCA_SYNC_LAUNCH(0, 4);
+            } else {
+                if (ck == 1) WICCA_SYNC_LAUNCH(1, 2 * kJpegMaxComp);
+                else if (ck == 2) WICCA_SYNC_LAUNCH(2, 2 * kJpegMaxComp);
+                else WICCA_SYNC_LAUNCH(0, 2 * kJpegMaxComp);
+            }
+#undef WICCA_SYNC_LAUNCH
+            return hipGetLastError();
+        };
+        e = sync(ck_mode ? 1 : 0, r0, r0, 0, nullptr, stats_on ? stats : nullptr);
         if (e != hipSuccess) return e;
-        SubResult* older = rc;
-        SubResult* cur = ra;
-        SubResult* nxt = rb;
+        SubResult* const bufs[3] = {ra, rb, rc};
+        const SubResult* older = nullptr;
+        SubResult* cur = r0;
         int rounds = 0;
         for (;;) {
             int h_changed = 0;
             e = hipMemsetAsync(changed, 0, sizeof(int), s);
             if (e != hipSuccess) return e;
+            SubResult* nxt = bufs[rounds % 3];
             int* st_r = stats_on && rounds + 1 < kStatRounds ? stats + 2 * (rounds + 1) : nullptr;
-            if (ck_mode && rounds == 0)
-                hipLaunchKernelGGL(jpeg_sync_kernel<2>, dim3(grid), dim3(kJThreads), 0, s, P, cur, nxt, rounds + 1,
-                                   changed, (const SubResult*)older, cks, st_r);
-            else
-                hipLaunchKernelGGL(jpeg_sync_kernel<0>, dim3(grid), dim3(kJThreads), 0, s, P, cur, nxt, rounds + 1,
-                                   changed, (const SubResult*)older, cks, st_r);
-            e = hipGetLastError();
+            e = sync(ck_mode ? 2 : 0, cur, nxt, rounds + 1, older, st_r);
             if (e == hipSuccess) e = hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e != hipSuccess) return e;
-            SubResult* t = older;
             older = cur;
             cur = nxt;
-            nxt = t;
             ++rounds;
             if (!h_changed || rounds > P.n_sub) break;
         }
@@ -1497,10 +1644,6 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
         }
         hipLaunchKernelGGL(jpeg_scan_kernel, dim3((uint32_t)P.n_seg), dim3(256), 0, s, P, cur, sb);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        static const bool force6 = [] {  // WICCA_JPEG_WRITE_SLOTS=6: the 6-table kernel for every batch (tests)
-            const char* e = getenv("WICCA_JPEG_WRITE_SLOTS");
-            return e && atoi(e) == 6;
-        }();
         if (P.max_tabs <= 4 && !force6)
             hipLaunchKernelGGL(jpeg_write_kernel<4>, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
         else

@@ -423,7 +423,8 @@ void jpeg_destuff(const JpegInfo& info, std::vector<uint8_t>& out, std::vector<i
     out.resize(jpeg_destuff_into(info, out.data(), seg_off));
 }
 
-void build_huff_dev(const JpegHuffTable& t, HuffDev* d)
+template <int B>
+static void build_huff_lut(const JpegHuffTable& t, HuffDevT<B>* d)
 {
     memset(d, 0, sizeof(*d));
     int code = 0, k = 0;
@@ -434,9 +435,9 @@ void build_huff_dev(const JpegHuffTable& t, HuffDev* d)
         } else {
             d->valoff[l] = k - code;
             for (int i = 0; i < t.bits[l]; ++i, ++k, ++code) {
-                if (l <= kHuffLutBits) {
-                    const int lo = code << (kHuffLutBits - l);
-                    const int hi = std::min((code + 1) << (kHuffLutBits - l), 1 << kHuffLutBits);
+                if (l <= B) {
+                    const int lo = code << (B - l);
+                    const int hi = std::min((code + 1) << (B - l), 1 << B);
                     for (int e = lo; e < hi; ++e) d->lut[e] = (uint16_t)((l << 8) | t.vals[k]);
                 }
             }
@@ -448,6 +449,9 @@ void build_huff_dev(const JpegHuffTable& t, HuffDev* d)
     d->maxcode[17] = INT_MAX;  // sentinel
     memcpy(d->vals, t.vals, 256);
 }
+
+void build_huff_dev(const JpegHuffTable& t, HuffDev* d) { build_huff_lut(t, d); }
+void build_huff_dev(const JpegHuffTable& t, HuffDevSync* d) { build_huff_lut(t, d); }
 
 }  // namespace wicca
 
