@@ -229,15 +229,14 @@ def test_batch_larger_than_one_device_pass():
         assert np.array_equal(got[i], J.decode_rgb(blobs[i])), i
 
 
-@pytest.mark.parametrize("env", [{"WICCA_JPEG_WRITE_SLOTS": "6"}, {"WICCA_JPEG_SYNC_CK": "0"},
-                                 {"WICCA_JPEG_GROUPS": "2"}],
-                         ids=["slots6", "no-checkpoints", "two-groups"])
+@pytest.mark.parametrize("env", [{"WICCA_JPEG_WRITE_SLOTS": "6"}, {"WICCA_JPEG_SYNC_CK": "0"}],
+                         ids=["slots6", "no-checkpoints"])
 def test_write_and_sync_variants_subprocess(env):
     """The sync and write passes have 4-table builds (every baseline file) and
     6-table ones (extended-sequential files with separate tables per
-    component; WICCA_JPEG_WRITE_SLOTS=6 forces them); the
-    sync passes run with or without checkpoints; a batch can split into two
-    pipelined groups.  Each variant in a child process on the golden files."""
+    component; WICCA_JPEG_WRITE_SLOTS=6 forces them); the sync passes run with
+    or without checkpoints.  Each variant in a child process on the golden
+    files."""
     import subprocess
     import sys
     code = (

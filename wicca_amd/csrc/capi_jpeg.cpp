@@ -7,9 +7,6 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
-#include <condition_variable>
-#include <functional>
-#include <mutex>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -108,17 +105,9 @@ double now_ms()
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// Upload ordering hooks for the two-group pipeline (jpeg_decode_groups):
-// the stream waits for `wait` before this call's first upload, records `done`
-// after its last, then `issued()` runs on the calling thread.
-struct UploadOrder {
-    hipEvent_t wait = nullptr, done = nullptr;
-    std::function<void()> issued;
-};
-
 int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
                           uint8_t* const* dst, const int64_t* dpitch, bool orient, hipStream_t stream,
-                          int* rounds_out, const UploadOrder* order = nullptr)
+                          int* rounds_out)
 {
     // at most kJpegMaxJobs (image, component) IDCT jobs per device pass
     constexpr int64_t kChunk = wicca::kJpegMaxJobs / wicca::kJpegMaxComp;
@@ -126,7 +115,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         for (int64_t a = 0; a < n; a += kChunk) {
             const int64_t m = std::min(kChunk, n - a);
             int rc = jpeg_decode_to_device(ws, data + a, sizes + a, m, dst + a, dpitch + a, orient, stream,
-                                           rounds_out, a == 0 ? order : nullptr);
+                                           rounds_out);
             if (rc) return rc;
         }
         return WICCA_OK;
@@ -174,7 +163,6 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     HIP_TRY(ws->jstream.reserve(stream_bytes));
     uint8_t* stream_d = (uint8_t*)ws->jstream.ptr;
     SyncOnExit sync_on_exit{stream};
-    if (order && order->wait) HIP_TRY(hipStreamWaitEvent(stream, order->wait, 0));
     HIP_TRY(hipMemcpyAsync(stream_d + img_off[(size_t)n], stream_h + img_off[(size_t)n], 64,
                            hipMemcpyHostToDevice, stream));
     std::vector<std::vector<int64_t>> seg_off((size_t)n);
@@ -214,10 +202,6 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         for (auto& t : th) t.join();
     }
     if (upload_err) return fail(WICCA_ERR_HIP, "JPEG stream upload failed");
-    if (order) {
-        if (order->done) HIP_TRY(hipEventRecord(order->done, stream));
-        if (order->issued) order->issued();
-    }
     const double t_destuffed = now_ms();
     int64_t total_bits = 0;
     for (int64_t i = 0; i < n; ++i) total_bits += seg_off[(size_t)i].back() * 8;
@@ -385,77 +369,6 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         fprintf(stderr, "[wicca jpeg] %lld files: parse+destuff %.2f ms, tables+upload issue %.2f ms, "
                 "device decode %.2f ms (%d sync passes), sub_bits %lld\n", (long long)n, t_destuffed - t_start,
                 t_upload - t_destuffed, now_ms() - t_upload, rounds, (long long)S);
-    return WICCA_OK;
-}
-
-// Two-group pipeline (WICCA_JPEG_GROUPS=2): the batch splits at its
-// compressed-size midpoint; the second group runs on a second workspace and
-// stream from a second host thread, starting its host work once the first
-// group's uploads are issued and its uploads once they have landed, so the
-// first group's device decode runs while the second group's bytes cross PCIe.
-int jpeg_groups()
-{
-    static const int g = [] {
-        const char* e = getenv("WICCA_JPEG_GROUPS");
-        return e ? std::max(1, std::min(2, atoi(e))) : 1;
-    }();
-    return g;
-}
-
-int jpeg_decode_groups(int dev, Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
-                       uint8_t* const* dst, const int64_t* dpitch, bool orient, hipStream_t stream, int* rounds_out)
-{
-    if (jpeg_groups() < 2 || n < 2)
-        return jpeg_decode_to_device(ws, data, sizes, n, dst, dpitch, orient, stream, rounds_out);
-    int64_t total = 0, acc = 0, k = 0;
-    for (int64_t i = 0; i < n; ++i) total += sizes[i];
-    while (k < n - 1 && acc + sizes[k] <= total / 2) acc += sizes[k++];
-    k = std::max<int64_t>(k, 1);
-    WorkspaceLease lease2;
-    int rc = acquire(dev, lease2);
-    if (rc) return rc;
-    Workspace* ws2 = lease2.ws;
-    hipEvent_t landed = nullptr;
-    HIP_TRY(hipEventCreateWithFlags(&landed, hipEventDisableTiming));
-    std::mutex mu;
-    std::condition_variable cv;
-    bool go = false;
-    UploadOrder first;
-    first.done = landed;
-    first.issued = [&] {
-        std::lock_guard<std::mutex> g(mu);
-        go = true;
-        cv.notify_all();
-    };
-    int rc2 = WICCA_OK, rounds2 = 0;
-    std::string err2;
-    std::thread second([&] {
-        (void)hipSetDevice(dev);
-        {
-            std::unique_lock<std::mutex> g(mu);
-            cv.wait(g, [&] { return go; });
-        }
-        UploadOrder o2;
-        o2.wait = landed;
-        rc2 = jpeg_decode_to_device(ws2, data + k, sizes + k, n - k, dst + k, dpitch + k, orient, ws2->stream,
-                                    &rounds2, &o2);
-        if (rc2) err2 = t_last_error;
-    });
-    int rounds1 = 0;
-    rc = jpeg_decode_to_device(ws, data, sizes, k, dst, dpitch, orient, stream, &rounds1, &first);
-    {  // a first group that failed before its uploads must still release the second
-        std::lock_guard<std::mutex> g(mu);
-        go = true;
-        cv.notify_all();
-    }
-    second.join();
-    (void)hipEventDestroy(landed);
-    if (rounds_out) *rounds_out = std::max(rounds1, rounds2);
-    if (rc) return rc;
-    if (rc2) {
-        t_last_error = err2;
-        return rc2;
-    }
     return WICCA_OK;
 }
 
@@ -643,8 +556,8 @@ int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64
             off += p[(size_t)i] * oh[i];
         }
     }
-    if ((rc = jpeg_decode_groups(dev, ws, data, sizes, n, d.data(), p.data(), apply_orientation != 0, stream,
-                                 &t_jpeg_rounds)))
+    if ((rc = jpeg_decode_to_device(ws, data, sizes, n, d.data(), p.data(), apply_orientation != 0, stream,
+                                    &t_jpeg_rounds)))
         return rc;
     if (!dst_is_device) {
         for (int64_t i = 0; i < n; ++i)

@@ -205,12 +205,13 @@ struct BlockPos {
 // write the same bytes.
 constexpr int kLaneBlock = 64;  // coefficients per lane in LDS: one block
 #ifndef WICCA_JPEG_STAGE
-// 0: every coefficient leaves as its own 2-B store (no LDS staging);
-// 1: int16 staging (128 B per lane); 2: int8 staging (64 B per lane: the DC
-//    in a register, |v| >= 128 as a -128 marker plus a per-lane list)
+// 0: every coefficient leaves as its own 2-B store (no LDS staging); 1: int16
+// staging, 128 B per lane.  (An int8 staging, 64 B per lane with the DC in a
+// register and |v| >= 128 escaped to a per-lane list, reached 6 waves per SIMD
+// instead of 4 but measured 2.83 ms against 2.66: the widening in the flush
+// cost more than the occupancy gained.)
 #define WICCA_JPEG_STAGE 1
 #endif
-constexpr int kEsc = 3;  // STAGE 2: large AC coefficients per block before it spills to direct stores
 
 // Per-wave LDS of the write pass: every lane's block under assembly, and the
 // owner lanes of the blocks completed in the current iteration; and the
@@ -218,52 +219,10 @@ constexpr int kEsc = 3;  // STAGE 2: large AC coefficients per block before it s
 // per-lane k compiles to a global load, and waiting for it also waited for
 // the bit reader's prefetch on every AC coefficient).
 struct WaveStage {
-    int16_t* blocks;     // 64 * kLaneBlock (STAGE 1)
+    int16_t* blocks;     // 64 * kLaneBlock
     uint8_t* owner;      // 64
     const uint8_t* nat;  // 80
-    int8_t* blocks8;     // 64 * kLaneBlock (STAGE 2)
-    uint32_t* esc;       // 64 * kEsc (STAGE 2): (natural index << 16) | value
 };
-
-// STAGE 2: chunk q (natural positions 8q .. 8q+7) of a lane's int8 block as 8
-// int16: bytes sign-extended two per 16-bit lane, the DC from the register
-// copy, -128 markers from the escape list.
-__device__ __forceinline__ uint4 expand_chunk(uint2 raw, int q, int dcv, const uint32_t* esc, int nesc)
-{
-    typedef short s16x2 __attribute__((ext_vector_type(2)));
-    auto sx = [](uint32_t x, uint32_t sel) -> uint32_t {  // two bytes of x -> two sign-extended int16
-        const uint32_t t = __builtin_amdgcn_perm(0u, x, sel) ^ 0x00800080u;
-        s16x2 v = __builtin_bit_cast(s16x2, t) - s16x2{128, 128};
-        return __builtin_bit_cast(uint32_t, v);
-    };
-    uint4 w;
-    w.x = sx(raw.x, 0x0c010c00u);
-    w.y = sx(raw.x, 0x0c030c02u);
-    w.z = sx(raw.y, 0x0c010c00u);
-    w.w = sx(raw.y, 0x0c030c02u);
-    if (q == 0) w.x = (w.x & 0xFFFF0000u) | ((uint32_t)dcv & 0xFFFFu);
-    const auto marked = [](uint32_t x) {  // any byte == 0x80
-        const uint32_t t = x ^ 0x80808080u;
-        return ((t - 0x01010101u) & ~t & 0x80808080u) != 0;
-    };
-    if (nesc > 0 && (marked(raw.x) || marked(raw.y))) {
-        for (int e = 0; e < nesc; ++e) {
-            const uint32_t ent = esc[e];
-            const int n = (int)(ent >> 16);
-            if ((n >> 3) != q) continue;
-            const int j = n & 7;
-            const bool hi = j & 1;
-            auto patch = [&](uint32_t d) {
-                return hi ? ((d & 0xFFFFu) | (ent << 16)) : ((d & 0xFFFF0000u) | (ent & 0xFFFFu));
-            };
-            if ((j >> 1) == 0) w.x = patch(w.x);
-            else if ((j >> 1) == 1) w.y = patch(w.y);
-            else if ((j >> 1) == 2) w.z = patch(w.z);
-            else w.w = patch(w.w);
-        }
-    }
-    return w;
-}
 
 __device__ __forceinline__ void wave_lds_sync()
 {
@@ -288,8 +247,7 @@ __device__ __forceinline__ int64_t shfl64(int64_t v, int src)
 // VALU).  The block index comes from the owner lane by shuffle; every active
 // lane runs every round of the loop (owners are active), only the stores are
 // predicated.
-__device__ __forceinline__ void flush_blocks(bool done, int64_t blk, int dcv, int nesc, const WaveStage& ws,
-                                             int16_t* coef)
+__device__ __forceinline__ void flush_blocks(bool done, int64_t blk, const WaveStage& ws, int16_t* coef)
 {
     const uint64_t pend = __ballot(done);
     if (pend == 0) return;  // uniform over the active lanes
@@ -307,23 +265,10 @@ __device__ __forceinline__ void flush_blocks(bool done, int64_t blk, int dcv, in
         const int bi = valid ? c >> 3 : 0, q = c & 7;
         const int o = ws.owner[bi];
         const int64_t ob = shfl64(blk, o);
-        int od = 0, on = 0;
-        if (WICCA_JPEG_STAGE == 2) {
-            od = __shfl(dcv, o, 64);
-            on = __shfl(nesc, o, 64);
-        }
         if (valid) {
-            uint4 v;
-            if (WICCA_JPEG_STAGE == 2) {
-                uint2* chunk = reinterpret_cast<uint2*>(ws.blocks8 + o * kLaneBlock + q * 8);
-                const uint2 raw = *chunk;
-                *chunk = uint2{0, 0};
-                v = expand_chunk(raw, q, od, ws.esc + o * kEsc, on);
-            } else {
-                uint4* chunk = reinterpret_cast<uint4*>(ws.blocks + o * kLaneBlock + q * 8);
-                v = *chunk;
-                *chunk = uint4{0, 0, 0, 0};
-            }
+            uint4* chunk = reinterpret_cast<uint4*>(ws.blocks + o * kLaneBlock + q * 8);
+            const uint4 v = *chunk;
+            *chunk = uint4{0, 0, 0, 0};
 #ifndef WICCA_JPEG_ABLATE_STORES
             *reinterpret_cast<uint4*>(coef + ob * 64 + q * 8) = v;
 #else
@@ -368,15 +313,8 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BitReader& br, int6
     int zk = 0;  // next zigzag position of a block written position by position (not staged)
     BlockPos pos;
     int16_t* lb = nullptr;
-    int8_t* lb8 = nullptr;    // STAGE 2: the lane's int8 block,
-    uint32_t* lesc = nullptr; // its escape list,
-    int dcv = 0, nesc = 0;    // the block's DC and escape count
     if (WRITE) {
-        if (WICCA_JPEG_STAGE == 1) lb = ws->blocks + (threadIdx.x & 63) * kLaneBlock;
-        if (WICCA_JPEG_STAGE == 2) {
-            lb8 = ws->blocks8 + (threadIdx.x & 63) * kLaneBlock;
-            lesc = ws->esc + (threadIdx.x & 63) * kEsc;
-        }
+        if (WICCA_JPEG_STAGE) lb = ws->blocks + (threadIdx.x & 63) * kLaneBlock;
         pos.init(im, g < 0 ? 0 : g);
         if (g >= block_lo && g < block_end) blk = pos.index(im);
         zk = st.k;  // the block in progress at the start: this lane owns [st.k, ...)
@@ -431,11 +369,7 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BitReader& br, int6
                 ++g;
                 blk = (g >= block_lo && g < block_end) ? pos.index(im) : -1;
                 if (blk >= 0) {
-                    if (WICCA_JPEG_STAGE == 2) {
-                        dcv = dc[c];
-                        nesc = 0;
-                        staged = true;
-                    } else if (WICCA_JPEG_STAGE) {
+                    if (WICCA_JPEG_STAGE) {
                         lb[0] = (int16_t)dc[c];
                         staged = true;
                     } else {
@@ -451,24 +385,7 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BitReader& br, int6
                 st.k += r;
                 if (WRITE && blk >= 0 && st.k < 64) {
                     const int n = ws->nat[st.k];
-                    if (staged && WICCA_JPEG_STAGE == 2 && (unsigned)(v + 127) > 254u) {
-                        if (nesc < kEsc) {  // |v| >= 128: a marker and the escape list
-                            lesc[nesc++] = ((uint32_t)n << 16) | ((uint32_t)v & 0xFFFFu);
-                            lb8[n] = (int8_t)-128;
-                        } else {  // spill (rare): the block so far straight to HBM, then unstaged
-                            uint2* ch = reinterpret_cast<uint2*>(lb8);
-                            uint4* d = reinterpret_cast<uint4*>(coef + blk * 64);
-                            for (int q = 0; q < 8; ++q) {
-                                d[q] = expand_chunk(ch[q], q, dcv, lesc, nesc);
-                                ch[q] = uint2{0, 0};
-                            }
-                            staged = false;
-                            coef[blk * 64 + n] = (int16_t)v;
-                            zk = st.k + 1;
-                        }
-                    } else if (staged && WICCA_JPEG_STAGE == 2) {
-                        lb8[n] = (int8_t)v;
-                    } else if (staged) {
+                    if (staged) {
                         lb[n] = (int16_t)v;
                     } else {
                         zero_zig(coef, ws->nat, blk, zk, st.k);
@@ -498,19 +415,11 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BitReader& br, int6
         // every codeword: deferring the flush until 4 / 8 / 16 blocks wait (the
         // finished lanes idle meanwhile) measured 6.1 / 7.4 / 7.5 ms per 25 x 8K
         // call against 3.0 ms
-        if (WRITE && WICCA_JPEG_STAGE) flush_blocks(done, blk, dcv, nesc, *ws, coef);
+        if (WRITE && WICCA_JPEG_STAGE) flush_blocks(done, blk, *ws, coef);
     }
     if (WRITE && blk >= 0 && st.k > 0) {  // the range ends inside block blk: this lane's part [.., st.k)
         const int kend = min(st.k, 64);
-        if (staged && WICCA_JPEG_STAGE == 2) {
-            const uint2* ch = reinterpret_cast<const uint2*>(lb8);
-            for (int z = 0; z < kend; ++z) {
-                const int n = ws->nat[z];
-                const uint4 w = expand_chunk(ch[n >> 3], n >> 3, dcv, lesc, nesc);
-                const uint32_t d = (n & 7) < 2 ? w.x : (n & 7) < 4 ? w.y : (n & 7) < 6 ? w.z : w.w;
-                coef[blk * 64 + n] = (int16_t)((n & 1) ? d >> 16 : d & 0xFFFFu);
-            }
-        } else if (staged) {
+        if (staged) {
             for (int z = 0; z < kend; ++z) {
                 const int n = ws->nat[z];
                 coef[blk * 64 + n] = lb[n];  // zeros where the block set nothing
@@ -763,32 +672,22 @@ __global__ __launch_bounds__(256) void jpeg_scan_kernel(JpegPlan P, const SubRes
 // image: 2 DC + 2 AC tables) keeps the workgroup's LDS under 40 KB, i.e. 4
 // workgroups per CU instead of 3.
 template <int NS>
-__global__ __launch_bounds__(kJThreads, NS > 4 ? 1 : WICCA_JPEG_STAGE == 2 ? 6 : 4) void jpeg_write_kernel(JpegPlan P, const SubResult* res,
+__global__ __launch_bounds__(kJThreads, NS <= 4 ? 4 : 1) void jpeg_write_kernel(JpegPlan P, const SubResult* res,
                                                                  const SubBase* base)
 {
     const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
     __shared__ ImgTabs<NS> tabs;
-#if WICCA_JPEG_STAGE == 1
+#if WICCA_JPEG_STAGE
     __shared__ __attribute__((aligned(16))) int16_t lanes[kJThreads * kLaneBlock];
-    __shared__ uint8_t s_owner[kJThreads];
-#elif WICCA_JPEG_STAGE == 2
-    __shared__ __attribute__((aligned(16))) int8_t lanes8[kJThreads * kLaneBlock];
-    __shared__ uint32_t s_esc[kJThreads * kEsc];
     __shared__ uint8_t s_owner[kJThreads];
 #endif
     __shared__ uint8_t s_nat[80];
     if (threadIdx.x < 80) s_nat[threadIdx.x] = (uint8_t)kNatural[threadIdx.x];
-#if WICCA_JPEG_STAGE == 1
+#if WICCA_JPEG_STAGE
     {  // every lane block starts zeroed (decode_run writes only what a block sets)
         uint4* z = reinterpret_cast<uint4*>(lanes + threadIdx.x * kLaneBlock);
 #pragma unroll
         for (int q = 0; q < 8; ++q) z[q] = uint4{0, 0, 0, 0};
-    }
-#elif WICCA_JPEG_STAGE == 2
-    {
-        uint4* z = reinterpret_cast<uint4*>(lanes8 + threadIdx.x * kLaneBlock);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) z[q] = uint4{0, 0, 0, 0};
     }
 #endif
     stage_tables(P, P.imgs + P.sub_img[blockIdx.x], tabs);  // its barrier covers s_nat and the zeroing
@@ -810,13 +709,11 @@ __global__ __launch_bounds__(kJThreads, NS > 4 ? 1 : WICCA_JPEG_STAGE == 2 ? 6 :
     int64_t started = 0;
     BitReader br;
     br.reset(P.stream, st.p);
+#if WICCA_JPEG_STAGE
     const int w0 = (int)(threadIdx.x & ~63u);  // the wave's first lane
-#if WICCA_JPEG_STAGE == 1
-    const WaveStage ws{lanes + w0 * kLaneBlock, s_owner + w0, s_nat, nullptr, nullptr};
-#elif WICCA_JPEG_STAGE == 2
-    const WaveStage ws{nullptr, s_owner + w0, s_nat, lanes8 + w0 * kLaneBlock, s_esc + w0 * kEsc};
+    const WaveStage ws{lanes + w0 * kLaneBlock, s_owner + w0, s_nat};
 #else
-    const WaveStage ws{nullptr, nullptr, s_nat, nullptr, nullptr};
+    const WaveStage ws{nullptr, nullptr, s_nat};
 #endif
     // the block in progress at the start was started by an earlier lane
     decode_run<true>(im, tabs.t, br, b1, st, started, dc, sg.block0 + b.block - 1, sg.block0,
