@@ -521,8 +521,15 @@ template <int CK, int NS>
 __global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(JpegPlan P, const SubResult* prev,
                                                              SubResult* next, int round, int* changed,
                                                              const SubResult* older, SyncCk* cks, int* stats,
-                                                             const SubResult* r0res)
+                                                             const SubResult* r0res, const int* prev_changed)
 {
+    // launched ahead of the host's look at the flags: once a round moved no
+    // end state, every later round repeats its results
+    if (prev_changed && *prev_changed == 0) {
+        const int64_t li = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
+        if (li < P.n_sub) next[li] = prev[li];
+        return;
+    }
     const int64_t i = (int64_t)blockIdx.x * kJThreads + threadIdx.x;
     __shared__ ImgTabs<NS, HuffDevSync> tabs;
     // this lane's start state, and whether it has to decode at all (every
@@ -1426,7 +1433,7 @@ bool jpeg_fused()
 size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg)
 {
     (void)n_seg;
-    return (size_t)n_sub * (4 * sizeof(SubResult) + sizeof(SubBase) + kSyncCk * sizeof(SyncCk)) + 64 +
+    return (size_t)n_sub * (4 * sizeof(SubResult) + sizeof(SubBase) + kSyncCk * sizeof(SyncCk)) + 256 +
            kJpegMaxJobs * sizeof(IdctJob);
 }
 
@@ -1439,8 +1446,8 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     SubResult* rc = rb + P.n_sub;
     SubResult* r0 = rc + P.n_sub;  // round 0's results: kept for every later round's checkpoint hits
     SubBase* sb = (SubBase*)(r0 + P.n_sub);
-    int* changed = (int*)(sb + P.n_sub);
-    IdctJob* jobs = (IdctJob*)((uint8_t*)changed + 64);
+    int* flags = (int*)(sb + P.n_sub);  // [0, kFlagRing): per-round "an end state changed"; then stats
+    IdctJob* jobs = (IdctJob*)((uint8_t*)flags + 256);
     SyncCk* cks = (SyncCk*)(jobs + kJpegMaxJobs);
     // IDCT jobs: every (image, component); uploaded first, while the stream
     // still waits for the entropy-coded data
@@ -1482,7 +1489,8 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
         }();
         static const bool stats_on = getenv("WICCA_JPEG_TIMING") != nullptr;
         constexpr int kStatRounds = 6;
-        int* stats = changed + 4;  // [round][decoding lanes, checkpoint hits]
+        constexpr int kFlagRing = 16, kSpec = 4;  // flag slots (a ring), rounds launched per host look
+        int* stats = flags + kFlagRing;  // [round][decoding lanes, checkpoint hits]
         if (stats_on && (e = hipMemsetAsync(stats, 0, 2 * kStatRounds * sizeof(int), s)) != hipSuccess) return e;
         // the 4-slot kernels (18 KB of 11-bit tables: 8 workgroups per CU)
         // serve every baseline image; 6 slots only for extended-sequential
@@ -1494,9 +1502,11 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
         const bool ns4 = P.max_tabs <= 4 && !force6;
         auto sync = [&](int ck, const SubResult* prev, SubResult* next, int round, const SubResult* older,
                         int* st) {
+            int* changed = flags + round % kFlagRing;
+            const int* prev_changed = round >= 2 ? flags + (round - 1) % kFlagRing : nullptr;
 #define WICCA_SYNC_LAUNCH(CKV, NSV)                                                                        \
     hipLaunchKernelGGL((jpeg_sync_kernel<CKV, NSV>), dim3(grid), dim3(kJThreads), 0, s, P, prev, next, round, \
-                       changed, older, cks, st, (const SubResult*)r0)
+                       changed, older, cks, st, (const SubResult*)r0, prev_changed)
             if (ns4) {
                 if (ck == 1) WICCA_SYNC_LAUNCH(1, 4);
                 else if (ck == 2) WICCA_SYNC_LAUNCH(2, 4);
@@ -1511,24 +1521,43 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
         };
         e = sync(ck_mode ? 1 : 0, r0, r0, 0, nullptr, stats_on ? stats : nullptr);
         if (e != hipSuccess) return e;
+        // rounds go out kSpec at a time with one host look per batch (a round
+        // whose predecessor changed nothing copies its results and exits), so
+        // the usual three rounds cost one host round trip instead of three
         SubResult* const bufs[3] = {ra, rb, rc};
         const SubResult* older = nullptr;
         SubResult* cur = r0;
-        int rounds = 0;
+        int rounds = 0;  // rounds whose results are final in `cur`
+        int launched = 0;
         for (;;) {
-            int h_changed = 0;
-            e = hipMemsetAsync(changed, 0, sizeof(int), s);
+            int* slot0 = flags + (launched + 1) % kFlagRing;
+            if ((launched + 1) % kFlagRing + kSpec <= kFlagRing) {
+                e = hipMemsetAsync(slot0, 0, kSpec * sizeof(int), s);
+            } else {
+                for (int r = launched + 1; r <= launched + kSpec && e == hipSuccess; ++r)
+                    e = hipMemsetAsync(flags + r % kFlagRing, 0, sizeof(int), s);
+            }
             if (e != hipSuccess) return e;
-            SubResult* nxt = bufs[rounds % 3];
-            int* st_r = stats_on && rounds + 1 < kStatRounds ? stats + 2 * (rounds + 1) : nullptr;
-            e = sync(ck_mode ? 2 : 0, cur, nxt, rounds + 1, older, st_r);
-            if (e == hipSuccess) e = hipMemcpyAsync(&h_changed, changed, sizeof(int), hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e != hipSuccess) return e;
-            older = cur;
-            cur = nxt;
-            ++rounds;
-            if (!h_changed || rounds > P.n_sub) break;
+            for (int r = launched + 1; r <= launched + kSpec; ++r) {
+                SubResult* nxt = bufs[(r - 1) % 3];
+                int* st_r = stats_on && r < kStatRounds ? stats + 2 * r : nullptr;
+                if ((e = sync(ck_mode ? 2 : 0, cur, nxt, r, older, st_r)) != hipSuccess) return e;
+                older = cur;
+                cur = nxt;
+            }
+            int h[kFlagRing];
+            if ((e = hipMemcpyAsync(h, flags, sizeof(h), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+            if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+            int conv = 0;  // the first round of the batch that changed nothing
+            for (int r = launched + 1; r <= launched + kSpec && !conv; ++r)
+                if (!h[r % kFlagRing]) conv = r;
+            launched += kSpec;
+            if (conv) {
+                rounds = conv;
+                break;
+            }
+            rounds = launched;
+            if (rounds > P.n_sub) break;
         }
         if (sync_rounds) *sync_rounds = rounds;
         if (stats_on) {
