@@ -286,6 +286,25 @@ int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64
 /* Synchronisation passes of the calling thread's last JPEG decode (diagnostic). */
 int wicca_jpeg_last_sync_rounds(void);
 
+/* wicca_jpeg_decode_u8 into DEVICE buffers without waiting for the device: it
+ * returns once the host's part is done (parse, de-stuffing, uploads issued,
+ * kernels queued on a stream of its own) with *ticket set; the images are
+ * complete when wicca_jpeg_wait(*ticket) returns 0.  A data loader issues
+ * batch k+1 before waiting for batch k, so k+1's host work and PCIe transfer
+ * overlap k's device decode (each call in flight holds its own workspace).
+ * data[i] must stay valid until the wait (a decode whose Huffman
+ * synchronisation needs more passes than were launched ahead is redone there,
+ * synchronously).  No per-file status: a file that fails to parse fails the
+ * call, as with status == NULL.  *ticket == 0: nothing was queued (n == 0, or
+ * a batch larger than one device pass, which decodes before returning). */
+int wicca_jpeg_decode_u8_async(const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                               uint8_t* const* dsts, const int64_t* dst_pitches,
+                               int apply_orientation, int device, int64_t* ticket);
+
+/* Wait for an asynchronous decode and release its workspace (ticket 0: no-op).
+ * Returns its status; an unknown ticket is WICCA_ERR_ARG. */
+int wicca_jpeg_wait(int64_t ticket);
+
 /* The quantised DCT coefficients of a JPEG file as the host entropy decoder
  * produces them for multi-scan files (progressive SOF2, or sequential with a
  * scan per component; jdhuff.c / jdphuff.c semantics): components back to

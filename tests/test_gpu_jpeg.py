@@ -117,6 +117,41 @@ def test_multiscan_sequential_matches_libjpeg(kind, H, W, sub, q, order, ri):
     assert np.array_equal(got[1], ref) and np.array_equal(got[0], J.decode_rgb(base))
 
 
+def test_async_decode_matches_libjpeg():
+    """wicca_jpeg_decode_u8_async / wicca_jpeg_wait through decode_batches:
+    several batches in flight (baseline, progressive, grayscale, EXIF-rotated,
+    restart intervals), every image equal to libjpeg-turbo's decode."""
+    specs = [("scene", 480, 640, 2, 90, 0, False, 1), ("noise", 200, 300, 0, 70, 4, False, 1),
+             ("scene", 333, 517, 1, 85, 0, True, 1), ("gray", 97, 55, 0, 80, 0, False, 1),
+             ("smooth", 256, 384, 2, 60, 0, False, 6)]
+    batches = []
+    for k in range(5):
+        batch = []
+        for i, (kind, h, w, sub, q, rb, prog, orient) in enumerate(specs[k % 3:] + specs[:k % 3]):
+            img = J.test_image(kind, h + k, w + 2 * k, 31 * k + i)
+            batch.append(J.encode(img, q, sub, rb, progressive=prog, orientation=orient))
+        batches.append(batch)
+    got = list(WJ.decode_batches(batches, depth=2))
+    assert len(got) == len(batches)
+    for blobs, outs in zip(batches, got):
+        for b, o in zip(blobs, outs):
+            assert np.array_equal(o.cpu().numpy(), J.decode_rgb(b))
+    # depth 1 (no overlap) gives the same
+    again = list(WJ.decode_batches(batches[:2], depth=1))
+    for a, b in zip(got[:2], again):
+        assert all(np.array_equal(x.cpu().numpy(), y.cpu().numpy()) for x, y in zip(a, b))
+
+
+def test_async_decode_errors():
+    from wicca_amd import _lib
+    lib = _lib.load()
+    assert lib.wicca_jpeg_wait(0) == 0
+    assert lib.wicca_jpeg_wait(987654321) == _lib.WICCA_ERR_ARG
+    good = J.encode(J.test_image("scene", 64, 64, 5), 80, 2)
+    with pytest.raises(ValueError):
+        list(WJ.decode_batches([[good], [good[:40]]]))
+
+
 def test_mixed_progressive_and_baseline_batch(tmp_path):
     """One decode call over baseline (device Huffman decode) and progressive
     (host entropy decode) files, and the file-based caller stage over them."""

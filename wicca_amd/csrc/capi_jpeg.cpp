@@ -10,7 +10,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "capi_internal.h"
@@ -97,7 +100,11 @@ bool jpeg_timing()
 // stream: the next call rewrites that staging (jhost, jtab) on the host.
 struct SyncOnExit {
     hipStream_t s;
-    ~SyncOnExit() { (void)hipStreamSynchronize(s); }
+    bool active = true;  // an asynchronous call that issued everything returns without waiting
+    ~SyncOnExit()
+    {
+        if (active) (void)hipStreamSynchronize(s);
+    }
 };
 
 double now_ms()
@@ -105,9 +112,12 @@ double now_ms()
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// async_rounds > 0 (n <= one pass): everything is issued on `stream` and the
+// call returns without waiting; *async_flags gets the device flags to check
+// once the stream is done (jpeg_decode_device).
 int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
                           uint8_t* const* dst, const int64_t* dpitch, bool orient, hipStream_t stream,
-                          int* rounds_out)
+                          int* rounds_out, int async_rounds = 0, const int** async_flags = nullptr)
 {
     // at most kJpegMaxJobs (image, component) IDCT jobs per device pass
     constexpr int64_t kChunk = wicca::kJpegMaxJobs / wicca::kJpegMaxComp;
@@ -319,7 +329,8 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     uint8_t* m = (uint8_t*)ws->jmeta.ptr;
     // the small tables, packed in pinned memory (a pageable copy would make the
     // host wait for the stream uploads before issuing the decode)
-    HIP_TRY(ws->jtab.reserve(meta_bytes, 1 << 20));
+    const size_t jobs_off = round_up((int64_t)meta_bytes, 256);  // the IDCT job list's pinned staging follows
+    HIP_TRY(ws->jtab.reserve(jobs_off + wicca::jpeg_jobs_bytes(), 1 << 20));
     uint8_t* packed = ws->jtab.ptr;
     memset(packed, 0, meta_bytes);
     memcpy(packed, segs.data(), segs.size() * sizeof(wicca::JpegSegDev));
@@ -356,13 +367,18 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     }
     int rounds = 0;
     const double t_upload = now_ms();
-    HIP_TRY(wicca::jpeg_decode_device(P, ims.data(), ws->jscratch.ptr, n, &rounds, stream));
+    HIP_TRY(wicca::jpeg_decode_device(P, ims.data(), ws->jscratch.ptr, n, &rounds, stream, async_rounds,
+                                      async_flags, ws->jtab.ptr + jobs_off));
     if (rounds_out) *rounds_out = rounds;
     for (int64_t i = 0; i < n; ++i)
         if (tmp_off[(size_t)i] >= 0)
             HIP_TRY(wicca::launch_orient(ims[(size_t)i].dst, ims[(size_t)i].dst_pitch, info[(size_t)i].W,
                                          info[(size_t)i].H, info[(size_t)i].orientation, dst[i], dpitch[i],
                                          stream));
+    if (async_rounds > 0) {  // the caller holds the workspace (and its pinned staging) until it waits
+        sync_on_exit.active = false;
+        return WICCA_OK;
+    }
     // the pinned staging (streams, tables) is reused by the next call
     HIP_TRY(hipStreamSynchronize(stream));
     if (jpeg_timing())
@@ -480,9 +496,101 @@ int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, c
     return WICCA_OK;
 }
 
+// Asynchronous decodes in flight (wicca_jpeg_decode_u8_async): each holds
+// its workspace — stream, device buffers and pinned staging — until its
+// wicca_jpeg_wait, so the next call takes another workspace from the pool and
+// its host work and uploads overlap this one's device work.
+struct AsyncDecode {
+    WorkspaceLease lease;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    const int* flags = nullptr;  // device ring of per-round "changed" flags
+    std::vector<const uint8_t*> data;  // for the synchronous redo if the rounds launched did not converge
+    std::vector<int64_t> sizes, pitches;
+    std::vector<uint8_t*> dsts;
+    bool orient = true;
+};
+constexpr int kAsyncRounds = 8;  // synchronisation rounds launched ahead (3 suffice on the corpus)
+std::mutex g_async_mu;
+std::unordered_map<int64_t, std::unique_ptr<AsyncDecode>> g_async;
+int64_t g_async_next = 1;
+
 }  // namespace
 
 extern "C" {
+
+int wicca_jpeg_decode_u8_async(const uint8_t* const* data, const int64_t* sizes, int64_t n, uint8_t* const* dsts,
+                               const int64_t* dst_pitches, int apply_orientation, int device, int64_t* ticket)
+{
+    if (!ticket) return fail(WICCA_ERR_ARG, "null ticket");
+    *ticket = 0;
+    if (n < 0 || (n > 0 && (!data || !sizes || !dsts || !dst_pitches))) return fail(WICCA_ERR_ARG, "bad arrays");
+    if (n == 0) return WICCA_OK;
+    if (n > wicca::kJpegMaxJobs / wicca::kJpegMaxComp)  // more than one device pass: decode synchronously
+        return wicca_jpeg_decode_u8(data, sizes, n, dsts, dst_pitches, apply_orientation, 1, device, nullptr,
+                                    nullptr);
+    int rc;
+    for (int64_t i = 0; i < n; ++i) {
+        wicca::JpegInfo f;
+        if ((rc = parse_one(data[i], sizes[i], &f, i))) return rc;
+        int64_t oh, ow;
+        oriented_dims(f, apply_orientation != 0, &oh, &ow);
+        if (!dsts[i] || dst_pitches[i] < ow * 3) return fail(WICCA_ERR_ARG, "bad output %lld", (long long)i);
+    }
+    DeviceGuard dg;
+    int dev;
+    if ((rc = select_device(device, &dev, dg))) return rc;
+    std::unique_ptr<AsyncDecode> st(new AsyncDecode);
+    if ((rc = acquire(dev, st->lease))) return rc;
+    st->device = dev;
+    st->stream = st->lease.ws->stream;
+    int rounds = 0;
+    if ((rc = jpeg_decode_to_device(st->lease.ws, data, sizes, n, dsts, dst_pitches, apply_orientation != 0,
+                                    st->stream, &rounds, kAsyncRounds, &st->flags)))
+        return rc;
+    st->data.assign(data, data + n);
+    st->sizes.assign(sizes, sizes + n);
+    st->dsts.assign(dsts, dsts + n);
+    st->pitches.assign(dst_pitches, dst_pitches + n);
+    st->orient = apply_orientation != 0;
+    std::lock_guard<std::mutex> g(g_async_mu);
+    const int64_t id = g_async_next++;
+    g_async[id] = std::move(st);
+    *ticket = id;
+    return WICCA_OK;
+}
+
+int wicca_jpeg_wait(int64_t ticket)
+{
+    if (ticket == 0) return WICCA_OK;
+    std::unique_ptr<AsyncDecode> st;
+    {
+        std::lock_guard<std::mutex> g(g_async_mu);
+        auto it = g_async.find(ticket);
+        if (it == g_async.end()) return fail(WICCA_ERR_ARG, "unknown JPEG ticket %lld", (long long)ticket);
+        st = std::move(it->second);
+        g_async.erase(it);
+    }
+    DeviceGuard dg;
+    int dev, rc;
+    if ((rc = select_device(st->device, &dev, dg))) return rc;
+    HIP_TRY(hipStreamSynchronize(st->stream));
+    if (st->flags) {
+        int h[16];
+        HIP_TRY(hipMemcpy(h, st->flags, sizeof(h), hipMemcpyDeviceToHost));
+        bool converged = false;
+        for (int r = 1; r <= kAsyncRounds; ++r) converged |= h[r % 16] == 0;
+        if (!converged) {  // rare: redo with the host looking at every round
+            int rounds = 0;
+            if ((rc = jpeg_decode_to_device(st->lease.ws, st->data.data(), st->sizes.data(),
+                                            (int64_t)st->data.size(), st->dsts.data(), st->pitches.data(),
+                                            st->orient, st->stream, &rounds)))
+                return rc;
+        }
+    }
+    return WICCA_OK;
+}
+
 
 int wicca_jpeg_info(const uint8_t* data, int64_t size, int apply_orientation, int64_t* height, int64_t* width,
                     int* components, int* orientation)

@@ -158,8 +158,18 @@ constexpr int kJpegLanes = 256;
 // jpeg_scratch_bytes).  *sync_rounds receives the synchronisation passes run.
 constexpr int kJpegMaxJobs = 4096;  // (image, component) pairs per call
 size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg);
+// async_rounds > 0: launch exactly that many synchronisation rounds (<= 15)
+// without reading their flags on the host (nothing in the call waits for
+// the device); *async_flags then points at the device ring of per-round
+// "changed" flags: the decode converged iff some round r in 1..async_rounds
+// has flags[r % 16] == 0 (check after the stream completes).
+// pinned_jobs: jpeg_jobs_bytes() of pinned host memory for the IDCT job list's
+// upload (a pageable source makes hipMemcpyAsync wait for the stream's earlier
+// work, i.e. the whole batch's uploads); nullptr: pageable.
+size_t jpeg_jobs_bytes();
 hipError_t jpeg_decode_device(const JpegPlan& plan, const JpegImageDev* ims, void* scratch, int64_t n_images,
-                              int* sync_rounds, hipStream_t s);
+                              int* sync_rounds, hipStream_t s, int async_rounds = 0,
+                              const int** async_flags = nullptr, void* pinned_jobs = nullptr);
 
 // RGB image (W x H) -> its EXIF-oriented copy (orientation 1..8; 5-8 swap W/H).
 hipError_t launch_orient(const uint8_t* src, int64_t sp, int W, int H, int orient, uint8_t* dst, int64_t dp,

@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "jpeg.h"
@@ -1430,6 +1431,8 @@ bool jpeg_fused()
     return on;
 }
 
+size_t jpeg_jobs_bytes() { return kJpegMaxJobs * sizeof(IdctJob); }
+
 size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg)
 {
     (void)n_seg;
@@ -1438,8 +1441,10 @@ size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg)
 }
 
 hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* scratch, int64_t n_images,
-                              int* sync_rounds, hipStream_t s)
+                              int* sync_rounds, hipStream_t s, int async_rounds, const int** async_flags,
+                              void* pinned_jobs)
 {
+    if (async_flags) *async_flags = nullptr;  // no device Huffman decode: nothing to check
     uint8_t* base = (uint8_t*)scratch;
     SubResult* ra = (SubResult*)base;
     SubResult* rb = ra + P.n_sub;
@@ -1469,8 +1474,10 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             max_blocks = std::max<int64_t>(max_blocks, (int64_t)j.bw * j.bh);
         }
     if (hj.size() > (size_t)kJpegMaxJobs) return hipErrorInvalidValue;
+    if (pinned_jobs && !hj.empty()) memcpy(pinned_jobs, hj.data(), sizeof(IdctJob) * hj.size());
     hipError_t e = hj.empty() ? hipSuccess
-                              : hipMemcpyAsync(jobs, hj.data(), sizeof(IdctJob) * hj.size(), hipMemcpyHostToDevice, s);
+                              : hipMemcpyAsync(jobs, pinned_jobs ? pinned_jobs : hj.data(), sizeof(IdctJob) * hj.size(),
+                                               hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return e;
     // the device Huffman decode (every image not decoded on the host)
     if (P.n_sub > 0) {
@@ -1529,29 +1536,35 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
         SubResult* cur = r0;
         int rounds = 0;  // rounds whose results are final in `cur`
         int launched = 0;
+        const int batch = async_rounds > 0 ? std::min(async_rounds, kFlagRing - 1) : kSpec;
+        if (async_flags) *async_flags = flags;
         for (;;) {
             int* slot0 = flags + (launched + 1) % kFlagRing;
-            if ((launched + 1) % kFlagRing + kSpec <= kFlagRing) {
-                e = hipMemsetAsync(slot0, 0, kSpec * sizeof(int), s);
+            if ((launched + 1) % kFlagRing + batch <= kFlagRing) {
+                e = hipMemsetAsync(slot0, 0, batch * sizeof(int), s);
             } else {
-                for (int r = launched + 1; r <= launched + kSpec && e == hipSuccess; ++r)
+                for (int r = launched + 1; r <= launched + batch && e == hipSuccess; ++r)
                     e = hipMemsetAsync(flags + r % kFlagRing, 0, sizeof(int), s);
             }
             if (e != hipSuccess) return e;
-            for (int r = launched + 1; r <= launched + kSpec; ++r) {
+            for (int r = launched + 1; r <= launched + batch; ++r) {
                 SubResult* nxt = bufs[(r - 1) % 3];
                 int* st_r = stats_on && r < kStatRounds ? stats + 2 * r : nullptr;
                 if ((e = sync(ck_mode ? 2 : 0, cur, nxt, r, older, st_r)) != hipSuccess) return e;
                 older = cur;
                 cur = nxt;
             }
+            if (async_rounds > 0) {  // the caller checks the flags once the stream is done
+                rounds = -1;
+                break;
+            }
             int h[kFlagRing];
             if ((e = hipMemcpyAsync(h, flags, sizeof(h), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
             if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
             int conv = 0;  // the first round of the batch that changed nothing
-            for (int r = launched + 1; r <= launched + kSpec && !conv; ++r)
+            for (int r = launched + 1; r <= launched + batch && !conv; ++r)
                 if (!h[r % kFlagRing]) conv = r;
-            launched += kSpec;
+            launched += batch;
             if (conv) {
                 rounds = conv;
                 break;
@@ -1560,7 +1573,7 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             if (rounds > P.n_sub) break;
         }
         if (sync_rounds) *sync_rounds = rounds;
-        if (stats_on) {
+        if (stats_on && async_rounds <= 0) {
             int h[2 * kStatRounds];
             if ((e = hipMemcpy(h, stats, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess) return e;
             fprintf(stderr, "[wicca jpeg] %lld subsequences; decoding lanes / checkpoint hits per round:",

@@ -90,6 +90,54 @@ def decode_batch(blobs: Sequence[bytes], apply_orientation: bool = True,
     return outs
 
 
+def decode_batches(batches, apply_orientation: bool = True, device: int = 0, depth: int = 2):
+    """Pipelined GPU decode of a stream of JPEG batches (a data loader's
+    loop): yields, per batch of file bytes, a list of device RGB
+    ``torch.uint8`` tensors (H, W, 3).  Up to ``depth`` batches are in flight
+    (``wicca_jpeg_decode_u8_async``): batch k+1's parse, de-stuffing and PCIe
+    transfer overlap batch k's device decode.  Each yielded batch is complete
+    (its ``wicca_jpeg_wait`` returned); files that do not parse raise."""
+    import collections
+    if depth < 1:
+        raise ValueError("depth must be >= 1")
+    lib = _lib.load()
+    pending = collections.deque()
+
+    def finish():
+        ticket, outs, keep = pending.popleft()
+        _lib.check(lib.wicca_jpeg_wait(ticket))
+        del keep
+        return outs
+
+    try:
+        yield from _decode_batches_loop(batches, apply_orientation, device, depth, lib, pending, finish)
+    finally:  # an exception or an abandoned generator still waits for what is in flight
+        while pending:
+            lib.wicca_jpeg_wait(pending.popleft()[0])
+
+
+def _decode_batches_loop(batches, apply_orientation, device, depth, lib, pending, finish):
+    import torch
+    for blobs in batches:
+        blobs = list(blobs)
+        outs = []
+        for b in blobs:
+            h, w, _, _ = info(b, apply_orientation)
+            outs.append(torch.empty((h, w, 3), dtype=torch.uint8, device=f"cuda:{device}"))
+        n = len(blobs)
+        keep, ptrs, sizes = _buffers(blobs)
+        dsts = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
+        pitches = (ctypes.c_int64 * n)(*[o.shape[1] * 3 for o in outs])
+        if len(pending) >= depth:
+            yield finish()
+        ticket = ctypes.c_int64(0)
+        _lib.check(lib.wicca_jpeg_decode_u8_async(ptrs, sizes, n, dsts, pitches, int(apply_orientation),
+                                                  int(device), ctypes.byref(ticket)))
+        pending.append((ticket.value, outs, (keep, blobs)))
+    while pending:
+        yield finish()
+
+
 def decode(data: bytes, apply_orientation: bool = True, device: int | None = None) -> np.ndarray:
     """RGB (H, W, 3) uint8 array of one JPEG file's bytes."""
     return decode_batch([data], apply_orientation, device)[0]
