@@ -338,6 +338,45 @@ int wicca_jpeg_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* s
                                     const int* devices, int n_devices, int* status);
 
 /*
+ * Any-format file decode: the rest of cv2.imread's formats on the reference's
+ * path (ClassifierProcessor counts .jpg .jpeg .png .bmp files,
+ * classifying_tools.py:162; load_image is cv2.imread IMREAD_COLOR +
+ * BGR2RGB, data_loader.py:53-58).  Each file is sniffed: JPEG as above, PNG
+ * (every colour type and bit depth, Adam7; zlib inflate and row
+ * reconstruction on host threads, pixel conversion on the device: palette
+ * expanded, gray replicated, alpha stripped, 16-bit samples -> high byte),
+ * BMP (1/4/8-bit palette, 16-bit 5-5-5 / 5-6-5, 24, 32-bit; bottom-up or
+ * top-down).  RLE BMP, TIFF, GIF: WICCA_ERR_UNSUPPORTED / WICCA_ERR_DECODE.
+ * Same arguments and per-slot status semantics as the wicca_jpeg_* calls;
+ * with a status array a PNG whose compressed data turns out corrupt during
+ * the decode also fails only its own slot.
+ */
+
+/* Decoded size of a file (EXIF orientation applied to JPEG when
+ * apply_orientation); kind: 1 JPEG, 2 PNG, 3 BMP. */
+int wicca_image_info(const uint8_t* data, int64_t size, int apply_orientation,
+                     int64_t* height, int64_t* width, int* kind);
+
+/* wicca_jpeg_decode_u8 for JPEG, PNG and BMP files (one call, mixed). */
+int wicca_image_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                          uint8_t* const* dsts, const int64_t* dst_pitches,
+                          int apply_orientation, int dst_is_device, int device, void* stream,
+                          int* status);
+
+/* wicca_jpeg_icon_stage_u8 for JPEG, PNG and BMP files. */
+int wicca_image_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                              int depth, int border_type, int border_constant,
+                              int64_t out_w, int64_t out_h, int interpolation,
+                              uint8_t* resized, uint8_t* resized_icons, int device, int* status);
+
+/* wicca_jpeg_icon_stage_multi_gpu for JPEG, PNG and BMP files. */
+int wicca_image_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                                     int depth, int border_type, int border_constant,
+                                     int64_t out_w, int64_t out_h, int interpolation,
+                                     uint8_t* resized, uint8_t* resized_icons,
+                                     const int* devices, int n_devices, int* status);
+
+/*
  * Deterministic synthetic images on device (no PCIe in timed regions):
  * byte (i, y, x, c) = splitmix64-hash of (seed, i, y*W*C + x*C + c), see
  * wicca_amd/synth.py for the host restatement.

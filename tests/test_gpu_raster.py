@@ -1,0 +1,225 @@
+"""GPU PNG / BMP decode (load_image's cv2.imread for the .png / .bmp inputs
+ClassifierProcessor counts, classifying_tools.py:162; data_loader.py:53-58)
+against the restatement in oracle/raster_ref.py (itself pinned to Pillow
+12.2.0 in tests/test_raster_oracle.py) and, at sizes the pure-Python
+restatement is slow for, against Pillow directly; mixed-format batches; the
+file-based caller stage; corrupt files failing their own slot."""
+import hashlib
+import io
+import json
+import os
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import wicca_amd
+from oracle import c_oracle
+from oracle import jpeg_pil as J
+from oracle import raster_ref as rr
+from oracle import resize_cv as R
+from wicca_amd import jpeg as WJ
+
+pytestmark = pytest.mark.gpu
+
+from test_raster_oracle import PNG_CASES, png_samples  # noqa: E402
+
+
+@pytest.mark.parametrize("interlace", [False, True])
+@pytest.mark.parametrize("ct,bits", PNG_CASES)
+def test_png_types_vs_oracle(ct, bits, interlace):
+    blobs = []
+    for i, (h, w) in enumerate([(1, 1), (3, 5), (37, 29), (64, 131)]):
+        s, pal = png_samples(ct, bits, h, w, seed=ct * 1000 + bits * 10 + i)
+        blobs.append(rr.encode_png(s, ct, bits, interlace=interlace, palette=pal))
+    outs = WJ.decode_batch(blobs)
+    for b, o in zip(blobs, outs):
+        assert np.array_equal(o, rr.decode_png(b))
+    assert WJ.image_info(blobs[2])[:3] == (37, 29, "png")
+
+
+@pytest.mark.parametrize("f", range(5))
+@pytest.mark.parametrize("ct,bits", [(2, 8), (6, 16), (0, 4), (3, 8)])
+def test_png_each_filter(ct, bits, f):
+    s, pal = png_samples(ct, bits, 23, 41, seed=f)
+    data = rr.encode_png(s, ct, bits, palette=pal, filters=f)
+    assert np.array_equal(WJ.decode(data), rr.decode_png(data))
+
+
+def test_png_split_idat_and_ancillary_chunks():
+    s, _ = png_samples(2, 8, 50, 70, seed=9)
+    anc = [(b"gAMA", struct.pack(">I", 45455)), (b"tEXt", b"Comment\x00hello"), (b"sRGB", b"\x00")]
+    data = rr.encode_png(s, 2, 8, idat_split=97, extra_chunks=anc)
+    assert np.array_equal(WJ.decode(data), rr.pillow_rgb(data))
+    # an ancillary chunk with a bad CRC is ignored (libpng: a warning)
+    k = data.index(b"tEXt")
+    bad = data[:k + 4] + b"X" + data[k + 5:]
+    assert np.array_equal(WJ.decode(bad), rr.pillow_rgb(data))
+
+
+@pytest.mark.parametrize("mode", ["RGB", "RGBA", "L", "LA", "P", "1"])
+@pytest.mark.parametrize("H,W", [(480, 640), (1080, 1920)])
+def test_pillow_written_png(mode, H, W):
+    from PIL import Image
+    img = J.test_image("scene", H, W, H + len(mode))
+    b = io.BytesIO()
+    Image.fromarray(img).convert(mode).save(b, "PNG", compress_level=1)
+    data = b.getvalue()
+    assert np.array_equal(WJ.decode(data), rr.pillow_rgb(data))
+
+
+def test_png_8k_rgb_vs_pillow():
+    from PIL import Image
+    img = J.test_image("scene", 4320, 7680, 11)
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, "PNG", compress_level=1)
+    assert np.array_equal(WJ.decode(b.getvalue()), img)
+
+
+@pytest.mark.parametrize("bpp", [1, 4, 8, 24, 32])
+@pytest.mark.parametrize("top_down", [False, True])
+def test_bmp_vs_oracle(bpp, top_down):
+    rng = np.random.default_rng(bpp + 10 * top_down)
+    blobs = []
+    for (h, w) in [(1, 1), (7, 3), (19, 23), (100, 257)]:
+        if bpp <= 8:
+            idx = rng.integers(0, 1 << bpp, (h, w), dtype=np.uint8)
+            pal = rng.integers(0, 256, (1 << bpp, 3), dtype=np.uint8)
+            blobs.append(rr.encode_bmp(idx, bpp, palette=pal, top_down=top_down))
+        else:
+            blobs.append(rr.encode_bmp(rng.integers(0, 256, (h, w, 3), dtype=np.uint8), bpp, top_down=top_down))
+    for b, o in zip(blobs, WJ.decode_batch(blobs)):
+        assert np.array_equal(o, rr.decode_bmp(b))
+        assert np.array_equal(o, rr.pillow_rgb(b))
+
+
+@pytest.mark.parametrize("fields565", [None, False, True])
+def test_bmp16(fields565):
+    img = np.random.default_rng(3).integers(0, 256, (31, 45, 3), dtype=np.uint8)
+    data = rr.encode_bmp(img, 16, fields565=fields565)
+    assert np.array_equal(WJ.decode(data), rr.decode_bmp(data))  # OpenCV's shifts (unpinned)
+
+
+def test_bmp_core_header_and_pillow_written():
+    from PIL import Image
+    rng = np.random.default_rng(8)
+    idx = rng.integers(0, 256, (33, 47), dtype=np.uint8)
+    pal = rng.integers(0, 256, (256, 3), dtype=np.uint8)
+    data = rr.encode_bmp(idx, 8, palette=pal, core_header=True)
+    assert np.array_equal(WJ.decode(data), pal[idx])
+    img = J.test_image("scene", 300, 401, 4)
+    for mode in ["RGB", "L", "P", "1"]:
+        b = io.BytesIO()
+        Image.fromarray(img).convert(mode).save(b, "BMP")
+        assert np.array_equal(WJ.decode(b.getvalue()), rr.pillow_rgb(b.getvalue())), mode
+
+
+def _mixed_files(tmp_path):
+    from PIL import Image
+    paths, refs = [], []
+    specs = [("jpg", 480, 640), ("png", 333, 517), ("bmp", 600, 401), ("png", 1080, 1920), ("jpg", 250, 333),
+             ("bmp", 91, 123)]
+    for i, (fmt, h, w) in enumerate(specs):
+        img = J.test_image("scene", h, w, 70 + i)
+        if fmt == "jpg":
+            data = J.encode(img, 85, 2)
+            ref = J.decode_rgb(data)
+        else:
+            b = io.BytesIO()
+            Image.fromarray(img).save(b, "PNG" if fmt == "png" else "BMP")
+            data = b.getvalue()
+            ref = img
+        p = tmp_path / f"{i}.{fmt}"
+        p.write_bytes(data)
+        paths.append(str(p))
+        refs.append(ref)
+    return paths, refs
+
+
+def test_mixed_format_batch_decode(tmp_path):
+    paths, refs = _mixed_files(tmp_path)
+    outs = WJ.decode_batch([open(p, "rb").read() for p in paths])
+    for o, r in zip(outs, refs):
+        assert np.array_equal(o, r)
+    for p, r in zip(paths, refs):
+        assert np.array_equal(wicca_amd.load_image(p), r)
+
+
+@pytest.mark.parametrize("depth,shape", [(5, (224, 224)), (3, (299, 299))])
+def test_mixed_format_file_caller_stage(tmp_path, depth, shape):
+    paths, refs = _mixed_files(tmp_path)
+    imgs, icons = wicca_amd.get_img_batch(paths, shape, depth)
+    for i, rgb in enumerate(refs):
+        assert np.array_equal(imgs[i], R.resize(rgb, shape, R.INTER_AREA)), i
+        icon = c_oracle.ll_int_block(rgb, depth)[0]
+        assert np.array_equal(icons[i], R.resize(icon, shape, R.INTER_AREA)), i
+    two = wicca_amd.get_img_batch(paths, shape, depth, devices=[0, 0])
+    assert np.array_equal(two[0], imgs) and np.array_equal(two[1], icons)
+
+
+def _recrc(data: bytes, at: int) -> bytes:
+    """Fix the CRC of the chunk whose type starts at `at`."""
+    n = struct.unpack(">I", data[at - 4:at])[0]
+    crc = struct.pack(">I", zlib.crc32(data[at:at + 4 + n]) & 0xFFFFFFFF)
+    return data[:at + 4 + n] + crc + data[at + 8 + n:]
+
+
+def test_corrupt_png_and_bmp_fail_their_slot(tmp_path, capsys):
+    s, _ = png_samples(2, 8, 40, 60, seed=1)
+    good_png = rr.encode_png(s, 2, 8, filters=4)
+    k = good_png.index(b"IDAT")
+    idat_crc = good_png[:k + 10] + bytes([good_png[k + 10] ^ 0xFF]) + good_png[k + 11:]  # CRC mismatch
+    raw = zlib.decompress(good_png[k + 4:k + 4 + struct.unpack(">I", good_png[k - 4:k])[0]])
+    bad_filter_raw = bytes([7]) + raw[1:]
+    comp = zlib.compress(bad_filter_raw)
+    bad_filter = good_png[:k - 4] + struct.pack(">I", len(comp)) + b"IDAT" + comp + b"\0\0\0\0" + \
+        good_png[k + 8 + struct.unpack(">I", good_png[k - 4:k])[0]:]
+    bad_filter = _recrc(bad_filter, k)
+    short_comp = zlib.compress(raw[: len(raw) // 2])
+    short = good_png[:k - 4] + struct.pack(">I", len(short_comp)) + b"IDAT" + short_comp + b"\0\0\0\0" + \
+        good_png[k + 8 + struct.unpack(">I", good_png[k - 4:k])[0]:]
+    short = _recrc(short, k)
+    no_iend = good_png[:-12]
+    img = np.random.default_rng(2).integers(0, 256, (20, 30, 3), dtype=np.uint8)
+    good_bmp = rr.encode_bmp(img, 24)
+    trunc_bmp = good_bmp[:-50]
+    rle_bmp = good_bmp[:30] + struct.pack("<I", 1) + good_bmp[34:]
+    blobs = [good_png, idat_crc, good_bmp, bad_filter, short, no_iend, trunc_bmp, rle_bmp, b"GIF89a" + b"\0" * 30]
+    outs = WJ.decode_batch(blobs, errors="none")
+    assert [o is None for o in outs] == [False, True, False, True, True, True, True, True, True]
+    assert np.array_equal(outs[0], s.astype(np.uint8)) and np.array_equal(outs[2], img)
+    with pytest.raises((ValueError, NotImplementedError)):
+        WJ.decode_batch(blobs)
+    with pytest.raises(NotImplementedError):
+        WJ.decode(rle_bmp)
+    paths = []
+    for i, b in enumerate(blobs):
+        p = tmp_path / f"c{i}.png"
+        p.write_bytes(b)
+        paths.append(str(p))
+    imgs, icons = wicca_amd.get_img_batch(paths, (224, 224), 3, errors="zero")
+    printed = capsys.readouterr().out
+    for i, o in enumerate(outs):
+        if o is None:
+            assert not imgs[i].any() and not icons[i].any(), i
+            assert f"Error loading image {paths[i]}" in printed
+        else:
+            assert np.array_equal(imgs[i], R.resize(o, (224, 224), R.INTER_AREA))
+            assert np.array_equal(icons[i], R.resize(c_oracle.ll_int_block(o, 3)[0], (224, 224), R.INTER_AREA))
+    for p, o in zip(paths, outs):
+        got = wicca_amd.load_image(p)
+        assert (got is None) == (o is None)
+
+
+GOLD_CASES = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "raster", "cases.json")))["cases"]
+
+
+@pytest.mark.parametrize("case", GOLD_CASES, ids=[c["file"] for c in GOLD_CASES])
+def test_golden_files(case):
+    """The committed files (tests/golden/make_raster_seeds.py), expected RGB
+    SHA-256 from Pillow 12.2.0 (from the restatement for the two unpinned kinds)."""
+    data = open(os.path.join(os.path.dirname(__file__), "golden", "raster", case["file"]), "rb").read()
+    rgb = WJ.decode(data)
+    assert rgb.shape == (case["height"], case["width"], 3)
+    assert hashlib.sha256(rgb.tobytes()).hexdigest() == case["sha256_rgb"]

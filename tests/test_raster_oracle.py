@@ -1,0 +1,123 @@
+"""CPU: pin the PNG / BMP restatement (oracle/raster_ref.py) to Pillow 12.2.0.
+
+Every case the GPU test (tests/test_gpu_raster.py) compares against the
+restatement is checked here against Pillow's own decoders first, except the
+two parity-unpinned cases named in the oracle's header (16-bit gray PNG,
+16-bit BMP), which are checked against hand-computed values instead.
+"""
+from __future__ import annotations
+
+import io
+
+import numpy as np
+import pytest
+
+from oracle import raster_ref as rr
+
+PNG_CASES = [  # (colour type, bits)
+    (0, 1), (0, 2), (0, 4), (0, 8), (2, 8), (2, 16), (3, 1), (3, 2), (3, 4), (3, 8), (4, 8), (4, 16),
+    (6, 8), (6, 16),
+]
+
+
+def png_samples(ct: int, bits: int, h: int, w: int, seed: int):
+    rng = np.random.default_rng(seed)
+    ch = rr.CHANNELS[ct]
+    hi = (1 << bits) if ct != 3 else min(1 << bits, 200)
+    s = rng.integers(0, hi, (h, w, ch), dtype=np.int64)
+    # smooth regions so the filters see non-trivial predictions
+    s[: h // 2, : w // 2] = (np.arange(w // 2)[None, :, None] * 7 + np.arange(h // 2)[:, None, None] * 3) % hi
+    pal = rng.integers(0, 256, (hi, 3), dtype=np.int64).astype(np.uint8) if ct == 3 else None
+    return s, pal
+
+
+@pytest.mark.parametrize("interlace", [False, True])
+@pytest.mark.parametrize("ct,bits", PNG_CASES)
+def test_png_oracle_vs_pillow(ct, bits, interlace):
+    s, pal = png_samples(ct, bits, 37, 29, seed=ct * 100 + bits)
+    data = rr.encode_png(s, ct, bits, interlace=interlace, palette=pal)
+    got = rr.decode_png(data)
+    assert got.shape == (37, 29, 3) and got.dtype == np.uint8
+    if ct == 0 and bits == 16:
+        return  # unpinned: checked in test_png16_gray_high_byte
+    np.testing.assert_array_equal(got, rr.pillow_rgb(data))
+
+
+@pytest.mark.parametrize("f", range(5))
+def test_png_each_filter(f):
+    s, _ = png_samples(2, 8, 16, 21, seed=f)
+    data = rr.encode_png(s, 2, 8, filters=f)
+    np.testing.assert_array_equal(rr.decode_png(data), rr.pillow_rgb(data))
+    np.testing.assert_array_equal(rr.decode_png(data), s.astype(np.uint8))
+
+
+def test_png16_gray_high_byte():
+    s = np.array([[0, 255, 256, 65535, 0x1234]], np.int64)
+    got = rr.decode_png(rr.encode_png(s, 0, 16))
+    np.testing.assert_array_equal(got[0, :, 0], [0, 0, 1, 255, 0x12])
+
+
+def test_png_tiny_interlaced_empty_passes():
+    for h, w in [(1, 1), (1, 5), (3, 1), (2, 2), (5, 3)]:
+        s, _ = png_samples(2, 8, h, w, seed=h * 10 + w)
+        data = rr.encode_png(s, 2, 8, interlace=True)
+        np.testing.assert_array_equal(rr.decode_png(data), rr.pillow_rgb(data))
+
+
+def test_pillow_written_png():
+    from PIL import Image
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, (40, 33, 3), dtype=np.uint8)
+    for mode in ["RGB", "RGBA", "L", "LA", "P", "1"]:
+        im = Image.fromarray(img).convert(mode)
+        b = io.BytesIO()
+        im.save(b, "PNG")
+        np.testing.assert_array_equal(rr.decode_png(b.getvalue()), rr.pillow_rgb(b.getvalue()))
+
+
+@pytest.mark.parametrize("bpp", [1, 4, 8, 24, 32])
+@pytest.mark.parametrize("top_down", [False, True])
+def test_bmp_oracle_vs_pillow(bpp, top_down):
+    rng = np.random.default_rng(bpp)
+    h, w = 19, 23
+    if bpp <= 8:
+        img = rng.integers(0, 1 << bpp, (h, w), dtype=np.uint8)
+        pal = rng.integers(0, 256, (1 << bpp, 3), dtype=np.uint8)
+    else:
+        img = rng.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        pal = None
+    data = rr.encode_bmp(img, bpp, palette=pal, top_down=top_down)
+    want = pal[img] if bpp <= 8 else img
+    np.testing.assert_array_equal(rr.decode_bmp(data), want)
+    np.testing.assert_array_equal(rr.decode_bmp(data), rr.pillow_rgb(data))
+
+
+def test_bmp_core_header_vs_pillow():
+    rng = np.random.default_rng(7)
+    img = rng.integers(0, 16, (9, 14), dtype=np.uint8)
+    pal = rng.integers(0, 256, (16, 3), dtype=np.uint8)
+    data = rr.encode_bmp(img, 4, palette=pal, core_header=True)
+    np.testing.assert_array_equal(rr.decode_bmp(data), pal[img])
+    np.testing.assert_array_equal(rr.decode_bmp(data), rr.pillow_rgb(data))
+
+
+def test_pillow_written_bmp():
+    from PIL import Image
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, (21, 30, 3), dtype=np.uint8)
+    for mode in ["RGB", "L", "P", "1"]:
+        b = io.BytesIO()
+        Image.fromarray(img).convert(mode).save(b, "BMP")
+        np.testing.assert_array_equal(rr.decode_bmp(b.getvalue()), rr.pillow_rgb(b.getvalue()))
+
+
+@pytest.mark.parametrize("fields565", [None, False, True])
+def test_bmp16_opencv_shifts(fields565):
+    # unpinned (Pillow rescales by 255/31): OpenCV's icvCvt_BGR5552BGR / 5652BGR shifts
+    img = np.array([[[255, 255, 255], [8, 4, 0], [0, 0, 255], [100, 50, 25]]], np.uint8)
+    got = rr.decode_bmp(rr.encode_bmp(img, 16, fields565=fields565))
+    if fields565:
+        want = np.stack([img[..., 0] & 0xF8, img[..., 1] & 0xFC, img[..., 2] & 0xF8], axis=2)
+    else:
+        want = img & 0xF8
+    np.testing.assert_array_equal(got, want)

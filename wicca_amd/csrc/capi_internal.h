@@ -118,11 +118,15 @@ struct Workspace {
     HostBuf jhost;  // pinned host staging of the de-stuffed JPEG streams
     HostBuf jtab;   // pinned host staging of the decode tables
     HostBuf jhcoef; // pinned coefficients of host-decoded (multi-scan / progressive) JPEG files
+    // PNG / BMP decode (capi_raster.cpp): raw rows (pinned staging + device) and descriptors
+    DevBuf rraw, rmeta;
+    HostBuf rhost, rmeta_pin;
     size_t bytes() const
     {
         return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
                slot[0].cap + slot[1].cap + icon[0].cap + icon[1].cap + jstream.cap + jmeta.cap + jcoef.cap +
-               jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap + rscratch.cap + smeta.cap + rtab.cap;
+               jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap + rscratch.cap + smeta.cap + rtab.cap + rraw.cap +
+               rmeta.cap;
     }
     hipError_t ensure_pipeline()
     {
@@ -168,6 +172,10 @@ struct Workspace {
         jhost.release();
         jtab.release();
         jhcoef.release();
+        rraw.release();
+        rmeta.release();
+        rhost.release();
+        rmeta_pin.release();
     }
     void destroy()
     {
@@ -248,5 +256,14 @@ int check_resize(int64_t H, int64_t W, int64_t C, int64_t out_w, int64_t out_h, 
 int run_resize(wicca::ResizeParams rp, const uint8_t* src, int64_t src_pitch, int64_t src_stride,
                uint8_t* dst, int64_t dst_pitch, int64_t dst_stride, int64_t n, hipStream_t stream,
                Workspace* ws, bool scratch_ok = true);
+
+// PNG / BMP files (capi_raster.cpp) -> RGB device images dst[i] (pitch
+// dpitch[i]); every file already parsed.  Host threads inflate / copy the raw
+// rows into pinned staging and upload each file as it completes; one launch
+// converts the batch; synchronous.  status: NULL (the first file whose data
+// turns out corrupt fails the call) or n ints set to 0 / WICCA_ERR_DECODE (a
+// failed file's dst is not written).
+int raster_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                            uint8_t* const* dst, const int64_t* dpitch, hipStream_t stream, int* status);
 
 }  // namespace wicca_capi

@@ -18,6 +18,7 @@
 
 #include "capi_internal.h"
 #include "jpeg.h"
+#include "raster.h"
 #include "stage.h"
 
 using namespace wicca_capi;
@@ -57,11 +58,45 @@ int parse_one(const uint8_t* data, int64_t size, wicca::JpegInfo* info, int64_t 
     return WICCA_OK;
 }
 
+void oriented_dims(const wicca::JpegInfo& in, bool apply, int64_t* h, int64_t* w);
+
+// A file's decoded size.  any: JPEG, PNG or BMP (the wicca_image_* entries,
+// cv2.imread's formats on the reference's path); otherwise JPEG only.
+// kind: 1 JPEG, 2 PNG, 3 BMP.
+int probe_file(const uint8_t* data, int64_t size, int64_t i, bool any, bool orient, int64_t* H, int64_t* W,
+               int* kind = nullptr)
+{
+    if (any && data && size > 0) {
+        const int rk = wicca::raster_kind(data, (size_t)size);
+        if (rk != wicca::RK_NONE) {
+            wicca::RasterInfo r;
+            std::string err;
+            const int rc = wicca::raster_parse(data, (size_t)size, &r, &err);
+            if (rc == -2) return fail(WICCA_ERR_UNSUPPORTED, "image %lld: %s", (long long)i, err.c_str());
+            if (rc) return fail(WICCA_ERR_DECODE, "image %lld: %s", (long long)i, err.c_str());
+            *H = r.H;
+            *W = r.W;
+            if (kind) *kind = rk == wicca::RK_PNG ? 2 : 3;
+            return WICCA_OK;
+        }
+        if (size < 2 || data[0] != 0xFF || data[1] != 0xD8)
+            return fail(WICCA_ERR_DECODE, "image %lld: unrecognised image format (JPEG, PNG and BMP are decoded)",
+                        (long long)i);
+    }
+    wicca::JpegInfo f;
+    const int rc = parse_one(data, size, &f, i);
+    if (rc) return rc;
+    oriented_dims(f, orient, H, W);
+    if (kind) *kind = 1;
+    return WICCA_OK;
+}
+
 // Parse every file; status[i] = 0 or its error code (the first failure's
 // message stays in the thread's last error).  good: the files that parse.
 // Without a status array nothing is screened: every index is "good" and the
 // first bad file fails the whole call, as before.
-int screen_files(const uint8_t* const* data, const int64_t* sizes, int64_t n, int* status, std::vector<int64_t>* good)
+int screen_files(const uint8_t* const* data, const int64_t* sizes, int64_t n, int* status, std::vector<int64_t>* good,
+                 bool any = false)
 {
     good->clear();
     std::string first;
@@ -70,8 +105,8 @@ int screen_files(const uint8_t* const* data, const int64_t* sizes, int64_t n, in
             good->push_back(i);
             continue;
         }
-        wicca::JpegInfo f;
-        const int rc = parse_one(data[i], sizes[i], &f, i);
+        int64_t h, w;
+        const int rc = probe_file(data[i], sizes[i], i, any, true, &h, &w);
         status[i] = rc;
         if (rc == WICCA_OK) good->push_back(i);
         else if (first.empty()) first = t_last_error;
@@ -390,6 +425,57 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
 
 thread_local int t_jpeg_rounds = 0;
 
+// Any-format decode of n parsed files into device RGB images: PNG / BMP
+// files through raster_decode_to_device, JPEG files through the device JPEG
+// decoder.  late: NULL, or n ints receiving WICCA_ERR_DECODE for a PNG whose
+// compressed data turns out corrupt (its dst is not written; 0 otherwise).
+int decode_files_to_device(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                           uint8_t* const* dst, const int64_t* dpitch, bool orient, hipStream_t stream, bool any,
+                           int* late)
+{
+    if (late)
+        for (int64_t i = 0; i < n; ++i) late[i] = WICCA_OK;
+    if (!any) return jpeg_decode_to_device(ws, data, sizes, n, dst, dpitch, orient, stream, &t_jpeg_rounds);
+    std::vector<int64_t> ras, jpg;
+    for (int64_t i = 0; i < n; ++i)
+        (data[i] && sizes[i] > 0 && wicca::raster_kind(data[i], (size_t)sizes[i]) != wicca::RK_NONE ? ras : jpg)
+            .push_back(i);
+    auto gather = [&](const std::vector<int64_t>& idx, std::vector<const uint8_t*>* d, std::vector<int64_t>* sz,
+                      std::vector<uint8_t*>* o, std::vector<int64_t>* p) {
+        for (int64_t i : idx) {
+            d->push_back(data[i]);
+            sz->push_back(sizes[i]);
+            o->push_back(dst[i]);
+            p->push_back(dpitch[i]);
+        }
+    };
+    int rc;
+    if (!ras.empty()) {
+        std::vector<const uint8_t*> d;
+        std::vector<int64_t> sz, p;
+        std::vector<uint8_t*> o;
+        gather(ras, &d, &sz, &o, &p);
+        std::vector<int> st(ras.size(), 0);
+        if ((rc = raster_decode_to_device(ws, d.data(), sz.data(), (int64_t)ras.size(), o.data(), p.data(), stream,
+                                          late ? st.data() : nullptr)))
+            return rc;
+        if (late)
+            for (size_t j = 0; j < ras.size(); ++j) late[ras[j]] = st[j];
+    }
+    if (!jpg.empty()) {
+        const std::string ras_err = t_last_error;
+        std::vector<const uint8_t*> d;
+        std::vector<int64_t> sz, p;
+        std::vector<uint8_t*> o;
+        gather(jpg, &d, &sz, &o, &p);
+        if ((rc = jpeg_decode_to_device(ws, d.data(), sz.data(), (int64_t)jpg.size(), o.data(), p.data(), orient,
+                                        stream, &t_jpeg_rounds)))
+            return rc;
+        t_last_error = ras_err;
+    }
+    return WICCA_OK;
+}
+
 // WICCA_STAGE_FUSED=0: the per-image resize / icon / icon-resize launches
 // (each decoded image read twice) instead of the fused stage.
 bool stage_fused()
@@ -604,15 +690,15 @@ int wicca_jpeg_info(const uint8_t* data, int64_t size, int apply_orientation, in
     return WICCA_OK;
 }
 
-int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, uint8_t* const* dsts,
-                         const int64_t* dst_pitches, int apply_orientation, int dst_is_device, int device,
-                         void* stream_in, int* status)
+static int decode_u8_impl(const uint8_t* const* data, const int64_t* sizes, int64_t n, uint8_t* const* dsts,
+                          const int64_t* dst_pitches, int apply_orientation, int dst_is_device, int device,
+                          void* stream_in, int* status, bool any)
 {
     if (n < 0 || (n > 0 && (!data || !sizes || !dsts || !dst_pitches))) return fail(WICCA_ERR_ARG, "bad arrays");
     if (n == 0) return WICCA_OK;
     // per-slot statuses: a file that does not parse fails its own slot only
     std::vector<int64_t> good;
-    int rc = screen_files(data, sizes, n, status, &good);
+    int rc = screen_files(data, sizes, n, status, &good, any);
     if (rc) return rc;
     if (good.size() < (size_t)n) {
         const int64_t m = (int64_t)good.size();
@@ -627,16 +713,16 @@ int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64
             gp[(size_t)j] = dst_pitches[good[(size_t)j]];
         }
         std::string first_err = t_last_error;
-        rc = wicca_jpeg_decode_u8(gd.data(), gs.data(), m, gdst.data(), gp.data(), apply_orientation, dst_is_device,
-                                  device, stream_in, nullptr);
+        std::vector<int> gst((size_t)m, 0);
+        rc = decode_u8_impl(gd.data(), gs.data(), m, gdst.data(), gp.data(), apply_orientation, dst_is_device,
+                            device, stream_in, gst.data(), any);
+        for (int64_t j = 0; j < m && rc == WICCA_OK; ++j) status[good[(size_t)j]] = gst[(size_t)j];
         if (rc == WICCA_OK) t_last_error = first_err;  // the failed slots' first message
         return rc;
     }
     std::vector<int64_t> oh((size_t)n), ow((size_t)n);
     for (int64_t i = 0; i < n; ++i) {
-        wicca::JpegInfo f;
-        if ((rc = parse_one(data[i], sizes[i], &f, i))) return rc;
-        oriented_dims(f, apply_orientation != 0, &oh[i], &ow[i]);
+        if ((rc = probe_file(data[i], sizes[i], i, any, apply_orientation != 0, &oh[i], &ow[i]))) return rc;
         if (!dsts[i] || dst_pitches[i] < ow[i] * 3) return fail(WICCA_ERR_ARG, "bad output %lld", (long long)i);
     }
     DeviceGuard dg;
@@ -664,15 +750,48 @@ int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64
             off += p[(size_t)i] * oh[i];
         }
     }
-    if ((rc = jpeg_decode_to_device(ws, data, sizes, n, d.data(), p.data(), apply_orientation != 0, stream,
-                                    &t_jpeg_rounds)))
+    std::vector<int> late((size_t)n, 0);
+    if ((rc = decode_files_to_device(ws, data, sizes, n, d.data(), p.data(), apply_orientation != 0, stream, any,
+                                     status ? late.data() : nullptr)))
         return rc;
     if (!dst_is_device) {
         for (int64_t i = 0; i < n; ++i)
-            HIP_TRY(hipMemcpy2DAsync(dsts[i], dst_pitches[i], d[(size_t)i], p[(size_t)i], ow[i] * 3, oh[i],
-                                     hipMemcpyDeviceToHost, stream));
+            if (late[(size_t)i] == WICCA_OK)
+                HIP_TRY(hipMemcpy2DAsync(dsts[i], dst_pitches[i], d[(size_t)i], p[(size_t)i], ow[i] * 3, oh[i],
+                                         hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
     }
+    if (status)
+        for (int64_t i = 0; i < n; ++i) status[i] = late[(size_t)i];
+    return WICCA_OK;
+}
+
+int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, uint8_t* const* dsts,
+                         const int64_t* dst_pitches, int apply_orientation, int dst_is_device, int device,
+                         void* stream_in, int* status)
+{
+    return decode_u8_impl(data, sizes, n, dsts, dst_pitches, apply_orientation, dst_is_device, device, stream_in,
+                          status, false);
+}
+
+int wicca_image_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, uint8_t* const* dsts,
+                          const int64_t* dst_pitches, int apply_orientation, int dst_is_device, int device,
+                          void* stream_in, int* status)
+{
+    return decode_u8_impl(data, sizes, n, dsts, dst_pitches, apply_orientation, dst_is_device, device, stream_in,
+                          status, true);
+}
+
+int wicca_image_info(const uint8_t* data, int64_t size, int apply_orientation, int64_t* height, int64_t* width,
+                     int* kind)
+{
+    int64_t h = 0, w = 0;
+    int k = 0;
+    const int rc = probe_file(data, size, 0, true, apply_orientation != 0, &h, &w, &k);
+    if (rc) return rc;
+    if (height) *height = h;
+    if (width) *width = w;
+    if (kind) *kind = k;
     return WICCA_OK;
 }
 
@@ -716,14 +835,15 @@ int wicca_jpeg_host_coefficients(const uint8_t* data, int64_t size, int force_ho
     return WICCA_OK;
 }
 
-int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
-                             int border_type, int border_constant, int64_t out_w, int64_t out_h,
-                             int interpolation, uint8_t* resized, uint8_t* resized_icons, int device, int* status);
+static int icon_stage_impl(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
+                           int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                           int interpolation, uint8_t* resized, uint8_t* resized_icons, int device, int* status,
+                           bool any);
 
-int wicca_jpeg_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
-                                    int border_type, int border_constant, int64_t out_w, int64_t out_h,
-                                    int interpolation, uint8_t* resized, uint8_t* resized_icons,
-                                    const int* devices, int n_devices, int* status)
+static int icon_stage_multi_impl(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
+                                 int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                                 int interpolation, uint8_t* resized, uint8_t* resized_icons,
+                                 const int* devices, int n_devices, int* status, bool any)
 {
     if (n < 0 || (n > 0 && (!data || !sizes))) return fail(WICCA_ERR_ARG, "bad arrays");
     if (n == 0) return WICCA_OK;
@@ -733,15 +853,50 @@ int wicca_jpeg_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* s
     // balanced by file size (the compressed bytes are what each device decodes)
     std::vector<int64_t> w(sizes, sizes + n);
     return split_over_devices(w, devices, n_devices, [&](int64_t a, int64_t b, int dev) {
-        return wicca_jpeg_icon_stage_u8(data + a, sizes + a, b - a, depth, border_type, border_constant, out_w,
-                                        out_h, interpolation, resized + a * ob, resized_icons + a * ob, dev,
-                                        status ? status + a : nullptr);
+        return icon_stage_impl(data + a, sizes + a, b - a, depth, border_type, border_constant, out_w, out_h,
+                               interpolation, resized + a * ob, resized_icons + a * ob, dev,
+                               status ? status + a : nullptr, any);
     });
+}
+
+int wicca_jpeg_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
+                                    int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                                    int interpolation, uint8_t* resized, uint8_t* resized_icons,
+                                    const int* devices, int n_devices, int* status)
+{
+    return icon_stage_multi_impl(data, sizes, n, depth, border_type, border_constant, out_w, out_h, interpolation,
+                                 resized, resized_icons, devices, n_devices, status, false);
+}
+
+int wicca_image_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
+                                     int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                                     int interpolation, uint8_t* resized, uint8_t* resized_icons,
+                                     const int* devices, int n_devices, int* status)
+{
+    return icon_stage_multi_impl(data, sizes, n, depth, border_type, border_constant, out_w, out_h, interpolation,
+                                 resized, resized_icons, devices, n_devices, status, true);
 }
 
 int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
                              int border_type, int border_constant, int64_t out_w, int64_t out_h,
                              int interpolation, uint8_t* resized, uint8_t* resized_icons, int device, int* status)
+{
+    return icon_stage_impl(data, sizes, n, depth, border_type, border_constant, out_w, out_h, interpolation, resized,
+                           resized_icons, device, status, false);
+}
+
+int wicca_image_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
+                              int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                              int interpolation, uint8_t* resized, uint8_t* resized_icons, int device, int* status)
+{
+    return icon_stage_impl(data, sizes, n, depth, border_type, border_constant, out_w, out_h, interpolation, resized,
+                           resized_icons, device, status, true);
+}
+
+static int icon_stage_impl(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
+                           int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                           int interpolation, uint8_t* resized, uint8_t* resized_icons, int device, int* status,
+                           bool any)
 {
     if (n < 0 || (n > 0 && (!data || !sizes))) return fail(WICCA_ERR_ARG, "bad arrays");
     if (n == 0) return WICCA_OK;
@@ -749,7 +904,7 @@ int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, i
     if (status) {  // a file that does not parse fails its own slot (zero outputs) only
         if (out_w <= 0 || out_h <= 0 || out_w > 65535 || out_h > 65535) return fail(WICCA_ERR_ARG, "bad output size");
         std::vector<int64_t> good;
-        int rc = screen_files(data, sizes, n, status, &good);
+        int rc = screen_files(data, sizes, n, status, &good, any);
         if (rc) return rc;
         if (good.size() < (size_t)n) {
             const int64_t ob = out_w * out_h * 3, m = (int64_t)good.size();
@@ -767,12 +922,14 @@ int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, i
             }
             std::vector<uint8_t> r((size_t)(m * ob)), c((size_t)(m * ob));
             std::string first_err = t_last_error;
-            rc = wicca_jpeg_icon_stage_u8(gd.data(), gs.data(), m, depth, border_type, border_constant, out_w, out_h,
-                                          interpolation, r.data(), c.data(), device, nullptr);
+            std::vector<int> gst((size_t)m, 0);
+            rc = icon_stage_impl(gd.data(), gs.data(), m, depth, border_type, border_constant, out_w, out_h,
+                                 interpolation, r.data(), c.data(), device, gst.data(), any);
             if (rc) return rc;
             for (int64_t j = 0; j < m; ++j) {
                 memcpy(resized + good[(size_t)j] * ob, r.data() + j * ob, (size_t)ob);
                 memcpy(resized_icons + good[(size_t)j] * ob, c.data() + j * ob, (size_t)ob);
+                status[good[(size_t)j]] = gst[(size_t)j];
             }
             t_last_error = first_err;
             return WICCA_OK;
@@ -781,10 +938,8 @@ int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, i
     std::vector<int64_t> H((size_t)n), W((size_t)n), ih((size_t)n), iw((size_t)n);
     int64_t max_icon = 0, rgb_total = 0;
     for (int64_t i = 0; i < n; ++i) {
-        wicca::JpegInfo f;
-        int rc = parse_one(data[i], sizes[i], &f, i);
+        int rc = probe_file(data[i], sizes[i], i, any, true, &H[i], &W[i]);
         if (rc) return rc;
-        oriented_dims(f, true, &H[i], &W[i]);
         if ((rc = check_image((const uint8_t*)1, H[i], W[i], 3, W[i] * 3, depth, border_type))) return rc;
         wicca::ResizeParams probe{};
         if ((rc = check_resize(H[i], W[i], 3, out_w, out_h, interpolation, &probe))) return rc;
@@ -813,7 +968,10 @@ int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, i
         off += p[(size_t)i] * H[i];
     }
     // data_loader.py:53-58  cv2.imread + BGR2RGB, on the GPU (+ EXIF orientation)
-    if ((rc = jpeg_decode_to_device(ws, data, sizes, n, d.data(), p.data(), true, cs, &t_jpeg_rounds))) return rc;
+    std::vector<int> late((size_t)n, 0);
+    if ((rc = decode_files_to_device(ws, data, sizes, n, d.data(), p.data(), true, cs, any,
+                                     status ? late.data() : nullptr)))
+        return rc;
     uint8_t* dres = (uint8_t*)ws->out.ptr;
     uint8_t* dico = dres + n * out_bytes;
     // classifying_tools.py:315-318 for the whole batch, each decoded image read
@@ -845,6 +1003,13 @@ int wicca_jpeg_icon_stage_u8(const uint8_t* const* data, const int64_t* sizes, i
     HIP_TRY(hipMemcpyAsync(resized, dres, (size_t)(n * out_bytes), hipMemcpyDeviceToHost, cs));
     HIP_TRY(hipMemcpyAsync(resized_icons, dico, (size_t)(n * out_bytes), hipMemcpyDeviceToHost, cs));
     HIP_TRY(hipStreamSynchronize(cs));
+    for (int64_t i = 0; i < n && status; ++i) {  // a PNG whose data turned out corrupt: zero outputs
+        status[i] = late[(size_t)i];
+        if (late[(size_t)i]) {
+            memset(resized + i * out_bytes, 0, (size_t)out_bytes);
+            memset(resized_icons + i * out_bytes, 0, (size_t)out_bytes);
+        }
+    }
     return WICCA_OK;
 }
 

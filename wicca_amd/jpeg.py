@@ -1,17 +1,21 @@
-"""GPU JPEG decode: the reference's ``load_image``.
+"""GPU image decode: the reference's ``load_image``.
 
 ``/root/reference/wicca/data_loader.py:31-63`` reads every file with
-``cv2.imread`` (libjpeg-turbo, BGR) and converts it to RGB.  Here baseline
-JPEG files are decoded on the GPU (``wicca_jpeg_decode_u8``,
-``wicca_amd/csrc/jpeg.hip``), restating libjpeg-turbo's default arithmetic
-bit for bit (checked against Pillow 12.2.0 / libjpeg-turbo 3.1.4.1,
-``tests/test_gpu_jpeg.py``), EXIF orientation applied as ``cv2.imread`` does.
+``cv2.imread`` (BGR) and converts it to RGB.  Here JPEG files are decoded on
+the GPU (``wicca_amd/csrc/jpeg.hip``), restating libjpeg-turbo's default
+arithmetic bit for bit (checked against Pillow 12.2.0 / libjpeg-turbo
+3.1.4.1, ``tests/test_gpu_jpeg.py``), EXIF orientation applied as
+``cv2.imread`` does; PNG and BMP files (the other formats
+``ClassifierProcessor`` counts, ``classifying_tools.py:162``) are inflated /
+copied on host threads and converted to RGB on the GPU
+(``wicca_amd/csrc/raster.hip``, ``tests/test_gpu_raster.py``).  The entry
+points sniff each file (``wicca_image_*``), so a batch may mix formats.
 
 :func:`load_image` keeps the reference's contract: empty path ->
 ``ValueError("File path cannot be empty")``; any failure -> prints
-``Error loading image {path}: {err}`` and returns ``None``.  Files the GPU
-decoder does not handle (PNG, progressive JPEG, ...) fail that way too —
-there is no CPU decoder behind it.
+``Error loading image {path}: {err}`` and returns ``None``.  Files no GPU
+decoder handles (TIFF, GIF, RLE BMP, ...) fail that way too — there is no
+CPU decoder behind it.
 """
 from __future__ import annotations
 
@@ -42,10 +46,24 @@ def info(data: bytes, apply_orientation: bool = True) -> tuple[int, int, int, in
     return h.value, w.value, c.value, o.value
 
 
+KINDS = {1: "jpeg", 2: "png", 3: "bmp"}
+
+
+def image_info(data: bytes, apply_orientation: bool = True) -> tuple[int, int, str]:
+    """(height, width, format) of a JPEG, PNG or BMP file's bytes (format
+    "jpeg" / "png" / "bmp"; JPEG sizes after EXIF orientation)."""
+    arr = np.frombuffer(data, np.uint8)
+    h, w = ctypes.c_int64(), ctypes.c_int64()
+    k = ctypes.c_int()
+    _lib.check(_lib.load().wicca_image_info(arr.ctypes.data, arr.size, int(apply_orientation),
+                                            ctypes.byref(h), ctypes.byref(w), ctypes.byref(k)))
+    return h.value, w.value, KINDS[k.value]
+
+
 def _slot_error(data: bytes) -> str:
     """The parser's message for one file (re-parsed; host only)."""
     try:
-        info(data)
+        image_info(data)
     except Exception as e:  # the message of the C ABI's failure
         return str(e)
     return "decode failed"
@@ -53,7 +71,7 @@ def _slot_error(data: bytes) -> str:
 
 def decode_batch(blobs: Sequence[bytes], apply_orientation: bool = True,
                  device: int | None = None, errors: str = "raise") -> list[np.ndarray | None]:
-    """RGB (H, W, 3) uint8 arrays of JPEG files, decoded in one GPU pass.
+    """RGB (H, W, 3) uint8 arrays of JPEG / PNG / BMP files, decoded in one GPU pass.
 
     errors="raise": the first file that does not parse raises (nothing is
     decoded); errors="none": such a file gives None in its slot and the others
@@ -67,7 +85,7 @@ def decode_batch(blobs: Sequence[bytes], apply_orientation: bool = True,
     outs: list[np.ndarray | None] = []
     for b in blobs:
         try:
-            h, w, _, _ = info(b, apply_orientation)
+            h, w, _ = image_info(b, apply_orientation)
         except (ValueError, NotImplementedError):
             if errors == "raise":
                 raise
@@ -80,8 +98,8 @@ def decode_batch(blobs: Sequence[bytes], apply_orientation: bool = True,
     dsts = (ctypes.c_void_p * n)(*[o.ctypes.data if o is not None else holder.ctypes.data for o in outs])
     pitches = (ctypes.c_int64 * n)(*[o.shape[1] * 3 if o is not None else 3 for o in outs])
     status = (ctypes.c_int * n)() if errors == "none" else None
-    _lib.check(_lib.load().wicca_jpeg_decode_u8(ptrs, sizes, n, dsts, pitches, int(apply_orientation),
-                                                0, -1 if device is None else int(device), None, status))
+    _lib.check(_lib.load().wicca_image_decode_u8(ptrs, sizes, n, dsts, pitches, int(apply_orientation),
+                                                 0, -1 if device is None else int(device), None, status))
     del keep
     if status is not None:
         for i in range(n):
@@ -139,7 +157,7 @@ def _decode_batches_loop(batches, apply_orientation, device, depth, lib, pending
 
 
 def decode(data: bytes, apply_orientation: bool = True, device: int | None = None) -> np.ndarray:
-    """RGB (H, W, 3) uint8 array of one JPEG file's bytes."""
+    """RGB (H, W, 3) uint8 array of one JPEG / PNG / BMP file's bytes."""
     return decode_batch([data], apply_orientation, device)[0]
 
 
@@ -191,12 +209,12 @@ def get_img_batch(file_paths: Sequence[str], shape, transform_depth: int, interp
     status = (ctypes.c_int * n)() if errors == "zero" else None
     if devices is not None and len(devices) > 1:
         devs = (ctypes.c_int * len(devices))(*devices)
-        _lib.check(lib.wicca_jpeg_icon_stage_multi_gpu(
+        _lib.check(lib.wicca_image_icon_stage_multi_gpu(
             ptrs, sizes, n, _depth_index(transform_depth), int(border_type), k, out_w, out_h,
             int(interpolation), resized.ctypes.data, icons.ctypes.data, devs, len(devices), status))
     else:
         dev = devices[0] if devices else (-1 if device is None else int(device))
-        _lib.check(lib.wicca_jpeg_icon_stage_u8(
+        _lib.check(lib.wicca_image_icon_stage_u8(
             ptrs, sizes, n, _depth_index(transform_depth), int(border_type), k, out_w, out_h,
             int(interpolation), resized.ctypes.data, icons.ctypes.data, dev, status))
     del keep
