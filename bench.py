@@ -40,7 +40,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=["batch", "tiled", "multi", "ragged", "stage", "jpeg"],
+    ap.add_argument("--config", choices=["batch", "tiled", "multi", "ragged", "stage", "jpeg", "png", "bmp"],
                     default="batch",
                     help="batch: configs[2]/[3] image-parallel (default); "
                          "tiled: configs[4], one 65536^2 RGB image row-sharded at depth 8; "
@@ -49,7 +49,8 @@ def parse():
                          "stage: the caller's whole per-image stage from host arrays "
                          "(resize + icon + icon resize, HaarCoder.icon_stage); "
                          "jpeg: GPU decode of 8K JPEG files (load_image) and the file-based "
-                         "caller stage (decode + resize + icon + icon resize)")
+                         "caller stage (decode + resize + icon + icon resize); "
+                         "png / bmp: the same for 8K PNG (zlib level 6) / 24-bit BMP files")
     ap.add_argument("--quality", type=int, default=90, help="--config jpeg: encoder quality")
     ap.add_argument("--shape", default="224,224", help="--config stage: classifier input (w,h)")
     ap.add_argument("--interpolation", type=int, default=3, help="--config stage: cv2.INTER_*")
@@ -625,6 +626,112 @@ def run_jpeg(args, torch, rank):
     }
 
 
+def run_raster(args, torch, rank):
+    """load_image for PNG / BMP files (data_loader.py:53; ClassifierProcessor
+    counts .png / .bmp, classifying_tools.py:162): B files of the configs[2]
+    size decoded in one wicca_image_decode_u8 call into device RGB (PNG:
+    inflate + row reconstruction on host threads, pixel conversion on the
+    device; BMP: rows copied, converted on the device), then the file-based
+    caller stage.  The CPU baseline is Pillow's decoder of the same files
+    (zlib + its own unfilter for PNG, as libpng under cv2.imread)."""
+    import io
+    from concurrent.futures import ThreadPoolExecutor
+
+    from PIL import Image
+
+    from oracle import jpeg_pil
+    from wicca_amd import _lib
+    lib = _lib.load()
+    fmt = args.config
+    B = 25 if args.images == 128 else args.images
+    H, W, D = args.height, args.width, args.depth
+    srcs = [jpeg_pil.test_image("scene", H, W, 40 + k) for k in range(4)]
+    distinct = []
+    for img in srcs:
+        b = io.BytesIO()
+        Image.fromarray(img).save(b, "PNG" if fmt == "png" else "BMP")
+        distinct.append(b.getvalue())
+    blobs = [distinct[i % 4] for i in range(B)]
+    keep = [np.frombuffer(b, np.uint8) for b in blobs]
+    ptrs = (ctypes.c_void_p * B)(*[k.ctypes.data for k in keep])
+    sizes = (ctypes.c_int64 * B)(*[k.size for k in keep])
+    pitch = (W * 3 + 127) // 128 * 128
+    dev = torch.empty(B * H * pitch, dtype=torch.uint8, device="cuda")
+    dsts = (ctypes.c_void_p * B)(*[dev.data_ptr() + i * H * pitch for i in range(B)])
+    pitches = (ctypes.c_int64 * B)(*([pitch] * B))
+    stream = torch.cuda.Stream()
+    sh = ctypes.c_void_p(stream.cuda_stream)
+
+    def decode():
+        _lib.check(lib.wicca_image_decode_u8(ptrs, sizes, B, dsts, pitches, 1, 1, -1, sh, None))
+        stream.synchronize()
+
+    steps = max(1, args.steps // 4) if fmt == "png" else args.steps  # PNG calls take ~0.5 s
+    for _ in range(min(args.warmup, 1) if fmt == "png" else args.warmup):
+        decode()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        decode()
+    dec_s = (time.perf_counter() - t0) / steps
+    verified = None
+    if not args.no_verify:
+        for i in range(min(B, 4)):
+            got = dev[i * H * pitch:(i + 1) * H * pitch].view(H, pitch)[:, :W * 3].cpu().numpy().reshape(H, W, 3)
+            verified = bool(np.array_equal(got, srcs[i])) and verified is not False
+        if not verified:
+            raise SystemExit(f"{fmt} bench verification FAILED")
+    shape = tuple(int(x) for x in args.shape.split(","))
+    res = np.empty((B, shape[1], shape[0], 3), np.uint8)
+    ico = np.empty_like(res)
+
+    def stage():
+        _lib.check(lib.wicca_image_icon_stage_u8(ptrs, sizes, B, D, 1, 0, shape[0], shape[1],
+                                                 args.interpolation, res.ctypes.data, ico.ctypes.data, -1, None))
+
+    stage()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        stage()
+    stage_s = (time.perf_counter() - t0) / steps
+    mpix = B * H * W / 1e6
+
+    def pil(b):
+        im = Image.open(io.BytesIO(b))
+        return np.asarray(im.convert("RGB"))
+
+    n1, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 3.0 and n1 < 8:
+        pil(blobs[n1 % 4])
+        n1 += 1
+    single = n1 * H * W / 1e6 / (time.perf_counter() - t0)
+    threads = min(16, len(os.sched_getaffinity(0)))
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(pil, blobs[:threads]))
+        t0 = time.perf_counter()
+        list(ex.map(pil, blobs))
+        pool = B * H * W / 1e6 / (time.perf_counter() - t0)
+    import PIL
+    return {
+        "metric": f"megapixels/sec {fmt.upper()} decode (load_image) into device RGB", "value": round(mpix / dec_s, 1),
+        "unit": "MP/s", "n_gpus": 1, "steps": steps, "warmup": args.warmup,
+        "ms_per_step": round(dec_s * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": f"synthetic scenes written by Pillow {PIL.__version__} "
+                f"({'PNG, zlib level 6, adaptive filters' if fmt == 'png' else '24-bit BMP'}), files in host "
+                "memory; decoded into device RGB (decoded rows cross PCIe inside the timed region)",
+        "config": {"workload": f"{B} x {W}x{H} {fmt.upper()} files per call", "images": B,
+                   "mean_file_MB": round(sum(len(b) for b in blobs) / B / 1e6, 2)},
+        "file_stage": {"ms_per_batch": round(stage_s * 1e3, 3), "MP_per_s": round(mpix / stage_s, 1),
+                       "what": f"decode + cv2.resize to {shape} + icon depth {D} + icon resize, "
+                               "outputs to host (classifying_tools.py:312-323)"},
+        "cpu_baseline": {"value": round(pool, 1), "unit": "MP/s", "cores": threads, "kind": "port",
+                         "sample": f"Pillow {PIL.__version__} decode + convert('RGB') of the same files, "
+                                   f"ThreadPoolExecutor({threads}), {B} files",
+                         "single_thread_value": round(single, 1)},
+        "roofline": None, "verified_vs_source_pixels": verified,
+    }
+
+
 def run_multi(args, torch, rank):
     """All depths of configs[2]'s sweep from ONE read of the batch
     (wicca_haar_ll_u8_multi_uniform), against one launch per depth."""
@@ -762,6 +869,11 @@ def main():
         return
     if args.config == "jpeg":
         out = run_jpeg(args, torch, rank)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        return
+    if args.config in ("png", "bmp"):
+        out = run_raster(args, torch, rank)
         if rank == 0:
             print(json.dumps(out), flush=True)
         return

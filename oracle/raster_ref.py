@@ -1,4 +1,4 @@
-"""PNG / BMP decode checker and test-file writer — TEST INFRASTRUCTURE.
+"""PNG / BMP / TIFF decode checker and test-file writer — TEST INFRASTRUCTURE.
 
 The reference's ``load_image`` is ``cv2.imread(path)`` (IMREAD_COLOR) +
 ``cvtColor(BGR2RGB)`` (``/root/reference/wicca/data_loader.py:53-58``);
@@ -23,7 +23,14 @@ alpha and expands palettes / gray the same way).  16-bit PNG RGB(A) is pinned
 the same way (Pillow keeps the high byte).  16-bit gray PNG (Pillow clips
 instead of taking the high byte) and 16-bit BMP (Pillow rescales 5-bit values
 by 255/31; OpenCV shifts) are **parity unpinned**: the restatement follows
-OpenCV's code as described above.  Only ``tests/`` uses this module.
+OpenCV's code as described above.
+
+* TIFF (OpenCV ``TiffDecoder``: 8-bit output goes through libtiff's RGBA
+  interface): checked against Pillow 12.2.0 (libtiff 4.7.1 for the
+  compressed strips) for gray / WhiteIsZero / RGB / palette / bilevel files,
+  none / LZW / Deflate / PackBits, predictor 2, strips and tiles, both byte
+  orders; RGBA with unassociated alpha follows libtiff's premultiplication
+  (``decode_tiff``, parity unpinned).  Only ``tests/`` uses this module.
 """
 from __future__ import annotations
 
@@ -315,13 +322,161 @@ def encode_bmp(img: np.ndarray, bpp: int = 24, palette: np.ndarray | None = None
     return b"BM" + struct.pack("<IHHI", total, 0, 0, off) + hdr + pal + px.tobytes()
 
 
+# ----------------------------------------------------------------------------- TIFF
+def _packbits(b: bytes) -> bytes:
+    out = bytearray()
+    i = 0
+    while i < len(b):
+        j = i
+        while j < len(b) and j - i < 128 and b[j] == b[i]:
+            j += 1
+        if j - i >= 3:
+            out += bytes([(257 - (j - i)) & 255, b[i]])
+            i = j
+            continue
+        j = i
+        while j < len(b) and j - i < 128 and not (j + 2 < len(b) and b[j] == b[j + 1] == b[j + 2]):
+            j += 1
+        out += bytes([j - i - 1]) + b[i:j]
+        i = j
+    return bytes(out)
+
+
+def _tiff_rows(samples: np.ndarray, bits: int) -> np.ndarray:
+    h = samples.shape[0]
+    return _pack(samples.reshape(h, -1), bits)
+
+
+def encode_tiff(samples: np.ndarray, photometric: int, bits: int = 8, compression: int = 1, predictor: int = 1,
+                tile=None, rows_per_strip: int = 8, big_endian: bool = False, colormap=None,
+                extra_samples=None) -> bytes:
+    """A TIFF file of (H, W[, spp]) samples: compression 1 none / 8 Deflate /
+    32773 PackBits, predictor 2 (8-bit), strips of rows_per_strip rows or
+    tiles (tw, th), either byte order; colormap (2**bits, 3) 16-bit values."""
+    samples = np.asarray(samples)
+    if samples.ndim == 2:
+        samples = samples[..., None]
+    h, w, spp = samples.shape
+    e = ">" if big_endian else "<"
+
+    def code(seg_samples):
+        rows = _tiff_rows(seg_samples, bits).astype(np.uint8)
+        if predictor == 2:
+            r = rows.astype(np.int64).reshape(rows.shape[0], -1, spp)
+            d = r.copy()
+            d[:, 1:] = r[:, 1:] - r[:, :-1]
+            rows = (d & 255).astype(np.uint8).reshape(rows.shape[0], -1)
+        raw = rows.tobytes()
+        if compression == 8:
+            return zlib.compress(raw)
+        if compression == 32773:
+            return b"".join(_packbits(rows[i].tobytes()) for i in range(rows.shape[0]))
+        return raw
+
+    segs = []
+    if tile:
+        tw, th = tile
+        for ty in range(0, h, th):
+            for tx in range(0, w, tw):
+                t = np.zeros((th, tw, spp), samples.dtype)
+                blk = samples[ty:ty + th, tx:tx + tw]
+                t[:blk.shape[0], :blk.shape[1]] = blk
+                segs.append(code(t))
+    else:
+        for y in range(0, h, rows_per_strip):
+            segs.append(code(samples[y:y + rows_per_strip]))
+    body = bytearray(b"MM\x00*" if big_endian else b"II*\x00") + b"\0\0\0\0"
+    offs = []
+    for sgm in segs:
+        offs.append(len(body))
+        body += sgm
+        if len(body) % 2:
+            body += b"\0"
+    entries = []  # (tag, type, values)
+
+    def arr(vals, typ):
+        fmt = {3: "H", 4: "I"}[typ]
+        nonlocal body
+        if len(vals) * (2 if typ == 3 else 4) <= 4:
+            return None
+        at = len(body)
+        body += struct.pack(e + fmt * len(vals), *vals)
+        return at
+
+    entries.append((256, 4, [w]))
+    entries.append((257, 4, [h]))
+    entries.append((258, 3, [bits] * spp))
+    entries.append((259, 3, [compression]))
+    entries.append((262, 3, [photometric]))
+    if not tile:
+        entries.append((273, 4, offs))
+    entries.append((277, 3, [spp]))
+    if not tile:
+        entries.append((278, 4, [rows_per_strip]))
+        entries.append((279, 4, [len(x) for x in segs]))
+    entries.append((284, 3, [1]))
+    if predictor != 1:
+        entries.append((317, 3, [predictor]))
+    if colormap is not None:
+        cm = np.asarray(colormap, np.int64)
+        entries.append((320, 3, list(cm[:, 0]) + list(cm[:, 1]) + list(cm[:, 2])))
+    if tile:
+        entries.append((322, 3, [tile[0]]))
+        entries.append((323, 3, [tile[1]]))
+        entries.append((324, 4, offs))
+        entries.append((325, 4, [len(x) for x in segs]))
+    if extra_samples is not None:
+        entries.append((338, 3, [extra_samples]))
+    laid = []
+    for tag, typ, vals in sorted(entries):
+        at = arr([int(v) for v in vals], typ)
+        laid.append((tag, typ, [int(v) for v in vals], at))
+    if len(body) % 2:
+        body += b"\0"
+    ifd = len(body)
+    body[4:8] = struct.pack(e + "I", ifd)
+    body += struct.pack(e + "H", len(laid))
+    for tag, typ, vals, at in laid:
+        if at is None:
+            fmt = {3: "H", 4: "I"}[typ]
+            v = struct.pack(e + fmt * len(vals), *vals).ljust(4, b"\0")
+        else:
+            v = struct.pack(e + "I", at)
+        body += struct.pack(e + "HHI", tag, typ, len(vals)) + v
+    body += b"\0\0\0\0"
+    return bytes(body)
+
+
+def decode_tiff(data: bytes) -> np.ndarray:
+    """RGB of a TIFF as cv2.imread's 8-bit path sees it (libtiff's RGBA
+    interface): Pillow's decode (libtiff 4.7.1 underneath for the compressed
+    files), with libtiff's unassociated-alpha premultiplication
+    ((v * a + 127) // 255, tif_getimage.c) applied to RGBA files whose
+    ExtraSamples is 2 — that rule is parity unpinned."""
+    import io
+    from PIL import Image
+    im = Image.open(io.BytesIO(data))
+    im.load()
+    extra = im.tag_v2.get(338)
+    if im.mode == "RGBA" and (extra == 1 or extra == (1,)):
+        # associated alpha: libtiff hands the stored (premultiplied) colours
+        # through; Pillow un-premultiplies them, so it cannot be the checker
+        raise NotImplementedError("associated-alpha TIFF: compare against the stored samples")
+    if im.mode == "RGBA" and (extra == 2 or extra == (2,)):
+        a = np.asarray(im).astype(np.uint32)
+        return ((a[..., :3] * a[..., 3:4] + 127) // 255).astype(np.uint8)
+    return np.asarray(im.convert("RGB")).copy()
+
+
 def decode_rgb(data: bytes) -> np.ndarray:
-    """The restatement for either format."""
+    """The restatement for any of the formats."""
     if data[:8] == SIG:
         return decode_png(data)
     if data[:2] == b"BM":
         return decode_bmp(data)
-    raise ValueError("not a PNG or BMP file")
+    if data[:4] in (b"II*\x00", b"MM\x00*"):
+        return decode_tiff(data)
+    raise ValueError("not a PNG, BMP or TIFF file")
 
 
 def pillow_rgb(data: bytes) -> np.ndarray:

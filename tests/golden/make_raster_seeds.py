@@ -1,8 +1,10 @@
-"""Writes tests/golden/raster/: small PNG / BMP files (every PNG colour type
-family, Adam7, each filter, BMP palette / 16 / 24 / 32-bit, top-down) and
+"""Writes tests/golden/raster/: small PNG / BMP / TIFF files (every PNG
+colour type family, Adam7, each filter, BMP palette / 16 / 24 / 32-bit,
+top-down, TIFF LZW / Deflate + predictor + tiles + big-endian / PackBits /
+WhiteIsZero / unassociated alpha) and
 cases.json with each file's expected RGB SHA-256 from Pillow 12.2.0 (the pin;
-the two parity-unpinned kinds, 16-bit gray PNG and 16-bit BMP, from the
-restatement oracle/raster_ref.py).  They seed the ASan/UBSan mutation fuzz
+the parity-unpinned kinds, 16-bit gray PNG, 16-bit BMP and unassociated-alpha
+TIFF, from the restatement oracle/raster_ref.py).  They seed the ASan/UBSan mutation fuzz
 (tests/native/raster_fuzz.cpp) and are decoded on the GPU by
 tests/test_gpu_raster.py::test_golden_files.
 
@@ -50,11 +52,23 @@ def main():
     files["pal8.bmp"] = rr.encode_bmp(idx, 8, palette=rng.integers(0, 256, (256, 3), dtype=np.uint8))
     files["pal1_topdown.bmp"] = rr.encode_bmp(idx & 1, 1, palette=np.array([[10, 20, 30], [200, 100, 50]], np.uint8),
                                               top_down=True)
+    from PIL import Image
+    import io
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, "TIFF", compression="tiff_lzw")
+    files["rgb_lzw.tif"] = b.getvalue()
+    gray = rng.integers(0, 256, (35, 33), dtype=np.uint8)
+    files["gray_deflate_pred_tiled_be.tif"] = rr.encode_tiff(gray, 1, 8, 8, 2, tile=(16, 16), big_endian=True)
+    cm = rng.integers(0, 256, (16, 3), dtype=np.int64) * 257
+    files["pal4_packbits.tif"] = rr.encode_tiff(idx & 15, 3, 4, 32773, colormap=cm, rows_per_strip=5)
+    files["white1.tif"] = rr.encode_tiff(idx & 1, 0, 1, 1)
+    rgba = rng.integers(0, 256, (9, 11, 4), dtype=np.uint8)
+    files["rgba_unassoc.tif"] = rr.encode_tiff(rgba, 2, 8, 8, extra_samples=2)
     cases = []
     for name, data in sorted(files.items()):
         with open(os.path.join(OUT, name), "wb") as f:
             f.write(data)
-        unpinned = name in ("gray16.png", "bgr565.bmp")
+        unpinned = name in ("gray16.png", "bgr565.bmp", "rgba_unassoc.tif")
         rgb = rr.decode_rgb(data)
         if not unpinned:
             assert np.array_equal(rgb, rr.pillow_rgb(data)), name

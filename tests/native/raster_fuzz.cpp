@@ -151,6 +151,40 @@ std::vector<uint8_t> mutate_bmp(const std::vector<uint8_t>& f, std::mt19937& rng
     return g;
 }
 
+// TIFF: an IFD entry's type / count / value, a byte of the header or of the
+// strip data, or a truncation
+std::vector<uint8_t> mutate_tiff(const std::vector<uint8_t>& f, std::mt19937& rng)
+{
+    std::vector<uint8_t> g = f;
+    if (f.size() < 16) return g;  // a mutant already cut short
+    const bool le = f[0] == 'I';
+    auto u32 = [&](size_t o) {
+        return le ? (uint32_t)f[o] | f[o + 1] << 8 | f[o + 2] << 16 | (uint32_t)f[o + 3] << 24
+                  : (uint32_t)f[o] << 24 | f[o + 1] << 16 | f[o + 2] << 8 | f[o + 3];
+    };
+    const size_t ifd = u32(4);
+    const size_t cnt = ifd + 2 <= f.size() ? (le ? f[ifd] | f[ifd + 1] << 8 : f[ifd] << 8 | f[ifd + 1]) : 0;
+    switch (rng() % 5) {
+    case 0: case 1: {  // one IFD entry: a field of it
+        if (!cnt) break;
+        const size_t e = ifd + 2 + 12 * (rng() % cnt) + 2 + rng() % 10;
+        if (e >= g.size()) break;
+        g[e] = rng() % 2 ? (uint8_t)rng() : (uint8_t)(rng() % 8);
+        break;
+    }
+    case 2:  // random bytes in the data
+        for (int k = 0, nk = 1 + rng() % 8; k < nk; ++k) g[8 + rng() % (g.size() - 8)] = (uint8_t)rng();
+        break;
+    case 3:  // the IFD offset
+        g[4 + rng() % 4] = (uint8_t)rng();
+        break;
+    default:  // truncate
+        g.resize(rng() % (g.size() + 1));
+        break;
+    }
+    return g;
+}
+
 // raster.hip's reads for pixel (y, x), relative to the image's raw rows:
 // the largest byte offset touched must lie inside lay.bytes.
 bool device_reads_in_bounds(const wicca::RasterInfo& f, const wicca::RasterLayout& L)
@@ -166,6 +200,31 @@ bool device_reads_in_bounds(const wicca::RasterInfo& f, const wicca::RasterLayou
         return 0;
     };
     static const int sx_shift[7] = {3, 3, 2, 2, 1, 1, 0}, sy_shift[7] = {3, 3, 3, 2, 2, 1, 1};
+    // bytes per pixel of the byte-aligned formats (raster.hip pixel_bytes)
+    const int w16 = f.bits == 16 ? 2 : 1;
+    int pb = 2;
+    switch (f.fmt) {
+    case wicca::RF_GRAY: pb = f.bits >= 8 ? w16 : 0; break;
+    case wicca::RF_GRAYA: pb = 2 * w16; break;
+    case wicca::RF_RGB: pb = 3 * w16; break;
+    case wicca::RF_RGBA: pb = 4 * w16; break;
+    case wicca::RF_PAL: pb = f.bits == 8 ? 1 : 0; break;
+    case wicca::RF_BGR: pb = 3; break;
+    case wicca::RF_BGRX: pb = 4; break;
+    }
+    if (pb > 0 && !f.interlaced) {
+        // the fast path: each lane reads pb + 1 aligned dwords from its 4-pixel
+        // window; the device buffer has 64 B of slack past the image's rows
+        // (raw bases are 256-B aligned, so offsets here align as on the device)
+        for (int64_t y = 0; y < f.H; ++y) {
+            const int64_t row = L.pass_off[0] + skip + (f.bottom_up ? f.H - 1 - y : y) * L.pass_pitch[0];
+            for (int64_t x0 = 0; x0 < f.W; x0 += 4) {
+                const int64_t a = (row + x0 * pb) & ~(int64_t)3;
+                if (a < 0 || a + 4 * (pb + 1) > L.bytes + 64) return false;
+            }
+        }
+        return true;
+    }
     for (int64_t y = 0; y < f.H; ++y) {
         for (int64_t x = 0; x < f.W; ++x) {
             int p = 0;
@@ -212,8 +271,12 @@ int main(int argc, char** argv)
     for (long it = 0; it < iters; ++it) {
         const std::vector<uint8_t>& s = seeds[(size_t)it % seeds.size()];
         const bool png = s.size() > 8 && s[0] == 0x89;
-        std::vector<uint8_t> g = png ? mutate_png(s, rng) : mutate_bmp(s, rng);
-        if (rng() % 3 == 0) g = png ? mutate_png(g, rng) : mutate_bmp(g, rng);
+        const bool tif = s.size() > 8 && (s[0] == 'I' || s[0] == 'M');
+        auto mut = [&](const std::vector<uint8_t>& f) {
+            return png ? mutate_png(f, rng) : tif ? mutate_tiff(f, rng) : mutate_bmp(f, rng);
+        };
+        std::vector<uint8_t> g = mut(s);
+        if (rng() % 3 == 0) g = mut(g);
         std::unique_ptr<uint8_t[]> buf(new uint8_t[g.size() ? g.size() : 1]);
         if (!g.empty()) memcpy(buf.get(), g.data(), g.size());
         wicca::RasterInfo info;

@@ -223,3 +223,67 @@ def test_golden_files(case):
     rgb = WJ.decode(data)
     assert rgb.shape == (case["height"], case["width"], 3)
     assert hashlib.sha256(rgb.tobytes()).hexdigest() == case["sha256_rgb"]
+
+
+from test_raster_oracle import TIFF_KINDS, tiff_case  # noqa: E402
+
+
+@pytest.mark.parametrize("kind", TIFF_KINDS)
+@pytest.mark.parametrize("comp,pred,tile,be", [(1, 1, None, False), (8, 2, None, True), (32773, 1, (16, 32), False),
+                                              (8, 1, (32, 16), True), (8, 2, (16, 16), False)])
+def test_tiff_vs_oracle(kind, comp, pred, tile, be):
+    blobs, wants = [], []
+    for i, (h, w) in enumerate([(1, 1), (5, 3), (37, 45), (130, 257)]):
+        s, photo, bits, cm, extra = tiff_case(kind, h, w, seed=i + len(kind))
+        p = pred if bits == 8 else 1
+        data = rr.encode_tiff(s, photo, bits, comp, p, tile=tile, big_endian=be, colormap=cm, extra_samples=extra,
+                              rows_per_strip=7)
+        blobs.append(data)
+        wants.append(s[..., :3] if kind == "rgba_assoc" else rr.decode_tiff(data))
+    for o, want in zip(WJ.decode_batch(blobs), wants):
+        assert np.array_equal(o, want)
+
+
+def test_tiff_unassociated_alpha():
+    s = np.random.default_rng(4).integers(0, 256, (33, 50, 4), dtype=np.uint8)
+    data = rr.encode_tiff(s, 2, extra_samples=2, compression=8)
+    want = ((s[..., :3].astype(np.uint32) * s[..., 3:4] + 127) // 255).astype(np.uint8)
+    assert np.array_equal(WJ.decode(data), want)
+    assert np.array_equal(rr.decode_tiff(data), want)
+
+
+@pytest.mark.parametrize("mode", ["RGB", "L", "P", "1", "LA"])
+@pytest.mark.parametrize("comp", [None, "tiff_lzw", "tiff_deflate", "packbits"])
+def test_pillow_written_tiff(mode, comp):
+    from PIL import Image
+    img = J.test_image("scene", 300, 401, 7)
+    b = io.BytesIO()
+    Image.fromarray(img).convert(mode).save(b, "TIFF", compression=comp)
+    data = b.getvalue()
+    assert np.array_equal(WJ.decode(data), rr.pillow_rgb(data))
+    assert WJ.image_info(data) == (300, 401, "tiff")
+
+
+def test_tiff_lzw_8k_vs_pillow():
+    from PIL import Image
+    img = J.test_image("scene", 4320, 7680, 12)
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, "TIFF", compression="tiff_lzw")
+    assert np.array_equal(WJ.decode(b.getvalue()), img)
+
+
+def test_tiff_unsupported_and_corrupt():
+    from PIL import Image
+    img = J.test_image("scene", 40, 60, 3)
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, "TIFF", compression="jpeg")
+    with pytest.raises(NotImplementedError):
+        WJ.decode(b.getvalue())
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, "TIFF", compression="tiff_lzw")
+    good = b.getvalue()
+    s = np.frombuffer(good, np.uint8)
+    cut = good[:200]  # strips outside the file
+    outs = WJ.decode_batch([good, cut, good[:7]], errors="none")
+    assert np.array_equal(outs[0], img) and outs[1] is None and outs[2] is None
+    assert s.size > 200

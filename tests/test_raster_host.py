@@ -1,4 +1,4 @@
-"""CPU: the PNG / BMP host half of the any-format decode (raster_host.cpp
+"""CPU: the PNG / BMP / TIFF host half of the any-format decode (raster_host.cpp
 through wicca_image_info, no device): format sniffing, header validation
 with libpng / OpenCV BmpDecoder error behaviour, the committed golden files'
 sizes, and the ASan + UBSan mutation fuzz (tests/native/raster_fuzz.cpp)."""
@@ -22,7 +22,7 @@ def test_golden_info(case):
     data = open(os.path.join(GOLD, case["file"]), "rb").read()
     h, w, kind = WJ.image_info(data)
     assert (h, w) == (case["height"], case["width"])
-    assert kind == case["file"].rsplit(".", 1)[1]
+    assert kind == {"tif": "tiff"}.get(case["file"].rsplit(".", 1)[1], case["file"].rsplit(".", 1)[1])
 
 
 def _ihdr_png(w=4, h=3, bits=8, ct=2, il=0, crc_ok=True, idat=True, iend=True):
@@ -66,8 +66,22 @@ def test_bmp_header_errors():
             WJ.image_info(bad)
 
 
+def test_tiff_header_errors():
+    img = np.zeros((6, 5, 3), np.uint8)
+    good = rr.encode_tiff(img, 2, compression=8)
+    assert WJ.image_info(good) == (6, 5, "tiff")
+    for bad in (good[:7], b"II*\x00" + b"\0" * 20, good[:4] + b"\xff\xff\xff\x7f" + good[8:]):
+        with pytest.raises(ValueError):
+            WJ.image_info(bad)
+    for unsup in (rr.encode_tiff(img.astype(np.uint16) * 257, 2, bits=16),          # 16-bit samples
+                  rr.encode_tiff(np.zeros((6, 5, 4), np.uint8), 5),                 # CMYK
+                  rr.encode_tiff(img, 2, compression=7)):                           # JPEG-in-TIFF
+        with pytest.raises(NotImplementedError):
+            WJ.image_info(unsup)
+
+
 def test_unrecognised_formats():
-    for data in (b"GIF89a" + b"\0" * 20, b"II*\x00" + b"\0" * 20, b"", b"B"):
+    for data in (b"GIF89a" + b"\0" * 20, b"", b"B"):
         with pytest.raises(ValueError):
             WJ.image_info(data)
 

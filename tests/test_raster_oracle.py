@@ -1,4 +1,4 @@
-"""CPU: pin the PNG / BMP restatement (oracle/raster_ref.py) to Pillow 12.2.0.
+"""CPU: pin the PNG / BMP / TIFF restatement (oracle/raster_ref.py) to Pillow 12.2.0.
 
 Every case the GPU test (tests/test_gpu_raster.py) compares against the
 restatement is checked here against Pillow's own decoders first, except the
@@ -121,3 +121,55 @@ def test_bmp16_opencv_shifts(fields565):
     else:
         want = img & 0xF8
     np.testing.assert_array_equal(got, want)
+
+
+# ----------------------------------------------------------------------------- TIFF
+def tiff_case(kind: str, h: int, w: int, seed: int):
+    """(samples, photometric, bits, colormap, extra) for a TIFF test image."""
+    rng = np.random.default_rng(seed)
+    if kind == "rgb":
+        return rng.integers(0, 256, (h, w, 3), dtype=np.uint8), 2, 8, None, None
+    if kind == "gray":
+        return rng.integers(0, 256, (h, w), dtype=np.uint8), 1, 8, None, None
+    if kind == "white":
+        return rng.integers(0, 256, (h, w), dtype=np.uint8), 0, 8, None, None
+    if kind in ("gray1", "gray4"):
+        b = 1 if kind == "gray1" else 4
+        return rng.integers(0, 1 << b, (h, w), dtype=np.uint8), 1, b, None, None
+    if kind in ("pal8", "pal4"):
+        b = 8 if kind == "pal8" else 4
+        cm = rng.integers(0, 256, (1 << b, 3), dtype=np.int64) * 257
+        return rng.integers(0, 1 << b, (h, w), dtype=np.uint8), 3, b, cm, None
+    if kind == "rgba_assoc":
+        return rng.integers(0, 256, (h, w, 4), dtype=np.uint8), 2, 8, None, 1
+    raise ValueError(kind)
+
+
+TIFF_KINDS = ["rgb", "gray", "white", "gray1", "gray4", "pal8", "pal4", "rgba_assoc"]
+
+
+@pytest.mark.parametrize("kind", TIFF_KINDS)
+@pytest.mark.parametrize("comp,pred,tile,be", [(1, 1, None, False), (8, 2, None, True), (32773, 1, (16, 32), False),
+                                              (8, 1, (32, 16), True)])
+def test_tiff_oracle_vs_pillow(kind, comp, pred, tile, be):
+    s, photo, bits, cm, extra = tiff_case(kind, 37, 45, seed=len(kind))
+    if bits != 8:
+        pred = 1
+    data = rr.encode_tiff(s, photo, bits, comp, pred, tile=tile, big_endian=be, colormap=cm, extra_samples=extra)
+    if kind == "rgba_assoc":  # Pillow un-premultiplies; libtiff (cv2) keeps the stored colours
+        with pytest.raises(NotImplementedError):
+            rr.decode_tiff(data)
+        return
+    got = rr.decode_tiff(data)
+    np.testing.assert_array_equal(got, rr.pillow_rgb(data))
+    if kind == "rgb":
+        np.testing.assert_array_equal(got, s)
+    if kind == "white":
+        np.testing.assert_array_equal(got[..., 0], 255 - s)
+
+
+def test_tiff_unassociated_alpha_premultiplied():
+    # unpinned (Pillow drops alpha): libtiff's RGBA interface premultiplies
+    px = np.array([[[200, 100, 50, 128], [255, 255, 255, 0], [10, 20, 30, 255]]], np.uint8)
+    got = rr.decode_tiff(rr.encode_tiff(px, 2, extra_samples=2))
+    np.testing.assert_array_equal(got[0], [[100, 50, 25], [0, 0, 0], [10, 20, 30]])

@@ -35,7 +35,11 @@
 
 namespace wicca {
 
-enum RasterKind { RK_NONE = 0, RK_PNG = 1, RK_BMP = 2 };
+enum RasterKind { RK_NONE = 0, RK_PNG = 1, RK_BMP = 2, RK_TIFF = 3 };
+
+// RasterImageDev::flags
+constexpr int kRasterInvert = 1;   // TIFF WhiteIsZero gray: 255 - v
+constexpr int kRasterPremul = 2;   // TIFF unassociated alpha: v = (v * a + 127) / 255 (libtiff's RGBA interface)
 
 // Layout of the raw rows the device converts.
 enum RasterFmt {
@@ -70,6 +74,14 @@ struct RasterInfo {
     size_t data_off = 0;
     int64_t stride = 0;
     bool bottom_up = false;
+    // TIFF (first IFD): strips or tiles (offset, byte count), layout, coding
+    int flags = 0;                 // kRasterInvert / kRasterPremul
+    int spp = 1;                   // samples per pixel
+    int compression = 1;           // 1 none, 5 LZW, 8 / 32946 Deflate, 32773 PackBits
+    int predictor = 1;             // 1 none, 2 horizontal differencing
+    int64_t rows_per_strip = 0;
+    int64_t tile_w = 0, tile_h = 0;  // 0: strips
+    std::vector<std::pair<uint64_t, uint64_t>> segs;
 };
 
 // Adam7 pass p: first row/column and steps (PNG spec 8.2).
@@ -78,7 +90,7 @@ constexpr int kAdam7Y0[7] = {0, 0, 4, 0, 2, 0, 1};
 constexpr int kAdam7DX[7] = {8, 8, 4, 4, 2, 2, 1};
 constexpr int kAdam7DY[7] = {8, 8, 8, 4, 4, 2, 2};
 
-// Sniff the file's format (RK_NONE if neither PNG nor BMP).
+// Sniff the file's format (RK_NONE if not PNG, BMP or TIFF).
 int raster_kind(const uint8_t* data, size_t size);
 
 // Parse the headers.  0, or a negative code with *err set: -1 corrupt /
@@ -112,7 +124,7 @@ struct RasterImageDev {
     int32_t fmt, bits;
     int32_t interlaced, bottom_up;
     int32_t row0;     // first global row-tile index of this image
-    int32_t pad;
+    int32_t flags;    // kRasterInvert / kRasterPremul
     uint8_t pal[256 * 3];
 };
 

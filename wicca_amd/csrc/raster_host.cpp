@@ -17,6 +17,17 @@
 // grfmt_bmp.cpp): BITMAPINFOHEADER and later (size >= 36) or OS/2 core
 // headers (size 12); BI_RGB 1/4/8/16/24/32 bits, BI_BITFIELDS 16 (5-5-5 or
 // 5-6-5 masks only) and 32 bits; RLE4 / RLE8 are reported unsupported.
+// TIFF (6.0; the first IFD, as cv2.imread reads page 0): OpenCV's
+// TiffDecoder decodes 8-bit output through libtiff's RGBA interface
+// (TIFFReadRGBAStrip / TIFFReadRGBATile), whose conversions are restated:
+// BlackIsZero / WhiteIsZero gray (1/2/4/8 bits, scaled; WhiteIsZero
+// inverted), RGB and RGBA (unassociated alpha premultiplied,
+// (v * a + 127) / 255, then dropped), palette (1/2/4/8-bit indices, a 16-bit
+// ColorMap taken >> 8 unless every entry is < 256); strips or tiles,
+// chunky samples, compression none / LZW (with the early code-width change)
+// / Deflate / PackBits, horizontal predictor.  16-bit samples, planar
+// configuration 2, JPEG / CCITT compression, CMYK / YCbCr / Lab and
+// orientations other than top-left are reported unsupported.
 #include <string.h>
 #include <zlib.h>
 
@@ -33,6 +44,7 @@ uint32_t le32(const uint8_t* p) { return (uint32_t)p[3] << 24 | (uint32_t)p[2] <
 uint16_t le16(const uint8_t* p) { return (uint16_t)(p[1] << 8 | p[0]); }
 
 const uint8_t kPngSig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
+const uint8_t kTiffLE[4] = {'I', 'I', 42, 0}, kTiffBE[4] = {'M', 'M', 0, 42};
 constexpr int64_t kMaxDim = 65535;  // the device stage's limit (as for JPEG)
 
 int bad(std::string* err, int code, const char* msg)
@@ -212,6 +224,333 @@ int parse_bmp(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
     return 0;
 }
 
+// ----------------------------------------------------------------------------- TIFF
+struct TiffReader {
+    const uint8_t* d;
+    size_t n;
+    bool le;
+    uint32_t u16(size_t o) const { return le ? (uint32_t)d[o] | (uint32_t)d[o + 1] << 8 : (uint32_t)d[o] << 8 | d[o + 1]; }
+    uint32_t u32(size_t o) const
+    {
+        return le ? le32(d + o) : be32(d + o);
+    }
+};
+
+struct TiffEntry {
+    uint32_t type = 0, count = 0;
+    size_t at = 0;  // offset of the value(s)
+};
+
+int type_size(uint32_t t)
+{
+    switch (t) {
+    case 1: case 2: case 6: case 7: return 1;  // BYTE ASCII SBYTE UNDEFINED
+    case 3: case 8: return 2;                   // SHORT SSHORT
+    case 4: case 9: case 11: return 4;          // LONG SLONG FLOAT
+    case 5: case 10: case 12: return 8;         // RATIONAL SRATIONAL DOUBLE
+    }
+    return 0;
+}
+
+// value k of an integer (BYTE / SHORT / LONG) entry
+bool tiff_value(const TiffReader& r, const TiffEntry& e, uint32_t k, uint64_t* v)
+{
+    if (k >= e.count) return false;
+    switch (e.type) {
+    case 1: *v = r.d[e.at + k]; return true;
+    case 3: *v = r.u16(e.at + 2 * (size_t)k); return true;
+    case 4: *v = r.u32(e.at + 4 * (size_t)k); return true;
+    }
+    return false;
+}
+
+int parse_tiff(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
+{
+    info->kind = RK_TIFF;
+    if (n < 8) return bad(err, -1, "TIFF: truncated header");
+    TiffReader r{d, n, d[0] == 'I'};
+    const uint32_t ifd = r.u32(4);
+    if (ifd < 8 || (size_t)ifd + 2 > n) return bad(err, -1, "TIFF: bad IFD offset");
+    const uint32_t cnt = r.u16(ifd);
+    if ((size_t)ifd + 2 + 12 * (size_t)cnt > n) return bad(err, -1, "TIFF: truncated IFD");
+    TiffEntry tag[512];  // baseline tags (< 512) by number; the others are ignored
+    bool seen[512] = {false};
+    for (uint32_t i = 0; i < cnt; ++i) {
+        const size_t e = (size_t)ifd + 2 + 12 * (size_t)i;
+        const uint32_t t = r.u16(e);
+        if (t >= 512) continue;
+        const int k = (int)t;
+        TiffEntry te;
+        te.type = r.u16(e + 2);
+        te.count = r.u32(e + 4);
+        const int ts = type_size(te.type);
+        if (ts == 0) continue;  // unknown type: ignored (libtiff warns)
+        const uint64_t bytes = (uint64_t)ts * te.count;
+        te.at = bytes <= 4 ? e + 8 : (size_t)r.u32(e + 8);
+        if (bytes > 4 && (te.at > n || bytes > n - te.at)) return bad(err, -1, "TIFF: tag data outside the file");
+        tag[k] = te;
+        seen[k] = true;
+    }
+    auto get = [&](int t, uint64_t dflt, uint64_t* v) -> bool {
+        if (!seen[t]) {
+            *v = dflt;
+            return true;
+        }
+        return tiff_value(r, tag[t], 0, v);
+    };
+    uint64_t W, H, comp, photo, spp, planar, pred, orient, rps, bits = 1;
+    if (!seen[256] || !seen[257]) return bad(err, -1, "TIFF: missing image size");
+    if (!get(256, 0, &W) || !get(257, 0, &H) || !get(259, 1, &comp) || !get(277, 1, &spp) ||
+        !get(284, 1, &planar) || !get(317, 1, &pred) || !get(274, 1, &orient) || !get(278, 0xFFFFFFFFu, &rps))
+        return bad(err, -1, "TIFF: malformed tag");
+    if (W == 0 || H == 0) return bad(err, -1, "TIFF: invalid image size");
+    if (spp == 0 || spp > 8) return bad(err, -1, "TIFF: invalid SamplesPerPixel");
+    if (seen[258]) {
+        uint64_t b0 = 0;
+        if (!tiff_value(r, tag[258], 0, &b0)) return bad(err, -1, "TIFF: malformed BitsPerSample");
+        for (uint32_t k = 1; k < tag[258].count && k < spp; ++k) {
+            uint64_t bk;
+            if (!tiff_value(r, tag[258], k, &bk) || bk != b0) return bad(err, -2, "TIFF: mixed BitsPerSample");
+        }
+        bits = b0;
+    }
+    if (!seen[262]) photo = spp >= 3 ? 2 : 1;  // libtiff's guess when the tag is missing
+    else if (!get(262, 1, &photo)) return bad(err, -1, "TIFF: malformed PhotometricInterpretation");
+    if (planar != 1) return bad(err, -2, "TIFF: planar configuration 2 is not decoded");
+    if (orient != 1) return bad(err, -2, "TIFF: orientations other than top-left are not decoded");
+    if (!(comp == 1 || comp == 5 || comp == 8 || comp == 32946 || comp == 32773))
+        return bad(err, -2, "TIFF: compression scheme not decoded (none, LZW, Deflate, PackBits are)");
+    if (comp == 1 || comp == 32773) pred = 1;  // libtiff applies predictors in the LZW / Deflate codecs only
+    if (!(pred == 1 || (pred == 2 && bits == 8))) return bad(err, -2, "TIFF: predictor not decoded");
+    int extra_alpha = 0;  // ExtraSamples[0]: 0 unspecified, 1 associated, 2 unassociated
+    if (seen[338]) {
+        uint64_t es = 0;
+        if (tiff_value(r, tag[338], 0, &es)) extra_alpha = (int)es;
+    }
+    info->W = (int64_t)W;
+    info->H = (int64_t)H;
+    info->bits = (int)bits;
+    info->spp = (int)spp;
+    info->compression = (int)comp;
+    info->predictor = (int)pred;
+    memset(info->pal, 0, sizeof(info->pal));
+    if (photo == 0 || photo == 1) {  // WhiteIsZero / BlackIsZero
+        if (!(bits == 1 || bits == 2 || bits == 4 || bits == 8)) return bad(err, -2, "TIFF: gray bit depth not decoded");
+        if (spp == 1) info->fmt = RF_GRAY;
+        else if (spp == 2 && bits == 8) info->fmt = RF_GRAYA;
+        else return bad(err, -2, "TIFF: gray sample layout not decoded");
+        if (photo == 0) info->flags |= kRasterInvert;
+    } else if (photo == 2) {
+        if (bits != 8 || (spp != 3 && spp != 4)) return bad(err, -2, "TIFF: RGB layout not decoded");
+        info->fmt = spp == 3 ? RF_RGB : RF_RGBA;
+        if (spp == 4 && extra_alpha == 2) info->flags |= kRasterPremul;
+    } else if (photo == 3) {
+        if (spp != 1 || !(bits == 1 || bits == 2 || bits == 4 || bits == 8)) return bad(err, -2, "TIFF: palette layout");
+        if (!seen[320] || tag[320].type != 3 || tag[320].count < 3u * (1u << bits))
+            return bad(err, -1, "TIFF: missing or short ColorMap");
+        const uint32_t nc = 1u << bits;
+        bool sixteen = false;  // libtiff checkcmap: 16-bit entries unless every one is < 256
+        for (uint32_t k = 0; k < 3 * nc; ++k)
+            if (r.u16(tag[320].at + 2 * (size_t)k) >= 256) sixteen = true;
+        for (uint32_t k = 0; k < nc; ++k)
+            for (int c = 0; c < 3; ++c) {
+                const uint32_t v = r.u16(tag[320].at + 2 * ((size_t)c * nc + k));
+                info->pal[k][c] = (uint8_t)(sixteen ? v >> 8 : v);
+            }
+        info->npal = (int)nc;
+        info->fmt = RF_PAL;
+    } else {
+        return bad(err, -2, "TIFF: photometric interpretation not decoded (gray, RGB, palette are)");
+    }
+    // strips or tiles
+    const bool tiled = seen[322] || seen[323];
+    int off_tag = tiled ? 324 : 273, cnt_tag = tiled ? 325 : 279;
+    if (!seen[off_tag] || !seen[cnt_tag]) return bad(err, -1, "TIFF: missing strip / tile offsets or byte counts");
+    uint64_t nseg;
+    if (tiled) {
+        uint64_t tw, th;
+        if (!get(322, 0, &tw) || !get(323, 0, &th) || tw == 0 || th == 0 || tw % 16 || th % 16 || tw > 65536 ||
+            th > 65536)
+            return bad(err, -1, "TIFF: invalid tile size");
+        info->tile_w = (int64_t)tw;
+        info->tile_h = (int64_t)th;
+        nseg = ((W + tw - 1) / tw) * ((H + th - 1) / th);
+    } else {
+        if (rps == 0) return bad(err, -1, "TIFF: RowsPerStrip 0");
+        info->rows_per_strip = (int64_t)std::min<uint64_t>(rps, H);
+        nseg = (H + info->rows_per_strip - 1) / info->rows_per_strip;
+    }
+    if (tag[off_tag].count < nseg || tag[cnt_tag].count < nseg) return bad(err, -1, "TIFF: too few strips / tiles");
+    info->segs.resize((size_t)nseg);
+    for (uint64_t k = 0; k < nseg; ++k) {
+        uint64_t o, c;
+        if (!tiff_value(r, tag[off_tag], (uint32_t)k, &o) || !tiff_value(r, tag[cnt_tag], (uint32_t)k, &c))
+            return bad(err, -1, "TIFF: malformed strip / tile table");
+        if (o > n || c > n - o) return bad(err, -1, "TIFF: strip / tile outside the file");
+        info->segs[(size_t)k] = {o, c};
+    }
+    if (info->W > kMaxDim || info->H > kMaxDim) return bad(err, -2, "TIFF: image larger than 65535 pixels");
+    return 0;
+}
+
+// TIFF LZW (MSB-first 9..12-bit codes, Clear 256, EOI 257, code width
+// growing one code early as libtiff's LZWDecode does); fills out[0, len).
+bool tiff_lzw(const uint8_t* in, size_t n, uint8_t* out, size_t len)
+{
+    static thread_local std::vector<uint16_t> prefix(4096);
+    static thread_local std::vector<uint8_t> suffix(4096), first(4096);
+    static thread_local std::vector<uint16_t> length(4096);
+    for (int c = 0; c < 256; ++c) {
+        suffix[c] = first[c] = (uint8_t)c;
+        length[c] = 1;
+    }
+    uint64_t acc = 0;
+    int have = 0, nbits = 9;
+    size_t ip = 0, op = 0;
+    int next = 258, old = -1;
+    while (op < len) {
+        while (have < nbits) {
+            acc = acc << 8 | (ip < n ? in[ip] : 0);
+            if (ip++ >= n + 2) return false;  // ran out of data (two zero bytes of grace for a final code)
+            have += 8;
+        }
+        const int code = (int)((acc >> (have - nbits)) & ((1u << nbits) - 1));
+        have -= nbits;
+        if (code == 257) break;
+        if (code == 256) {
+            nbits = 9;
+            next = 258;
+            old = -1;
+            continue;
+        }
+        int cur = code;
+        if (old < 0) {
+            if (code > 255) return false;
+            out[op++] = (uint8_t)code;
+            old = code;
+            continue;
+        }
+        if (code > next || code > 4095) return false;
+        uint8_t fb;
+        if (code == next) {  // KwKwK: the old string + its first byte
+            fb = first[old];
+            cur = old;
+        } else {
+            fb = first[code];
+        }
+        // emit string(cur) (+ fb when code == next), clipped at len
+        const int L = length[cur];
+        const size_t end = op + (size_t)L + (code == next ? 1 : 0);
+        size_t w = op + (size_t)L;
+        for (int c = cur; ; c = prefix[c]) {
+            --w;
+            if (w < len) out[w] = suffix[c];
+            if (length[c] == 1) break;
+        }
+        if (code == next && op + (size_t)L < len) out[op + (size_t)L] = fb;
+        op = std::min(end, len);
+        if (next < 4096) {
+            prefix[next] = (uint16_t)old;
+            suffix[next] = fb;
+            first[next] = first[old];
+            length[next] = (uint16_t)(length[old] + 1);
+            ++next;
+            if (next >= (1 << nbits) - 1 && nbits < 12) ++nbits;
+        }
+        old = code;
+    }
+    return op >= len;
+}
+
+bool tiff_packbits(const uint8_t* in, size_t n, uint8_t* out, size_t len)
+{
+    size_t ip = 0, op = 0;
+    while (op < len && ip < n) {
+        const int c = (int8_t)in[ip++];
+        if (c >= 0) {
+            const size_t k = std::min<size_t>((size_t)c + 1, std::min(len - op, n - ip));
+            memcpy(out + op, in + ip, k);
+            op += k;
+            ip += (size_t)c + 1;
+        } else if (c != -128) {
+            if (ip >= n) break;
+            const size_t k = std::min<size_t>((size_t)(1 - c), len - op);
+            memset(out + op, in[ip++], k);
+            op += k;
+        }
+    }
+    return op >= len;
+}
+
+bool tiff_inflate(const uint8_t* in, size_t n, uint8_t* out, size_t len)
+{
+    z_stream zs;
+    memset(&zs, 0, sizeof(zs));
+    if (inflateInit(&zs) != Z_OK) return false;
+    zs.next_in = (Bytef*)in;
+    zs.avail_in = (uInt)n;
+    zs.next_out = out;
+    zs.avail_out = (uInt)len;
+    int rc;
+    do {
+        rc = inflate(&zs, Z_NO_FLUSH);
+    } while (rc == Z_OK && zs.avail_out > 0 && zs.avail_in > 0);
+    const bool ok = zs.avail_out == 0;
+    inflateEnd(&zs);
+    return ok;
+}
+
+bool tiff_segment(const RasterInfo& f, const uint8_t* in, size_t n, uint8_t* out, size_t len)
+{
+    switch (f.compression) {
+    case 1:
+        if (n < len) return false;
+        memcpy(out, in, len);
+        return true;
+    case 5: return tiff_lzw(in, n, out, len);
+    case 32773: return tiff_packbits(in, n, out, len);
+    default: return tiff_inflate(in, n, out, len);
+    }
+}
+
+// horizontal differencing (Predictor 2), 8-bit samples, rows of `w` pixels
+void tiff_undiff(uint8_t* p, int64_t rows, int64_t pitch, int64_t w, int spp)
+{
+    for (int64_t y = 0; y < rows; ++y) {
+        uint8_t* q = p + y * pitch;
+        for (int64_t i = spp; i < w * spp; ++i) q[i] = (uint8_t)(q[i] + q[i - spp]);
+    }
+}
+
+int unpack_tiff(const uint8_t* data, const RasterInfo& f, const RasterLayout& lay, uint8_t* out, std::string* err)
+{
+    const int64_t pitch = lay.pass_pitch[0];
+    if (!f.tile_w) {
+        for (size_t k = 0; k < f.segs.size(); ++k) {
+            const int64_t y0 = (int64_t)k * f.rows_per_strip, rows = std::min(f.rows_per_strip, f.H - y0);
+            uint8_t* dst = out + y0 * pitch;
+            if (!tiff_segment(f, data + f.segs[k].first, (size_t)f.segs[k].second, dst, (size_t)(rows * pitch)))
+                return bad(err, -1, "TIFF: corrupt or short strip data");
+            if (f.predictor == 2) tiff_undiff(dst, rows, pitch, f.W, f.spp);
+        }
+        return 0;
+    }
+    const int64_t tpitch = (f.tile_w * f.spp * f.bits + 7) / 8;
+    std::vector<uint8_t> tile((size_t)(tpitch * f.tile_h));
+    const int64_t across = (f.W + f.tile_w - 1) / f.tile_w;
+    for (size_t k = 0; k < f.segs.size(); ++k) {
+        const int64_t tx = (int64_t)k % across, ty = (int64_t)k / across;
+        if (!tiff_segment(f, data + f.segs[k].first, (size_t)f.segs[k].second, tile.data(), tile.size()))
+            return bad(err, -1, "TIFF: corrupt or short tile data");
+        if (f.predictor == 2) tiff_undiff(tile.data(), f.tile_h, tpitch, f.tile_w, f.spp);
+        const int64_t x_byte = tx * tpitch;  // tile widths are multiples of 16: whole bytes
+        const int64_t wbytes = std::min(tpitch, pitch - x_byte);
+        for (int64_t r = 0; r < f.tile_h && ty * f.tile_h + r < f.H; ++r)
+            memcpy(out + (ty * f.tile_h + r) * pitch + x_byte, tile.data() + r * tpitch, (size_t)wbytes);
+    }
+    return 0;
+}
+
 // PNG row reconstruction (spec 9.2) of one row in place; prev = the previous
 // reconstructed row of the same pass (nullptr for its first row).
 int unfilter_row(uint8_t* row, const uint8_t* prev, int64_t len, int bpp)
@@ -262,6 +601,7 @@ int raster_kind(const uint8_t* data, size_t size)
 {
     if (size >= 8 && memcmp(data, kPngSig, 8) == 0) return RK_PNG;
     if (size >= 2 && data[0] == 'B' && data[1] == 'M') return RK_BMP;
+    if (size >= 4 && (memcmp(data, kTiffLE, 4) == 0 || memcmp(data, kTiffBE, 4) == 0)) return RK_TIFF;
     return RK_NONE;
 }
 
@@ -271,13 +611,21 @@ int raster_parse(const uint8_t* data, size_t size, RasterInfo* info, std::string
     switch (raster_kind(data, size)) {
     case RK_PNG: return parse_png(data, size, info, err);
     case RK_BMP: return parse_bmp(data, size, info, err);
+    case RK_TIFF: return parse_tiff(data, size, info, err);
     }
-    return bad(err, -1, "not a PNG or BMP file");
+    return bad(err, -1, "not a PNG, BMP or TIFF file");
 }
 
 void raster_layout(const RasterInfo& info, RasterLayout* lay)
 {
     *lay = RasterLayout();
+    if (info.kind == RK_TIFF) {
+        lay->pass_pitch[0] = (info.W * info.spp * info.bits + 7) / 8;
+        lay->pass_w[0] = info.W;
+        lay->pass_h[0] = info.H;
+        lay->bytes = lay->pass_pitch[0] * info.H;
+        return;
+    }
     if (info.kind == RK_BMP) {
         lay->pass_pitch[0] = info.stride;
         lay->pass_w[0] = info.W;
@@ -313,7 +661,8 @@ int raster_unpack(const uint8_t* data, size_t size, const RasterInfo& info, cons
         memcpy(out, data + info.data_off, (size_t)lay.bytes);
         return 0;
     }
-    if (info.kind != RK_PNG) return bad(err, -1, "not a PNG or BMP file");
+    if (info.kind == RK_TIFF) return unpack_tiff(data, info, lay, out, err);
+    if (info.kind != RK_PNG) return bad(err, -1, "not a PNG, BMP or TIFF file");
     for (const RasterInfo::Chunk& c : info.idat) {  // IDAT is critical: a CRC mismatch fails the file
         const uint8_t* type = data + c.off - 4;
         if ((uint32_t)crc32(crc32(0L, Z_NULL, 0), type, (uInt)(4 + c.len)) != c.crc) return bad(err, -1, "PNG: CRC error");

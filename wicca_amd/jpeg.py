@@ -46,12 +46,12 @@ def info(data: bytes, apply_orientation: bool = True) -> tuple[int, int, int, in
     return h.value, w.value, c.value, o.value
 
 
-KINDS = {1: "jpeg", 2: "png", 3: "bmp"}
+KINDS = {1: "jpeg", 2: "png", 3: "bmp", 4: "tiff"}
 
 
 def image_info(data: bytes, apply_orientation: bool = True) -> tuple[int, int, str]:
-    """(height, width, format) of a JPEG, PNG or BMP file's bytes (format
-    "jpeg" / "png" / "bmp"; JPEG sizes after EXIF orientation)."""
+    """(height, width, format) of a JPEG, PNG, BMP or TIFF file's bytes
+    (format "jpeg" / "png" / "bmp" / "tiff"; JPEG sizes after EXIF orientation)."""
     arr = np.frombuffer(data, np.uint8)
     h, w = ctypes.c_int64(), ctypes.c_int64()
     k = ctypes.c_int()
