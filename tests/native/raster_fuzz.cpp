@@ -13,6 +13,7 @@
 // reads (raster.hip's index arithmetic, restated below) are checked to stay
 // inside the rows the unpack produced.
 #include "../../wicca_amd/csrc/raster_host.cpp"
+#include "../../wicca_amd/csrc/inflate.h"
 
 #include <cstdio>
 #include <fstream>
@@ -102,9 +103,20 @@ std::vector<uint8_t> mutate_png(const std::vector<uint8_t>& f, std::mt19937& rng
             else if (what == 1) raw.resize(rng() % raw.size());                     // short data
             else raw.insert(raw.end(), 1 + rng() % 64, (uint8_t)rng());             // extra data
         }
-        std::vector<uint8_t> comp(compressBound(raw.size()));
-        uLongf cl = comp.size();
-        compress(comp.data(), &cl, raw.data(), raw.size());
+        // every block type: stored (level 0), fixed Huffman (Z_FIXED), dynamic
+        std::vector<uint8_t> comp(compressBound(raw.size()) + 64);
+        z_stream zs;
+        memset(&zs, 0, sizeof(zs));
+        const int level = (int)(rng() % 10), strategy = rng() % 3 == 0 ? Z_FIXED : Z_DEFAULT_STRATEGY;
+        deflateInit2(&zs, level, Z_DEFLATED, 15, 8, strategy);
+        zs.next_in = raw.data();
+        zs.avail_in = (uInt)raw.size();
+        zs.next_out = comp.data();
+        zs.avail_out = (uInt)comp.size();
+        deflate(&zs, Z_FINISH);
+        uLongf cl = zs.total_out;
+        deflateEnd(&zs);
+        if (cl > 2 && rng() % 3 == 0) comp[2 + rng() % (cl - 2)] ^= (uint8_t)(1u << (rng() % 8));  // damaged stream
         std::vector<uint8_t> h(g.begin(), g.begin() + (std::ptrdiff_t)c.at);
         for (int k = 0; k < 4; ++k) h.push_back((uint8_t)(cl >> (24 - 8 * k)));
         h.insert(h.end(), {'I', 'D', 'A', 'T'});
@@ -252,6 +264,49 @@ bool device_reads_in_bounds(const wicca::RasterInfo& f, const wicca::RasterLayou
     return true;
 }
 
+// Differential check of the PNG path's inflate (inflate.cpp) against zlib on
+// the IDAT stream of an accepted PNG mutant: both must agree on whether the
+// image's `cap` bytes can be produced, and on the bytes.
+bool inflate_agrees(const std::vector<uint8_t>& g, const wicca::RasterInfo& info, int64_t cap)
+{
+    std::vector<uint8_t> z;
+    for (const auto& c : info.idat) z.insert(z.end(), g.begin() + (std::ptrdiff_t)c.off,
+                                             g.begin() + (std::ptrdiff_t)(c.off + c.len));
+    std::unique_ptr<uint8_t[]> a(new uint8_t[cap ? (size_t)cap : 1]), b(new uint8_t[cap ? (size_t)cap : 1]);
+    std::string err;
+    const bool own_ok = wicca::zlib_inflate(z.data(), z.size(), a.get(), cap, nullptr, &err) == 0;
+    z_stream zs;
+    memset(&zs, 0, sizeof(zs));
+    inflateInit(&zs);
+    zs.next_in = z.data();
+    zs.avail_in = (uInt)z.size();
+    zs.next_out = b.get();
+    zs.avail_out = (uInt)cap;
+    int r;
+    do {
+        r = inflate(&zs, Z_NO_FLUSH);
+    } while (r == Z_OK && zs.avail_out > 0);
+    const bool zlib_ok = zs.avail_out == 0;
+    inflateEnd(&zs);
+    if (own_ok != zlib_ok) {
+        fprintf(stderr, "inflate disagrees with zlib: own %d (%s), zlib %d (rc %d)\n", own_ok, err.c_str(), zlib_ok, r);
+        if (const char* dump = getenv("RASTER_FUZZ_DUMP")) {
+            FILE* fp = fopen(dump, "wb");
+            if (fp) {
+                fwrite(z.data(), 1, z.size(), fp);
+                fwrite(&cap, sizeof(cap), 1, fp);
+                fclose(fp);
+            }
+        }
+        return false;
+    }
+    if (own_ok && memcmp(a.get(), b.get(), (size_t)cap) != 0) {
+        fprintf(stderr, "inflate output differs from zlib's\n");
+        return false;
+    }
+    return true;
+}
+
 }  // namespace
 
 int main(int argc, char** argv)
@@ -288,6 +343,7 @@ int main(int argc, char** argv)
         wicca::RasterLayout lay;
         wicca::raster_layout(info, &lay);
         if (lay.bytes > ((int64_t)64 << 20) || info.W * info.H > (1 << 22)) continue;
+        if (info.kind == wicca::RK_PNG && !inflate_agrees(g, info, lay.bytes)) return 1;
         std::unique_ptr<uint8_t[]> out(new uint8_t[lay.bytes ? (size_t)lay.bytes : 1]);
         if (wicca::raster_unpack(buf.get(), g.size(), info, lay, out.get(), &err) == 0) ++unpacked;
         if (!device_reads_in_bounds(info, lay)) {

@@ -663,7 +663,10 @@ int wicca_jpeg_wait(int64_t ticket)
     HIP_TRY(hipStreamSynchronize(st->stream));
     if (st->flags) {
         int h[16];
-        HIP_TRY(hipMemcpy(h, st->flags, sizeof(h), hipMemcpyDeviceToHost));
+        // on the call's own stream: a hipMemcpy (legacy null stream) would
+        // also wait for the next batch's work queued on another blocking stream
+        HIP_TRY(hipMemcpyAsync(h, st->flags, sizeof(h), hipMemcpyDeviceToHost, st->stream));
+        HIP_TRY(hipStreamSynchronize(st->stream));
         bool converged = false;
         for (int r = 1; r <= kAsyncRounds; ++r) converged |= h[r % 16] == 0;
         if (!converged) {  // rare: redo with the host looking at every round

@@ -31,8 +31,11 @@
 #include <string.h>
 #include <zlib.h>
 
+#include <stdlib.h>
+
 #include <algorithm>
 
+#include "inflate.h"
 #include "raster.h"
 
 namespace wicca {
@@ -665,44 +668,82 @@ int raster_unpack(const uint8_t* data, size_t size, const RasterInfo& info, cons
     if (info.kind != RK_PNG) return bad(err, -1, "not a PNG, BMP or TIFF file");
     for (const RasterInfo::Chunk& c : info.idat) {  // IDAT is critical: a CRC mismatch fails the file
         const uint8_t* type = data + c.off - 4;
-        if ((uint32_t)crc32(crc32(0L, Z_NULL, 0), type, (uInt)(4 + c.len)) != c.crc) return bad(err, -1, "PNG: CRC error");
+        if (crc32_fast(0, type, 4 + c.len) != c.crc) return bad(err, -1, "PNG: CRC error");
     }
     const int bits_pp = png_channels(info.color_type) * info.bits;
     const int bpp = std::max(1, bits_pp / 8);
+    // rows reconstructed so far: pass p, row y (passes in order, empty ones skipped)
+    struct Rows : InflateProgress {
+        const RasterLayout& lay;
+        uint8_t* out;
+        int bpp;
+        int p = 0;
+        int64_t y = 0;
+        Rows(const RasterLayout& l, uint8_t* o, int b) : lay(l), out(o), bpp(b) { skip_empty(); }
+        void skip_empty()
+        {
+            while (p < 7 && (lay.pass_pitch[p] == 0 || y >= lay.pass_h[p])) {
+                ++p;
+                y = 0;
+            }
+        }
+        // reconstruct every row that ends at or before `upto`
+        bool upto(int64_t limit)
+        {
+            while (p < 7) {
+                const int64_t pitch = lay.pass_pitch[p];
+                uint8_t* row = out + lay.pass_off[p] + y * pitch;
+                if (row + pitch > out + limit) break;
+                if (unfilter_row(row, y ? row - pitch : nullptr, pitch - 1, bpp)) return false;
+                ++y;
+                skip_empty();
+            }
+            return true;
+        }
+        // the decoder still reads the last 32 KiB it wrote (its LZ77 window)
+        bool advance(int64_t produced) override
+        {
+            return upto(produced >= lay.bytes ? produced : produced - 32768);
+        }
+        const char* error() const override { return "PNG: bad adaptive filter value"; }
+    } rows(lay, out, bpp);
+    // one contiguous zlib stream (IDAT payloads concatenated when split)
+    const uint8_t* zin = info.idat.empty() ? data : data + info.idat[0].off;
+    size_t zlen = info.idat.empty() ? 0 : info.idat[0].len;
+    std::vector<uint8_t> joined;
+    if (info.idat.size() > 1) {
+        size_t total = 0;
+        for (const RasterInfo::Chunk& c : info.idat) total += c.len;
+        joined.resize(total);
+        size_t at = 0;
+        for (const RasterInfo::Chunk& c : info.idat) {
+            memcpy(joined.data() + at, data + c.off, c.len);
+            at += c.len;
+        }
+        zin = joined.data();
+        zlen = total;
+    }
+    static const bool use_zlib = [] {
+        const char* e = getenv("WICCA_PNG_INFLATE");
+        return e && strcmp(e, "zlib") == 0;
+    }();
+    if (!use_zlib) return zlib_inflate(zin, zlen, out, lay.bytes, &rows, err);
+    // zlib (WICCA_PNG_INFLATE=zlib; A/B and cross-checks): 1 MiB slices, its
+    // own window, so rows are reconstructed as soon as they are complete
     const int64_t total = lay.bytes;
     z_stream zs;
     memset(&zs, 0, sizeof(zs));
     if (inflateInit(&zs) != Z_OK) return bad(err, -1, "PNG: zlib init failed");
-    size_t chunk = 0;
+    zs.next_in = (Bytef*)zin;
+    zs.avail_in = (uInt)zlen;
     int64_t produced = 0;
-    // rows reconstructed so far: pass p, row y (passes in order, empty ones skipped)
-    int p = 0;
-    int64_t y = 0;
-    auto advance_empty = [&] {
-        while (p < 7 && (lay.pass_pitch[p] == 0 || y >= lay.pass_h[p])) {
-            ++p;
-            y = 0;
-        }
-    };
-    advance_empty();
     int rc = 0;
-    // inflate in 1 MiB slices, reconstructing each row as soon as it is complete
     while (produced < total) {
-        if (zs.avail_in == 0) {
-            if (chunk == info.idat.size()) {
-                rc = bad(err, -1, "PNG: not enough image data");
-                break;
-            }
-            zs.next_in = (Bytef*)(data + info.idat[chunk].off);
-            zs.avail_in = (uInt)info.idat[chunk].len;
-            ++chunk;
-            continue;
-        }
         zs.next_out = out + produced;
         zs.avail_out = (uInt)std::min<int64_t>(total - produced, 1 << 20);
         const int r = inflate(&zs, Z_NO_FLUSH);
         produced = (int64_t)(zs.next_out - out);
-        if (r == Z_STREAM_END && produced < total) {
+        if ((r == Z_STREAM_END || r == Z_BUF_ERROR) && produced < total && zs.avail_out > 0) {
             rc = bad(err, -1, "PNG: not enough image data");
             break;
         }
@@ -710,19 +751,10 @@ int raster_unpack(const uint8_t* data, size_t size, const RasterInfo& info, cons
             rc = bad(err, -1, "PNG: corrupt compressed data");
             break;
         }
-        while (p < 7) {
-            const int64_t pitch = lay.pass_pitch[p];
-            uint8_t* row = out + lay.pass_off[p] + y * pitch;
-            if (row + pitch > out + produced) break;
-            if (unfilter_row(row, y ? row - pitch : nullptr, pitch - 1, bpp)) {
-                rc = bad(err, -1, "PNG: bad adaptive filter value");
-                break;
-            }
-            ++y;
-            advance_empty();
-            if (!info.interlaced && y >= lay.pass_h[0]) p = 7;
+        if (!rows.upto(produced)) {
+            rc = bad(err, -1, "PNG: bad adaptive filter value");
+            break;
         }
-        if (rc) break;
     }
     inflateEnd(&zs);
     return rc;
