@@ -588,6 +588,38 @@ def run_jpeg(args, torch, rank):
     for _ in range(args.steps):
         stage()
     stage_s = (time.perf_counter() - t0) / args.steps
+    # the same stage in a data loader's loop (wicca_image_icon_stage_async,
+    # one batch in flight ahead), two output sets alternating
+    outs = [(res, ico), (np.empty_like(res), np.empty_like(ico))]
+
+    def issue_stage(k):
+        t = ctypes.c_int64(0)
+        r, c = outs[k % 2]
+        _lib.check(lib.wicca_image_icon_stage_async(ptrs, sizes, B, D, 1, 0, shape[0], shape[1], args.interpolation,
+                                                    r.ctypes.data, c.ctypes.data, -1, ctypes.byref(t)))
+        return t.value
+
+    prev = issue_stage(0)
+    for k in range(1, max(2, args.warmup + 1)):
+        cur = issue_stage(k)
+        _lib.check(lib.wicca_image_stage_wait(prev))
+        prev = cur
+    _lib.check(lib.wicca_image_stage_wait(prev))
+    t0 = time.perf_counter()
+    prev = issue_stage(0)
+    for k in range(1, args.steps):
+        cur = issue_stage(k)
+        _lib.check(lib.wicca_image_stage_wait(prev))
+        prev = cur
+    _lib.check(lib.wicca_image_stage_wait(prev))
+    stage_pipe_s = (time.perf_counter() - t0) / args.steps
+    if not args.no_verify:
+        ref_r, ref_c = np.empty_like(res), np.empty_like(ico)
+        _lib.check(lib.wicca_jpeg_icon_stage_u8(ptrs, sizes, B, D, 1, 0, shape[0], shape[1], args.interpolation,
+                                                ref_r.ctypes.data, ref_c.ctypes.data, -1, None))
+        last_r, last_c = outs[(args.steps - 1) % 2]
+        if not (np.array_equal(last_r, ref_r) and np.array_equal(last_c, ref_c)):
+            raise SystemExit("jpeg bench verification FAILED (pipelined file stage)")
     mpix = B * H * W / 1e6
     # CPU: libjpeg-turbo (Pillow) decode, one thread and a pool over the affinity set
     n1, t0 = 0, time.perf_counter()
@@ -618,6 +650,10 @@ def run_jpeg(args, torch, rank):
         "file_stage": {"ms_per_batch": round(stage_s * 1e3, 3), "MP_per_s": round(mpix / stage_s, 1),
                        "what": f"decode + cv2.resize to {shape} + icon depth {D} + icon resize, "
                                "outputs to host (classifying_tools.py:312-323)"},
+        "file_stage_pipelined": {"ms_per_batch": round(stage_pipe_s * 1e3, 3),
+                                 "MP_per_s": round(mpix / stage_pipe_s, 1),
+                                 "what": "the same stage through wicca_image_icon_stage_async with one batch in "
+                                         "flight ahead (get_img_batches)"},
         "cpu_baseline": {"value": round(pool, 1), "unit": "MP/s", "cores": threads, "kind": "reference",
                          "sample": f"Pillow/libjpeg-turbo {jpeg_pil.libjpeg_version()} decode of the same "
                                    f"files, ThreadPoolExecutor({threads}), {2 * B} files",

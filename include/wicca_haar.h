@@ -376,6 +376,24 @@ int wicca_image_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* 
                                      uint8_t* resized, uint8_t* resized_icons,
                                      const int* devices, int n_devices, int* status);
 
+/* wicca_image_icon_stage_u8 without waiting for the device: a data loader's
+ * loop issues batch k+1 before waiting for batch k, so k+1's host parse /
+ * de-stuffing and PCIe transfer overlap k's device decode and stage.  The
+ * call returns once the host's part is queued (*ticket set); resized /
+ * resized_icons (and data[i]) must stay valid until wicca_image_stage_wait
+ * (*ticket) returns 0, which fills them.  Batches of JPEG files within one
+ * device pass with the fused stage run asynchronously; any other batch (PNG,
+ * BMP, TIFF, larger, depth > 8) completes before the call returns
+ * (*ticket = 0).  No per-file status: a file that fails fails the call. */
+int wicca_image_icon_stage_async(const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                                 int depth, int border_type, int border_constant,
+                                 int64_t out_w, int64_t out_h, int interpolation,
+                                 uint8_t* resized, uint8_t* resized_icons, int device,
+                                 int64_t* ticket);
+
+/* Wait for an asynchronous file stage and copy its outputs (ticket 0: no-op). */
+int wicca_image_stage_wait(int64_t ticket);
+
 /*
  * Deterministic synthetic images on device (no PCIe in timed regions):
  * byte (i, y, x, c) = splitmix64-hash of (seed, i, y*W*C + x*C + c), see

@@ -404,3 +404,35 @@ def test_batch_with_unreadable_files_fails_per_slot(tmp_path, capsys):
         wicca_amd.get_img_batch(paths, (224, 224), 4)
     two = wicca_amd.get_img_batch(paths, (224, 224), 4, devices=[0, 0], errors="zero")
     assert np.array_equal(two[0], imgs) and np.array_equal(two[1], icons)
+
+
+def test_file_stage_pipelined_matches_synchronous(tmp_path):
+    """get_img_batches (wicca_image_icon_stage_async, batches in flight) gives
+    get_img_batch's outputs batch by batch; a PNG batch runs synchronously
+    inside it; an abandoned generator leaves nothing in flight."""
+    from PIL import Image
+    import io
+    batches = []
+    for b in range(4):
+        paths = []
+        for i, (h, w) in enumerate([(480, 640), (333, 517), (1080, 1920)]):
+            p = tmp_path / f"b{b}_{i}.jpg"
+            p.write_bytes(J.encode(J.test_image("scene", h, w, 10 * b + i), 85, 2, orientation=6 if i == 1 else 1))
+            paths.append(str(p))
+        batches.append(paths)
+    png = tmp_path / "x.png"
+    buf = io.BytesIO()
+    Image.fromarray(J.test_image("scene", 300, 200, 5)).save(buf, "PNG")
+    png.write_bytes(buf.getvalue())
+    batches.insert(2, [str(png), batches[0][0]])
+    for depth in (1, 2, 3):
+        got = list(wicca_amd.get_img_batches(batches, (224, 224), 4, depth=depth))
+        assert len(got) == len(batches)
+        for paths, (imgs, icons) in zip(batches, got):
+            want = wicca_amd.get_img_batch(paths, (224, 224), 4)
+            assert np.array_equal(imgs, want[0]) and np.array_equal(icons, want[1])
+    gen = wicca_amd.get_img_batches(batches, (299, 299), 3)
+    next(gen)
+    gen.close()
+    with pytest.raises(ValueError):
+        list(wicca_amd.get_img_batches([[str(tmp_path / "b0_0.jpg")], [str(tmp_path / "missing.jpg")]], (224, 224), 4))

@@ -11,7 +11,7 @@ kernels behind the C ABI in ``include/wicca_haar.h``.
 from .coder import (BORDER_CONSTANT, BORDER_REFLECT, BORDER_REFLECT_101, BORDER_REPLICATE,
                     BORDER_WRAP, HaarCoder, WaveletCoder)
 from .normalization import normalize_depth
-from .jpeg import get_img_batch, load_image
+from .jpeg import get_img_batch, get_img_batches, load_image
 from .resize import (INTER_AREA, INTER_CUBIC, INTER_LANCZOS4, INTER_LINEAR, INTER_LINEAR_EXACT, INTER_NEAREST,
                      INTER_NEAREST_EXACT, resize)
 from .validation import validate_image
@@ -19,5 +19,5 @@ from .validation import validate_image
 __all__ = ["HaarCoder", "WaveletCoder", "validate_image", "normalize_depth", "BORDER_CONSTANT", "BORDER_REPLICATE",
            "BORDER_REFLECT", "BORDER_WRAP", "BORDER_REFLECT_101", "resize", "INTER_NEAREST",
            "INTER_LINEAR", "INTER_AREA", "INTER_CUBIC", "INTER_LANCZOS4", "INTER_LINEAR_EXACT",
-           "INTER_NEAREST_EXACT", "load_image", "get_img_batch"]
+           "INTER_NEAREST_EXACT", "load_image", "get_img_batch", "get_img_batches"]
 __version__ = "0.2.0"

@@ -121,6 +121,7 @@ struct Workspace {
     // PNG / BMP decode (capi_raster.cpp): raw rows (pinned staging + device) and descriptors
     DevBuf rraw, rmeta;
     HostBuf rhost, rmeta_pin;
+    HostBuf opin;   // pinned outputs of an asynchronous file stage (wicca_image_icon_stage_async)
     size_t bytes() const
     {
         return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
@@ -176,6 +177,7 @@ struct Workspace {
         rmeta.release();
         rhost.release();
         rmeta_pin.release();
+        opin.release();
     }
     void destroy()
     {

@@ -597,6 +597,25 @@ struct AsyncDecode {
     bool orient = true;
 };
 constexpr int kAsyncRounds = 8;  // synchronisation rounds launched ahead (3 suffice on the corpus)
+
+// An asynchronous file stage (wicca_image_icon_stage_async): the decode and
+// the stage kernels are queued on the workspace's stream, the outputs copied
+// into its pinned `opin`; the wait copies them to the caller's arrays.
+struct AsyncStage {
+    WorkspaceLease lease;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    const int* flags = nullptr;
+    std::vector<const uint8_t*> data;
+    std::vector<int64_t> sizes;
+    int depth = 0, border = 1, k = 0, interpolation = 3;
+    int64_t out_w = 0, out_h = 0;
+    uint8_t* resized = nullptr;
+    uint8_t* icons = nullptr;
+};
+std::mutex g_stage_mu;
+std::unordered_map<int64_t, std::unique_ptr<AsyncStage>> g_stage;
+int64_t g_stage_next = 1;
 std::mutex g_async_mu;
 std::unordered_map<int64_t, std::unique_ptr<AsyncDecode>> g_async;
 int64_t g_async_next = 1;
@@ -1013,6 +1032,122 @@ static int icon_stage_impl(const uint8_t* const* data, const int64_t* sizes, int
             memset(resized_icons + i * out_bytes, 0, (size_t)out_bytes);
         }
     }
+    return WICCA_OK;
+}
+
+int wicca_image_icon_stage_async(const uint8_t* const* data, const int64_t* sizes, int64_t n, int depth,
+                                 int border_type, int border_constant, int64_t out_w, int64_t out_h,
+                                 int interpolation, uint8_t* resized, uint8_t* resized_icons, int device,
+                                 int64_t* ticket)
+{
+    if (!ticket) return fail(WICCA_ERR_ARG, "null ticket");
+    *ticket = 0;
+    if (n < 0 || (n > 0 && (!data || !sizes))) return fail(WICCA_ERR_ARG, "bad arrays");
+    if (n == 0) return WICCA_OK;
+    if (!resized || !resized_icons) return fail(WICCA_ERR_ARG, "output buffer is NULL");
+    // the asynchronous form covers single-pass batches of JPEG files whose
+    // stage is the fused one; anything else runs synchronously here
+    bool async_ok = n <= wicca::kJpegMaxJobs / wicca::kJpegMaxComp && stage_fused() && depth >= 1 && depth <= 8 &&
+                    out_h <= 65535 && out_w > 0 && out_h > 0;
+    std::vector<int64_t> H((size_t)n), W((size_t)n), ih((size_t)n), iw((size_t)n);
+    int64_t rgb_total = 0;
+    for (int64_t i = 0; i < n && async_ok; ++i) {
+        int kind = 0;
+        int rc = probe_file(data[i], sizes[i], i, true, true, &H[i], &W[i], &kind);
+        if (rc) return rc;
+        if ((rc = check_image((const uint8_t*)1, H[i], W[i], 3, W[i] * 3, depth, border_type))) return rc;
+        wicca::ResizeParams probe{};
+        if ((rc = check_resize(H[i], W[i], 3, out_w, out_h, interpolation, &probe))) return rc;
+        icon_dims(H[i], W[i], depth, &ih[i], &iw[i]);
+        if ((rc = check_resize(ih[i], iw[i], 3, out_w, out_h, interpolation, &probe))) return rc;
+        async_ok = kind == 1 && wicca::stage_row_ok(W[i], 3);
+        rgb_total += round_up(W[i] * 3, kStagePitch) * H[i];
+    }
+    if (!async_ok)
+        return icon_stage_impl(data, sizes, n, depth, border_type, border_constant, out_w, out_h, interpolation,
+                               resized, resized_icons, device, nullptr, true);
+    DeviceGuard dg;
+    int dev, rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
+    std::unique_ptr<AsyncStage> st(new AsyncStage);
+    if ((rc = acquire(dev, st->lease))) return rc;
+    Workspace* ws = st->lease.ws;
+    hipStream_t cs = ws->stream;
+    const int64_t out_bytes = out_w * out_h * 3;
+    HIP_TRY(ws->jrgb.reserve((size_t)rgb_total));
+    HIP_TRY(ws->out.reserve((size_t)(2 * n * out_bytes)));
+    if (ws->opin.reserve((size_t)(2 * n * out_bytes), 1 << 20) != hipSuccess)
+        return fail(WICCA_ERR_NOMEM, "pinned staging of %lld bytes", (long long)(2 * n * out_bytes));
+    std::vector<uint8_t*> d((size_t)n);
+    std::vector<int64_t> p((size_t)n);
+    int64_t off = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        d[(size_t)i] = (uint8_t*)ws->jrgb.ptr + off;
+        p[(size_t)i] = round_up(W[i] * 3, kStagePitch);
+        off += p[(size_t)i] * H[i];
+    }
+    int rounds = 0;
+    if ((rc = jpeg_decode_to_device(ws, data, sizes, n, d.data(), p.data(), true, cs, &rounds, kAsyncRounds,
+                                    &st->flags)))
+        return rc;
+    SyncOnExit sync_on_exit{cs};  // the decode's pinned staging is in use until the stream is done
+    uint8_t* dres = (uint8_t*)ws->out.ptr;
+    uint8_t* dico = dres + n * out_bytes;
+    if ((rc = fused_stage(ws, cs, n, d.data(), p.data(), H.data(), W.data(), ih.data(), iw.data(), depth, border_type,
+                          border_constant, out_w, out_h, interpolation, dres, dico)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(ws->opin.ptr, dres, (size_t)(2 * n * out_bytes), hipMemcpyDeviceToHost, cs));
+    sync_on_exit.active = false;
+    st->device = dev;
+    st->stream = cs;
+    st->data.assign(data, data + n);
+    st->sizes.assign(sizes, sizes + n);
+    st->depth = depth;
+    st->border = border_type;
+    st->k = border_constant;
+    st->interpolation = interpolation;
+    st->out_w = out_w;
+    st->out_h = out_h;
+    st->resized = resized;
+    st->icons = resized_icons;
+    std::lock_guard<std::mutex> g(g_stage_mu);
+    const int64_t id = g_stage_next++;
+    g_stage[id] = std::move(st);
+    *ticket = id;
+    return WICCA_OK;
+}
+
+int wicca_image_stage_wait(int64_t ticket)
+{
+    if (ticket == 0) return WICCA_OK;
+    std::unique_ptr<AsyncStage> st;
+    {
+        std::lock_guard<std::mutex> g(g_stage_mu);
+        auto it = g_stage.find(ticket);
+        if (it == g_stage.end()) return fail(WICCA_ERR_ARG, "unknown stage ticket %lld", (long long)ticket);
+        st = std::move(it->second);
+        g_stage.erase(it);
+    }
+    DeviceGuard dg;
+    int dev, rc;
+    if ((rc = select_device(st->device, &dev, dg))) return rc;
+    HIP_TRY(hipStreamSynchronize(st->stream));
+    int h[16];
+    HIP_TRY(hipMemcpyAsync(h, st->flags, sizeof(h), hipMemcpyDeviceToHost, st->stream));
+    HIP_TRY(hipStreamSynchronize(st->stream));
+    bool converged = false;
+    for (int r = 1; r <= kAsyncRounds; ++r) converged |= h[r % 16] == 0;
+    const int64_t n = (int64_t)st->data.size();
+    if (!converged) {  // rare: the whole stage again, synchronously, with the host looking at every round
+        const AsyncStage a = {WorkspaceLease(), st->device, nullptr, nullptr, st->data, st->sizes, st->depth,
+                              st->border, st->k, st->interpolation, st->out_w, st->out_h, st->resized, st->icons};
+        st.reset();  // the workspace goes back to the pool before the synchronous call leases one
+        return icon_stage_impl(a.data.data(), a.sizes.data(), n, a.depth, a.border, a.k, a.out_w, a.out_h,
+                               a.interpolation, a.resized, a.icons, a.device, nullptr, true);
+    }
+    const int64_t out_bytes = st->out_w * st->out_h * 3;
+    memcpy(st->resized, st->lease.ws->opin.ptr, (size_t)(n * out_bytes));
+    memcpy(st->icons, st->lease.ws->opin.ptr + n * out_bytes, (size_t)(n * out_bytes));
     return WICCA_OK;
 }
 

@@ -223,3 +223,56 @@ def get_img_batch(file_paths: Sequence[str], shape, transform_depth: int, interp
             if status[i] != 0:  # as load_image reports it (data_loader.py:61-63)
                 print(f"Error loading image {file_paths[i]}: {_slot_error(blobs[i])}")
     return resized, icons
+
+
+def get_img_batches(batches, shape, transform_depth: int, interpolation: int = 3, border_type: int = 1,
+                    border_constant: int = 0, device: int | None = None, depth: int = 2):
+    """``get_img_batch`` over a stream of batches of file paths (the loop of
+    ``ClassifierProcessor._process_core``, classifying_tools.py:356-387):
+    yields ``(batch_images, batch_icons)`` per batch, with up to ``depth``
+    batches in flight (``wicca_image_icon_stage_async``) so that batch k+1's
+    file parse, de-stuffing and PCIe transfer overlap batch k's device decode
+    and stage.  Same outputs as ``get_img_batch`` (errors="raise")."""
+    import collections
+    from .coder import _border_value, _depth_index
+    if depth < 1:
+        raise ValueError("depth must be >= 1")
+    lib = _lib.load()
+    out_w, out_h = int(shape[0]), int(shape[1])
+    k = _border_value(border_constant) if int(border_type) == 0 else 0
+    dev = -1 if device is None else int(device)
+    pending = collections.deque()
+
+    def finish():
+        ticket, res, ico, keep = pending.popleft()
+        _lib.check(lib.wicca_image_stage_wait(ticket))
+        del keep
+        return res, ico
+
+    try:
+        for paths in batches:
+            blobs = []
+            for p in paths:
+                if not p:
+                    raise ValueError("File path cannot be empty")
+                with open(p, "rb") as f:
+                    blobs.append(f.read())
+            if not blobs:
+                raise ValueError("need at least one array to stack")
+            n = len(blobs)
+            res = np.empty((n, out_h, out_w, 3), np.uint8)
+            ico = np.empty((n, out_h, out_w, 3), np.uint8)
+            keep, ptrs, sizes = _buffers(blobs)
+            if len(pending) >= depth:
+                yield finish()
+            ticket = ctypes.c_int64(0)
+            _lib.check(lib.wicca_image_icon_stage_async(ptrs, sizes, n, _depth_index(transform_depth),
+                                                        int(border_type), k, out_w, out_h, int(interpolation),
+                                                        res.ctypes.data, ico.ctypes.data, dev,
+                                                        ctypes.byref(ticket)))
+            pending.append((ticket.value, res, ico, (keep, blobs)))
+        while pending:
+            yield finish()
+    finally:  # an exception or an abandoned generator still waits for what is in flight
+        while pending:
+            lib.wicca_image_stage_wait(pending.popleft()[0])
