@@ -434,5 +434,5 @@ def test_file_stage_pipelined_matches_synchronous(tmp_path):
     gen = wicca_amd.get_img_batches(batches, (299, 299), 3)
     next(gen)
     gen.close()
-    with pytest.raises(ValueError):
+    with pytest.raises(OSError):  # a missing file (batch 1) while batch 0 is in flight
         list(wicca_amd.get_img_batches([[str(tmp_path / "b0_0.jpg")], [str(tmp_path / "missing.jpg")]], (224, 224), 4))

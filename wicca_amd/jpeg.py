@@ -131,7 +131,9 @@ def decode_batches(batches, apply_orientation: bool = True, device: int = 0, dep
         yield from _decode_batches_loop(batches, apply_orientation, device, depth, lib, pending, finish)
     finally:  # an exception or an abandoned generator still waits for what is in flight
         while pending:
-            lib.wicca_jpeg_wait(pending.popleft()[0])
+            item = pending.popleft()  # its outputs and file bytes stay alive until the wait returns
+            lib.wicca_jpeg_wait(item[0])
+            del item
 
 
 def _decode_batches_loop(batches, apply_orientation, device, depth, lib, pending, finish):
@@ -228,7 +230,7 @@ def get_img_batch(file_paths: Sequence[str], shape, transform_depth: int, interp
 def get_img_batches(batches, shape, transform_depth: int, interpolation: int = 3, border_type: int = 1,
                     border_constant: int = 0, device: int | None = None, depth: int = 2):
     """``get_img_batch`` over a stream of batches of file paths (the loop of
-    ``ClassifierProcessor._process_core``, classifying_tools.py:356-387):
+    ``ClassifierProcessor._classify``, classifying_tools.py:339-345):
     yields ``(batch_images, batch_icons)`` per batch, with up to ``depth``
     batches in flight (``wicca_image_icon_stage_async``) so that batch k+1's
     file parse, de-stuffing and PCIe transfer overlap batch k's device decode
@@ -275,4 +277,6 @@ def get_img_batches(batches, shape, transform_depth: int, interpolation: int = 3
             yield finish()
     finally:  # an exception or an abandoned generator still waits for what is in flight
         while pending:
-            lib.wicca_image_stage_wait(pending.popleft()[0])
+            item = pending.popleft()  # the output arrays it writes stay alive until the wait returns
+            lib.wicca_image_stage_wait(item[0])
+            del item
