@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <string>
 #include <thread>
 #include <vector>
@@ -71,9 +72,15 @@ int raster_decode_to_device(Workspace* ws, const uint8_t* const* data, const int
                         upload_err = 1;
                     continue;
                 }
-                if (wicca::raster_unpack(data[i], (size_t)sizes[i], info[(size_t)i], lay[(size_t)i], host + a,
-                                         &errs[(size_t)i]))
-                    continue;  // errs[i] is set
+                int urc;
+                try {  // no exception may leave a worker thread (host scratch: IDAT join, TIFF tiles)
+                    urc = wicca::raster_unpack(data[i], (size_t)sizes[i], info[(size_t)i], lay[(size_t)i], host + a,
+                                               &errs[(size_t)i]);
+                } catch (const std::exception&) {
+                    errs[(size_t)i] = "out of host memory";
+                    urc = -1;
+                }
+                if (urc) continue;  // errs[i] is set
                 if (hipMemcpyAsync(raw + a, host + a, (size_t)lay[(size_t)i].bytes, hipMemcpyHostToDevice, stream) !=
                     hipSuccess)
                     upload_err = 1;

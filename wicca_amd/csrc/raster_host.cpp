@@ -375,6 +375,8 @@ int parse_tiff(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
         if (!get(322, 0, &tw) || !get(323, 0, &th) || tw == 0 || th == 0 || tw % 16 || th % 16 || tw > 65536 ||
             th > 65536)
             return bad(err, -1, "TIFF: invalid tile size");
+        // one decoded tile is host scratch: keep it bounded (256 MiB) for any header
+        if (tw * th * spp * bits > ((uint64_t)256 << 23)) return bad(err, -2, "TIFF: tiles larger than 256 MiB");
         info->tile_w = (int64_t)tw;
         info->tile_h = (int64_t)th;
         nseg = ((W + tw - 1) / tw) * ((H + th - 1) / th);
