@@ -147,6 +147,11 @@ double now_ms()
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// WICCA_JPEG_TIMING with asynchronous calls: events around each call's device
+// work (recorded once its uploads are queued, and after its last kernel), so
+// that the wait can report how long the device idled between calls
+thread_local hipEvent_t t_async_ready = nullptr, t_async_done = nullptr;
+
 // async_rounds > 0 (n <= one pass): everything is issued on `stream` and the
 // call returns without waiting; *async_flags gets the device flags to check
 // once the stream is done (jpeg_decode_device).
@@ -402,6 +407,11 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     }
     int rounds = 0;
     const double t_upload = now_ms();
+    if (async_rounds > 0 && jpeg_timing()) {
+        (void)hipEventCreate(&t_async_ready);
+        (void)hipEventCreate(&t_async_done);
+        (void)hipEventRecord(t_async_ready, stream);
+    }
     HIP_TRY(wicca::jpeg_decode_device(P, ims.data(), ws->jscratch.ptr, n, &rounds, stream, async_rounds,
                                       async_flags, ws->jtab.ptr + jobs_off));
     if (rounds_out) *rounds_out = rounds;
@@ -410,6 +420,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
             HIP_TRY(wicca::launch_orient(ims[(size_t)i].dst, ims[(size_t)i].dst_pitch, info[(size_t)i].W,
                                          info[(size_t)i].H, info[(size_t)i].orientation, dst[i], dpitch[i],
                                          stream));
+    if (async_rounds > 0 && t_async_done) (void)hipEventRecord(t_async_done, stream);
     if (async_rounds > 0) {  // the caller holds the workspace (and its pinned staging) until it waits
         sync_on_exit.active = false;
         return WICCA_OK;
@@ -595,7 +606,11 @@ struct AsyncDecode {
     std::vector<int64_t> sizes, pitches;
     std::vector<uint8_t*> dsts;
     bool orient = true;
+    hipEvent_t ready = nullptr, done = nullptr;  // WICCA_JPEG_TIMING
+    double issue_ms = 0;
 };
+std::mutex g_timing_mu;
+hipEvent_t g_prev_done = nullptr;  // the previous waited call's end (WICCA_JPEG_TIMING)
 constexpr int kAsyncRounds = 8;  // synchronisation rounds launched ahead (3 suffice on the corpus)
 
 // An asynchronous file stage (wicca_image_icon_stage_async): the decode and
@@ -650,9 +665,14 @@ int wicca_jpeg_decode_u8_async(const uint8_t* const* data, const int64_t* sizes,
     st->device = dev;
     st->stream = st->lease.ws->stream;
     int rounds = 0;
+    const double t0 = now_ms();
+    t_async_ready = t_async_done = nullptr;
     if ((rc = jpeg_decode_to_device(st->lease.ws, data, sizes, n, dsts, dst_pitches, apply_orientation != 0,
                                     st->stream, &rounds, kAsyncRounds, &st->flags)))
         return rc;
+    st->ready = t_async_ready;
+    st->done = t_async_done;
+    st->issue_ms = now_ms() - t0;
     st->data.assign(data, data + n);
     st->sizes.assign(sizes, sizes + n);
     st->dsts.assign(dsts, dsts + n);
@@ -680,6 +700,19 @@ int wicca_jpeg_wait(int64_t ticket)
     int dev, rc;
     if ((rc = select_device(st->device, &dev, dg))) return rc;
     HIP_TRY(hipStreamSynchronize(st->stream));
+    if (st->ready && st->done) {  // WICCA_JPEG_TIMING
+        float work = 0, idle = -1;
+        (void)hipEventElapsedTime(&work, st->ready, st->done);
+        std::lock_guard<std::mutex> g(g_timing_mu);
+        if (g_prev_done) {
+            (void)hipEventElapsedTime(&idle, g_prev_done, st->ready);
+            (void)hipEventDestroy(g_prev_done);
+        }
+        fprintf(stderr, "[wicca jpeg async] host issue %.2f ms; device work %.2f ms; its data ready %.2f ms after "
+                "the previous call's device work ended (> 0: the device idled)\n", st->issue_ms, work, idle);
+        g_prev_done = st->done;
+        (void)hipEventDestroy(st->ready);
+    }
     if (st->flags) {
         int h[16];
         // on the call's own stream: a hipMemcpy (legacy null stream) would
