@@ -17,11 +17,14 @@ build() {  # name, extra flags
   /opt/rocm/bin/hipcc $F "$@" -c "$R/wicca_amd/csrc/stage.hip" -o "$B/stage.o" &
   /opt/rocm/bin/hipcc $F "$@" -c "$R/wicca_amd/csrc/jpeg.hip" -o "$B/jpeg.o" &
   /opt/rocm/bin/hipcc $F "$@" -x hip -c "$R/wicca_amd/csrc/jpeg_host.cpp" -o "$B/jpeg_host.o" &
-  for c in capi capi_resize capi_jpeg; do
+  /opt/rocm/bin/hipcc $F "$@" -c "$R/wicca_amd/csrc/raster.hip" -o "$B/raster.o" &
+  /opt/rocm/bin/hipcc $F "$@" -x hip -c "$R/wicca_amd/csrc/raster_host.cpp" -o "$B/raster_host.o" &
+  g++ -O3 -std=c++17 -fPIC -c "$R/wicca_amd/csrc/inflate.cpp" -o "$B/inflate.o" &
+  for c in capi capi_resize capi_jpeg capi_raster; do
     /opt/rocm/bin/hipcc $F "$@" -x hip -c "$R/wicca_amd/csrc/$c.cpp" -o "$B/$c.o" &
   done
   wait
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/lib_$name.so" "$B"/haar_ll.o "$B"/haar_multi*.o "$B/resize.o" "$B/stage.o" "$B/jpeg.o" "$B/jpeg_host.o" "$B"/capi*.o
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/lib_$name.so" "$B"/haar_ll.o "$B"/haar_multi*.o "$B/resize.o" "$B/stage.o" "$B/jpeg.o" "$B/jpeg_host.o" "$B/raster.o" "$B/raster_host.o" "$B/inflate.o" "$B"/capi*.o -lz
   rm -rf "$B"
 }
 for spec in "$@"; do
