@@ -1120,9 +1120,15 @@ int wicca_image_icon_stage_async(const uint8_t* const* data, const int64_t* size
         off += p[(size_t)i] * H[i];
     }
     int rounds = 0;
+    t_async_ready = t_async_done = nullptr;
     if ((rc = jpeg_decode_to_device(ws, data, sizes, n, d.data(), p.data(), true, cs, &rounds, kAsyncRounds,
                                     &st->flags)))
         return rc;
+    for (hipEvent_t* e : {&t_async_ready, &t_async_done})  // the decode's timing events: not reported here
+        if (*e) {
+            (void)hipEventDestroy(*e);
+            *e = nullptr;
+        }
     SyncOnExit sync_on_exit{cs};  // the decode's pinned staging is in use until the stream is done
     uint8_t* dres = (uint8_t*)ws->out.ptr;
     uint8_t* dico = dres + n * out_bytes;

@@ -219,11 +219,11 @@ int parse_bmp(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
     } else {
         info->fmt = bpp == 24 ? RF_BGR : RF_BGRX;
     }
+    if (info->W > kMaxDim || info->H > kMaxDim) return bad(err, -2, "BMP: image larger than 65535 pixels");
     info->stride = (info->W * bpp + 31) / 32 * 4;
     info->data_off = off;
     if ((uint64_t)off > n || (uint64_t)(n - off) < (uint64_t)info->stride * (uint64_t)info->H)
         return bad(err, -1, "BMP: truncated pixel data");
-    if (info->W > kMaxDim || info->H > kMaxDim) return bad(err, -2, "BMP: image larger than 65535 pixels");
     return 0;
 }
 
