@@ -265,3 +265,19 @@ def test_all_slots_unreadable_needs_no_device(tmp_path, capsys):
     assert all(f"Error loading image {p}" in out for p in paths)
     with pytest.raises(ValueError):
         WJ.decode_batch(bad)
+
+
+def test_load_image_prints_the_reference_message(tmp_path, capsys, monkeypatch):
+    """An unreadable file: load_image prints what the reference prints for any
+    file cv2.imread cannot read (validate_image's message for None,
+    validation.py:94-95) and returns None; WICCA_LOAD_DETAIL=1 prints the
+    decoder's reason instead.  No device is needed (the file fails to parse)."""
+    import wicca_amd
+    p = tmp_path / "notes.txt"
+    p.write_bytes(b"not an image at all")
+    assert wicca_amd.load_image(str(p)) is None
+    assert capsys.readouterr().out.strip() == \
+        f"Error loading image {p}: Image didn't found. Please check your input."
+    monkeypatch.setenv("WICCA_LOAD_DETAIL", "1")
+    assert wicca_amd.load_image(str(p)) is None
+    assert "unrecognised image format" in capsys.readouterr().out

@@ -13,7 +13,11 @@ points sniff each file (``wicca_image_*``), so a batch may mix formats.
 
 :func:`load_image` keeps the reference's contract: empty path ->
 ``ValueError("File path cannot be empty")``; any failure -> prints
-``Error loading image {path}: {err}`` and returns ``None``.  Files no GPU
+``Error loading image {path}: Image didn't found. Please check your input.``
+(``cv2.imread`` returns None for every file it cannot read and
+``validate_image`` then raises that message, validation.py:94-95) and
+returns ``None``; ``WICCA_LOAD_DETAIL=1`` prints the decoder's own reason
+instead.  Files no GPU
 decoder handles (TIFF, GIF, RLE BMP, ...) fail that way too — there is no
 CPU decoder behind it.
 """
@@ -58,6 +62,15 @@ def image_info(data: bytes, apply_orientation: bool = True) -> tuple[int, int, s
     _lib.check(_lib.load().wicca_image_info(arr.ctypes.data, arr.size, int(apply_orientation),
                                             ctypes.byref(h), ctypes.byref(w), ctypes.byref(k)))
     return h.value, w.value, KINDS[k.value]
+
+
+# what the reference prints for any file cv2.imread cannot read (validation.py:94-95)
+_UNREADABLE = "Image didn't found. Please check your input."
+
+
+def _load_error(detail: str) -> str:
+    import os
+    return detail if os.environ.get("WICCA_LOAD_DETAIL") == "1" else _UNREADABLE
 
 
 def _slot_error(data: bytes) -> str:
@@ -167,12 +180,16 @@ def load_image(file_path: str) -> np.ndarray | None:
     """``wicca.data_loader.load_image`` (data_loader.py:31-63) with the decode on the GPU."""
     if not file_path:
         raise ValueError("File path cannot be empty")
+    _lib.load()  # a missing or unloadable library raises here, never as a per-file None
     try:
         with open(file_path, "rb") as f:
             data = f.read()
         return decode(data)
-    except Exception as e:  # the reference prints and returns None (data_loader.py:61-63)
-        print(f"Error loading image {file_path}: {str(e)}")
+    except (OSError, ValueError, NotImplementedError) as e:
+        # an unreadable / corrupt / unsupported file: the reference prints and
+        # returns None (data_loader.py:61-63); a missing library, a HIP error
+        # or an exhausted device still raise (they are not file problems)
+        print(f"Error loading image {file_path}: {_load_error(str(e))}")
         return None
 
 
@@ -223,7 +240,7 @@ def get_img_batch(file_paths: Sequence[str], shape, transform_depth: int, interp
     if status is not None:
         for i in range(n):
             if status[i] != 0:  # as load_image reports it (data_loader.py:61-63)
-                print(f"Error loading image {file_paths[i]}: {_slot_error(blobs[i])}")
+                print(f"Error loading image {file_paths[i]}: {_load_error(_slot_error(blobs[i]))}")
     return resized, icons
 
 
