@@ -377,7 +377,26 @@ int zlib_inflate(const uint8_t* in, size_t n, uint8_t* out, int64_t cap, Inflate
                     dst += 8;
                 } while (dst < stop);
                 op = stop;
-            } else {
+            } else if (oend - op >= (int64_t)len + 8) {  // d < 8: a periodic run (PNG's runs of equal bytes)
+                uint8_t* dst = op;
+                uint8_t* const stop = op + len;
+                if (d == 1) {
+                    memset(dst, src[0], len);
+                } else {
+                    // the run repeats with period d, so also with period `step` (a multiple of d >= 8):
+                    // its first `step` bytes byte by byte, then 8-byte chunks from `step` back
+                    uint32_t step = d;
+                    while (step < 8) step += d;
+                    const uint32_t head = std::min(step, len);
+                    for (uint32_t i = 0; i < head; ++i) dst[i] = src[i];
+                    for (dst += head; dst < stop; dst += 8) {
+                        uint64_t w;
+                        memcpy(&w, dst - step, 8);
+                        memcpy(dst, &w, 8);
+                    }
+                }
+                op = stop;
+            } else {  // the last bytes of the output
                 const uint32_t m = (uint32_t)std::min<int64_t>(len, oend - op);
                 for (uint32_t i = 0; i < m; ++i) op[i] = src[i];
                 op += m;
