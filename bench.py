@@ -729,6 +729,26 @@ def run_raster(args, torch, rank):
     for _ in range(steps):
         stage()
     stage_s = (time.perf_counter() - t0) / steps
+    # a loader loop: wicca_image_icon_stage_async with one batch in flight ahead
+    # (a PNG / BMP batch's stage runs on a host thread of its own)
+    outs = [(res, ico), (np.empty_like(res), np.empty_like(ico))]
+
+    def issue_stage(k):
+        t = ctypes.c_int64(0)
+        r, c = outs[k % 2]
+        _lib.check(lib.wicca_image_icon_stage_async(ptrs, sizes, B, D, 1, 0, shape[0], shape[1], args.interpolation,
+                                                    r.ctypes.data, c.ctypes.data, -1, ctypes.byref(t)))
+        return t.value
+
+    pipe_steps = max(2, steps)
+    t0 = time.perf_counter()
+    prev = issue_stage(0)
+    for k in range(1, pipe_steps):
+        cur = issue_stage(k)
+        _lib.check(lib.wicca_image_stage_wait(prev))
+        prev = cur
+    _lib.check(lib.wicca_image_stage_wait(prev))
+    stage_pipe_s = (time.perf_counter() - t0) / pipe_steps
     mpix = B * H * W / 1e6
 
     def pil(b):
@@ -760,6 +780,10 @@ def run_raster(args, torch, rank):
         "file_stage": {"ms_per_batch": round(stage_s * 1e3, 3), "MP_per_s": round(mpix / stage_s, 1),
                        "what": f"decode + cv2.resize to {shape} + icon depth {D} + icon resize, "
                                "outputs to host (classifying_tools.py:312-323)"},
+        "file_stage_pipelined": {"ms_per_batch": round(stage_pipe_s * 1e3, 3),
+                                 "MP_per_s": round(mpix / stage_pipe_s, 1),
+                                 "what": "the same stage through wicca_image_icon_stage_async, one batch in "
+                                         "flight ahead (the next batch's host inflate overlaps)"},
         "cpu_baseline": {"value": round(pool, 1), "unit": "MP/s", "cores": threads, "kind": "port",
                          "sample": f"Pillow {PIL.__version__} decode + convert('RGB') of the same files, "
                                    f"ThreadPoolExecutor({threads}), {B} files",

@@ -382,9 +382,11 @@ int wicca_image_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* 
  * call returns once the host's part is queued (*ticket set); resized /
  * resized_icons (and data[i]) must stay valid until wicca_image_stage_wait
  * (*ticket) returns 0, which fills them.  Batches of JPEG files within one
- * device pass with the fused stage run asynchronously; any other batch (PNG,
- * BMP, TIFF, larger, depth > 8) completes before the call returns
- * (*ticket = 0).  No per-file status: a file that fails fails the call. */
+ * device pass with the fused stage are queued on the device; any other batch
+ * (PNG, BMP, TIFF, larger, depth > 8) runs the synchronous stage on a host
+ * thread of its own, so its host work (inflate, ...) overlaps the caller's
+ * next batch.  Errors found while issuing are returned here, later ones by
+ * the wait.  No per-file status: a file that fails fails the batch. */
 int wicca_image_icon_stage_async(const uint8_t* const* data, const int64_t* sizes, int64_t n,
                                  int depth, int border_type, int border_constant,
                                  int64_t out_w, int64_t out_h, int interpolation,

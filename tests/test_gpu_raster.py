@@ -287,3 +287,23 @@ def test_tiff_unsupported_and_corrupt():
     outs = WJ.decode_batch([good, cut, good[:7]], errors="none")
     assert np.array_equal(outs[0], img) and outs[1] is None and outs[2] is None
     assert s.size > 200
+
+
+def test_pipelined_stage_with_png_batches(tmp_path):
+    """get_img_batches over PNG / BMP / mixed batches (their stage runs on a
+    host thread of its own): the same outputs as get_img_batch, batch by
+    batch; a corrupt PNG (found during the inflate) fails at its wait."""
+    paths, refs = _mixed_files(tmp_path)
+    batches = [paths[:3], paths[3:], [paths[1], paths[3]], paths]
+    for depth in (1, 2):
+        got = list(wicca_amd.get_img_batches(batches, (224, 224), 3, depth=depth))
+        for b, (imgs, icons) in zip(batches, got):
+            want = wicca_amd.get_img_batch(b, (224, 224), 3)
+            assert np.array_equal(imgs, want[0]) and np.array_equal(icons, want[1])
+    s, _ = png_samples(2, 8, 40, 60, seed=1)
+    good = rr.encode_png(s, 2, 8)
+    k = good.index(b"IDAT")
+    bad = tmp_path / "bad.png"
+    bad.write_bytes(good[:k + 10] + bytes([good[k + 10] ^ 0xFF]) + good[k + 11:])  # IDAT CRC error
+    with pytest.raises(ValueError):
+        list(wicca_amd.get_img_batches([paths[:2], [str(bad)], paths[2:4]], (224, 224), 3))

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -627,6 +628,15 @@ struct AsyncStage {
     int64_t out_w = 0, out_h = 0;
     uint8_t* resized = nullptr;
     uint8_t* icons = nullptr;
+    // other batches (PNG / BMP / TIFF files, depth > 8, ...): the synchronous
+    // stage on a host thread of its own; the wait joins it
+    std::thread worker;
+    int worker_rc = WICCA_OK;
+    std::string worker_err;
+    ~AsyncStage()
+    {
+        if (worker.joinable()) worker.join();  // a ticket dropped without its wait (process exit)
+    }
 };
 std::mutex g_stage_mu;
 std::unordered_map<int64_t, std::unique_ptr<AsyncStage>> g_stage;
@@ -1096,9 +1106,35 @@ int wicca_image_icon_stage_async(const uint8_t* const* data, const int64_t* size
         async_ok = kind == 1 && wicca::stage_row_ok(W[i], 3);
         rgb_total += round_up(W[i] * 3, kStagePitch) * H[i];
     }
-    if (!async_ok)
-        return icon_stage_impl(data, sizes, n, depth, border_type, border_constant, out_w, out_h, interpolation,
-                               resized, resized_icons, device, nullptr, true);
+    if (!async_ok) {
+        // the whole synchronous stage on a thread of its own: its host work
+        // (PNG inflate, ...) overlaps the caller's next batch
+        DeviceGuard dg0;
+        int dev0, rc0;
+        if ((rc0 = select_device(device, &dev0, dg0))) return rc0;  // "current device" is the caller's
+        std::unique_ptr<AsyncStage> st(new AsyncStage);
+        AsyncStage* a = st.get();
+        a->device = dev0;
+        a->data.assign(data, data + n);
+        a->sizes.assign(sizes, sizes + n);
+        a->worker = std::thread([a, n, depth, border_type, border_constant, out_w, out_h, interpolation, resized,
+                                 resized_icons] {
+            try {  // no exception may leave the thread
+                a->worker_rc = icon_stage_impl(a->data.data(), a->sizes.data(), n, depth, border_type,
+                                               border_constant, out_w, out_h, interpolation, resized, resized_icons,
+                                               a->device, nullptr, true);
+                if (a->worker_rc) a->worker_err = t_last_error;
+            } catch (const std::exception& e) {
+                a->worker_rc = WICCA_ERR_NOMEM;
+                a->worker_err = e.what();
+            }
+        });
+        std::lock_guard<std::mutex> g(g_stage_mu);
+        const int64_t id = g_stage_next++;
+        g_stage[id] = std::move(st);
+        *ticket = id;
+        return WICCA_OK;
+    }
     DeviceGuard dg;
     int dev, rc;
     if ((rc = select_device(device, &dev, dg))) return rc;
@@ -1166,6 +1202,11 @@ int wicca_image_stage_wait(int64_t ticket)
         if (it == g_stage.end()) return fail(WICCA_ERR_ARG, "unknown stage ticket %lld", (long long)ticket);
         st = std::move(it->second);
         g_stage.erase(it);
+    }
+    if (st->worker.joinable()) {  // a synchronous stage on its own thread
+        st->worker.join();
+        if (st->worker_rc) return fail(st->worker_rc, "%s", st->worker_err.c_str());
+        return WICCA_OK;
     }
     DeviceGuard dg;
     int dev, rc;
