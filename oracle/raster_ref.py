@@ -30,7 +30,13 @@ OpenCV's code as described above.
   compressed strips) for gray / WhiteIsZero / RGB / palette / bilevel files,
   none / LZW / Deflate / PackBits, predictor 2, strips and tiles, both byte
   orders; RGBA with unassociated alpha follows libtiff's premultiplication
-  (``decode_tiff``, parity unpinned).  Only ``tests/`` uses this module.
+  (``decode_tiff``, parity unpinned).
+* GIF (OpenCV ``GifDecoder``, first frame): a full-screen image without
+  transparency is checked against Pillow's decode; transparent and
+  uncovered pixels are black in the restatement (``gif_expected``: OpenCV
+  draws onto a zeroed BGRA canvas and drops alpha; Pillow fills with the
+  palette / background colour instead), parity unpinned.  Only ``tests/``
+  uses this module.
 """
 from __future__ import annotations
 
@@ -466,6 +472,109 @@ def decode_tiff(data: bytes) -> np.ndarray:
         a = np.asarray(im).astype(np.uint32)
         return ((a[..., :3] * a[..., 3:4] + 127) // 255).astype(np.uint8)
     return np.asarray(im.convert("RGB")).copy()
+
+
+# ----------------------------------------------------------------------------- GIF
+def _gif_lzw_encode(idx: np.ndarray, min_size: int) -> bytes:
+    """GIF LZW (LSB-first codes, a clear code first, width growing at 2^width)."""
+    clear, eoi = 1 << min_size, (1 << min_size) + 1
+    out, acc, nb = bytearray(), 0, 0
+    width = min_size + 1
+
+    def put(code):
+        nonlocal acc, nb
+        acc |= code << nb
+        nb += width
+        while nb >= 8:
+            out.append(acc & 255)
+            acc >>= 8
+            nb -= 8
+
+    table = {(i,): i for i in range(clear)}
+    nxt = eoi + 1
+    put(clear)
+    w = ()
+    for k in idx.reshape(-1).tolist():
+        wk = w + (k,)
+        if wk in table:
+            w = wk
+            continue
+        put(table[w])
+        if nxt < 4096:
+            table[wk] = nxt
+            nxt += 1
+            if nxt > (1 << width) and width < 12:
+                width += 1
+        else:  # table full: start over
+            put(clear)
+            table = {(i,): i for i in range(clear)}
+            nxt = eoi + 1
+            width = min_size + 1
+        w = (k,)
+    if w:
+        put(table[w])
+    put(eoi)
+    if nb:
+        out.append(acc & 255)
+    return bytes(out)
+
+
+def encode_gif(idx: np.ndarray, palette: np.ndarray, screen=None, pos=(0, 0), transparent=None,
+               interlace: bool = False, local_palette: bool = False) -> bytes:
+    """A one-image GIF89a: (h, w) indices into `palette` ((2^k, 3) RGB), drawn
+    at pos (x, y) on a screen (W, H) (default: the image's size)."""
+    idx = np.asarray(idx, np.uint8)
+    h, w = idx.shape
+    W, H = screen or (w, h)
+    pal = np.asarray(palette, np.uint8)
+    k = max(1, int(np.ceil(np.log2(len(pal)))))
+    table = np.zeros((1 << k, 3), np.uint8)
+    table[:len(pal)] = pal
+    min_size = max(2, k)
+    rows = idx
+    if interlace:
+        order = list(range(0, h, 8)) + list(range(4, h, 8)) + list(range(2, h, 4)) + list(range(1, h, 2))
+        rows = idx[order]
+    out = bytearray(b"GIF89a" + struct.pack("<HH", W, H))
+    if local_palette:
+        out += bytes([0x00, 0, 0])
+    else:
+        out += bytes([0x80 | (k - 1), 0, 0]) + table.tobytes()
+    if transparent is not None:
+        out += bytes([0x21, 0xF9, 4, 1, 0, 0, transparent, 0])
+    out += b"\x2c" + struct.pack("<HHHH", pos[0], pos[1], w, h)
+    out += bytes([(0x80 | (k - 1) if local_palette else 0) | (0x40 if interlace else 0)])
+    if local_palette:
+        out += table.tobytes()
+    data = _gif_lzw_encode(rows, min_size)
+    out += bytes([min_size])
+    for i in range(0, len(data), 255):
+        blk = data[i:i + 255]
+        out += bytes([len(blk)]) + blk
+    out += b"\x00\x3b"
+    return bytes(out)
+
+
+def gif_expected(idx: np.ndarray, palette: np.ndarray, screen=None, pos=(0, 0), transparent=None) -> np.ndarray:
+    """cv2.imread's first frame as restated (parity unpinned for transparency
+    and partial frames): a black canvas, the image's palette colours drawn at
+    pos, transparent pixels left black."""
+    idx = np.asarray(idx, np.uint8)
+    h, w = idx.shape
+    W, H = screen or (w, h)
+    pal = np.zeros((256, 3), np.uint8)
+    pal[:len(palette)] = palette
+    canvas = np.zeros((H, W, 3), np.uint8)
+    x0, y0 = pos
+    sub = idx[: max(0, min(h, H - y0)), : max(0, min(w, W - x0))]
+    rgb = pal[sub]
+    if transparent is not None:
+        keep = sub != transparent
+        region = canvas[y0:y0 + sub.shape[0], x0:x0 + sub.shape[1]]
+        region[keep] = rgb[keep]
+    else:
+        canvas[y0:y0 + sub.shape[0], x0:x0 + sub.shape[1]] = rgb
+    return canvas
 
 
 def decode_rgb(data: bytes) -> np.ndarray:

@@ -64,12 +64,21 @@ def main():
     files["white1.tif"] = rr.encode_tiff(idx & 1, 0, 1, 1)
     rgba = rng.integers(0, 256, (9, 11, 4), dtype=np.uint8)
     files["rgba_unassoc.tif"] = rr.encode_tiff(rgba, 2, 8, 8, extra_samples=2)
+    gidx = rng.integers(0, 16, (13, 17), dtype=np.uint8)
+    gpal = rng.integers(0, 256, (16, 3), dtype=np.uint8)
+    files["full.gif"] = rr.encode_gif(gidx, gpal)
+    files["partial_transparent_interlaced.gif"] = rr.encode_gif(gidx, gpal, screen=(25, 20), pos=(3, 4),
+                                                                transparent=5, interlace=True)
     cases = []
     for name, data in sorted(files.items()):
         with open(os.path.join(OUT, name), "wb") as f:
             f.write(data)
-        unpinned = name in ("gray16.png", "bgr565.bmp", "rgba_unassoc.tif")
-        rgb = rr.decode_rgb(data)
+        unpinned = name in ("gray16.png", "bgr565.bmp", "rgba_unassoc.tif", "partial_transparent_interlaced.gif")
+        if name.endswith(".gif"):
+            rgb = (rr.gif_expected(gidx, gpal) if name == "full.gif" else
+                   rr.gif_expected(gidx, gpal, screen=(25, 20), pos=(3, 4), transparent=5))
+        else:
+            rgb = rr.decode_rgb(data)
         if not unpinned:
             assert np.array_equal(rgb, rr.pillow_rgb(data)), name
         cases.append({"file": name, "height": int(rgb.shape[0]), "width": int(rgb.shape[1]),

@@ -307,3 +307,46 @@ def test_pipelined_stage_with_png_batches(tmp_path):
     bad.write_bytes(good[:k + 10] + bytes([good[k + 10] ^ 0xFF]) + good[k + 11:])  # IDAT CRC error
     with pytest.raises(ValueError):
         list(wicca_amd.get_img_batches([paths[:2], [str(bad)], paths[2:4]], (224, 224), 3))
+
+
+@pytest.mark.parametrize("interlace", [False, True])
+@pytest.mark.parametrize("local", [False, True])
+def test_gif_vs_expected(interlace, local):
+    """GIF first frame: full-screen images against Pillow; partial frames and
+    transparency against the restatement (black canvas, parity unpinned)."""
+    rng = np.random.default_rng(int(interlace) * 2 + int(local))
+    blobs, wants = [], []
+    for (h, w, npal, screen, pos, tr) in [(1, 1, 2, None, (0, 0), None), (7, 5, 4, None, (0, 0), None),
+                                          (40, 60, 256, None, (0, 0), None), (33, 17, 16, (50, 40), (9, 11), None),
+                                          (20, 30, 8, None, (0, 0), 3), (25, 25, 32, (30, 26), (5, 1), 0),
+                                          (300, 401, 256, None, (0, 0), None)]:
+        idx = rng.integers(0, npal, (h, w), dtype=np.uint8)
+        idx[: h // 2] = (np.arange(w) % npal)[None, :]
+        pal = rng.integers(0, 256, (npal, 3), dtype=np.uint8)
+        data = rr.encode_gif(idx, pal, screen=screen, pos=pos, transparent=tr, interlace=interlace,
+                             local_palette=local)
+        blobs.append(data)
+        want = rr.gif_expected(idx, pal, screen=screen, pos=pos, transparent=tr)
+        if screen is None and tr is None:
+            assert np.array_equal(want, rr.pillow_rgb(data))
+        wants.append(want)
+    for o, want in zip(WJ.decode_batch(blobs), wants):
+        assert np.array_equal(o, want)
+
+
+def test_pillow_written_gif_and_mixed_stage(tmp_path):
+    from PIL import Image
+    img = J.test_image("scene", 1080, 1920, 21)
+    b = io.BytesIO()
+    Image.fromarray(img).convert("P").save(b, "GIF")
+    data = b.getvalue()
+    assert np.array_equal(WJ.decode(data), rr.pillow_rgb(data))
+    p = tmp_path / "x.gif"
+    p.write_bytes(data)
+    paths, refs = _mixed_files(tmp_path)
+    paths.append(str(p))
+    refs.append(rr.pillow_rgb(data))
+    imgs, icons = wicca_amd.get_img_batch(paths, (224, 224), 4)
+    for i, rgb in enumerate(refs):
+        assert np.array_equal(imgs[i], R.resize(rgb, (224, 224), R.INTER_AREA)), i
+        assert np.array_equal(icons[i], R.resize(c_oracle.ll_int_block(rgb, 4)[0], (224, 224), R.INTER_AREA)), i

@@ -1,4 +1,4 @@
-"""CPU: the PNG / BMP / TIFF host half of the any-format decode (raster_host.cpp
+"""CPU: the PNG / BMP / TIFF / GIF host half of the any-format decode (raster_host.cpp
 through wicca_image_info, no device): format sniffing, header validation
 with libpng / OpenCV BmpDecoder error behaviour, the committed golden files'
 sizes, and the ASan + UBSan mutation fuzz (tests/native/raster_fuzz.cpp)."""
@@ -22,7 +22,8 @@ def test_golden_info(case):
     data = open(os.path.join(GOLD, case["file"]), "rb").read()
     h, w, kind = WJ.image_info(data)
     assert (h, w) == (case["height"], case["width"])
-    assert kind == {"tif": "tiff"}.get(case["file"].rsplit(".", 1)[1], case["file"].rsplit(".", 1)[1])
+    ext = case["file"].rsplit(".", 1)[1]
+    assert kind == {"tif": "tiff"}.get(ext, ext)
 
 
 def _ihdr_png(w=4, h=3, bits=8, ct=2, il=0, crc_ok=True, idat=True, iend=True):
@@ -80,8 +81,17 @@ def test_tiff_header_errors():
             WJ.image_info(unsup)
 
 
+def test_gif_header_errors():
+    idx = np.zeros((4, 6), np.uint8)
+    good = rr.encode_gif(idx, np.array([[0, 0, 0], [255, 255, 255]], np.uint8), screen=(10, 8), pos=(2, 1))
+    assert WJ.image_info(good) == (8, 10, "gif")
+    for bad in (good[:12], b"GIF89a" + b"\0" * 20, good[:13] + b"\x3b", good[:6] + b"\0\0" + good[8:]):
+        with pytest.raises(ValueError):
+            WJ.image_info(bad)
+
+
 def test_unrecognised_formats():
-    for data in (b"GIF89a" + b"\0" * 20, b"", b"B"):
+    for data in (b"GIF90a" + b"\0" * 20, b"", b"B", b"\x00\x00\x01\x00"):
         with pytest.raises(ValueError):
             WJ.image_info(data)
 

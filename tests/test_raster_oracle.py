@@ -173,3 +173,14 @@ def test_tiff_unassociated_alpha_premultiplied():
     px = np.array([[[200, 100, 50, 128], [255, 255, 255, 0], [10, 20, 30, 255]]], np.uint8)
     got = rr.decode_tiff(rr.encode_tiff(px, 2, extra_samples=2))
     np.testing.assert_array_equal(got[0], [[100, 50, 25], [0, 0, 0], [10, 20, 30]])
+
+
+# ----------------------------------------------------------------------------- GIF
+@pytest.mark.parametrize("interlace", [False, True])
+@pytest.mark.parametrize("h,w,npal", [(1, 1, 2), (7, 5, 4), (20, 30, 256), (64, 100, 16)])
+def test_gif_writer_and_expected_vs_pillow(h, w, npal, interlace):
+    rng = np.random.default_rng(h * w + npal)
+    idx = rng.integers(0, npal, (h, w), dtype=np.uint8)
+    pal = rng.integers(0, 256, (npal, 3), dtype=np.uint8)
+    data = rr.encode_gif(idx, pal, interlace=interlace)
+    np.testing.assert_array_equal(rr.gif_expected(idx, pal), rr.pillow_rgb(data))

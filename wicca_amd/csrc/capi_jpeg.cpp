@@ -63,7 +63,7 @@ void oriented_dims(const wicca::JpegInfo& in, bool apply, int64_t* h, int64_t* w
 
 // A file's decoded size.  any: JPEG, PNG, BMP or TIFF (the wicca_image_*
 // entries, cv2.imread's formats on the reference's path); otherwise JPEG
-// only.  kind: 1 JPEG, 2 PNG, 3 BMP, 4 TIFF.
+// only.  kind: 1 JPEG, 2 PNG, 3 BMP, 4 TIFF, 5 GIF.
 int probe_file(const uint8_t* data, int64_t size, int64_t i, bool any, bool orient, int64_t* H, int64_t* W,
                int* kind = nullptr)
 {
@@ -77,11 +77,11 @@ int probe_file(const uint8_t* data, int64_t size, int64_t i, bool any, bool orie
             if (rc) return fail(WICCA_ERR_DECODE, "image %lld: %s", (long long)i, err.c_str());
             *H = r.H;
             *W = r.W;
-            if (kind) *kind = rk == wicca::RK_PNG ? 2 : rk == wicca::RK_BMP ? 3 : 4;
+            if (kind) *kind = rk == wicca::RK_PNG ? 2 : rk == wicca::RK_BMP ? 3 : rk == wicca::RK_TIFF ? 4 : 5;
             return WICCA_OK;
         }
         if (size < 2 || data[0] != 0xFF || data[1] != 0xD8)
-            return fail(WICCA_ERR_DECODE, "image %lld: unrecognised image format (JPEG, PNG, BMP and TIFF are decoded)",
+            return fail(WICCA_ERR_DECODE, "image %lld: unrecognised image format (JPEG, PNG, BMP, TIFF and GIF are decoded)",
                         (long long)i);
     }
     wicca::JpegInfo f;

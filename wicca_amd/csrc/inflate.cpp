@@ -413,7 +413,8 @@ int zlib_inflate(const uint8_t* in, size_t n, uint8_t* out, int64_t cap, Inflate
         }
     }
 done:
-    if (op < oend) return fail("PNG: not enough image data");
+    // the last symbols must not have come from the zero bits fed past the end
+    if (op < oend || b.overrun()) return fail("PNG: not enough image data");
     if (progress && !progress->advance(cap)) return fail(progress->error());
     return 0;
 }

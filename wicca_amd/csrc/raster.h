@@ -35,7 +35,7 @@
 
 namespace wicca {
 
-enum RasterKind { RK_NONE = 0, RK_PNG = 1, RK_BMP = 2, RK_TIFF = 3 };
+enum RasterKind { RK_NONE = 0, RK_PNG = 1, RK_BMP = 2, RK_TIFF = 3, RK_GIF = 4 };
 
 // RasterImageDev::flags
 constexpr int kRasterInvert = 1;   // TIFF WhiteIsZero gray: 255 - v
@@ -82,6 +82,13 @@ struct RasterInfo {
     int64_t rows_per_strip = 0;
     int64_t tile_w = 0, tile_h = 0;  // 0: strips
     std::vector<std::pair<uint64_t, uint64_t>> segs;
+    // GIF: the first image's descriptor (position, size, interlace), its LZW
+    // data (first sub-block byte offset), minimum code size, transparency
+    int64_t fx = 0, fy = 0, fw = 0, fh = 0;
+    bool finterlaced = false;
+    size_t lzw_off = 0;
+    int lzw_min = 0;
+    int transparent = -1;
 };
 
 // Adam7 pass p: first row/column and steps (PNG spec 8.2).

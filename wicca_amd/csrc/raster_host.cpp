@@ -28,6 +28,13 @@
 // / Deflate / PackBits, horizontal predictor.  16-bit samples, planar
 // configuration 2, JPEG / CCITT compression, CMYK / YCbCr / Lab and
 // orientations other than top-left are reported unsupported.
+// GIF (87a / 89a; cv2.imread reads the first frame): the first image's LZW
+// codes (LSB-first, code width growing when the next code reaches 2^width,
+// 12-bit table without a forced clear) decoded into palette colours (local
+// table, else global), Adam-free 4-pass interlace undone, drawn at its
+// position on a logical-screen canvas that starts black; transparent and
+// uncovered pixels stay black (OpenCV composes onto a zeroed BGRA canvas and
+// drops alpha).  The host writes RGB rows; the device copies them out.
 #include <string.h>
 #include <zlib.h>
 
@@ -556,6 +563,197 @@ int unpack_tiff(const uint8_t* data, const RasterInfo& f, const RasterLayout& la
     return 0;
 }
 
+// ----------------------------------------------------------------------------- GIF
+int parse_gif(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
+{
+    info->kind = RK_GIF;
+    if (n < 13) return bad(err, -1, "GIF: truncated header");
+    if (memcmp(d, "GIF87a", 6) != 0 && memcmp(d, "GIF89a", 6) != 0) return bad(err, -1, "GIF: bad signature");
+    const int64_t W = le16(d + 6), H = le16(d + 8);
+    const int flags = d[10];
+    if (W == 0 || H == 0) return bad(err, -1, "GIF: invalid screen size");
+    size_t pos = 13;
+    memset(info->pal, 0, sizeof(info->pal));
+    if (flags & 0x80) {  // global colour table
+        const int cnt = 2 << (flags & 7);
+        if (pos + 3 * (size_t)cnt > n) return bad(err, -1, "GIF: truncated colour table");
+        for (int k = 0; k < cnt; ++k)
+            for (int c = 0; c < 3; ++c) info->pal[k][c] = d[pos + 3 * k + c];
+        info->npal = cnt;
+        pos += 3 * (size_t)cnt;
+    }
+    int transparent = -1;
+    for (;;) {
+        if (pos >= n) return bad(err, -1, "GIF: no image");
+        const uint8_t b = d[pos++];
+        if (b == 0x3B) return bad(err, -1, "GIF: no image");
+        if (b == 0x21) {  // extension: label, then sub-blocks
+            if (pos >= n) return bad(err, -1, "GIF: truncated extension");
+            const uint8_t label = d[pos++];
+            bool first = true;
+            for (;;) {
+                if (pos >= n) return bad(err, -1, "GIF: truncated extension");
+                const size_t len = d[pos++];
+                if (len == 0) break;
+                if (pos + len > n) return bad(err, -1, "GIF: truncated extension");
+                if (label == 0xF9 && first && len >= 4) transparent = (d[pos] & 1) ? d[pos + 3] : -1;
+                first = false;
+                pos += len;
+            }
+            continue;
+        }
+        if (b != 0x2C) return bad(err, -1, "GIF: unknown block");
+        if (pos + 9 > n) return bad(err, -1, "GIF: truncated image descriptor");
+        info->fx = le16(d + pos);
+        info->fy = le16(d + pos + 2);
+        info->fw = le16(d + pos + 4);
+        info->fh = le16(d + pos + 6);
+        const int lf = d[pos + 8];
+        pos += 9;
+        info->finterlaced = (lf & 0x40) != 0;
+        if (lf & 0x80) {  // local colour table replaces the global one for this image
+            const int cnt = 2 << (lf & 7);
+            if (pos + 3 * (size_t)cnt > n) return bad(err, -1, "GIF: truncated colour table");
+            memset(info->pal, 0, sizeof(info->pal));
+            for (int k = 0; k < cnt; ++k)
+                for (int c = 0; c < 3; ++c) info->pal[k][c] = d[pos + 3 * k + c];
+            info->npal = cnt;
+            pos += 3 * (size_t)cnt;
+        }
+        if (pos >= n) return bad(err, -1, "GIF: truncated image data");
+        info->lzw_min = d[pos++];
+        if (info->lzw_min < 2 || info->lzw_min > 8) return bad(err, -1, "GIF: invalid LZW code size");
+        info->lzw_off = pos;
+        break;
+    }
+    info->transparent = transparent;
+    info->W = W;
+    info->H = H;
+    info->fmt = RF_RGB;
+    info->bits = 8;
+    return 0;
+}
+
+// The first image's indices (fw x fh, in stream row order), LZW-decoded from
+// the sub-blocks at lzw_off.  A stream that ends early leaves the rest 0
+// (-1 only when not even one code is present).
+int gif_lzw(const uint8_t* d, size_t n, const RasterInfo& f, std::vector<uint8_t>& idx, std::string* err)
+{
+    const size_t need = (size_t)(f.fw * f.fh);
+    idx.assign(need, 0);
+    std::vector<uint16_t> prefix(4096);
+    std::vector<uint8_t> suffix(4096), first(4096);
+    std::vector<uint16_t> length(4096);
+    std::vector<uint8_t> stack(4097);
+    const int clear = 1 << f.lzw_min, eoi = clear + 1;
+    for (int c = 0; c < clear; ++c) {
+        suffix[c] = first[c] = (uint8_t)c;
+        length[c] = 1;
+    }
+    int width = f.lzw_min + 1, next = clear + 2, old = -1;
+    uint32_t acc = 0;
+    int have = 0;
+    size_t pos = f.lzw_off, block_left = 0, op = 0;
+    bool codes = false;
+    while (op < need) {
+        while (have < width) {  // next byte of the sub-block chain
+            if (block_left == 0) {
+                if (pos >= n) goto out;
+                block_left = d[pos++];
+                if (block_left == 0) goto out;  // terminator
+            }
+            if (pos >= n) goto out;
+            acc |= (uint32_t)d[pos++] << have;
+            have += 8;
+            --block_left;
+        }
+        {
+            const int code = (int)(acc & ((1u << width) - 1));
+            acc >>= width;
+            have -= width;
+            codes = true;
+            if (code == clear) {
+                width = f.lzw_min + 1;
+                next = clear + 2;
+                old = -1;
+                continue;
+            }
+            if (code == eoi) break;
+            int cur = code;
+            uint8_t fb;
+            if (old < 0) {
+                if (code >= clear) return bad(err, -1, "GIF: corrupt LZW data");
+                idx[op++] = (uint8_t)code;
+                old = code;
+                continue;
+            }
+            if (code < next && code != clear && code != eoi && (code < clear || code >= clear + 2)) {
+                fb = first[code];
+            } else if (code == next) {
+                fb = first[old];
+                cur = old;
+            } else {
+                return bad(err, -1, "GIF: corrupt LZW data");
+            }
+            // string(cur) (+ fb when code == next), clipped at the image's end
+            int sp = 0;
+            for (int c = cur;; c = prefix[c]) {
+                stack[sp++] = suffix[c];
+                if (length[c] == 1) break;
+            }
+            while (sp && op < need) idx[op++] = stack[--sp];
+            if (code == next && op < need) idx[op++] = fb;
+            if (next < 4096) {
+                prefix[next] = (uint16_t)old;
+                suffix[next] = fb;
+                first[next] = first[old];
+                length[next] = (uint16_t)(length[old] + 1);
+                ++next;
+                if (next == (1 << width) && width < 12) ++width;
+            }
+            old = code;
+        }
+    }
+out:
+    if (!codes) return bad(err, -1, "GIF: no image data");
+    return 0;
+}
+
+int unpack_gif(const uint8_t* data, size_t size, const RasterInfo& f, const RasterLayout& lay, uint8_t* out,
+               std::string* err)
+{
+    std::vector<uint8_t> idx;
+    if (gif_lzw(data, size, f, idx, err)) return -1;
+    memset(out, 0, (size_t)lay.bytes);  // the canvas starts black
+    const int64_t pitch = lay.pass_pitch[0];
+    // stream row r -> image row (the 4 interlace passes: every 8th from 0, from 4, every 4th from 2, odd rows)
+    int64_t r = 0;
+    auto place = [&](int64_t y) {
+        const int64_t cy = f.fy + y;
+        if (cy < f.H) {
+            uint8_t* row = out + cy * pitch;
+            const uint8_t* src = idx.data() + r * f.fw;
+            for (int64_t x = 0; x < f.fw && f.fx + x < f.W; ++x) {
+                const int k = src[x];
+                if (k == f.transparent) continue;
+                uint8_t* px = row + 3 * (f.fx + x);
+                px[0] = f.pal[k][0];
+                px[1] = f.pal[k][1];
+                px[2] = f.pal[k][2];
+            }
+        }
+        ++r;
+    };
+    if (f.finterlaced) {
+        static const int start[4] = {0, 4, 2, 1}, step[4] = {8, 8, 4, 2};
+        for (int p = 0; p < 4; ++p)
+            for (int64_t y = start[p]; y < f.fh; y += step[p]) place(y);
+    } else {
+        for (int64_t y = 0; y < f.fh; ++y) place(y);
+    }
+    return 0;
+}
+
 // PNG row reconstruction (spec 9.2) of one row in place; prev = the previous
 // reconstructed row of the same pass (nullptr for its first row).
 int unfilter_row(uint8_t* row, const uint8_t* prev, int64_t len, int bpp)
@@ -607,6 +805,7 @@ int raster_kind(const uint8_t* data, size_t size)
     if (size >= 8 && memcmp(data, kPngSig, 8) == 0) return RK_PNG;
     if (size >= 2 && data[0] == 'B' && data[1] == 'M') return RK_BMP;
     if (size >= 4 && (memcmp(data, kTiffLE, 4) == 0 || memcmp(data, kTiffBE, 4) == 0)) return RK_TIFF;
+    if (size >= 6 && (memcmp(data, "GIF87a", 6) == 0 || memcmp(data, "GIF89a", 6) == 0)) return RK_GIF;
     return RK_NONE;
 }
 
@@ -617,13 +816,21 @@ int raster_parse(const uint8_t* data, size_t size, RasterInfo* info, std::string
     case RK_PNG: return parse_png(data, size, info, err);
     case RK_BMP: return parse_bmp(data, size, info, err);
     case RK_TIFF: return parse_tiff(data, size, info, err);
+    case RK_GIF: return parse_gif(data, size, info, err);
     }
-    return bad(err, -1, "not a PNG, BMP or TIFF file");
+    return bad(err, -1, "not a PNG, BMP, TIFF or GIF file");
 }
 
 void raster_layout(const RasterInfo& info, RasterLayout* lay)
 {
     *lay = RasterLayout();
+    if (info.kind == RK_GIF) {  // RGB rows composed on the host
+        lay->pass_pitch[0] = info.W * 3;
+        lay->pass_w[0] = info.W;
+        lay->pass_h[0] = info.H;
+        lay->bytes = lay->pass_pitch[0] * info.H;
+        return;
+    }
     if (info.kind == RK_TIFF) {
         lay->pass_pitch[0] = (info.W * info.spp * info.bits + 7) / 8;
         lay->pass_w[0] = info.W;
@@ -667,6 +874,7 @@ int raster_unpack(const uint8_t* data, size_t size, const RasterInfo& info, cons
         return 0;
     }
     if (info.kind == RK_TIFF) return unpack_tiff(data, info, lay, out, err);
+    if (info.kind == RK_GIF) return unpack_gif(data, size, info, lay, out, err);
     if (info.kind != RK_PNG) return bad(err, -1, "not a PNG, BMP or TIFF file");
     for (const RasterInfo::Chunk& c : info.idat) {  // IDAT is critical: a CRC mismatch fails the file
         const uint8_t* type = data + c.off - 4;

@@ -50,7 +50,7 @@ def info(data: bytes, apply_orientation: bool = True) -> tuple[int, int, int, in
     return h.value, w.value, c.value, o.value
 
 
-KINDS = {1: "jpeg", 2: "png", 3: "bmp", 4: "tiff"}
+KINDS = {1: "jpeg", 2: "png", 3: "bmp", 4: "tiff", 5: "gif"}
 
 
 def image_info(data: bytes, apply_orientation: bool = True) -> tuple[int, int, str]:
