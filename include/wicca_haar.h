@@ -346,14 +346,16 @@ int wicca_jpeg_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* s
  * reconstruction on host threads, pixel conversion on the device: palette
  * expanded, gray replicated, alpha stripped, 16-bit samples -> high byte),
  * BMP (1/4/8-bit palette, 16-bit 5-5-5 / 5-6-5, 24, 32-bit; bottom-up or
- * top-down).  RLE BMP, TIFF, GIF: WICCA_ERR_UNSUPPORTED / WICCA_ERR_DECODE.
+ * top-down), TIFF (gray / RGB / RGBA / palette, none / LZW / Deflate /
+ * PackBits, strips or tiles), GIF (the first frame).  RLE BMP and the TIFF
+ * variants listed in DESIGN.md 4.9: WICCA_ERR_UNSUPPORTED.
  * Same arguments and per-slot status semantics as the wicca_jpeg_* calls;
  * with a status array a PNG whose compressed data turns out corrupt during
  * the decode also fails only its own slot.
  */
 
 /* Decoded size of a file (EXIF orientation applied to JPEG when
- * apply_orientation); kind: 1 JPEG, 2 PNG, 3 BMP. */
+ * apply_orientation); kind: 1 JPEG, 2 PNG, 3 BMP, 4 TIFF, 5 GIF. */
 int wicca_image_info(const uint8_t* data, int64_t size, int apply_orientation,
                      int64_t* height, int64_t* width, int* kind);
 

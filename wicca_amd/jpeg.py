@@ -5,7 +5,7 @@
 the GPU (``wicca_amd/csrc/jpeg.hip``), restating libjpeg-turbo's default
 arithmetic bit for bit (checked against Pillow 12.2.0 / libjpeg-turbo
 3.1.4.1, ``tests/test_gpu_jpeg.py``), EXIF orientation applied as
-``cv2.imread`` does; PNG and BMP files (the other formats
+``cv2.imread`` does; PNG, BMP, TIFF and GIF files (the other formats
 ``ClassifierProcessor`` counts, ``classifying_tools.py:162``) are inflated /
 copied on host threads and converted to RGB on the GPU
 (``wicca_amd/csrc/raster.hip``, ``tests/test_gpu_raster.py``).  The entry
