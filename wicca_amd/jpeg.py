@@ -17,9 +17,8 @@ points sniff each file (``wicca_image_*``), so a batch may mix formats.
 (``cv2.imread`` returns None for every file it cannot read and
 ``validate_image`` then raises that message, validation.py:94-95) and
 returns ``None``; ``WICCA_LOAD_DETAIL=1`` prints the decoder's own reason
-instead.  Files no GPU
-decoder handles (TIFF, GIF, RLE BMP, ...) fail that way too — there is no
-CPU decoder behind it.
+instead.  Files no decoder here handles (RLE BMP, JPEG-compressed TIFF,
+...) fail that way too — there is no CPU fallback behind it.
 """
 from __future__ import annotations
 
