@@ -153,6 +153,37 @@ double now_ms()
 // that the wait can report how long the device idled between calls
 thread_local hipEvent_t t_async_ready = nullptr, t_async_done = nullptr;
 
+// Asynchronous calls (a loader loop): a call's kernels wait for the previous
+// asynchronous call's kernels on the same device; its parse, de-stuffing and
+// uploads do not.  Two calls' latency-bound passes sharing the GPU ran each
+// call's kernels 1.5-2 ms longer: 25 x 8K batches at 9.9 ms per batch
+// serialised against 10.8-11.8 ms overlapped (profiles/r03aj_serial_ab.txt).
+// WICCA_JPEG_SERIAL_ASYNC=0 lets them overlap.
+bool jpeg_serial_async()
+{
+    static const bool on = [] {
+        const char* e = getenv("WICCA_JPEG_SERIAL_ASYNC");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+std::mutex g_serial_mu;
+hipEvent_t g_serial_last[64] = {};  // per device: the last asynchronous call's kernels done
+
+// The end of an asynchronous call's kernels (after the decode, or after the
+// file stage's kernels): the next asynchronous call's kernels wait for it.
+int serial_record(int device, hipStream_t stream)
+{
+    if (!jpeg_serial_async() || device < 0 || device >= 64) return WICCA_OK;
+    std::lock_guard<std::mutex> g(g_serial_mu);
+    hipEvent_t& last = g_serial_last[device];
+    if (last) (void)hipEventDestroy(last);
+    last = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&last, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(last, stream));
+    return WICCA_OK;
+}
+
 // async_rounds > 0 (n <= one pass): everything is issued on `stream` and the
 // call returns without waiting; *async_flags gets the device flags to check
 // once the stream is done (jpeg_decode_device).
@@ -412,6 +443,11 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         (void)hipEventCreate(&t_async_ready);
         (void)hipEventCreate(&t_async_done);
         (void)hipEventRecord(t_async_ready, stream);
+    }
+    const bool serial = async_rounds > 0 && jpeg_serial_async() && ws->device < 64;
+    if (serial) {
+        std::lock_guard<std::mutex> g(g_serial_mu);
+        if (g_serial_last[ws->device]) HIP_TRY(hipStreamWaitEvent(stream, g_serial_last[ws->device], 0));
     }
     HIP_TRY(wicca::jpeg_decode_device(P, ims.data(), ws->jscratch.ptr, n, &rounds, stream, async_rounds,
                                       async_flags, ws->jtab.ptr + jobs_off));
@@ -683,6 +719,7 @@ int wicca_jpeg_decode_u8_async(const uint8_t* const* data, const int64_t* sizes,
     st->ready = t_async_ready;
     st->done = t_async_done;
     st->issue_ms = now_ms() - t0;
+    if ((rc = serial_record(dev, st->stream))) return rc;
     st->data.assign(data, data + n);
     st->sizes.assign(sizes, sizes + n);
     st->dsts.assign(dsts, dsts + n);
@@ -1172,6 +1209,7 @@ int wicca_image_icon_stage_async(const uint8_t* const* data, const int64_t* size
                           border_constant, out_w, out_h, interpolation, dres, dico)))
         return rc;
     HIP_TRY(hipMemcpyAsync(ws->opin.ptr, dres, (size_t)(2 * n * out_bytes), hipMemcpyDeviceToHost, cs));
+    if ((rc = serial_record(dev, cs))) return rc;
     sync_on_exit.active = false;
     st->device = dev;
     st->stream = cs;
