@@ -350,3 +350,16 @@ def test_pillow_written_gif_and_mixed_stage(tmp_path):
     for i, rgb in enumerate(refs):
         assert np.array_equal(imgs[i], R.resize(rgb, (224, 224), R.INTER_AREA)), i
         assert np.array_equal(icons[i], R.resize(c_oracle.ll_int_block(rgb, 4)[0], (224, 224), R.INTER_AREA)), i
+
+
+def test_decode_batches_mixed_formats(tmp_path):
+    """jpeg.decode_batches over all-JPEG and mixed batches: device tensors
+    equal to the synchronous decode of the same files."""
+    paths, refs = _mixed_files(tmp_path)
+    blobs = [open(p, "rb").read() for p in paths]
+    batches = [[blobs[0], blobs[4]], blobs[:3], [blobs[4]], blobs]
+    got = list(WJ.decode_batches(batches, device=0))
+    assert len(got) == len(batches)
+    for batch, outs in zip(batches, got):
+        for b, t in zip(batch, outs):
+            assert np.array_equal(t.cpu().numpy(), WJ.decode(b))

@@ -53,8 +53,9 @@ KINDS = {1: "jpeg", 2: "png", 3: "bmp", 4: "tiff", 5: "gif"}
 
 
 def image_info(data: bytes, apply_orientation: bool = True) -> tuple[int, int, str]:
-    """(height, width, format) of a JPEG, PNG, BMP or TIFF file's bytes
-    (format "jpeg" / "png" / "bmp" / "tiff"; JPEG sizes after EXIF orientation)."""
+    """(height, width, format) of a JPEG, PNG, BMP, TIFF or GIF file's bytes
+    (format "jpeg" / "png" / "bmp" / "tiff" / "gif"; JPEG sizes after EXIF
+    orientation)."""
     arr = np.frombuffer(data, np.uint8)
     h, w = ctypes.c_int64(), ctypes.c_int64()
     k = ctypes.c_int()
@@ -83,7 +84,7 @@ def _slot_error(data: bytes) -> str:
 
 def decode_batch(blobs: Sequence[bytes], apply_orientation: bool = True,
                  device: int | None = None, errors: str = "raise") -> list[np.ndarray | None]:
-    """RGB (H, W, 3) uint8 arrays of JPEG / PNG / BMP files, decoded in one GPU pass.
+    """RGB (H, W, 3) uint8 arrays of JPEG / PNG / BMP / TIFF / GIF files, decoded in one GPU pass.
 
     errors="raise": the first file that does not parse raises (nothing is
     decoded); errors="none": such a file gives None in its slot and the others
@@ -121,12 +122,14 @@ def decode_batch(blobs: Sequence[bytes], apply_orientation: bool = True,
 
 
 def decode_batches(batches, apply_orientation: bool = True, device: int = 0, depth: int = 2):
-    """Pipelined GPU decode of a stream of JPEG batches (a data loader's
-    loop): yields, per batch of file bytes, a list of device RGB
-    ``torch.uint8`` tensors (H, W, 3).  Up to ``depth`` batches are in flight
-    (``wicca_jpeg_decode_u8_async``): batch k+1's parse, de-stuffing and PCIe
-    transfer overlap batch k's device decode.  Each yielded batch is complete
-    (its ``wicca_jpeg_wait`` returned); files that do not parse raise."""
+    """Pipelined GPU decode of a stream of batches of image files (a data
+    loader's loop): yields, per batch of file bytes, a list of device RGB
+    ``torch.uint8`` tensors (H, W, 3).  Up to ``depth`` all-JPEG batches are
+    in flight (``wicca_jpeg_decode_u8_async``): batch k+1's parse, de-stuffing
+    and PCIe transfer overlap batch k's device decode; a batch holding PNG /
+    BMP / TIFF / GIF files is decoded before it is queued.  Each yielded batch
+    is complete (its ``wicca_jpeg_wait`` returned); files that do not parse
+    raise."""
     import collections
     if depth < 1:
         raise ValueError("depth must be >= 1")
@@ -153,8 +156,10 @@ def _decode_batches_loop(batches, apply_orientation, device, depth, lib, pending
     for blobs in batches:
         blobs = list(blobs)
         outs = []
+        all_jpeg = True
         for b in blobs:
-            h, w, _, _ = info(b, apply_orientation)
+            h, w, kind = image_info(b, apply_orientation)
+            all_jpeg = all_jpeg and kind == "jpeg"
             outs.append(torch.empty((h, w, 3), dtype=torch.uint8, device=f"cuda:{device}"))
         n = len(blobs)
         keep, ptrs, sizes = _buffers(blobs)
@@ -163,15 +168,20 @@ def _decode_batches_loop(batches, apply_orientation, device, depth, lib, pending
         if len(pending) >= depth:
             yield finish()
         ticket = ctypes.c_int64(0)
-        _lib.check(lib.wicca_jpeg_decode_u8_async(ptrs, sizes, n, dsts, pitches, int(apply_orientation),
-                                                  int(device), ctypes.byref(ticket)))
+        if all_jpeg:
+            _lib.check(lib.wicca_jpeg_decode_u8_async(ptrs, sizes, n, dsts, pitches, int(apply_orientation),
+                                                      int(device), ctypes.byref(ticket)))
+        else:  # PNG / BMP / TIFF / GIF in the batch: decoded before the call returns (ticket 0)
+            torch.cuda.synchronize(device)  # the outputs' allocation is ordered before the library's stream
+            _lib.check(lib.wicca_image_decode_u8(ptrs, sizes, n, dsts, pitches, int(apply_orientation), 1,
+                                                 int(device), None, None))
         pending.append((ticket.value, outs, (keep, blobs)))
     while pending:
         yield finish()
 
 
 def decode(data: bytes, apply_orientation: bool = True, device: int | None = None) -> np.ndarray:
-    """RGB (H, W, 3) uint8 array of one JPEG / PNG / BMP file's bytes."""
+    """RGB (H, W, 3) uint8 array of one JPEG / PNG / BMP / TIFF / GIF file's bytes."""
     return decode_batch([data], apply_orientation, device)[0]
 
 
