@@ -18,6 +18,8 @@
 
 #include <string.h>
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <memory>
 
@@ -200,9 +202,116 @@ struct CrcTables {
     }
 };
 
+// Carry-less-multiply folding of the reflected CRC-32 (Gopal et al., "Fast
+// CRC Computation for Generic Polynomials Using PCLMULQDQ", Intel 2009: fold
+// constants k1..k5, Barrett constants P' and u of the bit-reflected
+// polynomial 0x1DB710641).  Takes and returns the inverted CRC register over
+// n bytes (n a multiple of 16, >= 64).
+__attribute__((target("pclmul,sse4.1"))) uint32_t crc32_clmul(uint32_t crc, const uint8_t* buf, size_t len)
+{
+    alignas(16) static const uint64_t k1k2[2] = {0x0154442bd4ull, 0x01c6e41596ull};
+    alignas(16) static const uint64_t k3k4[2] = {0x01751997d0ull, 0x00ccaa009eull};
+    alignas(16) static const uint64_t k5k0[2] = {0x0163cd6124ull, 0};
+    alignas(16) static const uint64_t poly[2] = {0x01db710641ull, 0x01f7011641ull};
+    __m128i x0, x1, x2, x3, x4, x5, x6, x7, x8;
+    x1 = _mm_loadu_si128((const __m128i*)(buf + 0x00));
+    x2 = _mm_loadu_si128((const __m128i*)(buf + 0x10));
+    x3 = _mm_loadu_si128((const __m128i*)(buf + 0x20));
+    x4 = _mm_loadu_si128((const __m128i*)(buf + 0x30));
+    x1 = _mm_xor_si128(x1, _mm_cvtsi32_si128((int)crc));
+    x0 = _mm_load_si128((const __m128i*)k1k2);
+    buf += 64;
+    len -= 64;
+    while (len >= 64) {  // four independent 128-bit lanes, folded 64 bytes at a time
+        x5 = _mm_clmulepi64_si128(x1, x0, 0x00);
+        x6 = _mm_clmulepi64_si128(x2, x0, 0x00);
+        x7 = _mm_clmulepi64_si128(x3, x0, 0x00);
+        x8 = _mm_clmulepi64_si128(x4, x0, 0x00);
+        x1 = _mm_clmulepi64_si128(x1, x0, 0x11);
+        x2 = _mm_clmulepi64_si128(x2, x0, 0x11);
+        x3 = _mm_clmulepi64_si128(x3, x0, 0x11);
+        x4 = _mm_clmulepi64_si128(x4, x0, 0x11);
+        x1 = _mm_xor_si128(_mm_xor_si128(x1, x5), _mm_loadu_si128((const __m128i*)(buf + 0x00)));
+        x2 = _mm_xor_si128(_mm_xor_si128(x2, x6), _mm_loadu_si128((const __m128i*)(buf + 0x10)));
+        x3 = _mm_xor_si128(_mm_xor_si128(x3, x7), _mm_loadu_si128((const __m128i*)(buf + 0x20)));
+        x4 = _mm_xor_si128(_mm_xor_si128(x4, x8), _mm_loadu_si128((const __m128i*)(buf + 0x30)));
+        buf += 64;
+        len -= 64;
+    }
+    x0 = _mm_load_si128((const __m128i*)k3k4);  // the four lanes into one
+    x5 = _mm_clmulepi64_si128(x1, x0, 0x00);
+    x1 = _mm_clmulepi64_si128(x1, x0, 0x11);
+    x1 = _mm_xor_si128(_mm_xor_si128(x1, x2), x5);
+    x5 = _mm_clmulepi64_si128(x1, x0, 0x00);
+    x1 = _mm_clmulepi64_si128(x1, x0, 0x11);
+    x1 = _mm_xor_si128(_mm_xor_si128(x1, x3), x5);
+    x5 = _mm_clmulepi64_si128(x1, x0, 0x00);
+    x1 = _mm_clmulepi64_si128(x1, x0, 0x11);
+    x1 = _mm_xor_si128(_mm_xor_si128(x1, x4), x5);
+    while (len >= 16) {
+        x2 = _mm_loadu_si128((const __m128i*)buf);
+        x5 = _mm_clmulepi64_si128(x1, x0, 0x00);
+        x1 = _mm_clmulepi64_si128(x1, x0, 0x11);
+        x1 = _mm_xor_si128(_mm_xor_si128(x1, x2), x5);
+        buf += 16;
+        len -= 16;
+    }
+    // 128 -> 64 bits, then Barrett reduction to 32
+    x2 = _mm_clmulepi64_si128(x1, x0, 0x10);
+    x3 = _mm_setr_epi32(~0, 0, ~0, 0);
+    x1 = _mm_srli_si128(x1, 8);
+    x1 = _mm_xor_si128(x1, x2);
+    x0 = _mm_loadl_epi64((const __m128i*)k5k0);
+    x2 = _mm_srli_si128(x1, 4);
+    x1 = _mm_and_si128(x1, x3);
+    x1 = _mm_clmulepi64_si128(x1, x0, 0x00);
+    x1 = _mm_xor_si128(x1, x2);
+    x0 = _mm_load_si128((const __m128i*)poly);
+    x2 = _mm_and_si128(x1, x3);
+    x2 = _mm_clmulepi64_si128(x2, x0, 0x10);
+    x2 = _mm_and_si128(x2, x3);
+    x2 = _mm_clmulepi64_si128(x2, x0, 0x00);
+    x1 = _mm_xor_si128(x1, x2);
+    return (uint32_t)_mm_extract_epi32(x1, 1);
+}
+
+uint32_t crc32_table(uint32_t crc, const uint8_t* p, size_t n);
+
+// The folding path is used only if this CPU has PCLMULQDQ / SSE4.1 and it
+// reproduces the table CRC on a self-test, checked once.
+bool clmul_ok()
+{
+    static const bool ok = [] {
+        if (!__builtin_cpu_supports("pclmul") || !__builtin_cpu_supports("sse4.1")) return false;
+        uint8_t buf[1031];
+        uint32_t x = 12345;
+        for (uint8_t& b : buf) b = (uint8_t)((x = x * 1103515245u + 12345u) >> 16);
+        for (size_t n : {(size_t)64, (size_t)80, (size_t)128, (size_t)1024}) {
+            const uint32_t want = crc32_table(0x1234u, buf + 7, n);
+            if (~crc32_clmul(~0x1234u, buf + 7, n) != want) return false;
+        }
+        return true;
+    }();
+    return ok;
+}
+
 }  // namespace
 
 uint32_t crc32_fast(uint32_t crc, const uint8_t* p, size_t n)
+{
+    if (n >= 64 && clmul_ok()) {
+        const size_t m = n & ~(size_t)15;
+        crc = ~crc32_clmul(~crc, p, m);
+        p += m;
+        n -= m;
+        if (!n) return crc;
+    }
+    return crc32_table(crc, p, n);
+}
+
+namespace {
+
+uint32_t crc32_table(uint32_t crc, const uint8_t* p, size_t n)
 {
     static const CrcTables T;
     uint32_t c = ~crc;
@@ -223,6 +332,8 @@ uint32_t crc32_fast(uint32_t crc, const uint8_t* p, size_t n)
     while (n--) c = T.t[0][(c ^ *p++) & 0xFF] ^ (c >> 8);
     return ~c;
 }
+
+}  // namespace
 
 int zlib_inflate(const uint8_t* in, size_t n, uint8_t* out, int64_t cap, InflateProgress* progress, std::string* err)
 {
