@@ -40,7 +40,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", choices=["batch", "tiled", "multi", "ragged", "stage", "jpeg", "png", "bmp"],
+    ap.add_argument("--config", choices=["batch", "tiled", "multi", "ragged", "stage", "jpeg", "png", "bmp", "plan"],
                     default="batch",
                     help="batch: configs[2]/[3] image-parallel (default); "
                          "tiled: configs[4], one 65536^2 RGB image row-sharded at depth 8; "
@@ -662,6 +662,94 @@ def run_jpeg(args, torch, rank):
     }
 
 
+# demo.ipynb's 14 classifiers (their input shapes, classifier[SHAPE]) and depth_range
+DEMO_CLASSIFIERS = [(224, 224)] * 9 + [(331, 331)] + [(299, 299)] * 3 + [(240, 240)]
+
+
+def run_plan(args, torch, rank):
+    """The stage plan (wicca_image_stage_plan_u8): the demo's
+    14 classifiers x 5 depths of _get_img_batch for one batch of B JPEG files
+    (the reference decodes, resizes and icons every file once per classifier
+    and depth: classifying_tools.py:546-551, 414-419, 339-346, 312-318) as ONE
+    call, against the per-call file stage run 70 times (wicca_image_icon_stage_u8
+    per (classifier, depth)).  Files in host memory; outputs to host arrays."""
+    from oracle import jpeg_pil
+    from wicca_amd import _lib
+    lib = _lib.load()
+    B = 25 if args.images == 128 else args.images
+    H, W = args.height, args.width
+    depths = [int(x) for x in args.depths.split(",")] if args.depths != "1,2,3,4,5,6" else [2, 3, 4, 5, 6]
+    distinct = [jpeg_pil.encode(jpeg_pil.test_image("scene", H, W, 40 + k), args.quality, 2) for k in range(4)]
+    blobs = [distinct[i % 4] for i in range(B)]
+    keep = [np.frombuffer(b, np.uint8) for b in blobs]
+    ptrs = (ctypes.c_void_p * B)(*[k.ctypes.data for k in keep])
+    sizes = (ctypes.c_int64 * B)(*[k.size for k in keep])
+    shapes = list(dict.fromkeys(DEMO_CLASSIFIERS))
+    res = [np.empty((B, h, w, 3), np.uint8) for (w, h) in shapes]
+    ico = [[np.empty((B, h, w, 3), np.uint8) for _ in depths] for (w, h) in shapes]
+    c_shapes = (ctypes.c_int64 * (2 * len(shapes)))(*[v for sh in shapes for v in sh])
+    c_depths = (ctypes.c_int * len(depths))(*depths)
+    c_res = (ctypes.c_void_p * len(shapes))(*[r.ctypes.data for r in res])
+    c_ico = (ctypes.c_void_p * (len(shapes) * len(depths)))(*[a.ctypes.data for row in ico for a in row])
+
+    def plan():
+        _lib.check(lib.wicca_image_stage_plan_u8(ptrs, sizes, B, c_shapes, len(shapes), c_depths, len(depths), 1, 0,
+                                                 args.interpolation, c_res, c_ico, -1, None))
+
+    for _ in range(max(1, args.warmup)):
+        plan()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        plan()
+    plan_s = (time.perf_counter() - t0) / args.steps
+    r1 = np.empty((B, 224, 224, 3), np.uint8)
+    pc = {sh: (np.empty((B, sh[1], sh[0], 3), np.uint8), np.empty((B, sh[1], sh[0], 3), np.uint8))
+          for sh in shapes}
+
+    def per_call(sh, d):
+        r, c = pc[sh]
+        _lib.check(lib.wicca_image_icon_stage_u8(ptrs, sizes, B, d, 1, 0, sh[0], sh[1], args.interpolation,
+                                                 r.ctypes.data, c.ctypes.data, -1, None))
+
+    per_call(shapes[0], depths[0])
+    loop_steps = max(1, min(args.steps, 2))
+    t0 = time.perf_counter()
+    for _ in range(loop_steps):
+        for d in depths:
+            for sh in DEMO_CLASSIFIERS:
+                per_call(sh, d)
+    loop_s = (time.perf_counter() - t0) / loop_steps
+    verified = None
+    if not args.no_verify:
+        verified = True
+        for si, sh in enumerate(shapes):
+            for di, d in enumerate(depths):
+                per_call(sh, d)
+                r, c = pc[sh]
+                verified &= bool(np.array_equal(res[si], r) and np.array_equal(ico[si][di], c))
+        if not verified:
+            raise SystemExit("plan bench verification FAILED")
+    del r1
+    pairs = len(DEMO_CLASSIFIERS) * len(depths)
+    mpix = B * H * W / 1e6
+    return {
+        "metric": "ms per batch for the demo's 14 classifiers x depths of _get_img_batch (stage plan)",
+        "value": round(plan_s * 1e3, 3), "unit": "ms", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(plan_s * 1e3, 3), "higher_is_better": False, "scaling": "weak",
+        "vs_baseline": None, "dtype": "u8",
+        "data": f"synthetic scenes encoded by libjpeg-turbo (q{args.quality}, 4:2:0), files in host memory; "
+                "every output copied to host arrays inside the timed region",
+        "config": {"workload": f"{B} x {W}x{H} JPEG files, shapes {shapes} (14 classifiers), depths {depths}",
+                   "images": B, "classifiers": len(DEMO_CLASSIFIERS), "depths": depths, "pairs": pairs},
+        "per_call_loop": {"ms_per_batch": round(loop_s * 1e3, 3),
+                          "what": f"wicca_image_icon_stage_u8 once per (classifier, depth): {pairs} calls, "
+                                  "each decoding, resizing and iconing the whole batch (the reference's structure)"},
+        "speedup_vs_per_call": round(loop_s / plan_s, 2),
+        "decoded_MP_per_s": round(mpix / plan_s, 1),
+        "verified_vs_per_call": verified, "roofline": None, "cpu_baseline": None,
+    }
+
+
 def run_raster(args, torch, rank):
     """load_image for PNG / BMP files (data_loader.py:53; ClassifierProcessor
     counts .png / .bmp, classifying_tools.py:162): B files of the configs[2]
@@ -929,6 +1017,11 @@ def main():
         return
     if args.config == "jpeg":
         out = run_jpeg(args, torch, rank)
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        return
+    if args.config == "plan":
+        out = run_plan(args, torch, rank)
         if rank == 0:
             print(json.dumps(out), flush=True)
         return

@@ -399,6 +399,29 @@ int wicca_image_icon_stage_async(const uint8_t* const* data, const int64_t* size
 int wicca_image_stage_wait(int64_t ticket);
 
 /*
+ * The stage plan: ClassifierProcessor's whole (classifier shape x depth)
+ * matrix of _get_img_batch for one batch of files.  The
+ * reference runs the per-file stage once per classifier and per depth
+ * (classifying_tools.py:546-551 depth loop, :414-419 one task per classifier,
+ * :339-346 batch loop, :312-318 decode + resize + icon + resize); here every
+ * file is decoded once, read once for the icons of every depth (K5 over the
+ * ragged batch) and once for the INTER_AREA source resizes of every shape.
+ *   shapes:  n_shapes (width, height) pairs (cv2.resize's dsize order)
+ *   depths:  n_depths transform depths (repeats allowed; <= 0 copies, > 8 the
+ *            float32 tail, as get_small_copy)
+ *   resized[s]:              (n, h_s, w_s, 3) host array, cv2.resize(image, shape_s)
+ *   icons[s * n_depths + d]: (n, h_s, w_s, 3) host array, cv2.resize(
+ *                            get_small_copy(image, depths[d]), shape_s)
+ * Each output equals wicca_image_icon_stage_u8(files, depths[d], shape_s)'s.
+ * status: as wicca_image_icon_stage_u8 (a file that fails gets zero outputs
+ * in every array; the others are processed).
+ */
+int wicca_image_stage_plan_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                              const int64_t* shapes, int n_shapes, const int* depths, int n_depths,
+                              int border_type, int border_constant, int interpolation,
+                              uint8_t* const* resized, uint8_t* const* icons, int device, int* status);
+
+/*
  * Deterministic synthetic images on device (no PCIe in timed regions):
  * byte (i, y, x, c) = splitmix64-hash of (seed, i, y*W*C + x*C + c), see
  * wicca_amd/synth.py for the host restatement.

@@ -292,7 +292,9 @@ def test_write_and_sync_variants_subprocess(env):
 
 
 STAGE = [(1, (224, 224), 3, 1, 0), (6, (224, 224), 3, 0, 77), (8, (331, 331), 3, 1, 0),
-         (4, (240, 240), 1, 0, 9), (3, (299, 299), 0, 1, 0), (7, (224, 224), 3, 0, 255)]
+         (4, (240, 240), 1, 0, 9), (3, (299, 299), 0, 1, 0), (7, (224, 224), 3, 0, 255),
+         # outputs wider than the row-sum kernel's 341 RGB columns: no row sums
+         (5, (384, 384), 3, 1, 0), (2, (600, 450), 3, 0, 5)]
 
 
 @pytest.mark.parametrize("depth,shape,interp,border,k", STAGE,

@@ -122,12 +122,16 @@ struct Workspace {
     DevBuf rraw, rmeta;
     HostBuf rhost, rmeta_pin;
     HostBuf opin;   // pinned outputs of an asynchronous file stage (wicca_image_icon_stage_async)
+    // stage plan (wicca_image_stage_plan_u8): descriptors (pinned + device),
+    // icon planes of every depth, INTER_AREA row sums of every shape
+    DevBuf pmeta, picons, phsum;
+    HostBuf ppin;
     size_t bytes() const
     {
         return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
                slot[0].cap + slot[1].cap + icon[0].cap + icon[1].cap + jstream.cap + jmeta.cap + jcoef.cap +
                jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap + rscratch.cap + smeta.cap + rtab.cap + rraw.cap +
-               rmeta.cap;
+               rmeta.cap + pmeta.cap + picons.cap + phsum.cap;
     }
     hipError_t ensure_pipeline()
     {
@@ -178,6 +182,10 @@ struct Workspace {
         rhost.release();
         rmeta_pin.release();
         opin.release();
+        pmeta.release();
+        picons.release();
+        phsum.release();
+        ppin.release();
     }
     void destroy()
     {
@@ -267,5 +275,15 @@ int run_resize(wicca::ResizeParams rp, const uint8_t* src, int64_t src_pitch, in
 // failed file's dst is not written).
 int raster_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
                             uint8_t* const* dst, const int64_t* dpitch, hipStream_t stream, int* status);
+
+// Any-format image files (capi_jpeg.cpp): decoded size after EXIF orientation;
+// per-slot screening (status[i] = 0 or the file's error; good = the files that
+// parse); decode of parsed files into device RGB images (orientation applied;
+// late: NULL or n ints set to 0 / WICCA_ERR_DECODE for data found corrupt).
+int image_file_probe(const uint8_t* data, int64_t size, int64_t i, int64_t* H, int64_t* W);
+int image_files_screen(const uint8_t* const* data, const int64_t* sizes, int64_t n, int* status,
+                       std::vector<int64_t>* good);
+int image_files_decode(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                       uint8_t* const* dst, const int64_t* dpitch, hipStream_t stream, int* late);
 
 }  // namespace wicca_capi

@@ -609,7 +609,7 @@ int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, c
     sp.k = (int32_t)saturate_k(k);
     sp.dw = (int32_t)out_w;
     sp.dh = (int32_t)out_h;
-    HIP_TRY(wicca::launch_stage_rows(sp, n, max_oh, cs));
+    HIP_TRY(wicca::launch_stage_rows(sp, n, max_oh, any_hsum, cs));
     if (any_hsum) HIP_TRY(wicca::launch_stage_vsum(sp, n, cs));
     for (int64_t i = 0; i < n; ++i) {  // source resizes the row kernel did not prepare
         if (sd[(size_t)i].hsum) continue;
@@ -1270,3 +1270,25 @@ int wicca_image_stage_wait(int64_t ticket)
 }
 
 }  // extern "C"
+
+// The file helpers the stage plan (capi_plan.cpp) shares with the file stage.
+namespace wicca_capi {
+
+int image_file_probe(const uint8_t* data, int64_t size, int64_t i, int64_t* H, int64_t* W)
+{
+    return probe_file(data, size, i, true, true, H, W);
+}
+
+int image_files_screen(const uint8_t* const* data, const int64_t* sizes, int64_t n, int* status,
+                       std::vector<int64_t>* good)
+{
+    return screen_files(data, sizes, n, status, good, true);
+}
+
+int image_files_decode(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                       uint8_t* const* dst, const int64_t* dpitch, hipStream_t stream, int* late)
+{
+    return decode_files_to_device(ws, data, sizes, n, dst, dpitch, true, stream, true, late);
+}
+
+}  // namespace wicca_capi

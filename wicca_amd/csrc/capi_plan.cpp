@@ -1,0 +1,465 @@
+// capi_plan.cpp — the stage plan: ClassifierProcessor's whole (classifier
+// shape x depth) matrix of _get_img_batch for one batch of files, with every
+// file decoded once, read once for all its icons and once for all its source
+// resizes.
+//
+// The reference runs the whole per-file stage once per classifier and per
+// depth: process_classifiers loops over the depths (classifying_tools.py:
+// 546-551), _parallel_proc submits one task per classifier (:414-419), each
+// task's _classify walks the folder in batches (:339-346) and _get_img_batch
+// decodes, resizes, icons and resizes again every file of the batch
+// (:312-318).  The demo's 14 classifiers x 5 depths decode each file 70 times.
+// Here one call serves every (shape, depth) pair of a batch:
+//   1. decode every file into HBM (JPEG on the GPU, other formats host
+//      inflate + GPU conversion: the file stage's decoder);
+//   2. icons of every depth 1..8 from ONE read of each image (K5 over the
+//      ragged batch, haar_multi_ragged_kernel; padding to the largest depth
+//      gives each smaller depth's icon as the top-left crop of its level,
+//      SURVEY A5); depths <= 0 / > 8 per image as get_small_copy computes them;
+//   3. the INTER_AREA source resize of every classifier shape from ONE more
+//      read of each image (plan_hsum_kernel: row sums of up to 4 shapes at a
+//      time, then plan_vsum_kernel); other interpolations per image;
+//   4. every icon resized to every shape (one launch per shape over the
+//      batch x depths);
+//   5. the dense (n, h, w, 3) outputs back to the caller's host arrays.
+// Outputs are the bytes the per-call file stage (wicca_image_icon_stage_u8)
+// gives for each (shape, depth) — checked by tests/test_gpu_plan.py.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "capi_internal.h"
+#include "stage.h"
+
+using namespace wicca_capi;
+
+namespace {
+
+struct PlanShape {
+    int64_t w, h;
+};
+
+// The call for a batch in which every file parses (status screening done).
+int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, const std::vector<PlanShape>& shapes,
+               const int* depths, int n_depths, int border, int k, int interpolation, uint8_t* const* resized,
+               uint8_t* const* icons, int device, int* late_status)
+{
+    const int S = (int)shapes.size();
+    // distinct depths: each is computed once, repeated entries are copied out
+    std::vector<int> ud;
+    std::vector<int> slot_of((size_t)n_depths);
+    for (int d = 0; d < n_depths; ++d) {
+        auto it = std::find(ud.begin(), ud.end(), depths[d]);
+        if (it == ud.end()) {
+            slot_of[(size_t)d] = (int)ud.size();
+            ud.push_back(depths[d]);
+        } else {
+            slot_of[(size_t)d] = (int)(it - ud.begin());
+        }
+    }
+    const int U = (int)ud.size();
+    std::vector<int64_t> H((size_t)n), W((size_t)n);
+    std::vector<int64_t> ih((size_t)n * U), iw((size_t)n * U);
+    for (int64_t i = 0; i < n; ++i) {
+        int rc = image_file_probe(data[i], sizes[i], i, &H[(size_t)i], &W[(size_t)i]);
+        if (rc) return rc;
+        for (int u = 0; u < U; ++u) {
+            if ((rc = check_image((const uint8_t*)1, H[(size_t)i], W[(size_t)i], 3, W[(size_t)i] * 3, ud[(size_t)u],
+                                  border)))
+                return rc;
+            icon_dims(H[(size_t)i], W[(size_t)i], ud[(size_t)u], &ih[(size_t)(i * U + u)], &iw[(size_t)(i * U + u)]);
+        }
+        for (const PlanShape& sh : shapes) {
+            wicca::ResizeParams probe{};
+            if ((rc = check_resize(H[(size_t)i], W[(size_t)i], 3, sh.w, sh.h, interpolation, &probe))) return rc;
+            for (int u = 0; u < U; ++u)
+                if ((rc = check_resize(ih[(size_t)(i * U + u)], iw[(size_t)(i * U + u)], 3, sh.w, sh.h, interpolation,
+                                       &probe)))
+                    return rc;
+        }
+    }
+    DeviceGuard dg;
+    int dev, rc;
+    if ((rc = select_device(device, &dev, dg))) return rc;
+    WorkspaceLease lease;
+    if ((rc = acquire(dev, lease))) return rc;
+    Workspace* ws = lease.ws;
+    hipStream_t cs = ws->stream;
+
+    // 1. decode (data_loader.py:53-58, cv2.imread + BGR2RGB, EXIF orientation)
+    int64_t rgb_total = 0;
+    for (int64_t i = 0; i < n; ++i) rgb_total += round_up(W[(size_t)i] * 3, kStagePitch) * H[(size_t)i];
+    HIP_TRY(ws->jrgb.reserve((size_t)rgb_total));
+    std::vector<uint8_t*> img((size_t)n);
+    std::vector<int64_t> pitch((size_t)n);
+    {
+        int64_t off = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            img[(size_t)i] = (uint8_t*)ws->jrgb.ptr + off;
+            pitch[(size_t)i] = round_up(W[(size_t)i] * 3, kStagePitch);
+            off += pitch[(size_t)i] * H[(size_t)i];
+        }
+    }
+    std::vector<int> late((size_t)n, 0);
+    if ((rc = image_files_decode(ws, data, sizes, n, img.data(), pitch.data(), cs,
+                                 late_status ? late.data() : nullptr)))
+        return rc;
+
+    // icon planes (device): image i, depth slot u at ipitch = round_up(iw * 3, 16)
+    std::vector<int64_t> ico_off((size_t)n * U), ico_pitch((size_t)n * U);
+    int64_t ico_total = 0;
+    for (int64_t i = 0; i < n; ++i)
+        for (int u = 0; u < U; ++u) {
+            const size_t j = (size_t)(i * U + u);
+            ico_pitch[j] = round_up(iw[j] * 3, 16);
+            ico_off[j] = ico_total;
+            ico_total += round_up(ico_pitch[j] * ih[j], 256);
+        }
+    HIP_TRY(ws->picons.reserve((size_t)std::max<int64_t>(ico_total, 256)));
+    auto icon_ptr = [&](int64_t i, int u) { return (uint8_t*)ws->picons.ptr + ico_off[(size_t)(i * U + u)]; };
+
+    // dense device outputs: per shape the resized images, then per depth slot the resized icons
+    std::vector<int64_t> ob((size_t)S), res_off((size_t)S), ico_out_off((size_t)S * U);
+    int64_t out_total = 0;
+    for (int s = 0; s < S; ++s) {
+        ob[(size_t)s] = shapes[(size_t)s].w * shapes[(size_t)s].h * 3;
+        res_off[(size_t)s] = out_total;
+        out_total += round_up(n * ob[(size_t)s], 256);
+        for (int u = 0; u < U; ++u) {
+            ico_out_off[(size_t)(s * U + u)] = out_total;
+            out_total += round_up(n * ob[(size_t)s], 256);
+        }
+    }
+    HIP_TRY(ws->out.reserve((size_t)out_total));
+    uint8_t* dout = (uint8_t*)ws->out.ptr;
+
+    // 2. which depths go through K5 (1..8, two or more of them), the rest alone
+    const int k5_lo = WICCA_MULTI_D1 ? 1 : 2;
+    std::vector<int> k5;
+    for (int u = 0; u < U; ++u)
+        if (ud[(size_t)u] >= k5_lo && ud[(size_t)u] <= 8) k5.push_back(u);
+    const bool use_k5 = k5.size() >= 2;
+    int dmin = 9, dmax = 0;
+    for (int u : k5) {
+        dmin = std::min(dmin, ud[(size_t)u]);
+        dmax = std::max(dmax, ud[(size_t)u]);
+    }
+
+    // 3. which shapes take their source resize from the plan's row sums
+    std::vector<wicca::ResizeParams> src_rp((size_t)S * n);
+    std::vector<int> area_shapes;
+    for (int s = 0; s < S; ++s) {
+        bool area = wicca::plan_hsum_ok(shapes[(size_t)s].w, 3);
+        for (int64_t i = 0; i < n; ++i) {
+            wicca::ResizeParams& rp = src_rp[(size_t)(s * n + i)];
+            wicca::plan_resize((int)H[(size_t)i], (int)W[(size_t)i], (int)shapes[(size_t)s].h,
+                               (int)shapes[(size_t)s].w, 3, interpolation, &rp);
+        }
+        if (area) area_shapes.push_back(s);
+    }
+    // an (image, shape) takes the row sums when its own plan is RS_AREA
+    auto hsum_wanted = [&](int s, int64_t i) {
+        return src_rp[(size_t)(s * n + i)].mode == wicca::RS_AREA && wicca::stage_row_ok(W[(size_t)i], 3);
+    };
+
+    // descriptors, packed into one pinned buffer and uploaded once:
+    //   [MultiImageDev x n | block map | per group of <= 4 area shapes: PlanImageDev x n |
+    //    ResizeParams x (S * U * n)]
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t o = off;
+        off += (size_t)round_up((int64_t)bytes, 256);
+        return o;
+    };
+    std::vector<wicca::MultiImageDev> md;
+    std::vector<uint32_t> bmap;
+    int64_t k5_blocks = 0;
+    int map_shift = 0;
+    size_t o_md = 0, o_map = 0;
+    if (use_k5) {
+        md.resize((size_t)n);
+        int64_t min_units = INT64_MAX;
+        for (int64_t i = 0; i < n; ++i) {
+            wicca::MultiImageDev& e = md[(size_t)i];
+            memset(&e, 0, sizeof(e));
+            e.src = img[(size_t)i];
+            e.src_pitch = pitch[(size_t)i];
+            e.H = H[(size_t)i];
+            e.W = W[(size_t)i];
+            e.blk0 = k5_blocks;
+            e.n_groups = wicca::multi_groups(W[(size_t)i], 3, dmax);
+            for (int u : k5) {
+                e.dst[ud[(size_t)u]] = icon_ptr(i, u);
+                e.dst_pitch[ud[(size_t)u]] = ico_pitch[(size_t)(i * U + u)];
+            }
+            const int64_t blocks = wicca::multi_bands(H[(size_t)i], dmax) * e.n_groups;
+            k5_blocks += blocks;
+            min_units = std::min(min_units, blocks);
+        }
+        map_shift = wicca::ragged_map_shift(min_units, k5_blocks);
+        const int64_t n_groups = (k5_blocks >> map_shift) + 1;
+        bmap.resize((size_t)n_groups);
+        int64_t im = 0;
+        for (int64_t g = 0; g < n_groups; ++g) {
+            const int64_t b = g << map_shift;
+            while (im + 1 < n && md[(size_t)(im + 1)].blk0 <= b) ++im;
+            bmap[(size_t)g] = (uint32_t)im;
+        }
+        o_md = take(sizeof(wicca::MultiImageDev) * (size_t)n);
+        o_map = take(sizeof(uint32_t) * bmap.size());
+    }
+    // groups of at most kPlanShapes area shapes, each with its PlanImageDev array
+    struct AreaGroup {
+        std::vector<int> shapes;
+        std::vector<wicca::PlanImageDev> imgs;
+        size_t off = 0;
+        bool any = false;
+    };
+    std::vector<AreaGroup> groups;
+    std::vector<int64_t> hsum_off((size_t)S * n, -1);
+    int64_t hsum_total = 0;
+    for (size_t a = 0; a < area_shapes.size(); a += wicca::kPlanShapes) {
+        AreaGroup g;
+        for (size_t b = a; b < std::min(area_shapes.size(), a + wicca::kPlanShapes); ++b)
+            g.shapes.push_back(area_shapes[b]);
+        g.imgs.resize((size_t)n);
+        for (int64_t i = 0; i < n; ++i) {
+            wicca::PlanImageDev& e = g.imgs[(size_t)i];
+            memset(&e, 0, sizeof(e));
+            e.src = img[(size_t)i];
+            e.src_pitch = pitch[(size_t)i];
+            e.H = (int32_t)H[(size_t)i];
+            e.W = (int32_t)W[(size_t)i];
+            for (size_t q = 0; q < g.shapes.size(); ++q) {
+                const int s = g.shapes[q];
+                if (!hsum_wanted(s, i)) continue;
+                const wicca::ResizeParams& rp = src_rp[(size_t)(s * n + i)];
+                hsum_off[(size_t)(s * n + i)] = hsum_total;
+                hsum_total += round_up(H[(size_t)i] * shapes[(size_t)s].w * 3 * (int64_t)sizeof(float), 256);
+                e.dst[q] = dout + res_off[(size_t)s] + i * ob[(size_t)s];
+                e.scale_x[q] = rp.scale_x;
+                e.scale_y[q] = rp.scale_y;
+                g.any = true;
+            }
+        }
+        g.off = take(sizeof(wicca::PlanImageDev) * (size_t)n);
+        groups.push_back(std::move(g));
+    }
+    if (hsum_total) HIP_TRY(ws->phsum.reserve((size_t)hsum_total));
+    for (AreaGroup& g : groups)
+        for (int64_t i = 0; i < n; ++i)
+            for (size_t q = 0; q < g.shapes.size(); ++q) {
+                const int64_t o = hsum_off[(size_t)(g.shapes[q] * n + i)];
+                if (o >= 0) g.imgs[(size_t)i].hsum[q] = (float*)((uint8_t*)ws->phsum.ptr + o);
+            }
+    // 4. icon resizes: (shape s, depth slot u, image i)
+    std::vector<wicca::ResizeParams> irp((size_t)S * U * n);
+    std::vector<bool> shape_per_image((size_t)S, false);  // a copy / cubic / Lanczos icon resize in the shape
+    for (int s = 0; s < S; ++s)
+        for (int u = 0; u < U; ++u)
+            for (int64_t i = 0; i < n; ++i) {
+                const size_t j = (size_t)(i * U + u);
+                wicca::ResizeParams& q = irp[(size_t)((s * U + u) * n + i)];
+                wicca::plan_resize((int)ih[j], (int)iw[j], (int)shapes[(size_t)s].h, (int)shapes[(size_t)s].w, 3,
+                                   interpolation, &q);
+                q.src = icon_ptr(i, u);
+                q.src_pitch = ico_pitch[j];
+                q.src_stride = 0;
+                q.dst = dout + ico_out_off[(size_t)(s * U + u)] + i * ob[(size_t)s];
+                q.dst_pitch = shapes[(size_t)s].w * 3;
+                q.dst_stride = 0;
+                if (q.mode == wicca::RS_COPY || q.mode == wicca::RS_KERNEL) shape_per_image[(size_t)s] = true;
+            }
+    const size_t o_irp = take(sizeof(wicca::ResizeParams) * irp.size());
+    const size_t meta_bytes = off;
+    HIP_TRY(ws->ppin.reserve(meta_bytes, 64 << 10));
+    HIP_TRY(ws->pmeta.reserve(meta_bytes));
+    uint8_t* hp = ws->ppin.ptr;
+    uint8_t* dp = (uint8_t*)ws->pmeta.ptr;
+    if (use_k5) {
+        memcpy(hp + o_md, md.data(), sizeof(wicca::MultiImageDev) * md.size());
+        memcpy(hp + o_map, bmap.data(), sizeof(uint32_t) * bmap.size());
+    }
+    for (AreaGroup& g : groups) memcpy(hp + g.off, g.imgs.data(), sizeof(wicca::PlanImageDev) * g.imgs.size());
+    memcpy(hp + o_irp, irp.data(), sizeof(wicca::ResizeParams) * irp.size());
+    // the decode's staging was waited for (synchronous decode); the pinned
+    // descriptors stay untouched until this call's final synchronise
+    HIP_TRY(hipMemcpyAsync(dp, hp, meta_bytes, hipMemcpyHostToDevice, cs));
+
+    // icons (wavelet_coder.py:50-67 per depth)
+    if (use_k5) {
+        wicca::MultiParams mp{};
+        mp.n_images = n;
+        mp.dmax = dmax;
+        mp.border = border;
+        mp.k = saturate_k(k);
+        for (int u : k5) mp.want |= 1u << ud[(size_t)u];
+        mp.imgs = (const wicca::MultiImageDev*)(dp + o_md);
+        mp.blk_map = (const uint32_t*)(dp + o_map);
+        mp.map_shift = map_shift;
+        HIP_TRY(wicca::launch_multi_ragged(mp, dmin, k5_blocks, cs));
+    }
+    for (int u = 0; u < U; ++u) {
+        if (use_k5 && std::find(k5.begin(), k5.end(), u) != k5.end()) continue;
+        const int d = ud[(size_t)u];
+        if (d >= 1 && d <= 8) {  // a lone depth: the ragged one-depth launch on this stream
+            std::vector<wicca_image_desc> dd((size_t)n);
+            for (int64_t i = 0; i < n; ++i) {
+                dd[(size_t)i].src = img[(size_t)i];
+                dd[(size_t)i].dst = icon_ptr(i, u);
+                dd[(size_t)i].height = H[(size_t)i];
+                dd[(size_t)i].width = W[(size_t)i];
+                dd[(size_t)i].src_pitch = pitch[(size_t)i];
+                dd[(size_t)i].dst_pitch = ico_pitch[(size_t)(i * U + u)];
+            }
+            if ((rc = wicca_haar_ll_u8_batch(dd.data(), n, 3, d, border, k, 1, 1, dev, (void*)cs))) return rc;
+            continue;
+        }
+        for (int64_t i = 0; i < n; ++i) {  // copies (depth <= 0) and the float tail (depth > 8)
+            bool scratch = false;
+            if ((rc = run_ll<uint8_t>(img[(size_t)i], 1, H[(size_t)i], W[(size_t)i], 3, pitch[(size_t)i], 0, d, border,
+                                      k, icon_ptr(i, u), ico_pitch[(size_t)(i * U + u)], 0, ws, cs, &scratch)))
+                return rc;
+        }
+    }
+    // source resizes (classifying_tools.py:315), every shape
+    for (AreaGroup& g : groups) {
+        if (!g.any) continue;
+        wicca::PlanParams pp{};
+        pp.imgs = (const wicca::PlanImageDev*)(dp + g.off);
+        pp.n_shapes = (int32_t)g.shapes.size();
+        pp.C = 3;
+        int max_h = 0;
+        for (int64_t i = 0; i < n; ++i) max_h = std::max(max_h, (int)H[(size_t)i]);
+        for (size_t q = 0; q < g.shapes.size(); ++q) {
+            pp.dw[q] = (int32_t)shapes[(size_t)g.shapes[q]].w;
+            pp.dh[q] = (int32_t)shapes[(size_t)g.shapes[q]].h;
+        }
+        HIP_TRY(wicca::launch_plan_hsum(pp, n, max_h, cs));
+        HIP_TRY(wicca::launch_plan_vsum(pp, n, cs));
+    }
+    for (int s = 0; s < S; ++s)
+        for (int64_t i = 0; i < n; ++i) {
+            if (hsum_off[(size_t)(s * n + i)] >= 0) continue;
+            if ((rc = run_resize(src_rp[(size_t)(s * n + i)], img[(size_t)i], pitch[(size_t)i], 0,
+                                 dout + res_off[(size_t)s] + i * ob[(size_t)s], shapes[(size_t)s].w * 3, 0, 1, cs,
+                                 ws)))
+                return rc;
+        }
+    // icon resizes (classifying_tools.py:318), one launch per shape over (depth, image)
+    for (int s = 0; s < S; ++s) {
+        if (!shape_per_image[(size_t)s]) {
+            HIP_TRY(wicca::launch_resize_desc(
+                (const wicca::ResizeParams*)(dp + o_irp) + (size_t)s * U * n, (int64_t)U * n,
+                (int)shapes[(size_t)s].h, (int)(shapes[(size_t)s].w * 3), cs));
+            continue;
+        }
+        for (int u = 0; u < U; ++u)
+            for (int64_t i = 0; i < n; ++i) {
+                const wicca::ResizeParams& q = irp[(size_t)((s * U + u) * n + i)];
+                if ((rc = run_resize(q, q.src, q.src_pitch, 0, q.dst, q.dst_pitch, 0, 1, cs, ws))) return rc;
+            }
+    }
+    // 5. the np.stack of :323 for every (shape, depth), to the caller's arrays
+    for (int s = 0; s < S; ++s) {
+        const size_t bytes = (size_t)(n * ob[(size_t)s]);
+        HIP_TRY(hipMemcpyAsync(resized[s], dout + res_off[(size_t)s], bytes, hipMemcpyDeviceToHost, cs));
+        for (int d = 0; d < n_depths; ++d)
+            HIP_TRY(hipMemcpyAsync(icons[s * n_depths + d], dout + ico_out_off[(size_t)(s * U + slot_of[(size_t)d])],
+                                   bytes, hipMemcpyDeviceToHost, cs));
+    }
+    HIP_TRY(hipStreamSynchronize(cs));
+    for (int64_t i = 0; i < n && late_status; ++i) {  // data found corrupt during the decode: zero outputs
+        late_status[i] = late[(size_t)i];
+        if (!late[(size_t)i]) continue;
+        for (int s = 0; s < S; ++s) {
+            memset(resized[s] + i * ob[(size_t)s], 0, (size_t)ob[(size_t)s]);
+            for (int d = 0; d < n_depths; ++d) memset(icons[s * n_depths + d] + i * ob[(size_t)s], 0, (size_t)ob[(size_t)s]);
+        }
+    }
+    return WICCA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int wicca_image_stage_plan_u8(const uint8_t* const* data, const int64_t* sizes, int64_t n, const int64_t* shapes,
+                              int n_shapes, const int* depths, int n_depths, int border_type, int border_constant,
+                              int interpolation, uint8_t* const* resized, uint8_t* const* icons, int device,
+                              int* status)
+{
+    if (n < 0 || (n > 0 && (!data || !sizes))) return fail(WICCA_ERR_ARG, "bad arrays");
+    if (n_shapes < 1 || n_shapes > 64 || !shapes || !resized) return fail(WICCA_ERR_ARG, "need 1..64 shapes");
+    if (n_depths < 1 || n_depths > 64 || !depths || !icons) return fail(WICCA_ERR_ARG, "need 1..64 depths");
+    std::vector<PlanShape> sh((size_t)n_shapes);
+    for (int s = 0; s < n_shapes; ++s) {
+        sh[(size_t)s].w = shapes[2 * s];
+        sh[(size_t)s].h = shapes[2 * s + 1];
+        if (sh[(size_t)s].w <= 0 || sh[(size_t)s].h <= 0 || sh[(size_t)s].w > 65535 || sh[(size_t)s].h > 65535)
+            return fail(WICCA_ERR_ARG, "bad output size for shape %d", s);
+        if (!resized[s]) return fail(WICCA_ERR_ARG, "output buffer is NULL");
+        for (int d = 0; d < n_depths; ++d)
+            if (!icons[s * n_depths + d]) return fail(WICCA_ERR_ARG, "output buffer is NULL");
+    }
+    for (int d = 0; d < n_depths; ++d)
+        if (depths[d] > 30) return fail(WICCA_ERR_ARG, "depth %d too large", depths[d]);
+    if (n == 0) return WICCA_OK;
+    if (!status) return plan_batch(data, sizes, n, sh, depths, n_depths, border_type, border_constant, interpolation,
+                                   resized, icons, device, nullptr);
+    // a file that does not parse fails its own slot (zero outputs) only
+    std::vector<int64_t> good;
+    int rc = image_files_screen(data, sizes, n, status, &good);
+    if (rc) return rc;
+    if (good.size() == (size_t)n)
+        return plan_batch(data, sizes, n, sh, depths, n_depths, border_type, border_constant, interpolation, resized,
+                          icons, device, status);
+    for (int64_t i = 0; i < n; ++i) {
+        if (!status[i]) continue;
+        for (int s = 0; s < n_shapes; ++s) {
+            const int64_t ob = sh[(size_t)s].w * sh[(size_t)s].h * 3;
+            memset(resized[s] + i * ob, 0, (size_t)ob);
+            for (int d = 0; d < n_depths; ++d) memset(icons[s * n_depths + d] + i * ob, 0, (size_t)ob);
+        }
+    }
+    const int64_t m = (int64_t)good.size();
+    if (m == 0) return WICCA_OK;
+    std::vector<const uint8_t*> gd((size_t)m);
+    std::vector<int64_t> gs((size_t)m);
+    for (int64_t j = 0; j < m; ++j) {
+        gd[(size_t)j] = data[good[(size_t)j]];
+        gs[(size_t)j] = sizes[good[(size_t)j]];
+    }
+    std::vector<std::vector<uint8_t>> tmp((size_t)n_shapes * (1 + n_depths));
+    std::vector<uint8_t*> tr((size_t)n_shapes), ti((size_t)n_shapes * n_depths);
+    for (int s = 0; s < n_shapes; ++s) {
+        const size_t bytes = (size_t)(m * sh[(size_t)s].w * sh[(size_t)s].h * 3);
+        tmp[(size_t)s * (1 + n_depths)].resize(bytes);
+        tr[(size_t)s] = tmp[(size_t)s * (1 + n_depths)].data();
+        for (int d = 0; d < n_depths; ++d) {
+            tmp[(size_t)s * (1 + n_depths) + 1 + d].resize(bytes);
+            ti[(size_t)(s * n_depths + d)] = tmp[(size_t)s * (1 + n_depths) + 1 + d].data();
+        }
+    }
+    const std::string first_err = t_last_error;
+    std::vector<int> gst((size_t)m, 0);
+    rc = plan_batch(gd.data(), gs.data(), m, sh, depths, n_depths, border_type, border_constant, interpolation,
+                    tr.data(), ti.data(), device, gst.data());
+    if (rc) return rc;
+    for (int64_t j = 0; j < m; ++j) {
+        const int64_t i = good[(size_t)j];
+        status[i] = gst[(size_t)j];
+        for (int s = 0; s < n_shapes; ++s) {
+            const int64_t ob = sh[(size_t)s].w * sh[(size_t)s].h * 3;
+            memcpy(resized[s] + i * ob, tr[(size_t)s] + j * ob, (size_t)ob);
+            for (int d = 0; d < n_depths; ++d)
+                memcpy(icons[s * n_depths + d] + i * ob, ti[(size_t)(s * n_depths + d)] + j * ob, (size_t)ob);
+        }
+    }
+    t_last_error = first_err;
+    return WICCA_OK;
+}
+
+}  // extern "C"

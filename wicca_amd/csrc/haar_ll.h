@@ -230,6 +230,18 @@ struct LLParams {
 // uniform batch, by block ranges for a ragged one).
 constexpr int64_t max_grid_blocks(int threads) { return (((int64_t)1 << 32) - 1) / threads; }
 
+// One image of a ragged multi-depth batch (device array): its geometry, its
+// first block in the launch's block order, and its icon buffers per depth.
+struct MultiImageDev {
+    const uint8_t* src;
+    int64_t src_pitch, H, W;
+    int64_t blk0;      // first block of this image (prefix over the batch)
+    int32_t n_groups;  // groups of 4 wave strips per band (bands = blocks / n_groups)
+    int32_t pad_;
+    uint8_t* dst[9];
+    int64_t dst_pitch[9];
+};
+
 // Multi-depth kernel parameters (icons of every wanted depth from one read).
 struct MultiParams {
     const uint8_t* src;
@@ -243,6 +255,13 @@ struct MultiParams {
     uint32_t k;
     uint8_t* dst[9];   // per depth t: icon base, row pitch, image stride
     int64_t dst_pitch[9], dst_stride[9];
+    // ragged batch (launch_multi_ragged): n_images descriptors, the group map
+    // (first image of every group of 2^map_shift blocks) and the first block
+    // of this launch (grids split at the HIP limit)
+    const MultiImageDev* imgs;
+    const uint32_t* blk_map;
+    int32_t map_shift;
+    uint32_t block_base;
 };
 // K5 flush window (level-DMIN blocks): 8 at DMIN = 1 (depths 1-6 +1.5 %), 16
 // otherwise (depths 2-6: 8 was -1.7 %; profiles/r02_ab_fw_*.json).
@@ -254,6 +273,14 @@ constexpr int multi_fw(int dmin) { return WICCA_MULTI_FW > 0 ? WICCA_MULTI_FW : 
 bool multi_kernel_ok(const uint8_t* src, int64_t src_pitch, int64_t src_stride, int64_t W, int C,
                      int dmin, int dmax);
 hipError_t launch_multi(MultiParams p, int dmin, int C, hipStream_t s);
+
+// Ragged multi-depth batch (C = 3, every image 16-B aligned): p.imgs /
+// p.blk_map / p.map_shift / p.n_images / p.dmax / p.want / border / k set;
+// total_blocks = the blocks of every image (multi_bands * multi_groups each).
+constexpr int kMultiRaggedC = 3;
+int32_t multi_groups(int64_t W, int C, int dmax);   // strip groups per band
+int64_t multi_bands(int64_t H, int dmax);           // bands of 2^dmax rows
+hipError_t launch_multi_ragged(const MultiParams& p, int dmin, int64_t total_blocks, hipStream_t s);
 
 // Name of the kernel launch_block_sum<uint8_t> dispatches for an aligned
 // (uniform or ragged) batch at depth L with C channels, as rocprofv3 prints it

@@ -20,6 +20,19 @@ WICCA_MULTI_EXTERN(5)
 WICCA_MULTI_EXTERN(6)
 WICCA_MULTI_EXTERN(7)
 #undef WICCA_MULTI_EXTERN
+// the ragged (per-image descriptor) kernels, C = 3, in haar_multi_ragged.hip
+#define WICCA_MULTI_RAGGED_EXTERN(D) \
+    extern template hipError_t launch_multi_ragged_dc<D, kMultiRaggedC>(int, const MultiParams&, int64_t, hipStream_t);
+#if WICCA_MULTI_D1
+WICCA_MULTI_RAGGED_EXTERN(1)
+#endif
+WICCA_MULTI_RAGGED_EXTERN(2)
+WICCA_MULTI_RAGGED_EXTERN(3)
+WICCA_MULTI_RAGGED_EXTERN(4)
+WICCA_MULTI_RAGGED_EXTERN(5)
+WICCA_MULTI_RAGGED_EXTERN(6)
+WICCA_MULTI_RAGGED_EXTERN(7)
+#undef WICCA_MULTI_RAGGED_EXTERN
 
 template <int C>
 static hipError_t launch_multi_c(int dmin, const MultiParams& p, int64_t blocks, hipStream_t s)
@@ -45,13 +58,54 @@ bool multi_kernel_ok(const uint8_t* src, int64_t src_pitch, int64_t src_stride, 
            W * C < ((int64_t)1 << 30) && aligned16(src, src_pitch, src_stride);
 }
 
+int32_t multi_groups(int64_t W, int C, int dmax)
+{
+    const int64_t R = (int64_t)1 << dmax;
+    const int64_t Wp = (W + R - 1) / R * R;
+    const int64_t strip = 64 * strip_lane_pixels(C);
+    return (int32_t)(((Wp + strip - 1) / strip + kMultiWaves - 1) / kMultiWaves);
+}
+
+int64_t multi_bands(int64_t H, int dmax)
+{
+    const int64_t R = (int64_t)1 << dmax;
+    return (H + R - 1) / R;
+}
+
+hipError_t launch_multi_ragged(const MultiParams& p, int dmin, int64_t total_blocks, hipStream_t s)
+{
+    if (total_blocks <= 0 || p.n_images <= 0) return hipSuccess;
+    if (!p.imgs || !p.blk_map || dmin < (WICCA_MULTI_D1 ? 1 : 2) || dmin >= p.dmax || p.dmax > 8)
+        return hipErrorInvalidValue;
+    const int64_t kMax = max_grid_blocks(64 * kMultiWaves);
+    for (int64_t b0 = 0; b0 < total_blocks; b0 += kMax) {
+        MultiParams q = p;
+        q.block_base = (uint32_t)b0;
+        const int64_t blocks = std::min(kMax, total_blocks - b0);
+        hipError_t e;
+        switch (dmin) {
+#if WICCA_MULTI_D1
+        case 1: e = launch_multi_ragged_dc<1, kMultiRaggedC>(q.dmax, q, blocks, s); break;
+#endif
+        case 2: e = launch_multi_ragged_dc<2, kMultiRaggedC>(q.dmax, q, blocks, s); break;
+        case 3: e = launch_multi_ragged_dc<3, kMultiRaggedC>(q.dmax, q, blocks, s); break;
+        case 4: e = launch_multi_ragged_dc<4, kMultiRaggedC>(q.dmax, q, blocks, s); break;
+        case 5: e = launch_multi_ragged_dc<5, kMultiRaggedC>(q.dmax, q, blocks, s); break;
+        case 6: e = launch_multi_ragged_dc<6, kMultiRaggedC>(q.dmax, q, blocks, s); break;
+        case 7: e = launch_multi_ragged_dc<7, kMultiRaggedC>(q.dmax, q, blocks, s); break;
+        default: e = hipErrorInvalidValue;
+        }
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_multi(MultiParams p, int dmin, int C, hipStream_t s)
 {
     const int64_t R = (int64_t)1 << p.dmax;
-    const int64_t Hp = (p.H + R - 1) / R * R, Wp = (p.W + R - 1) / R * R;
-    const int64_t strip = 64 * strip_lane_pixels(C);
+    const int64_t Hp = (p.H + R - 1) / R * R;
     p.n_bands = Hp / R;
-    p.n_groups = (int32_t)(((Wp + strip - 1) / strip + kMultiWaves - 1) / kMultiWaves);
+    p.n_groups = multi_groups(p.W, C, p.dmax);
     const int64_t per_image = p.n_bands * p.n_groups;
     if (per_image <= 0 || p.n_images <= 0) return hipSuccess;
     // at most max_grid_blocks per launch (HIP's grid limit): image ranges

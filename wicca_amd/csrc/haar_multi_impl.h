@@ -371,8 +371,11 @@ __device__ __forceinline__ void multi_wave_dot(const MultiParams& p, const Multi
     }
 }
 
+// One workgroup's work: strip group g of band `band` of image `img` (p holds
+// that image's geometry; img indexes the uniform batch's strides, 0 for a
+// ragged batch, whose kernel fills p from the image's descriptor).
 template <int DMIN, int DMAX, int C>
-__global__ __launch_bounds__(64 * kMultiWaves) void haar_multi_kernel(MultiParams p)
+__device__ __forceinline__ void haar_multi_body(const MultiParams& p, int g, int band, int img)
 {
     using Geo = StripGeom<C>;
     constexpr int NDW = Geo::NDW, STRIP = Geo::STRIP;
@@ -380,11 +383,6 @@ __global__ __launch_bounds__(64 * kMultiWaves) void haar_multi_kernel(MultiParam
     constexpr int CH = SB < 8 ? SB : 8;        // rows per load chunk (divides SB)
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    uint32_t b = logical_block(blockIdx.x, gridDim.x);
-    const int g = (int)(b % (uint32_t)p.n_groups);
-    b /= (uint32_t)p.n_groups;
-    const int band = (int)(b % (uint32_t)p.n_bands);
-    const int img = (int)(b / (uint32_t)p.n_bands);
     constexpr int R = 1 << DMAX;
     const int64_t Wp = ((p.W + R - 1) >> DMAX) << DMAX;
     using MS = MultiStage<DMIN, DMAX, C>;
@@ -461,11 +459,66 @@ __global__ __launch_bounds__(64 * kMultiWaves) void haar_multi_kernel(MultiParam
 }
 
 template <int DMIN, int DMAX, int C>
+__global__ __launch_bounds__(64 * kMultiWaves) void haar_multi_kernel(MultiParams p)
+{
+    uint32_t b = logical_block(blockIdx.x, gridDim.x);
+    const int g = (int)(b % (uint32_t)p.n_groups);
+    b /= (uint32_t)p.n_groups;
+    const int band = (int)(b % (uint32_t)p.n_bands);
+    const int img = (int)(b / (uint32_t)p.n_bands);
+    haar_multi_body<DMIN, DMAX, C>(p, g, band, img);
+}
+
+// Ragged batch (the file stage's decoded images, every size): the block's
+// image comes from the group map (first image of each group of 2^map_shift
+// blocks) and a scalar step along the images' first blocks, read through the
+// scalar cache as K1's ragged lookup does; the image's geometry and icon
+// buffers replace the uniform fields.
+template <int DMIN, int DMAX, int C>
+__global__ __launch_bounds__(64 * kMultiWaves) void haar_multi_ragged_kernel(MultiParams p0)
+{
+    typedef __attribute__((address_space(4))) const MultiImageDev* cimg;
+    typedef __attribute__((address_space(4))) const uint32_t* cmap;
+    const uint32_t b = logical_block(blockIdx.x, gridDim.x) + p0.block_base;
+    const cimg imgs = (cimg)p0.imgs;
+    int i = (int)((cmap)p0.blk_map)[b >> p0.map_shift];
+    while (i + 1 < (int)p0.n_images && imgs[i + 1].blk0 <= (int64_t)b) ++i;
+    i = __builtin_amdgcn_readfirstlane(i);
+    const uint32_t local = b - (uint32_t)imgs[i].blk0;
+    const uint32_t ng = (uint32_t)imgs[i].n_groups;
+    MultiParams p = p0;
+    p.src = imgs[i].src;
+    p.src_pitch = imgs[i].src_pitch;
+    p.src_image_stride = 0;
+    p.H = imgs[i].H;
+    p.W = imgs[i].W;
+    p.n_images = 1;
+#pragma unroll
+    for (int t = DMIN; t <= DMAX; ++t) {
+        p.dst[t] = imgs[i].dst[t];
+        p.dst_pitch[t] = imgs[i].dst_pitch[t];
+        p.dst_stride[t] = 0;
+    }
+    haar_multi_body<DMIN, DMAX, C>(p, (int)(local % ng), (int)(local / ng), 0);
+}
+
+template <int DMIN, int DMAX, int C>
 inline hipError_t launch_multi_k(const MultiParams& p, int64_t blocks, hipStream_t s)
 {
     if constexpr (DMIN < DMAX) {
         hipLaunchKernelGGL((haar_multi_kernel<DMIN, DMAX, C>), dim3((uint32_t)blocks), dim3(64 * kMultiWaves),
                            0, s, p);
+        return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+}
+
+template <int DMIN, int DMAX, int C>
+inline hipError_t launch_multi_ragged_k(const MultiParams& p, int64_t blocks, hipStream_t s)
+{
+    if constexpr (DMIN < DMAX) {
+        hipLaunchKernelGGL((haar_multi_ragged_kernel<DMIN, DMAX, C>), dim3((uint32_t)blocks),
+                           dim3(64 * kMultiWaves), 0, s, p);
         return hipGetLastError();
     }
     return hipErrorInvalidValue;
@@ -482,6 +535,21 @@ hipError_t launch_multi_dc(int dmax, const MultiParams& p, int64_t blocks, hipSt
     case 6: return launch_multi_k<DMIN, 6, C>(p, blocks, s);
     case 7: return launch_multi_k<DMIN, 7, C>(p, blocks, s);
     case 8: return launch_multi_k<DMIN, 8, C>(p, blocks, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <int DMIN, int C>
+hipError_t launch_multi_ragged_dc(int dmax, const MultiParams& p, int64_t blocks, hipStream_t s)
+{
+    switch (dmax) {
+    case 2: return launch_multi_ragged_k<DMIN, 2, C>(p, blocks, s);
+    case 3: return launch_multi_ragged_k<DMIN, 3, C>(p, blocks, s);
+    case 4: return launch_multi_ragged_k<DMIN, 4, C>(p, blocks, s);
+    case 5: return launch_multi_ragged_k<DMIN, 5, C>(p, blocks, s);
+    case 6: return launch_multi_ragged_k<DMIN, 6, C>(p, blocks, s);
+    case 7: return launch_multi_ragged_k<DMIN, 7, C>(p, blocks, s);
+    case 8: return launch_multi_ragged_k<DMIN, 8, C>(p, blocks, s);
     default: return hipErrorInvalidValue;
     }
 }

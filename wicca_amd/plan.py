@@ -1,0 +1,319 @@
+"""The stage plan: ``ClassifierProcessor``'s whole (classifier x depth) matrix
+of ``_get_img_batch`` computed ONCE per file.
+
+The reference recomputes the per-file stage for every classifier and every
+depth: ``process_classifiers`` loops over the depths
+(``/root/reference/wicca/classifying_tools.py:546-551``), ``_parallel_proc``
+submits one pool task per classifier (``:414-419``), each task's ``_classify``
+walks the folder in batches (``:339-346``), and ``_get_img_batch`` decodes,
+resizes, icons and resizes again every file of the batch (``:312-318``).  With
+the demo's 14 classifiers and 5 depths every file is decoded 70 times.
+
+:class:`StagePlan` is shared by those pool threads.  The first request for a
+batch computes, in one native call (``wicca_image_stage_plan_u8``), the
+outputs of every (shape, depth) pair the plan was given: each file is decoded
+into HBM once, read once for the icons of all depths and once for the
+INTER_AREA source resizes of all shapes, and every icon is resized to every
+shape.  Later requests for the same batch — the other classifiers, the later
+depths — are served from host memory.  A request for a pair the plan was not
+given falls back to the per-call file stage (:func:`wicca_amd.get_img_batch`),
+so the plan is never wrong, only sometimes not faster.
+
+Drop-in (``ClassifierProcessor`` itself unchanged; a subclass or a
+monkeypatch of one method)::
+
+    plan = StagePlan([c[SHAPE] for c in classifiers.values()], proc.depth,
+                     interpolation=proc.interpolation)
+    proc._get_img_batch = lambda paths, shape: plan.get_img_batch(paths, shape, proc.depth)
+
+(``proc.depth`` is the int ``process_classifiers`` sets before each depth's
+pool, ``classifying_tools.py:546-547``.)
+
+Every output is the bytes :func:`wicca_amd.get_img_batch` gives for that
+(shape, depth) (``tests/test_gpu_plan.py``).
+"""
+from __future__ import annotations
+
+import collections
+import ctypes
+import threading
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import _lib
+
+Shape = tuple  # (width, height): cv2.resize's dsize order, as classifier[SHAPE]
+
+
+def _norm_shape(shape) -> tuple[int, int]:
+    w, h = int(shape[0]), int(shape[1])
+    return (w, h)
+
+
+def _norm_depths(depths) -> tuple[int, ...]:
+    from .coder import _depth_index
+    if isinstance(depths, (tuple, list, range)):
+        out = []
+        for d in depths:
+            d = _depth_index(d)
+            if d not in out:
+                out.append(d)
+        return tuple(out)
+    return (_depth_index(depths),)
+
+
+def _read(paths: Sequence) -> list[bytes]:
+    blobs = []
+    for p in paths:
+        if not p:
+            raise ValueError("File path cannot be empty")
+        with open(p, "rb") as f:
+            blobs.append(f.read())
+    if not blobs:
+        raise ValueError("need at least one array to stack")
+    return blobs
+
+
+def get_img_matrix(file_paths: Sequence, shapes: Iterable, depths, interpolation: int = 3, border_type: int = 1,
+                   border_constant: int = 0, device: int | None = None,
+                   errors: str = "raise") -> dict:
+    """``_get_img_batch(file_paths, shape)`` at ``self.depth = depth`` for every
+    (shape, depth) pair, from one native call: ``{(shape, depth): (batch_images,
+    batch_icons)}`` with ``shape = (width, height)``.  errors: as
+    :func:`wicca_amd.get_img_batch` ("raise" or "zero")."""
+    from .coder import _border_value
+    from .jpeg import _load_error, _slot_error
+    if errors not in ("raise", "zero"):
+        raise ValueError("errors must be 'raise' or 'zero'")
+    shp = []
+    for s in shapes:
+        s = _norm_shape(s)
+        if s not in shp:
+            shp.append(s)
+    if not shp:
+        raise ValueError("need at least one shape")
+    dep = _norm_depths(depths)
+    if not dep:
+        raise ValueError("need at least one depth")
+    blobs = _read(file_paths)
+    n = len(blobs)
+    keep = [np.frombuffer(b, np.uint8) for b in blobs]
+    ptrs = (ctypes.c_void_p * n)(*[k.ctypes.data for k in keep])
+    sizes = (ctypes.c_int64 * n)(*[k.size for k in keep])
+    resized = [np.empty((n, h, w, 3), np.uint8) for (w, h) in shp]
+    icons = [[np.empty((n, h, w, 3), np.uint8) for _ in dep] for (w, h) in shp]
+    c_shapes = (ctypes.c_int64 * (2 * len(shp)))(*[v for s in shp for v in s])
+    c_depths = (ctypes.c_int * len(dep))(*dep)
+    c_res = (ctypes.c_void_p * len(shp))(*[r.ctypes.data for r in resized])
+    c_ico = (ctypes.c_void_p * (len(shp) * len(dep)))(*[a.ctypes.data for row in icons for a in row])
+    k = _border_value(border_constant) if int(border_type) == 0 else 0
+    status = (ctypes.c_int * n)() if errors == "zero" else None
+    _lib.check(_lib.load().wicca_image_stage_plan_u8(
+        ptrs, sizes, n, c_shapes, len(shp), c_depths, len(dep), int(border_type), k, int(interpolation),
+        c_res, c_ico, -1 if device is None else int(device), status))
+    del keep
+    if status is not None:
+        for i in range(n):
+            if status[i] != 0:  # as load_image reports it (data_loader.py:61-63)
+                print(f"Error loading image {file_paths[i]}: {_load_error(_slot_error(blobs[i]))}")
+    out = {}
+    for si, s in enumerate(shp):
+        for di, d in enumerate(dep):
+            out[(s, d)] = (resized[si], icons[si][di])
+    return out
+
+
+class _Entry:
+    __slots__ = ("event", "result", "error", "nbytes", "served")
+
+    def __init__(self):
+        self.event = threading.Event()
+        self.result = None
+        self.error = None
+        self.nbytes = 0
+        self.served = collections.Counter()
+
+
+class StagePlan:
+    """Shared, thread-safe cache of the stage matrix, keyed by batch.
+
+    shapes: the classifiers' input shapes, one per classifier (repeats count:
+        a (shape, depth) pair is expected once per classifier with that shape,
+        and a batch is dropped once every expected request was served);
+    depths: int / tuple / list / range (``normalize_depth``'s forms);
+    batches: optional, the folder's batches in ``_classify``'s order
+        (``os.listdir`` in steps of ``batch_size``): after a batch is computed
+        the next one is computed in the background, so its decode overlaps the
+        classifiers' inference;
+    devices: optional GPU ids; batch k of ``batches`` (or the k-th new batch)
+        runs on ``devices[k % len(devices)]``;
+    cache_bytes: the most host memory the cached outputs may hold (least
+        recently used batches are dropped first, and recomputed if asked again);
+    copy: hand each request its own arrays (the cached ones are never exposed).
+    """
+
+    def __init__(self, shapes: Iterable, depths, interpolation: int = 3, border_type: int = 1,
+                 border_constant: int = 0, *, batches: Sequence[Sequence] | None = None,
+                 device: int | None = None, devices: Sequence[int] | None = None, errors: str = "raise",
+                 cache_bytes: int = 32 << 30, copy: bool = True):
+        self.expected = collections.Counter(_norm_shape(s) for s in shapes)
+        if not self.expected:
+            raise ValueError("need at least one shape")
+        self.shapes = list(self.expected)
+        self.depths = _norm_depths(depths)
+        self.interpolation = int(interpolation)
+        self.border_type = int(border_type)
+        self.border_constant = border_constant
+        self.device = device
+        self.devices = list(devices) if devices else None
+        self.errors = errors
+        self.cache_bytes = int(cache_bytes)
+        self.copy = copy
+        self._order = {}
+        self._batches = [list(b) for b in batches] if batches is not None else None
+        if self._batches is not None:
+            for i, b in enumerate(self._batches):
+                self._order.setdefault(self._key(b), i)
+        self._lock = threading.Lock()
+        self._entries: collections.OrderedDict = collections.OrderedDict()
+        self._bytes = 0
+        self._new = 0
+        self._prefetch = None
+        self._retired = set()  # batches every expected request was served from (never prefetched again)
+        self._matrix = get_img_matrix  # the native call (tests inject a stand-in)
+        self.stats = collections.Counter()
+
+    @staticmethod
+    def _key(paths) -> tuple:
+        return tuple(str(p) for p in paths)
+
+    def _device_for(self, key) -> int | None:
+        if not self.devices:
+            return self.device
+        idx = self._order.get(key)
+        if idx is None:
+            idx = self._new
+            self._new += 1
+        return self.devices[idx % len(self.devices)]
+
+    def _compute(self, key, entry: _Entry, device) -> None:
+        try:
+            entry.result = self._matrix(list(key), self.shapes, self.depths, self.interpolation,
+                                        self.border_type, self.border_constant, device, self.errors)
+            # a shape's resized images are shared by its depths: count each array once
+            entry.nbytes = sum({id(a): a.nbytes for pair in entry.result.values() for a in pair}.values())
+        except BaseException as e:  # every requester of the batch sees the same failure
+            entry.error = e
+        finally:
+            with self._lock:
+                self.stats["computed"] += 1
+                if entry.result is not None and self._entries.get(key) is entry:
+                    self._bytes += entry.nbytes
+                    self._trim(keep=key)
+            entry.event.set()
+
+    def _trim(self, keep) -> None:
+        # lock held: drop least recently used finished batches above the cap
+        for k in list(self._entries):
+            if self._bytes <= self.cache_bytes:
+                break
+            e = self._entries[k]
+            if k == keep or not e.event.is_set():
+                continue
+            del self._entries[k]
+            self._bytes -= e.nbytes if e.result is not None else 0
+            self.stats["evicted"] += 1
+
+    def _start_prefetch(self, key) -> None:
+        idx = self._order.get(key)
+        if idx is None or idx + 1 >= len(self._batches):
+            return
+        nxt = self._key(self._batches[idx + 1])
+        with self._lock:
+            if nxt in self._entries or nxt in self._retired or (
+                    self._prefetch is not None and self._prefetch.is_alive()):
+                return
+            entry = _Entry()
+            self._entries[nxt] = entry
+            dev = self._device_for(nxt)
+            t = threading.Thread(target=self._compute, args=(nxt, entry, dev), daemon=True)
+            self._prefetch = t
+        self.stats["prefetched"] += 1
+        t.start()
+
+    def entry(self, file_paths) -> _Entry:
+        """The (computed) cache entry of a batch; computes it on first use."""
+        key = self._key(file_paths)
+        with self._lock:
+            entry = self._entries.get(key)
+            owner = entry is None
+            if owner:
+                entry = _Entry()
+                self._entries[key] = entry
+                dev = self._device_for(key)
+                self.stats["misses"] += 1
+            else:
+                self._entries.move_to_end(key)
+                self.stats["hits"] += 1
+        if owner:
+            self._compute(key, entry, dev)
+        else:
+            entry.event.wait()
+        if self._batches is not None:
+            self._start_prefetch(key)
+        return entry
+
+    def get_img_batch(self, file_paths, shape, transform_depth) -> tuple[np.ndarray, np.ndarray]:
+        """``ClassifierProcessor._get_img_batch(file_paths, shape)`` at
+        ``self.depth = transform_depth`` (classifying_tools.py:297-323)."""
+        from .coder import _depth_index
+        s = _norm_shape(shape)
+        d = _depth_index(transform_depth)
+        if s not in self.expected or d not in self.depths:  # not planned: the per-call stage
+            from .jpeg import get_img_batch
+            self.stats["unplanned"] += 1
+            return get_img_batch(list(file_paths), s, d, self.interpolation, self.border_type,
+                                 self.border_constant, self.device, errors=self.errors)
+        key = self._key(file_paths)
+        entry = self.entry(file_paths)
+        if entry.error is not None:
+            raise entry.error
+        images, icons = entry.result[(s, d)]
+        out = (images.copy(), icons.copy()) if self.copy else (images, icons)
+        with self._lock:
+            entry.served[(s, d)] += 1
+            done = all(entry.served[(sh, dd)] >= self.expected[sh] for sh in self.expected for dd in self.depths)
+            if done and self._entries.get(key) is entry:
+                del self._entries[key]
+                self._bytes -= entry.nbytes
+                self._retired.add(key)
+                self.stats["retired"] += 1
+        return out
+
+    def cached_batches(self) -> int:
+        with self._lock:
+            return len(self._entries)
+
+    def cached_bytes(self) -> int:
+        with self._lock:
+            return self._bytes
+
+    def close(self) -> None:
+        """Wait for a background batch and drop the cache."""
+        t = self._prefetch
+        if t is not None:
+            t.join()
+        with self._lock:
+            self._entries.clear()
+            self._retired.clear()
+            self._bytes = 0
+
+
+def folder_batches(folder, batch_size: int = 25) -> list[list]:
+    """``_classify``'s batches of a folder: ``os.listdir`` order in steps of
+    ``batch_size`` (classifying_tools.py:335-340), as full paths."""
+    import os
+    names = os.listdir(folder)
+    return [[os.path.join(str(folder), f) for f in names[i:i + batch_size]]
+            for i in range(0, len(names), batch_size)]
