@@ -53,6 +53,8 @@ def parse():
                          "png / bmp: the same for 8K PNG (zlib level 6) / 24-bit BMP files")
     ap.add_argument("--quality", type=int, default=90, help="--config jpeg: encoder quality")
     ap.add_argument("--shape", default="224,224", help="--config stage: classifier input (w,h)")
+    ap.add_argument("--plan-no-loop", action="store_true",
+                    help="--config plan: skip the per-call loop and its check (profiling runs)")
     ap.add_argument("--interpolation", type=int, default=3, help="--config stage: cv2.INTER_*")
     ap.add_argument("--depths", default="1,2,3,4,5,6", help="depth list of --config multi")
     ap.add_argument("--steps", type=int, default=20)
@@ -711,16 +713,18 @@ def run_plan(args, torch, rank):
         _lib.check(lib.wicca_image_icon_stage_u8(ptrs, sizes, B, d, 1, 0, sh[0], sh[1], args.interpolation,
                                                  r.ctypes.data, c.ctypes.data, -1, None))
 
-    per_call(shapes[0], depths[0])
-    loop_steps = max(1, min(args.steps, 2))
-    t0 = time.perf_counter()
-    for _ in range(loop_steps):
-        for d in depths:
-            for sh in DEMO_CLASSIFIERS:
-                per_call(sh, d)
-    loop_s = (time.perf_counter() - t0) / loop_steps
+    loop_s = float("nan")
+    if not args.plan_no_loop:
+        per_call(shapes[0], depths[0])
+        loop_steps = max(1, min(args.steps, 2))
+        t0 = time.perf_counter()
+        for _ in range(loop_steps):
+            for d in depths:
+                for sh in DEMO_CLASSIFIERS:
+                    per_call(sh, d)
+        loop_s = (time.perf_counter() - t0) / loop_steps
     verified = None
-    if not args.no_verify:
+    if not args.no_verify and not args.plan_no_loop:
         verified = True
         for si, sh in enumerate(shapes):
             for di, d in enumerate(depths):
@@ -741,10 +745,10 @@ def run_plan(args, torch, rank):
                 "every output copied to host arrays inside the timed region",
         "config": {"workload": f"{B} x {W}x{H} JPEG files, shapes {shapes} (14 classifiers), depths {depths}",
                    "images": B, "classifiers": len(DEMO_CLASSIFIERS), "depths": depths, "pairs": pairs},
-        "per_call_loop": {"ms_per_batch": round(loop_s * 1e3, 3),
+        "per_call_loop": {"ms_per_batch": round(loop_s * 1e3, 3) if loop_s == loop_s else None,
                           "what": f"wicca_image_icon_stage_u8 once per (classifier, depth): {pairs} calls, "
                                   "each decoding, resizing and iconing the whole batch (the reference's structure)"},
-        "speedup_vs_per_call": round(loop_s / plan_s, 2),
+        "speedup_vs_per_call": round(loop_s / plan_s, 2) if loop_s == loop_s else None,
         "decoded_MP_per_s": round(mpix / plan_s, 1),
         "verified_vs_per_call": verified, "roofline": None, "cpu_baseline": None,
     }

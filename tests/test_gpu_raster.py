@@ -363,3 +363,19 @@ def test_decode_batches_mixed_formats(tmp_path):
     for batch, outs in zip(batches, got):
         for b, t in zip(batch, outs):
             assert np.array_equal(t.cpu().numpy(), WJ.decode(b))
+
+
+def test_gif_oversized_frame_descriptor_is_cheap():
+    """A 1x1 canvas whose image descriptor claims a 65535 x 65535 frame (ADVICE
+    r03): the host decode holds one stream row at a time, so the file decodes
+    in well under a second to the canvas pixel the stream reaches."""
+    import time
+    idx = np.array([[1, 0, 1]], np.uint8)
+    pal = np.array([[10, 20, 30], [200, 100, 50]], np.uint8)
+    data = bytearray(rr.encode_gif(idx, pal, screen=(1, 1)))
+    k = data.index(b"\x2c")
+    data[k + 5:k + 9] = struct.pack("<HH", 65535, 65535)  # frame width / height
+    t0 = time.perf_counter()
+    got = WJ.decode(bytes(data))
+    assert time.perf_counter() - t0 < 5.0
+    assert got.shape == (1, 1, 3) and got[0, 0].tolist() == [200, 100, 50]

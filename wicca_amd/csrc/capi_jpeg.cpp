@@ -677,6 +677,32 @@ struct AsyncStage {
 std::mutex g_stage_mu;
 std::unordered_map<int64_t, std::unique_ptr<AsyncStage>> g_stage;
 int64_t g_stage_next = 1;
+
+// Tickets never waited for (a loader generator left unfinished at interpreter
+// exit): their workers are joined and streams drained from an atexit handler,
+// registered after the HIP runtime was loaded and so run before its teardown,
+// not by g_stage's static destructor (whose order against the runtime's is
+// unspecified).
+void drain_stage_tickets()
+{
+    std::unordered_map<int64_t, std::unique_ptr<AsyncStage>> left;
+    {
+        std::lock_guard<std::mutex> g(g_stage_mu);
+        left.swap(g_stage);
+    }
+    for (auto& kv : left) {
+        AsyncStage* a = kv.second.get();
+        if (a->worker.joinable()) a->worker.join();
+        if (a->stream) (void)hipStreamSynchronize(a->stream);
+    }
+    left.clear();
+}
+
+void register_stage_drain()
+{
+    static std::once_flag once;
+    std::call_once(once, [] { std::atexit(drain_stage_tickets); });
+}
 std::mutex g_async_mu;
 std::unordered_map<int64_t, std::unique_ptr<AsyncDecode>> g_async;
 int64_t g_async_next = 1;
@@ -719,7 +745,12 @@ int wicca_jpeg_decode_u8_async(const uint8_t* const* data, const int64_t* sizes,
     st->ready = t_async_ready;
     st->done = t_async_done;
     st->issue_ms = now_ms() - t0;
-    if ((rc = serial_record(dev, st->stream))) return rc;
+    if ((rc = serial_record(dev, st->stream))) {
+        // the decode is in flight from this workspace's pinned staging: wait
+        // before the lease goes back to the pool
+        (void)hipStreamSynchronize(st->stream);
+        return rc;
+    }
     st->data.assign(data, data + n);
     st->sizes.assign(sizes, sizes + n);
     st->dsts.assign(dsts, dsts + n);
@@ -1166,6 +1197,7 @@ int wicca_image_icon_stage_async(const uint8_t* const* data, const int64_t* size
                 a->worker_err = e.what();
             }
         });
+        register_stage_drain();
         std::lock_guard<std::mutex> g(g_stage_mu);
         const int64_t id = g_stage_next++;
         g_stage[id] = std::move(st);
@@ -1223,6 +1255,7 @@ int wicca_image_icon_stage_async(const uint8_t* const* data, const int64_t* size
     st->out_h = out_h;
     st->resized = resized;
     st->icons = resized_icons;
+    register_stage_drain();
     std::lock_guard<std::mutex> g(g_stage_mu);
     const int64_t id = g_stage_next++;
     g_stage[id] = std::move(st);

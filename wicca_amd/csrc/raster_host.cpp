@@ -635,12 +635,25 @@ int parse_gif(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
 }
 
 // The first image's indices (fw x fh, in stream row order), LZW-decoded from
-// the sub-blocks at lzw_off.  A stream that ends early leaves the rest 0
-// (-1 only when not even one code is present).
-int gif_lzw(const uint8_t* d, size_t n, const RasterInfo& f, std::vector<uint8_t>& idx, std::string* err)
+// the sub-blocks at lzw_off and handed over one stream row at a time
+// (emit(r, row)): only one row is held, whatever size the image descriptor
+// claims (a 1x1 canvas with a 65535 x 65535 frame must not allocate 4 GiB).
+// A stream that ends early leaves the rest 0 (-1 only when not even one code
+// is present).
+template <class Emit>
+int gif_lzw(const uint8_t* d, size_t n, const RasterInfo& f, Emit&& emit, std::string* err)
 {
-    const size_t need = (size_t)(f.fw * f.fh);
-    idx.assign(need, 0);
+    const size_t fw = (size_t)f.fw, need = (size_t)f.fw * (size_t)f.fh;
+    std::vector<uint8_t> row(std::max<size_t>(fw, 1), 0);
+    size_t col = 0;
+    int64_t r = 0;
+    auto put = [&](uint8_t v) {
+        row[col++] = v;
+        if (col == fw) {
+            emit(r++, row.data());
+            col = 0;
+        }
+    };
     std::vector<uint16_t> prefix(4096);
     std::vector<uint8_t> suffix(4096), first(4096);
     std::vector<uint16_t> length(4096);
@@ -683,7 +696,8 @@ int gif_lzw(const uint8_t* d, size_t n, const RasterInfo& f, std::vector<uint8_t
             uint8_t fb;
             if (old < 0) {
                 if (code >= clear) return bad(err, -1, "GIF: corrupt LZW data");
-                idx[op++] = (uint8_t)code;
+                put((uint8_t)code);
+                ++op;
                 old = code;
                 continue;
             }
@@ -701,8 +715,14 @@ int gif_lzw(const uint8_t* d, size_t n, const RasterInfo& f, std::vector<uint8_t
                 stack[sp++] = suffix[c];
                 if (length[c] == 1) break;
             }
-            while (sp && op < need) idx[op++] = stack[--sp];
-            if (code == next && op < need) idx[op++] = fb;
+            while (sp && op < need) {
+                put(stack[--sp]);
+                ++op;
+            }
+            if (code == next && op < need) {
+                put(fb);
+                ++op;
+            }
             if (next < 4096) {
                 prefix[next] = (uint16_t)old;
                 suffix[next] = fb;
@@ -716,42 +736,49 @@ int gif_lzw(const uint8_t* d, size_t n, const RasterInfo& f, std::vector<uint8_t
     }
 out:
     if (!codes) return bad(err, -1, "GIF: no image data");
+    if (fw > 0) {  // the rows the data did not reach: index 0
+        if (col > 0) {
+            std::fill(row.begin() + (std::ptrdiff_t)col, row.end(), (uint8_t)0);
+            emit(r++, row.data());
+        }
+        std::fill(row.begin(), row.end(), (uint8_t)0);
+        for (; r < f.fh; ++r) emit(r, row.data());
+    }
     return 0;
 }
 
 int unpack_gif(const uint8_t* data, size_t size, const RasterInfo& f, const RasterLayout& lay, uint8_t* out,
                std::string* err)
 {
-    std::vector<uint8_t> idx;
-    if (gif_lzw(data, size, f, idx, err)) return -1;
     memset(out, 0, (size_t)lay.bytes);  // the canvas starts black
     const int64_t pitch = lay.pass_pitch[0];
-    // stream row r -> image row (the 4 interlace passes: every 8th from 0, from 4, every 4th from 2, odd rows)
-    int64_t r = 0;
-    auto place = [&](int64_t y) {
-        const int64_t cy = f.fy + y;
-        if (cy < f.H) {
-            uint8_t* row = out + cy * pitch;
-            const uint8_t* src = idx.data() + r * f.fw;
-            for (int64_t x = 0; x < f.fw && f.fx + x < f.W; ++x) {
-                const int k = src[x];
-                if (k == f.transparent) continue;
-                uint8_t* px = row + 3 * (f.fx + x);
-                px[0] = f.pal[k][0];
-                px[1] = f.pal[k][1];
-                px[2] = f.pal[k][2];
-            }
-        }
-        ++r;
+    // stream row r -> image row y (the 4 interlace passes: every 8th from 0,
+    // from 4, every 4th from 2, the odd rows), then onto the canvas at (fx, fy)
+    const int64_t fh = f.fh;
+    const int64_t n8 = (fh + 7) / 8, n4 = (fh + 3) / 8, n2 = (fh + 1) / 4;
+    auto stream_row_y = [&](int64_t r) -> int64_t {
+        if (!f.finterlaced) return r;
+        if (r < n8) return 8 * r;
+        r -= n8;
+        if (r < n4) return 4 + 8 * r;
+        r -= n4;
+        if (r < n2) return 2 + 4 * r;
+        return 1 + 2 * (r - n2);
     };
-    if (f.finterlaced) {
-        static const int start[4] = {0, 4, 2, 1}, step[4] = {8, 8, 4, 2};
-        for (int p = 0; p < 4; ++p)
-            for (int64_t y = start[p]; y < f.fh; y += step[p]) place(y);
-    } else {
-        for (int64_t y = 0; y < f.fh; ++y) place(y);
-    }
-    return 0;
+    auto place = [&](int64_t r, const uint8_t* src) {
+        const int64_t cy = f.fy + stream_row_y(r);
+        if (cy >= f.H) return;
+        uint8_t* row = out + cy * pitch;
+        for (int64_t x = 0; x < f.fw && f.fx + x < f.W; ++x) {
+            const int k = src[x];
+            if (k == f.transparent) continue;
+            uint8_t* px = row + 3 * (f.fx + x);
+            px[0] = f.pal[k][0];
+            px[1] = f.pal[k][1];
+            px[2] = f.pal[k][2];
+        }
+    };
+    return gif_lzw(data, size, f, place, err) ? -1 : 0;
 }
 
 // PNG row reconstruction (spec 9.2) of one row in place; prev = the previous

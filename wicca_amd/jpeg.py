@@ -168,6 +168,10 @@ def _decode_batches_loop(batches, apply_orientation, device, depth, lib, pending
         if len(pending) >= depth:
             yield finish()
         ticket = ctypes.c_int64(0)
+        # the library writes the outputs from a stream of its own: the caching
+        # allocator may have handed out blocks that kernels queued on torch's
+        # current stream still read, so that stream is drained first
+        torch.cuda.current_stream(device).synchronize()
         if all_jpeg:
             _lib.check(lib.wicca_jpeg_decode_u8_async(ptrs, sizes, n, dsts, pitches, int(apply_orientation),
                                                       int(device), ctypes.byref(ticket)))
