@@ -99,6 +99,7 @@ CASES = [
     ((2, 3), [(224, 224)], 2, 0, 255),                   # INTER_CUBIC icons (host tables)
     ((4, 2, 4), [(384, 384), (600, 450), (224, 224)], 3, 1, 0),  # wide shapes (no plan row sums), repeats
     ((1, 2, 3, 4, 5, 6, 7), [(112, 112), (224, 224), (240, 240), (299, 299), (331, 331)], 3, 1, 0),  # 5 shapes
+    ((2, 5), [(1024, 600), (700, 300), (224, 224)], 3, 1, 0),  # groups split by column count
 ]
 
 
@@ -112,6 +113,22 @@ def test_plan_cases_match_per_call(tmp_path, depths, shapes, interp, border, k):
             want = wicca_amd.get_img_batch(paths, s, d, interp, border, k)
             assert np.array_equal(got[(s, d)][0], want[0]), (s, d)
             assert np.array_equal(got[(s, d)][1], want[1]), (s, d)
+
+
+def test_plan_integer_scales(tmp_path):
+    """INTER_AREA at integer scales (resizeAreaFast: 2x2 with (s + 2) >> 2,
+    others rounded from the exact sum) through the plan's row kernel."""
+    specs = [("scene", 448, 448, "jpg"), ("noise", 720, 960, "png"), ("scene", 480, 480, "jpg"),
+             ("smooth", 672, 896, "bmp")]
+    paths, refs = _files(tmp_path, specs)
+    shapes = [(224, 224), (240, 240), (112, 112)]
+    got = wicca_amd.get_img_matrix(paths, shapes, (2, 3))
+    for s in shapes:
+        for d in (2, 3):
+            want = wicca_amd.get_img_batch(paths, s, d)
+            assert np.array_equal(got[(s, d)][0], want[0]) and np.array_equal(got[(s, d)][1], want[1]), (s, d)
+        for i, rgb in enumerate(refs):
+            assert np.array_equal(got[(s, 2)][0][i], R.resize(rgb, s, R.INTER_AREA)), (i, s)
 
 
 def test_plan_8k_batch_matches_per_call(tmp_path):

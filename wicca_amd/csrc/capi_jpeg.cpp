@@ -550,7 +550,10 @@ int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, c
     int64_t icon_total = 0, hsum_total = 0;
     int max_oh = 0;
     const bool hs_ok = wicca::stage_hsum_ok(out_w, 3);
-    auto wants_hsum = [&](int64_t i) { return hs_ok && src_rp[(size_t)i].mode == wicca::RS_AREA; };
+    // INTER_AREA downscales (general or integer scale) take their row sums from the row kernel
+    auto wants_hsum = [&](int64_t i) {
+        return hs_ok && (src_rp[(size_t)i].mode == wicca::RS_AREA || src_rp[(size_t)i].mode == wicca::RS_AREA_FAST);
+    };
     for (int64_t i = 0; i < n; ++i) {
         wicca::plan_resize((int)H[i], (int)W[i], (int)out_h, (int)out_w, 3, interpolation, &src_rp[(size_t)i]);
         wicca::plan_resize((int)ih[i], (int)iw[i], (int)out_h, (int)out_w, 3, interpolation, &icon_rp[(size_t)i]);
@@ -561,7 +564,9 @@ int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, c
     HIP_TRY(ws->icon[0].reserve((size_t)icon_total));
     if (hsum_total) HIP_TRY(ws->rscratch.reserve((size_t)hsum_total));
     int64_t ioff = 0, hoff = 0;
-    bool any_hsum = false, any_copy = false;
+    bool any_copy = false;
+    int rounds = 0;
+    std::vector<std::vector<wicca::AreaTask>> tasks((size_t)n);
     for (int64_t i = 0; i < n; ++i) {
         wicca::StageImageDev& e = sd[(size_t)i];
         memset(&e, 0, sizeof(e));
@@ -576,11 +581,18 @@ int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, c
         e.ow = (int32_t)iw[i];
         e.dst = dres + i * out_bytes;
         if (wants_hsum(i)) {
+            const wicca::ResizeParams& rp = src_rp[(size_t)i];
+            const bool fast = rp.mode == wicca::RS_AREA_FAST;
             e.hsum = (float*)((uint8_t*)ws->rscratch.ptr + hoff);
             hoff += H[i] * out_w * 3 * (int64_t)sizeof(float);
-            e.scale_x = src_rp[(size_t)i].scale_x;
-            e.scale_y = src_rp[(size_t)i].scale_y;
-            any_hsum = true;
+            e.scale_x = rp.scale_x;
+            e.scale_y = rp.scale_y;
+            e.ky = fast ? rp.ky : 0;
+            e.kx = fast ? rp.kx : 0;
+            e.area_scale = rp.area_scale;
+            wicca::append_area_tasks((int)W[i], (int)out_w, rp.scale_x, fast, rp.kx, 0, tasks[(size_t)i]);
+            e.n_tasks = (int32_t)tasks[(size_t)i].size();
+            rounds = std::max(rounds, (int)((e.n_tasks + 255) / 256));
         }
         wicca::ResizeParams& q = icon_rp[(size_t)i];
         q.src = e.icon;
@@ -592,12 +604,23 @@ int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, c
         // copies and cubic / Lanczos-4 (host tables per image) take the per-image path
         any_copy = any_copy || q.mode == wicca::RS_COPY || q.mode == wicca::RS_KERNEL;
     }
-    // descriptors: [StageImageDev x n | ResizeParams x n], pinned, one upload
-    // (the call synchronises before it returns, so the staging is free again)
+    // descriptors: [StageImageDev x n | ResizeParams x n | task tables], pinned,
+    // one upload (the caller synchronises before the staging is reused)
     const size_t o_rp = (size_t)round_up((int64_t)(sizeof(wicca::StageImageDev) * (size_t)n), 256);
-    const size_t bytes = o_rp + sizeof(wicca::ResizeParams) * (size_t)n;
+    size_t bytes = (size_t)round_up((int64_t)(o_rp + sizeof(wicca::ResizeParams) * (size_t)n), 256);
+    std::vector<size_t> o_task((size_t)n, 0);
+    for (int64_t i = 0; i < n; ++i) {
+        o_task[(size_t)i] = bytes;
+        bytes += (size_t)round_up((int64_t)(sizeof(wicca::AreaTask) * tasks[(size_t)i].size()), 256);
+    }
     HIP_TRY(ws->spin.reserve(bytes, 64 << 10));
     HIP_TRY(ws->smeta.reserve(bytes));
+    for (int64_t i = 0; i < n; ++i) {
+        if (tasks[(size_t)i].empty()) continue;
+        memcpy(ws->spin.ptr + o_task[(size_t)i], tasks[(size_t)i].data(),
+               sizeof(wicca::AreaTask) * tasks[(size_t)i].size());
+        sd[(size_t)i].tasks = (const wicca::AreaTask*)((uint8_t*)ws->smeta.ptr + o_task[(size_t)i]);
+    }
     memcpy(ws->spin.ptr, sd.data(), sizeof(wicca::StageImageDev) * (size_t)n);
     memcpy(ws->spin.ptr + o_rp, icon_rp.data(), sizeof(wicca::ResizeParams) * (size_t)n);
     HIP_TRY(hipMemcpyAsync(ws->smeta.ptr, ws->spin.ptr, bytes, hipMemcpyHostToDevice, cs));
@@ -609,8 +632,8 @@ int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, c
     sp.k = (int32_t)saturate_k(k);
     sp.dw = (int32_t)out_w;
     sp.dh = (int32_t)out_h;
-    HIP_TRY(wicca::launch_stage_rows(sp, n, max_oh, any_hsum, cs));
-    if (any_hsum) HIP_TRY(wicca::launch_stage_vsum(sp, n, cs));
+    HIP_TRY(wicca::launch_stage_rows(sp, n, max_oh, rounds, cs));
+    if (rounds > 0) HIP_TRY(wicca::launch_stage_vsum(sp, n, cs));
     for (int64_t i = 0; i < n; ++i) {  // source resizes the row kernel did not prepare
         if (sd[(size_t)i].hsum) continue;
         int rc = run_resize(src_rp[(size_t)i], img[i], pitch[i], 0, dres + i * out_bytes, out_w * 3, 0, 1, cs, ws);

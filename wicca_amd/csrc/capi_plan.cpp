@@ -17,8 +17,8 @@
 //      gives each smaller depth's icon as the top-left crop of its level,
 //      SURVEY A5); depths <= 0 / > 8 per image as get_small_copy computes them;
 //   3. the INTER_AREA source resize of every classifier shape from ONE more
-//      read of each image (plan_hsum_kernel: row sums of up to 4 shapes at a
-//      time, then plan_vsum_kernel); other interpolations per image;
+//      read of each image (plan_rows_kernel: row sums of up to 4 shapes at a
+//      time, integer scales included, then plan_vsum_kernel); other interpolations per image;
 //   4. every icon resized to every shape (one launch per shape over the
 //      batch x depths);
 //   5. the dense (n, h, w, 3) outputs back to the caller's host arrays.
@@ -147,26 +147,102 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         dmax = std::max(dmax, ud[(size_t)u]);
     }
 
-    // 3. which shapes take their source resize from the plan's row sums
+    // 3. which (image, shape) pairs take their source resize from the plan's
+    // row sums: INTER_AREA downscales, general (RS_AREA) or integer (RS_AREA_FAST)
     std::vector<wicca::ResizeParams> src_rp((size_t)S * n);
-    std::vector<int> area_shapes;
-    for (int s = 0; s < S; ++s) {
-        bool area = wicca::plan_hsum_ok(shapes[(size_t)s].w, 3);
-        for (int64_t i = 0; i < n; ++i) {
-            wicca::ResizeParams& rp = src_rp[(size_t)(s * n + i)];
+    for (int s = 0; s < S; ++s)
+        for (int64_t i = 0; i < n; ++i)
             wicca::plan_resize((int)H[(size_t)i], (int)W[(size_t)i], (int)shapes[(size_t)s].h,
-                               (int)shapes[(size_t)s].w, 3, interpolation, &rp);
-        }
-        if (area) area_shapes.push_back(s);
-    }
-    // an (image, shape) takes the row sums when its own plan is RS_AREA
-    auto hsum_wanted = [&](int s, int64_t i) {
-        return src_rp[(size_t)(s * n + i)].mode == wicca::RS_AREA && wicca::stage_row_ok(W[(size_t)i], 3);
+                               (int)shapes[(size_t)s].w, 3, interpolation, &src_rp[(size_t)(s * n + i)]);
+    auto rows_wanted = [&](int s, int64_t i) {
+        const wicca::ResizeParams& rp = src_rp[(size_t)(s * n + i)];
+        return (rp.mode == wicca::RS_AREA || rp.mode == wicca::RS_AREA_FAST) &&
+               wicca::plan_hsum_ok(shapes[(size_t)s].w, 3) && wicca::stage_row_ok(W[(size_t)i], 3) &&
+               H[(size_t)i] <= 65535;
     };
-
+    // groups of at most kPlanShapes shapes and kPlanRounds * 256 pixel tasks
+    // (one launch each, one read of every image); per image one row-sum block
+    // with a plane per shape, and a task table
+    struct AreaGroup {
+        std::vector<int> shapes;
+        std::vector<wicca::PlanImageDev> imgs;
+        std::vector<std::vector<wicca::AreaTask>> tasks;
+        std::vector<size_t> task_off;
+        size_t off = 0;
+        int rounds = 0;
+    };
+    std::vector<AreaGroup> groups;
+    {
+        AreaGroup g;
+        int64_t cols = 0;
+        for (int s = 0; s < S; ++s) {
+            bool any = false;
+            for (int64_t i = 0; i < n && !any; ++i) any = rows_wanted(s, i);
+            if (!any) continue;
+            const int64_t w = shapes[(size_t)s].w;
+            if (!g.shapes.empty() &&
+                ((int)g.shapes.size() == wicca::kPlanShapes || cols + w > (int64_t)wicca::kPlanRounds * 256)) {
+                groups.push_back(std::move(g));
+                g = AreaGroup();
+                cols = 0;
+            }
+            g.shapes.push_back(s);
+            cols += w;
+        }
+        if (!g.shapes.empty()) groups.push_back(std::move(g));
+    }
+    std::vector<bool> by_rows((size_t)S * n, false);
+    int64_t hsum_total = 0;
+    std::vector<int64_t> hsum_img_off;
+    for (AreaGroup& g : groups) {
+        g.imgs.resize((size_t)n);
+        g.tasks.resize((size_t)n);
+        g.task_off.resize((size_t)n);
+        for (int64_t i = 0; i < n; ++i) {
+            wicca::PlanImageDev& e = g.imgs[(size_t)i];
+            memset(&e, 0, sizeof(e));
+            e.src = img[(size_t)i];
+            e.src_pitch = pitch[(size_t)i];
+            e.H = (int32_t)H[(size_t)i];
+            e.W = (int32_t)W[(size_t)i];
+            uint32_t plane = 0;  // floats into the image's row-sum block
+            const int64_t block0 = hsum_total;
+            for (size_t q = 0; q < g.shapes.size(); ++q) {
+                const int s = g.shapes[q];
+                if (!rows_wanted(s, i)) continue;
+                by_rows[(size_t)(s * n + i)] = true;
+                const wicca::ResizeParams& rp = src_rp[(size_t)(s * n + i)];
+                const bool fast = rp.mode == wicca::RS_AREA_FAST;
+                const int dw = (int)shapes[(size_t)s].w;
+                wicca::append_area_tasks((int)W[(size_t)i], dw, rp.scale_x, fast, rp.kx, plane, g.tasks[(size_t)i]);
+                e.dst[q] = dout + res_off[(size_t)s] + i * ob[(size_t)s];
+                e.scale_y[q] = rp.scale_y;
+                e.ky[q] = fast ? rp.ky : 0;
+                e.kx[q] = fast ? rp.kx : 0;
+                e.area_scale[q] = rp.area_scale;
+                e.hsum[q] = reinterpret_cast<float*>((intptr_t)(plane * sizeof(float)));  // relocated below
+                plane += (uint32_t)(H[(size_t)i] * 3 * dw);
+            }
+            e.hsum_base = reinterpret_cast<float*>((intptr_t)(block0 * (int64_t)sizeof(float)));  // relocated below
+            hsum_total += round_up((int64_t)plane, 64);
+            e.n_tasks = (int32_t)g.tasks[(size_t)i].size();
+            g.rounds = std::max(g.rounds, (int)((e.n_tasks + 255) / 256));
+        }
+    }
+    if (hsum_total * (int64_t)sizeof(float) > ((int64_t)1 << 35))
+        return fail(WICCA_ERR_NOMEM, "stage plan: %lld bytes of row sums", (long long)(hsum_total * 4));
+    if (hsum_total) HIP_TRY(ws->phsum.reserve((size_t)hsum_total * sizeof(float)));
+    for (AreaGroup& g : groups)
+        for (int64_t i = 0; i < n; ++i) {
+            wicca::PlanImageDev& e = g.imgs[(size_t)i];
+            uint8_t* base = (uint8_t*)ws->phsum.ptr + (intptr_t)e.hsum_base;
+            e.hsum_base = (float*)base;
+            for (size_t q = 0; q < g.shapes.size(); ++q)
+                if (by_rows[(size_t)(g.shapes[q] * n + i)]) e.hsum[q] = (float*)(base + (intptr_t)e.hsum[q]);
+        }
     // descriptors, packed into one pinned buffer and uploaded once:
-    //   [MultiImageDev x n | block map | per group of <= 4 area shapes: PlanImageDev x n |
-    //    ResizeParams x (S * U * n)]
+    //   [MultiImageDev x n | block map | ResizeParams x (S * U * n) | per row
+    //    group: PlanImageDev x n, then each image's task table]
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t o = off;
@@ -210,50 +286,6 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         o_md = take(sizeof(wicca::MultiImageDev) * (size_t)n);
         o_map = take(sizeof(uint32_t) * bmap.size());
     }
-    // groups of at most kPlanShapes area shapes, each with its PlanImageDev array
-    struct AreaGroup {
-        std::vector<int> shapes;
-        std::vector<wicca::PlanImageDev> imgs;
-        size_t off = 0;
-        bool any = false;
-    };
-    std::vector<AreaGroup> groups;
-    std::vector<int64_t> hsum_off((size_t)S * n, -1);
-    int64_t hsum_total = 0;
-    for (size_t a = 0; a < area_shapes.size(); a += wicca::kPlanShapes) {
-        AreaGroup g;
-        for (size_t b = a; b < std::min(area_shapes.size(), a + wicca::kPlanShapes); ++b)
-            g.shapes.push_back(area_shapes[b]);
-        g.imgs.resize((size_t)n);
-        for (int64_t i = 0; i < n; ++i) {
-            wicca::PlanImageDev& e = g.imgs[(size_t)i];
-            memset(&e, 0, sizeof(e));
-            e.src = img[(size_t)i];
-            e.src_pitch = pitch[(size_t)i];
-            e.H = (int32_t)H[(size_t)i];
-            e.W = (int32_t)W[(size_t)i];
-            for (size_t q = 0; q < g.shapes.size(); ++q) {
-                const int s = g.shapes[q];
-                if (!hsum_wanted(s, i)) continue;
-                const wicca::ResizeParams& rp = src_rp[(size_t)(s * n + i)];
-                hsum_off[(size_t)(s * n + i)] = hsum_total;
-                hsum_total += round_up(H[(size_t)i] * shapes[(size_t)s].w * 3 * (int64_t)sizeof(float), 256);
-                e.dst[q] = dout + res_off[(size_t)s] + i * ob[(size_t)s];
-                e.scale_x[q] = rp.scale_x;
-                e.scale_y[q] = rp.scale_y;
-                g.any = true;
-            }
-        }
-        g.off = take(sizeof(wicca::PlanImageDev) * (size_t)n);
-        groups.push_back(std::move(g));
-    }
-    if (hsum_total) HIP_TRY(ws->phsum.reserve((size_t)hsum_total));
-    for (AreaGroup& g : groups)
-        for (int64_t i = 0; i < n; ++i)
-            for (size_t q = 0; q < g.shapes.size(); ++q) {
-                const int64_t o = hsum_off[(size_t)(g.shapes[q] * n + i)];
-                if (o >= 0) g.imgs[(size_t)i].hsum[q] = (float*)((uint8_t*)ws->phsum.ptr + o);
-            }
     // 4. icon resizes: (shape s, depth slot u, image i)
     std::vector<wicca::ResizeParams> irp((size_t)S * U * n);
     std::vector<bool> shape_per_image((size_t)S, false);  // a copy / cubic / Lanczos icon resize in the shape
@@ -272,6 +304,10 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                 q.dst_stride = 0;
                 if (q.mode == wicca::RS_COPY || q.mode == wicca::RS_KERNEL) shape_per_image[(size_t)s] = true;
             }
+    for (AreaGroup& g : groups) {
+        g.off = take(sizeof(wicca::PlanImageDev) * (size_t)n);
+        for (int64_t i = 0; i < n; ++i) g.task_off[(size_t)i] = take(sizeof(wicca::AreaTask) * g.tasks[(size_t)i].size());
+    }
     const size_t o_irp = take(sizeof(wicca::ResizeParams) * irp.size());
     const size_t meta_bytes = off;
     HIP_TRY(ws->ppin.reserve(meta_bytes, 64 << 10));
@@ -282,7 +318,14 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         memcpy(hp + o_md, md.data(), sizeof(wicca::MultiImageDev) * md.size());
         memcpy(hp + o_map, bmap.data(), sizeof(uint32_t) * bmap.size());
     }
-    for (AreaGroup& g : groups) memcpy(hp + g.off, g.imgs.data(), sizeof(wicca::PlanImageDev) * g.imgs.size());
+    for (AreaGroup& g : groups) {
+        for (int64_t i = 0; i < n; ++i) {
+            const auto& tk = g.tasks[(size_t)i];
+            memcpy(hp + g.task_off[(size_t)i], tk.data(), sizeof(wicca::AreaTask) * tk.size());
+            g.imgs[(size_t)i].tasks = (const wicca::AreaTask*)(dp + g.task_off[(size_t)i]);
+        }
+        memcpy(hp + g.off, g.imgs.data(), sizeof(wicca::PlanImageDev) * g.imgs.size());
+    }
     memcpy(hp + o_irp, irp.data(), sizeof(wicca::ResizeParams) * irp.size());
     // the decode's staging was waited for (synchronous decode); the pinned
     // descriptors stay untouched until this call's final synchronise
@@ -326,7 +369,6 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
     }
     // source resizes (classifying_tools.py:315), every shape
     for (AreaGroup& g : groups) {
-        if (!g.any) continue;
         wicca::PlanParams pp{};
         pp.imgs = (const wicca::PlanImageDev*)(dp + g.off);
         pp.n_shapes = (int32_t)g.shapes.size();
@@ -337,12 +379,12 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
             pp.dw[q] = (int32_t)shapes[(size_t)g.shapes[q]].w;
             pp.dh[q] = (int32_t)shapes[(size_t)g.shapes[q]].h;
         }
-        HIP_TRY(wicca::launch_plan_hsum(pp, n, max_h, cs));
+        HIP_TRY(wicca::launch_plan_rows(pp, n, max_h, g.rounds, cs));
         HIP_TRY(wicca::launch_plan_vsum(pp, n, cs));
     }
     for (int s = 0; s < S; ++s)
         for (int64_t i = 0; i < n; ++i) {
-            if (hsum_off[(size_t)(s * n + i)] >= 0) continue;
+            if (by_rows[(size_t)(s * n + i)]) continue;
             if ((rc = run_resize(src_rp[(size_t)(s * n + i)], img[(size_t)i], pitch[(size_t)i], 0,
                                  dout + res_off[(size_t)s] + i * ob[(size_t)s], shapes[(size_t)s].w * 3, 0, 1, cs,
                                  ws)))

@@ -7,9 +7,15 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
 #include "resize.h"
 
 namespace wicca {
+
+struct AreaTask;
 
 // One image of the stage (device array).
 struct StageImageDev {
@@ -18,8 +24,12 @@ struct StageImageDev {
     uint8_t* icon;        // (oh, ow, C) at icon_pitch: get_small_copy(image, depth)
     int64_t icon_pitch;
     float* hsum;          // H x (dw * C) INTER_AREA row sums, or nullptr (source resized separately)
+    const AreaTask* tasks;  // its row-sum tasks (append_area_tasks), n_tasks of them
     uint8_t* dst;         // (dh, dw, C) dense: cv2.resize(image, (dw, dh), INTER_AREA)
     int32_t H, W, oh, ow;
+    int32_t n_tasks;
+    int32_t ky, kx;       // ky > 0: integer scale (RS_AREA_FAST), exact integer sums
+    float area_scale;
     double scale_x, scale_y;  // W / dw, H / dh (computeResizeAreaTab geometry)
 };
 
@@ -29,25 +39,80 @@ struct StageParams {
     int32_t dw, dh;       // classifier input size
 };
 
-// Limits of the fused row kernel: a source row fits the LDS stage, a lane
-// keeps at most 4 row-sum elements, depths 1..8 (exact integer block sums).
+// Limits of the fused row kernel: a source row fits the LDS stage, at most
+// kStageRounds row-sum tasks (output columns) per lane, RGB, depths 1..8
+// (exact integer block sums).
 constexpr int kStageRowMax = 24 * 1024;
-constexpr int kStageMaxEl = 4;
+constexpr int kStageRounds = 4;
 inline bool stage_row_ok(int64_t W, int64_t C) { return W * C <= kStageRowMax && C >= 1 && C <= 4; }
-inline bool stage_hsum_ok(int64_t dw, int64_t C) { return dw * C <= 256 * kStageMaxEl; }
+inline bool stage_hsum_ok(int64_t dw, int64_t C) { return C == 3 && dw >= 1 && dw <= 256 * kStageRounds; }
 
 // ---- the stage plan (wicca_image_stage_plan_u8): the source resizes of up
 // to kPlanShapes classifier shapes from ONE read of each decoded image.
 constexpr int kPlanShapes = 4;
-constexpr int kPlanRows = 16;  // source rows per workgroup of plan_hsum
+constexpr int kPlanRows = 16;    // source rows per workgroup of plan_rows
+constexpr int kPlanRounds = 6;   // task rounds per lane (<= 1536 pixel tasks per image)
+
+// One output column dx of one shape, for every staged row: the three channel
+// sums of OpenCV's INTER_AREA horizontal pass (computeResizeAreaTab: first
+// partial cell s1 - 1 with weight wa, full cells s1 .. s1 + len - 1 with wm,
+// last partial cell s1 + len with wb; a weight of 0 stands for an absent
+// cell).  Integer scales (RS_AREA_FAST) are the same with wa = wb = 0, wm = 1:
+// exact integer sums.  A row's sums go to hsum + out + y * n_el.
+struct AreaTask {
+    uint32_t s1len;  // s1 | len << 16
+    uint32_t out;    // first float of the column within the image's row-sum block
+    uint32_t n_el;   // floats per row of that shape's plane (dw * 3)
+    float wa, wm, wb;
+    uint32_t pad_[2];
+};
+
+// computeResizeAreaTab's entry for destination index d (host copy of
+// resize_device.h's area_tab: the same IEEE double operations).
+struct AreaTabHost {
+    int s1, s2;
+    bool has_a, has_b;
+    float wa, wm, wb;
+};
+inline AreaTabHost area_tab_host(int d, int ssize, double scale)
+{
+    const double f1 = d * scale;
+    const double f2 = f1 + scale;
+    const double cell = std::fmin(scale, (double)ssize - f1);
+    int s1 = (int)std::ceil(f1), s2 = (int)std::floor(f2);
+    s2 = std::min(s2, ssize - 1);
+    s1 = std::min(s1, s2);
+    AreaTabHost t;
+    t.s1 = s1;
+    t.s2 = s2;
+    t.has_a = (double)s1 - f1 > 1e-3;
+    t.wa = (float)(((double)s1 - f1) / cell);
+    t.wm = (float)(1.0 / cell);
+    t.has_b = f2 - (double)s2 > 1e-3;
+    t.wb = (float)(std::fmin(std::fmin(f2 - (double)s2, 1.0), cell) / cell);
+    return t;
+}
+
+// The pixel tasks of one (image, shape) (fast: integer scale kx), appended to
+// `tasks` in an order where each run of 32 tasks reads 32 different LDS banks
+// in the main loop (dword index floor(3 * s1 / 4) mod 32: a lane per output
+// column in column order would put columns 5 apart (about 128 dwords at an
+// 8K -> 224 scale) on one bank).
+void append_area_tasks(int W, int dw, double scale_x, bool fast, int kx, uint32_t out0, std::vector<AreaTask>& tasks);
 
 struct PlanImageDev {
-    const uint8_t* src;   // HWC uint8, rows 16-B aligned, pitch >= round_up(W * C, 16)
+    const uint8_t* src;   // HWC uint8 RGB, rows 16-B aligned, pitch >= round_up(W * 3, 16)
     int64_t src_pitch;
     int32_t H, W;
-    float* hsum[kPlanShapes];   // H x (dw_s * C) INTER_AREA row sums, or nullptr (shape s resized otherwise)
-    uint8_t* dst[kPlanShapes];  // (dh_s, dw_s, C) dense: cv2.resize(image, (dw_s, dh_s), INTER_AREA)
-    double scale_x[kPlanShapes], scale_y[kPlanShapes];
+    const AreaTask* tasks;  // every shape's pixel tasks (device)
+    int32_t n_tasks, pad_;
+    float* hsum_base;       // the image's row-sum block (tasks' `out` is relative to it)
+    float* hsum[kPlanShapes];   // H x (dw_s * 3) row sums of shape s, or nullptr (resized otherwise)
+    uint8_t* dst[kPlanShapes];  // (dh_s, dw_s, 3) dense: cv2.resize(image, (dw_s, dh_s), INTER_AREA)
+    double scale_y[kPlanShapes];
+    int32_t ky[kPlanShapes];    // > 0: integer scale (RS_AREA_FAST) ky rows per output row
+    int32_t kx[kPlanShapes];
+    float area_scale[kPlanShapes];
 };
 
 struct PlanParams {
@@ -56,19 +121,19 @@ struct PlanParams {
     int32_t dw[kPlanShapes], dh[kPlanShapes];
 };
 
-// A shape whose row sums the plan kernel takes: dw * C elements in at most
-// two pairs per lane, one table entry per output column in LDS.
-inline bool plan_hsum_ok(int64_t dw, int64_t C) { return C == 3 && dw * C <= 4 * 256 && dw <= 1024 / 3; }
+// A shape the plan's row kernel takes: RGB, at most kPlanRounds * 256 pixel
+// tasks per image over all shapes (checked by the caller), dw * 3 floats a row.
+inline bool plan_hsum_ok(int64_t dw, int64_t C) { return C == 3 && dw >= 1 && dw <= 1024; }
 
-// Row sums of every (image, shape) with hsum != nullptr: grid = (ceil(max H /
-// kPlanRows), n).  Then the vertical pass of each into dst.
-hipError_t launch_plan_hsum(const PlanParams& p, int64_t n, int max_h, hipStream_t s);
+// Row sums of every image's tasks: grid = (ceil(max H / kPlanRows), n);
+// rounds = ceil(max tasks / 256).  Then the vertical pass into dst.
+hipError_t launch_plan_rows(const PlanParams& p, int64_t n, int max_h, int rounds, hipStream_t s);
 hipError_t launch_plan_vsum(const PlanParams& p, int64_t n, hipStream_t s);
 
 // Icons of every image (and the row sums of those with hsum != nullptr):
-// grid = (largest icon height, n); any_hsum: some image has row sums (its
-// NE template is then ceil(dw * C / 256) <= 4).  Then area_vsum of those images.
-hipError_t launch_stage_rows(const StageParams& p, int64_t n, int max_oh, bool any_hsum, hipStream_t s);
+// grid = (largest icon height, n); rounds = ceil(most tasks / 256) (0: no
+// image has row sums).  Then the vertical pass of those images.
+hipError_t launch_stage_rows(const StageParams& p, int64_t n, int max_oh, int rounds, hipStream_t s);
 hipError_t launch_stage_vsum(const StageParams& p, int64_t n, hipStream_t s);
 
 }  // namespace wicca

@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstring>
 
 #include "resize_device.h"
 #include "stage.h"
@@ -38,11 +39,70 @@ using namespace rs;
 constexpr int kStThreads = 256;
 constexpr int kStChunks = kStageRowMax / 16 / kStThreads;  // 16-B chunks of a row per lane (6)
 
-// NE = the row-sum elements per lane, ceil(dw * C / 256) (1..4; 3 for 224 x 224 RGB)
-template <int NE>
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float ub(uint32_t v, int k) { return (float)((v >> (8 * k)) & 0xFFu); }
+
+// One AreaTask (stage.h) on one staged RGB row b (LDS, 64 B of slack past the
+// row): the output column's three channel sums in OpenCV's order — the first
+// partial cell, the full cells left to right, the last partial cell (a weight
+// of 0 stands for an absent cell: 0 + v * 0 = +0 and acc + 0 = acc exactly).
+// The full cells stream as 12-byte groups of four pixels: three new aligned
+// dwords per group realigned with v_alignbyte_b32 (one LDS read per four bytes
+// instead of one per byte; the host orders the tasks so that the 32 lanes of a
+// read touch 32 different banks), each byte converted by v_cvt_f32_ubyte{0..3},
+// the R and G chains advanced together by v_pk_mul_f32 / v_pk_add_f32 and B
+// alone: per term the same two roundings as OpenCV's `buf[dx] += S[sx] * alpha`.
+__device__ __forceinline__ void area_task_row(const uint8_t* b, const AreaTask& T, float* out)
+{
+    const int s1 = (int)(T.s1len & 0xFFFFu), len = (int)(T.s1len >> 16);
+    const f32x2 wm2 = {T.wm, T.wm};
+    // first partial cell (pixel s1 - 1; s1 = 0 only without one)
+    const int ia = max(3 * s1 - 3, 0);
+    f32x2 a01 = f32x2{0.f, 0.f} + f32x2{(float)b[ia], (float)b[ia + 1]} * f32x2{T.wa, T.wa};
+    float a2 = 0.f + (float)b[ia + 2] * T.wa;
+    // full cells, four pixels (12 bytes) a step
+    const int base = 3 * s1;
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(b + (base & ~3));
+    const uint32_t sh = (uint32_t)(base & 3);
+    const int G = len >> 2;
+    uint32_t d0 = w[0];
+    for (int g = 0; g < G; ++g) {
+        const uint32_t d1 = w[1], d2 = w[2], d3 = w[3];
+        w += 3;
+        const uint32_t r0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+        const uint32_t r1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+        const uint32_t r2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+        d0 = d3;
+        // pixel 0: r0.0 r0.1 r0.2 | 1: r0.3 r1.0 r1.1 | 2: r1.2 r1.3 r2.0 | 3: r2.1 r2.2 r2.3
+        a01 = a01 + f32x2{ub(r0, 0), ub(r0, 1)} * wm2;
+        a2 = a2 + ub(r0, 2) * T.wm;
+        a01 = a01 + f32x2{ub(r0, 3), ub(r1, 0)} * wm2;
+        a2 = a2 + ub(r1, 1) * T.wm;
+        a01 = a01 + f32x2{ub(r1, 2), ub(r1, 3)} * wm2;
+        a2 = a2 + ub(r2, 0) * T.wm;
+        a01 = a01 + f32x2{ub(r2, 1), ub(r2, 2)} * wm2;
+        a2 = a2 + ub(r2, 3) * T.wm;
+    }
+    // the rest of the full cells (0..3), then the last partial cell
+    const int rem = len - 4 * G;
+    const uint8_t* q = b + base + 12 * G;
+    for (int i = 0; i <= rem; ++i, q += 3) {
+        const float wv = i < rem ? T.wm : T.wb;
+        a01 = a01 + f32x2{(float)q[0], (float)q[1]} * f32x2{wv, wv};
+        a2 = a2 + (float)q[2] * wv;
+    }
+    out[0] = a01.x;
+    out[1] = a01.y;
+    out[2] = a2;
+}
+
+// NT = the row-sum task rounds per lane: ceil(tasks / 256) of the image with
+// the most (0: no image of the launch takes its source resize from row sums)
+template <int NT>
 __global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t buf[2][kStageRowMax];
+    __shared__ __attribute__((aligned(16))) uint8_t buf[2][kStageRowMax + 64];
     const StageImageDev& im = P.imgs[blockIdx.y];
     const int band = blockIdx.x;
     if (band >= im.oh) return;  // uniform: the grid is sized for the largest icon
@@ -51,17 +111,19 @@ __global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
     const int y0 = band * R;
     const int nq = (W * C + 15) >> 4;  // 16-B chunks of a row (the pitch covers them)
     const bool replicate = P.border == 1;
-    const bool hs = im.hsum != nullptr;  // uniform
-    const int n_el = P.dw * C;
+    const bool hs = NT > 0 && im.hsum != nullptr;  // uniform
     const int t = threadIdx.x;
 
-    // this lane's INTER_AREA output elements and their column tables
-    AreaTab tab[NE] = {};
-    if (hs) {
+    // this lane's row-sum tasks (output columns), for every row of the band
+    AreaTask tk[NT > 0 ? NT : 1];
 #pragma unroll
-        for (int i = 0; i < NE; ++i) {
-            const int e = t + i * kStThreads;
-            if (e < n_el) tab[i] = area_tab(e / C, W, im.scale_x);
+    for (int r = 0; r < (NT > 0 ? NT : 1); ++r) {
+        const int k = t + r * kStThreads;
+        if (hs && k < im.n_tasks) {
+            tk[r] = im.tasks[k];
+        } else {
+            tk[r].s1len = 0;
+            tk[r].n_el = 0;  // no task
         }
     }
     uint32_t lo[kStChunks][4], hi[kStChunks][4];
@@ -108,53 +170,10 @@ __global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
         if (r + 1 < rows_in) load_row(y + 1);  // in flight during the row sums below
         if (hrow) {
             __syncthreads();  // row y is in buf[r & 1]; buf[(r + 1) & 1] was last read before this
-            // the lane's elements are independent float chains: one loop over
-            // the longest window advances all of them, branch-free (a term
-            // past an element's window reads a valid LDS byte and is not
-            // added), so their LDS reads overlap; each chain keeps OpenCV's
-            // order: first partial cell, full cells left to right, last cell
-            float* out = im.hsum + (int64_t)y * n_el;
-            float acc[NE];
-            int len[NE], base[NE];
-            int minlen = 1 << 30, maxlen = 0;
-            const int last = nq * 16 - 1;  // the staged row's last byte
 #pragma unroll
-            for (int i = 0; i < NE; ++i) {
-                const int e = t + i * kStThreads;
-                const AreaTab& tx = tab[i];
-                const bool live = e < n_el;
-                const int c = e - (e / C) * C;
-                base[i] = live ? tx.s1 * C + c : 0;
-                len[i] = live ? tx.s2 - tx.s1 : 0;
-                if (live) minlen = min(minlen, len[i]);
-                maxlen = max(maxlen, len[i]);
-                const float a = (float)b[live && tx.has_a ? base[i] - C : 0] * tx.wa;
-                acc[i] = live && tx.has_a ? 0.f + a : 0.f;
-            }
-            if (minlen > maxlen) minlen = 0;  // no live element
-            // the windows of a lane's elements differ by at most one full cell
-            // (floor / ceil of the scale): the common part runs unpredicated
-            // (dead elements read a valid byte into a chain that is never stored)
-            int j = 0;
-#pragma unroll 4
-            for (; j < minlen; ++j) {
-#pragma unroll
-                for (int i = 0; i < NE; ++i) acc[i] = acc[i] + (float)b[base[i] + j * C] * tab[i].wm;
-            }
-            for (; j < maxlen; ++j) {
-#pragma unroll
-                for (int i = 0; i < NE; ++i) {
-                    const float v = (float)b[min(base[i] + j * C, last)];
-                    const float s0 = acc[i] + v * tab[i].wm;
-                    acc[i] = j < len[i] ? s0 : acc[i];
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < NE; ++i) {
-                const int e = t + i * kStThreads;
-                if (e >= n_el) continue;
-                if (tab[i].has_b) acc[i] = acc[i] + (float)b[base[i] + len[i] * C] * tab[i].wb;
-                out[e] = acc[i];
+            for (int k = 0; k < (NT > 0 ? NT : 1); ++k) {
+                if (tk[k].n_el == 0) continue;
+                area_task_row(b, tk[k], im.hsum + tk[k].out + (int64_t)y * tk[k].n_el);
             }
         }
     }
@@ -201,8 +220,16 @@ __global__ __launch_bounds__(kStThreads) void stage_vsum_kernel(StageParams P)
     const int e = blockIdx.x * kStThreads + threadIdx.x;
     if (e >= n_el) return;
     const int dy = blockIdx.y;
-    const AreaTab ty = area_tab(dy, im.H, im.scale_y);
     const float* col = im.hsum + e;
+    if (im.ky > 0) {  // RS_AREA_FAST: exact integer row sums and block sum
+        int isum = 0;
+        for (int r = 0; r < im.ky; ++r) isum += (int)col[(int64_t)(dy * im.ky + r) * n_el];
+        const bool half = im.kx == 2 && im.ky == 2 && P.C != 2;
+        im.dst[(int64_t)dy * n_el + e] =
+            half ? (uint8_t)((isum + 2) >> 2) : sat_u8(round_f32((float)isum * im.area_scale));
+        return;
+    }
+    const AreaTab ty = area_tab(dy, im.H, im.scale_y);
     float sum = 0.f;
     bool first = true;
     auto term = [&](int sy, float beta) {
@@ -222,44 +249,42 @@ __global__ __launch_bounds__(kStThreads) void stage_vsum_kernel(StageParams P)
 // (the reference resizes it once per classifier and depth,
 // classifying_tools.py:315 under the loops of :546-551 and :414-419).
 //
-// One workgroup per (image, kPlanRows source rows).  The shapes' column
-// tables (computeResizeAreaTab, doubles) are built once per workgroup into
-// LDS; each row is staged in LDS (two buffers, the next row's loads in flight)
-// and every lane advances two adjacent output elements at once with packed
-// float32 arithmetic (v_pk_mul_f32 / v_pk_add_f32: the same two roundings per
-// term as OpenCV's `buf[dx] += S[sx] * alpha`, two chains per instruction).
-// An element's terms are: the first partial cell (weight 0 when there is
-// none: 0 + v * 0 = +0, then 0 + x = x exactly as OpenCV's first add), the
-// full cells, the last partial cell (weight 0 when none: acc + 0 = acc); past
-// its own window a pair's shorter element adds v * 0 (exact, v is finite).
+// One workgroup per (image, kPlanRows source rows); each row is staged in LDS
+// as it is stored (RGB interleaved, two buffers, the next row's 16-B loads in
+// flight).  A lane owns up to NT pixel tasks (one output column of one shape,
+// its table entry in registers for all the rows) and forms the column's three
+// channel sums of each row in OpenCV's order: the first partial cell, the
+// full cells left to right, the last partial cell (a weight of 0 stands for
+// an absent cell: 0 + v * 0 = +0 and acc + 0 = acc exactly).  The full cells
+// stream as 12-byte groups of four pixels: three new aligned dwords per group
+// realigned with v_alignbyte_b32 (one LDS read per four bytes instead of one
+// per byte; the host orders the tasks so that the 32 lanes of a read touch 32
+// different banks), each byte converted by v_cvt_f32_ubyte{0..3}, the R and G
+// chains advanced together with v_pk_mul_f32 / v_pk_add_f32 and B alone: per
+// term the same two roundings as OpenCV's `buf[dx] += S[sx] * alpha`.
 // ---------------------------------------------------------------------------
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-constexpr int kPlanTab = 1024 / 3;  // output columns per shape (RGB)
-
-template <int C>
-__global__ __launch_bounds__(kStThreads) void plan_hsum_kernel(PlanParams P)
+template <int NT>
+__global__ __launch_bounds__(kStThreads) void plan_rows_kernel(PlanParams P)
 {
     __shared__ __attribute__((aligned(16))) uint8_t buf[2][kStageRowMax + 64];
-    __shared__ uint4 tab[kPlanShapes][kPlanTab];  // {s1 | len << 16, wa, wm, wb}
     const PlanImageDev& im = P.imgs[blockIdx.y];
     const int H = im.H, W = im.W;
     const int y0 = blockIdx.x * kPlanRows;
     if (y0 >= H) return;  // uniform: the grid is sized for the tallest image
     const int y1 = min(H, y0 + kPlanRows);
     const int t = threadIdx.x;
-    for (int s = 0; s < P.n_shapes; ++s) {
-        if (!im.hsum[s]) continue;  // uniform
-        for (int dx = t; dx < P.dw[s]; dx += kStThreads) {
-            const AreaTab a = area_tab(dx, W, im.scale_x[s]);
-            uint4 e;
-            e.x = (uint32_t)a.s1 | ((uint32_t)(a.s2 - a.s1) << 16);
-            e.y = __float_as_uint(a.has_a ? a.wa : 0.f);
-            e.z = __float_as_uint(a.wm);
-            e.w = __float_as_uint(a.has_b ? a.wb : 0.f);
-            tab[s][dx] = e;
+    AreaTask tk[NT];
+#pragma unroll
+    for (int r = 0; r < NT; ++r) {
+        const int k = t + r * kStThreads;
+        if (k < im.n_tasks) {
+            tk[r] = im.tasks[k];
+        } else {
+            tk[r].s1len = 0;
+            tk[r].n_el = 0;  // marks no task
         }
     }
-    const int nq = (W * C + 15) >> 4;
+    const int nq = (W * 3 + 15) >> 4;
     u32x4 v[kStChunks];
     auto load_row = [&](int y) {
         const u32x4* row = reinterpret_cast<const u32x4*>(im.src + (int64_t)y * im.src_pitch);
@@ -278,59 +303,18 @@ __global__ __launch_bounds__(kStThreads) void plan_hsum_kernel(PlanParams P)
             if (q < nq) reinterpret_cast<u32x4*>(b)[q] = v[m];
         }
         if (y + 1 < y1) load_row(y + 1);  // in flight during the sums below
-        __syncthreads();  // row y staged (and the tables, first time round)
-        for (int s = 0; s < P.n_shapes; ++s) {
-            if (!im.hsum[s]) continue;  // uniform
-            const int n_el = P.dw[s] * C;
-            const int n_pairs = (n_el + 1) >> 1;
-            float* out = im.hsum[s] + (int64_t)y * n_el;
-            for (int pr = t; pr < n_pairs; pr += kStThreads) {
-                const int e0 = 2 * pr, e1 = min(2 * pr + 1, n_el - 1);  // odd n_el: the last pair repeats e0
-                const int dx0 = e0 / C, c0 = e0 - dx0 * C;
-                const int dx1 = e1 / C, c1 = e1 - dx1 * C;
-                const uint4 t0 = tab[s][dx0], t1 = tab[s][dx1];
-                const int s10 = (int)(t0.x & 0xFFFFu), len0 = (int)(t0.x >> 16);
-                const int s11 = (int)(t1.x & 0xFFFFu), len1 = (int)(t1.x >> 16);
-                const uint8_t* r0 = b + s10 * C + c0;  // first full cell
-                const uint8_t* r1 = b + s11 * C + c1;
-                f32x2 acc = {0.f, 0.f};
-                {  // first partial cell (index s1 - 1; s1 = 0 only without one)
-                    const f32x2 va = {(float)b[max(s10 - 1, 0) * C + c0], (float)b[max(s11 - 1, 0) * C + c1]};
-                    const f32x2 wa = {__uint_as_float(t0.y), __uint_as_float(t1.y)};
-                    acc = acc + va * wa;
-                }
-                const f32x2 wm = {__uint_as_float(t0.z), __uint_as_float(t1.z)};
-                const int m = min(len0, len1);
-                int j = 0;
-                for (; j + 4 <= m; j += 4) {
+        __syncthreads();  // row y staged; the other buffer was last read before this
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const f32x2 vv = {(float)r0[(j + u) * C], (float)r1[(j + u) * C]};
-                        acc = acc + vv * wm;
-                    }
-                }
-                for (; j < m; ++j) {
-                    const f32x2 vv = {(float)r0[j * C], (float)r1[j * C]};
-                    acc = acc + vv * wm;
-                }
-                // the rest of the longer window, then each element's last
-                // partial cell at j == len (weight 0 past it)
-                const int M = max(len0, len1);
-                for (; j <= M; ++j) {
-                    const f32x2 vv = {(float)r0[j * C], (float)r1[j * C]};
-                    const f32x2 w = {j < len0 ? wm.x : (j == len0 ? __uint_as_float(t0.w) : 0.f),
-                                     j < len1 ? wm.y : (j == len1 ? __uint_as_float(t1.w) : 0.f)};
-                    acc = acc + vv * w;
-                }
-                out[e0] = acc.x;
-                if (e1 != e0) out[e1] = acc.y;
-            }
+        for (int r = 0; r < NT; ++r) {
+            if (tk[r].n_el == 0) continue;
+            area_task_row(b, tk[r], im.hsum_base + tk[r].out + (int64_t)y * tk[r].n_el);
         }
     }
 }
 
 // The vertical pass of every (image, shape) with row sums: blockIdx.z =
-// image * n_shapes + shape (stage_vsum_kernel's arithmetic).
+// image * n_shapes + shape (stage_vsum_kernel's arithmetic; integer scales:
+// the exact integer block sum, then resizeAreaFast's rounding).
 __global__ __launch_bounds__(kStThreads) void plan_vsum_kernel(PlanParams P)
 {
     const int s = (int)(blockIdx.z % (uint32_t)P.n_shapes);
@@ -340,8 +324,17 @@ __global__ __launch_bounds__(kStThreads) void plan_vsum_kernel(PlanParams P)
     const int e = blockIdx.x * kStThreads + threadIdx.x;
     const int dy = blockIdx.y;
     if (e >= n_el || dy >= P.dh[s]) return;
-    const AreaTab ty = area_tab(dy, im.H, im.scale_y[s]);
     const float* col = im.hsum[s] + e;
+    const int ky = im.ky[s];
+    if (ky > 0) {  // RS_AREA_FAST: every row sum is an exact integer, and so is their sum
+        int sum = 0;
+        for (int r = 0; r < ky; ++r) sum += (int)col[(int64_t)(dy * ky + r) * n_el];
+        const bool half = im.kx[s] == 2 && ky == 2 && P.C != 2;
+        im.dst[s][(int64_t)dy * n_el + e] =
+            half ? (uint8_t)((sum + 2) >> 2) : sat_u8(round_f32((float)sum * im.area_scale[s]));
+        return;
+    }
+    const AreaTab ty = area_tab(dy, im.H, im.scale_y[s]);
     float sum = 0.f;
     bool first = true;
     auto term = [&](int sy, float beta) {
@@ -357,14 +350,57 @@ __global__ __launch_bounds__(kStThreads) void plan_vsum_kernel(PlanParams P)
 
 }  // namespace
 
-hipError_t launch_plan_hsum(const PlanParams& p, int64_t n, int max_h, hipStream_t s)
+void append_area_tasks(int W, int dw, double scale_x, bool fast, int kx, uint32_t out0, std::vector<AreaTask>& tasks)
+{
+    std::vector<AreaTask> col((size_t)dw);
+    std::vector<std::vector<int>> bank(32);
+    for (int dx = 0; dx < dw; ++dx) {
+        AreaTask& k = col[(size_t)dx];
+        memset(&k, 0, sizeof(k));
+        int s1, len;
+        if (fast) {  // resizeAreaFast: kx whole pixels, exact integer sums
+            s1 = dx * kx;
+            len = kx;
+            k.wa = 0.f;
+            k.wm = 1.f;
+            k.wb = 0.f;
+        } else {
+            const AreaTabHost a = area_tab_host(dx, W, scale_x);
+            s1 = a.s1;
+            len = a.s2 - a.s1;
+            k.wa = a.has_a ? a.wa : 0.f;
+            k.wm = a.wm;
+            k.wb = a.has_b ? a.wb : 0.f;
+        }
+        k.s1len = (uint32_t)s1 | ((uint32_t)len << 16);
+        k.out = out0 + 3u * (uint32_t)dx;
+        k.n_el = 3u * (uint32_t)dw;
+        bank[(size_t)(((3 * s1) >> 2) & 31)].push_back(dx);
+    }
+    // deal one column per bank at a time: runs of 32 tasks read 32 banks
+    for (size_t left = (size_t)dw; left > 0;) {
+        for (auto& q : bank) {
+            if (q.empty()) continue;
+            tasks.push_back(col[(size_t)q.back()]);
+            q.pop_back();
+            --left;
+        }
+    }
+}
+
+hipError_t launch_plan_rows(const PlanParams& p, int64_t n, int max_h, int rounds, hipStream_t s)
 {
     if (n <= 0 || max_h <= 0) return hipSuccess;
-    if (n > 65535 || p.C != 3 || p.n_shapes < 1 || p.n_shapes > kPlanShapes) return hipErrorInvalidValue;
-    for (int i = 0; i < p.n_shapes; ++i)
-        if (!plan_hsum_ok(p.dw[i], p.C)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(plan_hsum_kernel<3>, dim3((uint32_t)((max_h + kPlanRows - 1) / kPlanRows), (uint32_t)n),
-                       dim3(kStThreads), 0, s, p);
+    if (n > 65535 || p.C != 3 || rounds < 1 || rounds > kPlanRounds) return hipErrorInvalidValue;
+    const dim3 grid((uint32_t)((max_h + kPlanRows - 1) / kPlanRows), (uint32_t)n);
+    switch (rounds) {
+    case 1: hipLaunchKernelGGL(plan_rows_kernel<1>, grid, dim3(kStThreads), 0, s, p); break;
+    case 2: hipLaunchKernelGGL(plan_rows_kernel<2>, grid, dim3(kStThreads), 0, s, p); break;
+    case 3: hipLaunchKernelGGL(plan_rows_kernel<3>, grid, dim3(kStThreads), 0, s, p); break;
+    case 4: hipLaunchKernelGGL(plan_rows_kernel<4>, grid, dim3(kStThreads), 0, s, p); break;
+    case 5: hipLaunchKernelGGL(plan_rows_kernel<5>, grid, dim3(kStThreads), 0, s, p); break;
+    default: hipLaunchKernelGGL(plan_rows_kernel<6>, grid, dim3(kStThreads), 0, s, p); break;
+    }
     return hipGetLastError();
 }
 
@@ -383,19 +419,18 @@ hipError_t launch_plan_vsum(const PlanParams& p, int64_t n, hipStream_t s)
     return hipGetLastError();
 }
 
-hipError_t launch_stage_rows(const StageParams& p, int64_t n, int max_oh, bool any_hsum, hipStream_t s)
+hipError_t launch_stage_rows(const StageParams& p, int64_t n, int max_oh, int rounds, hipStream_t s)
 {
     if (n <= 0 || max_oh <= 0) return hipSuccess;
-    if (n > 65535 || p.depth < 1 || p.depth > 8) return hipErrorInvalidValue;
-    // the row-sum tables exist only when some image takes its source resize
-    // from the row sums (then dw * C <= 1024, stage_hsum_ok); else one dummy slot
-    const int ne = any_hsum ? (p.dw * p.C + kStThreads - 1) / kStThreads : 1;
+    if (n > 65535 || p.depth < 1 || p.depth > 8 || rounds < 0 || rounds > kStageRounds) return hipErrorInvalidValue;
     const dim3 grid((uint32_t)max_oh, (uint32_t)n);
-    if (ne <= 1) hipLaunchKernelGGL(stage_rows_kernel<1>, grid, dim3(kStThreads), 0, s, p);
-    else if (ne == 2) hipLaunchKernelGGL(stage_rows_kernel<2>, grid, dim3(kStThreads), 0, s, p);
-    else if (ne == 3) hipLaunchKernelGGL(stage_rows_kernel<3>, grid, dim3(kStThreads), 0, s, p);
-    else if (ne == 4) hipLaunchKernelGGL(stage_rows_kernel<4>, grid, dim3(kStThreads), 0, s, p);
-    else return hipErrorInvalidValue;
+    switch (rounds) {
+    case 0: hipLaunchKernelGGL(stage_rows_kernel<0>, grid, dim3(kStThreads), 0, s, p); break;
+    case 1: hipLaunchKernelGGL(stage_rows_kernel<1>, grid, dim3(kStThreads), 0, s, p); break;
+    case 2: hipLaunchKernelGGL(stage_rows_kernel<2>, grid, dim3(kStThreads), 0, s, p); break;
+    case 3: hipLaunchKernelGGL(stage_rows_kernel<3>, grid, dim3(kStThreads), 0, s, p); break;
+    default: hipLaunchKernelGGL(stage_rows_kernel<4>, grid, dim3(kStThreads), 0, s, p); break;
+    }
     return hipGetLastError();
 }
 
