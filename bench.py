@@ -53,6 +53,7 @@ def parse():
                          "png / bmp: the same for 8K PNG (zlib level 6) / 24-bit BMP files")
     ap.add_argument("--quality", type=int, default=90, help="--config jpeg: encoder quality")
     ap.add_argument("--shape", default="224,224", help="--config stage: classifier input (w,h)")
+    ap.add_argument("--tiled-as-rank", default="", help=argparse.SUPPRESS)
     ap.add_argument("--plan-no-loop", action="store_true",
                     help="--config plan: skip the per-call loop and its check (profiling runs)")
     ap.add_argument("--interpolation", type=int, default=3, help="--config stage: cv2.INTER_*")
@@ -180,7 +181,7 @@ def cpu_baseline(args, budget_s: float):
     }
 
 
-def live_pmc(args, kernel: str, timeout_s: float = 150.0):
+def live_pmc(args, kernel: str, timeout_s: float = 150.0, extra=None):
     """roofline.traffic measured in this run: two child runs of this bench's
     workload under rocprofv3, one counter per pass (FETCH_SIZE, WRITE_SIZE;
     gfx950 TCC slots cannot hold both), corrected as tools/pmc_summary.py does
@@ -203,7 +204,7 @@ def live_pmc(args, kernel: str, timeout_s: float = 150.0):
              "--no-verify", "--no-cpu-baseline", "--no-live-pmc",
              "--images", str(args.images), "--height", str(args.height), "--width", str(args.width),
              "--channels", str(args.channels), "--depth", str(args.depth),
-             "--border", str(args.border), "--seed", str(args.seed)]
+             "--border", str(args.border), "--seed", str(args.seed)] + list(extra or [])
     env = dict(os.environ, TMPDIR="/tmp")
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
@@ -268,8 +269,11 @@ def run_tiled(args, torch, dist, world, rank, local_rank):
     H = args.height if args.height != 4320 else 65536
     W = args.width if args.width != 7680 else 65536
     C, D = args.channels, (args.depth if args.depth != 5 else 8)
-    bounds = aligned_bands(H, world, D)
-    y0, y1 = bounds[rank]
+    band_rank, band_world = rank, world
+    if args.tiled_as_rank:  # a single-process child timing one rank's band (live PMC of the N-rank line)
+        band_rank, band_world = (int(x) for x in args.tiled_as_rank.split("/"))
+    bounds = aligned_bands(H, band_world, D)
+    y0, y1 = bounds[band_rank]
     pitch = W * C
     if pitch % 16:
         raise SystemExit("tiled bench needs W*C % 16 == 0")
@@ -294,6 +298,12 @@ def run_tiled(args, torch, dist, world, rank, local_rank):
             slab_kernel()
             return icon_local
         return th(band, y0, H, bounds)
+
+    if args.tiled_as_rank:  # PMC child: the band kernel only
+        for _ in range(args.warmup + args.steps):
+            slab_kernel()
+        torch.cuda.synchronize()
+        return None
 
     for _ in range(args.warmup):
         step()
@@ -339,6 +349,11 @@ def run_tiled(args, torch, dist, world, rank, local_rank):
         return None
     ms = wall / args.steps * 1e3
     band_bytes = (y1 - y0) * W * C + ((y1 - y0 + r - 1) // r) * ow * C
+    kname = lib.wicca_kernel_name(D, C, 0).decode()
+    pmc = None
+    if not args.no_live_pmc:  # HBM bytes of rank 0's band kernel, two PMC child runs
+        pmc = live_pmc(args, kname.split("<")[0], extra=["--config", "tiled", "--tiled-as-rank",
+                                                         f"0/{world}"])
     return {
         "metric": BASELINE["metric"],
         "value": round(H * W / 1e6 / (ms / 1e3), 1),
@@ -353,8 +368,11 @@ def run_tiled(args, torch, dist, world, rank, local_rank):
         "roofline": {"bound": "hbm", "achieved": round(band_bytes / (kernel_ms / 1e3) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(band_bytes / (kernel_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": None, "kernel": lib.wicca_kernel_name(D, C, 0).decode() + " (rank-0 band)",
-                     "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": band_bytes},
+                     "traffic": round(pmc["hbm_bytes_per_launch"]) if pmc else None,
+                     "kernel": kname + " (rank-0 band)",
+                     "kernel_ms": round(kernel_ms, 4), "alg_bytes_per_launch": band_bytes,
+                     "pmc_source": "live (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child runs of rank 0's band)"
+                     if pmc else None},
         "cpu_baseline": None,
         "verified_vs_numpy_port": verified,
     }
@@ -1105,14 +1123,18 @@ def main():
     # against the NumPy port outside the timed region; the pass/fail flags are
     # reduced over ranks, so an N-rank line says verified only if all N passed
     verified = None
+    checked = []
     if not args.no_verify:
         from oracle import haar_numpy
         from wicca_amd.synth import synth_image
-        i = B - 1
-        img = synth_image(args.seed * 1000003 + rank, i, H, W, C)
-        ref = haar_numpy.get_small_copy(img, D, args.border)
-        got = dst.view(B, oh, opitch)[i, :, :ow * C].cpu().numpy().reshape(oh, ow, C)
-        ok = bool(np.array_equal(got, ref))
+        ok = True
+        # the first, a middle and the last image of the rank's batch (REPLICATE)
+        for i in sorted({0, B // 2, B - 1}):
+            img = synth_image(args.seed * 1000003 + rank, i, H, W, C)
+            ref = haar_numpy.get_small_copy(img, D, args.border)
+            got = dst.view(B, oh, opitch)[i, :, :ow * C].cpu().numpy().reshape(oh, ow, C)
+            ok = ok and bool(np.array_equal(got, ref))
+            checked.append(i)
         one = torch.empty(oh * opitch, dtype=torch.uint8, device="cuda")
         _lib.check(lib.wicca_haar_ll_u8_uniform(
             ctypes.c_void_p(src.data_ptr() + i * H * pitch), 1, H, W, C, pitch, H * pitch, D, 0, 77,
@@ -1142,11 +1164,15 @@ def main():
     achieved = alg_bytes / (kernel_ms / 1e3) / 1e9
     workload_key = f"b{B}_{W}x{H}x{C}_d{D}"
     kernel = lib.wicca_kernel_name(D, C, 0).decode()
-    pmc = live_pmc(args, kernel) if world == 1 and not args.no_live_pmc else None
-    pmc_source = "live (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child runs of this workload)" if pmc else None
+    # live HBM bytes: rank 0 (every rank runs the same per-GPU workload) starts
+    # two single-process PMC child runs on its own device after the timed
+    # region and the verification; the committed summary is only the fallback
+    pmc = live_pmc(args, kernel) if not args.no_live_pmc else None
+    pmc_source = ("live (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child runs of this per-GPU workload"
+                  + (" on rank 0's device)" if world > 1 else ")")) if pmc else None
     if pmc is None:
         pmc = read_pmc(args.pmc, workload_key)
-        pmc_source = os.path.relpath(args.pmc, REPO) if pmc else None
+        pmc_source = f"committed summary {os.path.relpath(args.pmc, REPO)} (not this run)" if pmc else None
     traffic = round(pmc["hbm_bytes_per_launch"]) if pmc else None
 
     out = {
@@ -1184,6 +1210,7 @@ def main():
         "cpu_baseline": None,
         "verified_vs_numpy_port": verified,
         "verified_ranks": world if verified else None,
+        "verified_images_per_rank": checked if verified else None,
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)

@@ -14,6 +14,10 @@
 // (data_loader.py:58).  tests/test_gpu_jpeg.py checks it bit for bit against
 // Pillow 12.2.0's libjpeg-turbo 3.1.4.1 decode.
 //
+// The IDCT, upsampling and colour arithmetic restate libjpeg-turbo's, which
+// derives from the Independent JPEG Group's libjpeg: this software is based in
+// part on the work of the Independent JPEG Group (see NOTICE.md).
+//
 // Parallel Huffman decoding: every restart segment is cut into subsequences
 // of `sub_bits` bits, one lane each.  A lane decodes codewords that START in
 // its subsequence, from a start state (bit position, MCU slot, coefficient

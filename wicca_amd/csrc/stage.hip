@@ -100,7 +100,8 @@ __device__ __forceinline__ void area_task_row(const uint8_t* b, const AreaTask& 
 // NT = the row-sum task rounds per lane: ceil(tasks / 256) of the image with
 // the most (0: no image of the launch takes its source resize from row sums)
 template <int NT>
-__global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kStThreads), amdgpu_waves_per_eu(NT <= 1 ? 3 : 2))) void
+stage_rows_kernel(StageParams P)
 {
     __shared__ __attribute__((aligned(16))) uint8_t buf[2][kStageRowMax + 64];
     const StageImageDev& im = P.imgs[blockIdx.y];
@@ -131,8 +132,10 @@ __global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
     for (int m = 0; m < kStChunks; ++m)
 #pragma unroll
         for (int w = 0; w < 4; ++w) lo[m][w] = hi[m][w] = 0;
-    u32x4 v[kStChunks];
-    auto load_row = [&](int y) {
+    // two rows in flight: row y + 2's loads go out as soon as row y is summed
+    // and staged (its registers are free again)
+    u32x4 va[kStChunks], vb[kStChunks];
+    auto load_row = [&](u32x4 (&v)[kStChunks], int y) {
         const u32x4* row = reinterpret_cast<const u32x4*>(im.src + (int64_t)min(y, H - 1) * im.src_pitch);
 #pragma unroll
         for (int m = 0; m < kStChunks; ++m) {
@@ -143,8 +146,7 @@ __global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
     // rows the block sums take: real rows, and under REPLICATE the clamped
     // copies of row H-1 below the image
     const int rows_in = replicate ? R : max(0, min(R, H - y0));
-    if (rows_in > 0) load_row(y0);
-    for (int r = 0; r < rows_in; ++r) {
+    auto row_step = [&](u32x4 (&v)[kStChunks], int r, uint8_t* b) {
         const int y = y0 + r;
 #pragma unroll
         for (int m = 0; m < kStChunks; ++m) {
@@ -159,7 +161,6 @@ __global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
             hi[m][3] += (a.w >> 8) & 0x00FF00FFu;
         }
         const bool hrow = hs && y < H;  // uniform
-        uint8_t* b = buf[r & 1];
         if (hrow) {
 #pragma unroll
             for (int m = 0; m < kStChunks; ++m) {
@@ -167,15 +168,21 @@ __global__ __launch_bounds__(kStThreads) void stage_rows_kernel(StageParams P)
                 if (q < nq) reinterpret_cast<u32x4*>(b)[q] = v[m];
             }
         }
-        if (r + 1 < rows_in) load_row(y + 1);  // in flight during the row sums below
+        if (r + 2 < rows_in) load_row(v, y + 2);  // in flight during the next two rows
         if (hrow) {
-            __syncthreads();  // row y is in buf[r & 1]; buf[(r + 1) & 1] was last read before this
+            __syncthreads();  // row y is in b; the other buffer was last read before this
 #pragma unroll
             for (int k = 0; k < (NT > 0 ? NT : 1); ++k) {
                 if (tk[k].n_el == 0) continue;
                 area_task_row(b, tk[k], im.hsum + tk[k].out + (int64_t)y * tk[k].n_el);
             }
         }
+    };
+    if (rows_in > 0) load_row(va, y0);
+    if (rows_in > 1) load_row(vb, y0 + 1);
+    for (int r = 0; r < rows_in; r += 2) {
+        row_step(va, r, buf[0]);
+        if (r + 1 < rows_in) row_step(vb, r + 1, buf[1]);
     }
     __syncthreads();  // the row buffers are free: they take the column sums
     // column sums as u16 per row byte (2 * W * C <= 48 KiB)
@@ -264,7 +271,7 @@ __global__ __launch_bounds__(kStThreads) void stage_vsum_kernel(StageParams P)
 // term the same two roundings as OpenCV's `buf[dx] += S[sx] * alpha`.
 // ---------------------------------------------------------------------------
 template <int NT>
-__global__ __launch_bounds__(kStThreads) void plan_rows_kernel(PlanParams P)
+__global__ __launch_bounds__(kStThreads, 3) void plan_rows_kernel(PlanParams P)
 {
     __shared__ __attribute__((aligned(16))) uint8_t buf[2][kStageRowMax + 64];
     const PlanImageDev& im = P.imgs[blockIdx.y];
@@ -285,8 +292,11 @@ __global__ __launch_bounds__(kStThreads) void plan_rows_kernel(PlanParams P)
         }
     }
     const int nq = (W * 3 + 15) >> 4;
-    u32x4 v[kStChunks];
-    auto load_row = [&](int y) {
+    // two rows in flight: row y + 2's loads go out as soon as row y is staged
+    // (its registers are free again), so a row's load latency overlaps two
+    // rows of sums instead of one
+    u32x4 va[kStChunks], vb[kStChunks];
+    auto load_row = [&](u32x4 (&v)[kStChunks], int y) {
         const u32x4* row = reinterpret_cast<const u32x4*>(im.src + (int64_t)y * im.src_pitch);
 #pragma unroll
         for (int m = 0; m < kStChunks; ++m) {
@@ -294,21 +304,25 @@ __global__ __launch_bounds__(kStThreads) void plan_rows_kernel(PlanParams P)
             v[m] = q < nq ? __builtin_nontemporal_load(row + q) : u32x4{0, 0, 0, 0};
         }
     };
-    load_row(y0);
-    for (int y = y0; y < y1; ++y) {
-        uint8_t* b = buf[(y - y0) & 1];
+    auto row_step = [&](u32x4 (&v)[kStChunks], int y, uint8_t* b) {
 #pragma unroll
         for (int m = 0; m < kStChunks; ++m) {
             const int q = t + m * kStThreads;
             if (q < nq) reinterpret_cast<u32x4*>(b)[q] = v[m];
         }
-        if (y + 1 < y1) load_row(y + 1);  // in flight during the sums below
+        if (y + 2 < y1) load_row(v, y + 2);  // in flight during the next two rows' sums
         __syncthreads();  // row y staged; the other buffer was last read before this
 #pragma unroll
         for (int r = 0; r < NT; ++r) {
             if (tk[r].n_el == 0) continue;
             area_task_row(b, tk[r], im.hsum_base + tk[r].out + (int64_t)y * tk[r].n_el);
         }
+    };
+    load_row(va, y0);
+    if (y0 + 1 < y1) load_row(vb, y0 + 1);
+    for (int y = y0; y < y1; y += 2) {
+        row_step(va, y, buf[0]);
+        if (y + 1 < y1) row_step(vb, y + 1, buf[1]);
     }
 }
 
