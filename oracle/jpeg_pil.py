@@ -24,11 +24,22 @@ def libjpeg_version() -> str:
     return str(features.version("libjpeg_turbo"))
 
 
-def decode_rgb(data: bytes, apply_orientation: bool = True) -> np.ndarray:
-    """RGB (H, W, 3) uint8 decode of a JPEG file's bytes."""
-    from PIL import Image, ImageOps
-    im = Image.open(io.BytesIO(data))
-    im.load()
+def decode_rgb(data: bytes, apply_orientation: bool = True, truncated: bool = False) -> np.ndarray:
+    """RGB (H, W, 3) uint8 decode of a JPEG file's bytes.
+
+    truncated=True: Pillow's ``ImageFile.LOAD_TRUNCATED_IMAGES`` — at the end
+    of the data libjpeg-turbo gets a fake EOI marker and finishes the image
+    with its "insufficient data" rule (missing blocks are all-zero, i.e. grey),
+    the same source-manager behaviour ``cv2.imread`` has on a damaged file
+    (libjpeg warns and returns the image)."""
+    from PIL import Image, ImageFile, ImageOps
+    prev = ImageFile.LOAD_TRUNCATED_IMAGES
+    ImageFile.LOAD_TRUNCATED_IMAGES = truncated
+    try:
+        im = Image.open(io.BytesIO(data))
+        im.load()
+    finally:
+        ImageFile.LOAD_TRUNCATED_IMAGES = prev
     if apply_orientation:
         im = ImageOps.exif_transpose(im)
     return np.asarray(im.convert("RGB")).copy()

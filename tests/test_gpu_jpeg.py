@@ -438,3 +438,49 @@ def test_file_stage_pipelined_matches_synchronous(tmp_path):
     gen.close()
     with pytest.raises(OSError):  # a missing file (batch 1) while batch 0 is in flight
         list(wicca_amd.get_img_batches([[str(tmp_path / "b0_0.jpg")], [str(tmp_path / "missing.jpg")]], (224, 224), 4))
+
+
+DAMAGE = [(kind, sub, rb, prog) for kind, sub, rb, prog in
+          [("scene", 2, 0, False), ("scene", 2, 8, False), ("noise", 0, 0, False), ("scene", 1, 3, False),
+           ("gray", 0, 0, False), ("scene", 2, 0, True), ("smooth", 2, 16, True)]]
+
+
+@pytest.mark.parametrize("kind,sub,rb,prog", DAMAGE, ids=[f"{k}-s{s}-r{r}-p{int(p)}" for k, s, r, p in DAMAGE])
+@pytest.mark.parametrize("cut", [0.3, 0.5, 0.7, 0.95])
+def test_truncated_file_whole_decode_matches_libjpeg(kind, sub, rb, prog, cut):
+    """cv2.imread returns a truncated JPEG (libjpeg-turbo warns, inserts a fake
+    EOI and finishes the image: missing blocks all-zero, i.e. grey), so the
+    classifiers see every pixel of it (data_loader.py:53-63): the whole decode
+    against libjpeg-turbo's through Pillow with LOAD_TRUNCATED_IMAGES, bit for
+    bit, with and without restart markers, progressive files included."""
+    img = J.test_image(kind, 200, 344, 17 + sub + rb)
+    if kind == "gray":
+        img = img[..., 0] if img.ndim == 3 else img
+    data = J.encode(img, 88, sub, rb, progressive=prog)
+    short = data[:int(len(data) * cut)]
+    want = J.decode_rgb(short, truncated=True)
+    assert np.array_equal(WJ.decode(short), want)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_corrupted_entropy_whole_decode_matches_libjpeg(seed):
+    """Bytes flipped inside the entropy-coded data (markers untouched):
+    libjpeg-turbo decodes on (a bad Huffman code decodes as a zero symbol,
+    jdhuff.c), so does cv2.imread; the whole image against Pillow's decode.
+    Where Pillow itself refuses the file the case is skipped (parity unpinned)."""
+    rng = np.random.default_rng(100 + seed)
+    kind = ("scene", "noise", "smooth")[seed % 3]
+    img = J.test_image(kind, 160, 232, seed)
+    data = bytearray(J.encode(img, 80, seed % 3, 8 if seed % 2 else 0))
+    sos = bytes(data).index(b"\xff\xda")
+    start = sos + 2 + int.from_bytes(data[sos + 2:sos + 4], "big")
+    for pos in rng.integers(start + 4, len(data) - 4, 3 + seed):
+        if data[pos] != 0xFF and data[pos - 1] != 0xFF:
+            nv = data[pos] ^ int(rng.integers(1, 255))
+            if nv != 0xFF:
+                data[pos] = nv
+    try:
+        want = J.decode_rgb(bytes(data), truncated=True)
+    except Exception as e:  # noqa: BLE001 — Pillow refuses: nothing to pin against
+        pytest.skip(f"Pillow refuses this file ({e}): parity unpinned")
+    assert np.array_equal(WJ.decode(bytes(data)), want)
