@@ -251,6 +251,29 @@ __global__ __launch_bounds__(256) void copyU(const u32x4* __restrict__ a, u32x4*
     }
 }
 
+// The guide's float4 copy (MI355X_MICROARCH.md: 6.29 TB/s): one 16-B vector
+// per lane, one launch covering the buffer (no grid-stride loop), plain or
+// non-temporal loads / stores; V vectors per lane 256 apart (V = 1: the plain
+// form).
+template <int V, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void copy_flat(const u32x4* __restrict__ a, u32x4* __restrict__ b, size_t n)
+{
+    const size_t i0 = (size_t)blockIdx.x * 256 * V + threadIdx.x;
+    u32x4 v[V];
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+        const size_t j = i0 + (size_t)u * 256;
+        v[u] = j < n ? (NTL ? __builtin_nontemporal_load(a + j) : a[j]) : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < V; ++u) {
+        const size_t j = i0 + (size_t)u * 256;
+        if (j < n) {
+            if constexpr (NTS) __builtin_nontemporal_store(v[u], b + j); else b[j] = v[u];
+        }
+    }
+}
+
 // Read n 16-B vectors, write n * NUM / DEN of them (a stream at the kernels'
 // write ratios): each block owns contiguous chunks of 256 * U vectors, loads
 // them U deep, and writes its share of the chunk contiguously.
@@ -310,6 +333,13 @@ int main(int argc, char** argv)
         u32x4* qq;
         CK(hipFree(q));
         CK(hipMalloc(&qq, bytes));  // stream_ratio 1/1 writes as much as it reads
+        for (size_t sz : {(size_t)1 << 30, (size_t)4 << 30}) {
+            const size_t fn = sz / 16;
+#define CF(V, A, B) { const unsigned nb = (unsigned)((fn + 256 * V - 1) / (256 * V)); \
+            float ms = timeit([&] { hipLaunchKernelGGL((copy_flat<V, A, B>), dim3(nb), dim3(256), 0, 0, p, qq, fn); }, reps); \
+            printf("copy_flat V=%d ntl=%d nts=%d bytes=%zu  %.3f ms  %.1f GB/s (read+write)\n", V, (int)A, (int)B, sz, ms, 2.0 * sz / ms / 1e6); }
+            CF(1, false, false) CF(1, true, true) CF(1, true, false) CF(2, false, false) CF(4, false, false) CF(4, true, true)
+        }
         for (int blocks : {1024, 2048, 4096}) {
 #define CU(U, A, B) { float ms = timeit([&] { hipLaunchKernelGGL((copyU<U, A, B>), dim3(blocks), dim3(256), 0, 0, p, qq, cn); }, reps); \
         printf("copyU U=%d ntl=%d nts=%d blocks=%d  %.3f ms  %.1f GB/s (read+write)\n", U, (int)A, (int)B, blocks, ms, 2.0 * cb / ms / 1e6); }
