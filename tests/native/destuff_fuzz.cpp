@@ -16,9 +16,10 @@ int main() {
         std::vector<uint8_t> o1(n + 64, 0xAA), o2(n + 64, 0xAA);
         std::vector<int64_t> s1, s2;
         s1.assign(1, 0); s2.assign(1, 0);
-        size_t a = wicca::destuff_scalar(in.data(), n, 0, o1.data(), 0, s1);
-        size_t b = wicca::destuff_avx2(in.data(), n, o2.data(), s2);
-        if (a != b || s1 != s2 || memcmp(o1.data(), o2.data(), a) != 0) { if (bad++ < 5) printf("mismatch t=%d n=%zu a=%zu b=%zu\n", t, n, a, b); }
+        bool r1 = false, r2 = false;
+        size_t a = wicca::destuff_scalar(in.data(), n, 0, o1.data(), 0, s1, r1);
+        size_t b = wicca::destuff_avx2(in.data(), n, o2.data(), s2, r2);
+        if (a != b || s1 != s2 || r1 != r2 || memcmp(o1.data(), o2.data(), a) != 0) { if (bad++ < 5) printf("mismatch t=%d n=%zu a=%zu b=%zu\n", t, n, a, b); }
     }
     printf("bad=%d\n", bad);
     return bad != 0;

@@ -281,3 +281,86 @@ def test_load_image_prints_the_reference_message(tmp_path, capsys, monkeypatch):
     monkeypatch.setenv("WICCA_LOAD_DETAIL", "1")
     assert wicca_amd.load_image(str(p)) is None
     assert "unrecognised image format" in capsys.readouterr().out
+
+
+def host_coefs_as_libjpeg_pixels(data: bytes, img, quality: int, sub: int):
+    """libjpeg-turbo's pixels for the host entropy decoder's coefficients of
+    `data`: the coefficients re-encoded as a sequential file (tests/jpeg_scans.py;
+    same quantisation tables: a baseline encode of the same image and quality)
+    and decoded by Pillow."""
+    from jpeg_scans import coefficients, split_scans
+    base = J.encode(img, quality, sub)
+    return J.decode_rgb(split_scans(base, coefficients(data, 1)))
+
+
+DAMAGED = [("scene", 2, 0), ("scene", 2, 8), ("noise", 0, 0), ("scene", 1, 3), ("gray", 0, 0), ("smooth", 2, 16)]
+
+
+@pytest.mark.parametrize("kind,sub,rb", DAMAGED, ids=[f"{k}-s{s}-r{r}" for k, s, r in DAMAGED])
+@pytest.mark.parametrize("cut", [0.2, 0.3, 0.5, 0.7, 0.95, 0.999])
+def test_host_decoder_on_truncated_files_matches_libjpeg(kind, sub, rb, cut):
+    """The host entropy decoder (which redoes every file the device marks
+    damaged) on a truncated file: its coefficients give libjpeg-turbo's pixels
+    for the file (Pillow with LOAD_TRUNCATED_IMAGES: the fake EOI cv2.imread's
+    source manager also inserts; the running MCU decoded on from zero bits,
+    the rest grey)."""
+    img = J.test_image(kind, 200, 344, 17 + sub + rb)
+    if kind == "gray":
+        img = img[..., 0] if img.ndim == 3 else img
+    data = J.encode(img, 88, sub, rb)
+    short = data[:int(len(data) * cut)]
+    assert np.array_equal(host_coefs_as_libjpeg_pixels(short, img, 88, sub), J.decode_rgb(short, truncated=True))
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_host_decoder_on_corrupted_files_matches_libjpeg(seed):
+    """Flipped bytes inside the entropy-coded data (markers intact): codes no
+    table has (17 bits, symbol 0), runs past coefficient 63 (written to 63),
+    segments whose data runs out; the host decoder's coefficients give
+    libjpeg-turbo's pixels."""
+    rng = np.random.default_rng(100 + seed)
+    kind = ("scene", "noise", "smooth")[seed % 3]
+    sub = seed % 3
+    img = J.test_image(kind, 160, 232, seed)
+    data = bytearray(J.encode(img, 80, sub, 8 if seed % 2 else 0))
+    sos = bytes(data).index(b"\xff\xda")
+    start = sos + 2 + int.from_bytes(data[sos + 2:sos + 4], "big")
+    for pos in rng.integers(start + 4, len(data) - 4, 3 + seed):
+        if data[pos] != 0xFF and data[pos - 1] != 0xFF:
+            nv = data[pos] ^ int(rng.integers(1, 255))
+            if nv != 0xFF:
+                data[pos] = nv
+    try:
+        got = host_coefs_as_libjpeg_pixels(bytes(data), img, 80, sub)
+    except KeyError:  # a coefficient the re-encoder's tables cannot code (size > 10)
+        pytest.skip("coefficients outside the baseline tables")
+    assert np.array_equal(got, J.decode_rgb(bytes(data), truncated=True))
+
+
+RST_DAMAGE = ["next1", "next2", "prior1", "far", "dropped", "garbage-ff00", "not-rst"]
+
+
+@pytest.mark.parametrize("how", RST_DAMAGE)
+def test_host_decoder_resyncs_restart_markers_like_libjpeg(how):
+    """Damaged restart markers: libjpeg's read_restart_marker /
+    jpeg_resync_to_restart (an RSTn one or two ahead leaves the segment empty,
+    one or two behind is skipped, one further off is taken; stray bytes with
+    FF00 pairs before a marker are skipped) -- the host decoder's coefficients
+    give libjpeg-turbo's pixels."""
+    img = J.test_image("scene", 160, 232, 5)
+    data = bytearray(J.encode(img, 85, 2, 4))
+    sos = bytes(data).index(b"\xff\xda")
+    start = sos + 2 + int.from_bytes(data[sos + 2:sos + 4], "big")
+    rst = [i for i in range(start, len(data) - 1) if data[i] == 0xFF and 0xD0 <= data[i + 1] <= 0xD7]
+    at = rst[len(rst) // 3]
+    num = data[at + 1] - 0xD0
+    if how in ("next1", "next2", "prior1", "far"):
+        data[at + 1] = 0xD0 + (num + {"next1": 1, "next2": 2, "prior1": -1, "far": 4}[how]) % 8
+    elif how == "dropped":
+        del data[at:at + 2]
+    elif how == "garbage-ff00":
+        data[at:at] = b"\x12\xff\x00\x34\xff\xff\x00\x56"
+    else:
+        data[at + 1] = 0x01  # TEM: a code below SOF0, skipped by the resync
+    got = host_coefs_as_libjpeg_pixels(bytes(data), img, 85, 2)
+    assert np.array_equal(got, J.decode_rgb(bytes(data), truncated=True))

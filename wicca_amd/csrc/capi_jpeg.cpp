@@ -187,9 +187,39 @@ int serial_record(int device, hipStream_t stream)
 // async_rounds > 0 (n <= one pass): everything is issued on `stream` and the
 // call returns without waiting; *async_flags gets the device flags to check
 // once the stream is done (jpeg_decode_device).
+// The single interleaved scan of a sequential file as a host scan (the host
+// entropy decoder then decodes it: damaged files, see JpegPlan::damage).
+void make_host_scan(wicca::JpegInfo& f)
+{
+    if (f.host_scans) return;
+    wicca::JpegScan sc;
+    sc.ns = f.ncomp;
+    // the scan's component order is the order of the MCU slots
+    int order = 0;
+    for (int k = 0; k < f.bpm && order < f.ncomp; ++k)
+        if (k == 0 || f.slot_comp[k] != f.slot_comp[k - 1]) sc.comp[order++] = f.slot_comp[k];
+    for (int i = 0; i < sc.ns; ++i) {
+        sc.dc[i] = f.dc[f.comp[sc.comp[i]].td];
+        sc.ac[i] = f.ac[f.comp[sc.comp[i]].ta];
+    }
+    sc.restart_interval = f.restart_interval;
+    sc.data = f.scan;
+    sc.len = wicca::scan_data_end(f.scan, f.scan_len, 0);
+    f.scans.push_back(sc);
+    f.host_scans = true;
+}
+
+// force_host: every file through the host entropy decoder (the redo of
+// damaged files).  damage_out (async calls): the device's per-image damage
+// flags, to be read once the stream is done; a synchronous call reads them
+// itself and redoes the damaged images with the host decoder, which follows
+// libjpeg-turbo's rules for damaged data (a code no table has, runs past
+// coefficient 63, data that ends inside an MCU: that MCU decoded on from zero
+// bits, the rest of the segment grey).
 int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
                           uint8_t* const* dst, const int64_t* dpitch, bool orient, hipStream_t stream,
-                          int* rounds_out, int async_rounds = 0, const int** async_flags = nullptr)
+                          int* rounds_out, int async_rounds = 0, const int** async_flags = nullptr,
+                          bool force_host = false, const int32_t** damage_out = nullptr)
 {
     // at most kJpegMaxJobs (image, component) IDCT jobs per device pass
     constexpr int64_t kChunk = wicca::kJpegMaxJobs / wicca::kJpegMaxComp;
@@ -197,7 +227,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         for (int64_t a = 0; a < n; a += kChunk) {
             const int64_t m = std::min(kChunk, n - a);
             int rc = jpeg_decode_to_device(ws, data + a, sizes + a, m, dst + a, dpitch + a, orient, stream,
-                                           rounds_out);
+                                           rounds_out, 0, nullptr, force_host);
             if (rc) return rc;
         }
         return WICCA_OK;
@@ -207,6 +237,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     for (int64_t i = 0; i < n; ++i) {
         int rc = parse_one(data[i], sizes[i], &info[(size_t)i], i);
         if (rc) return rc;
+        if (force_host) make_host_scan(info[(size_t)i]);
     }
     // coefficient layout: image i's components back to back from coef0[i]
     // blocks (component c: bw x bh blocks); multi-scan files (progressive,
@@ -248,6 +279,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     HIP_TRY(hipMemcpyAsync(stream_d + img_off[(size_t)n], stream_h + img_off[(size_t)n], 64,
                            hipMemcpyHostToDevice, stream));
     std::vector<std::vector<int64_t>> seg_off((size_t)n);
+    std::vector<char> rst_ok((size_t)n, 1);  // RSTn markers in sequence (else: a damaged file)
     std::atomic<int> upload_err{0};
     {
         const int nt = (int)std::min<int64_t>(n, 16);
@@ -269,8 +301,10 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
                         upload_err = 1;
                     continue;
                 }
+                bool in_order = true;
                 const size_t got = wicca::jpeg_destuff_into(info[(size_t)i], stream_h + img_off[(size_t)i],
-                                                            seg_off[(size_t)i]);
+                                                            seg_off[(size_t)i], &in_order);
+                rst_ok[(size_t)i] = in_order;
                 memset(stream_h + img_off[(size_t)i] + got, 0, info[(size_t)i].scan_len - got);
                 const int64_t a = img_off[(size_t)i], len = img_off[(size_t)i + 1] - a;
                 if (hipMemcpyAsync(stream_d + a, stream_h + a, (size_t)len, hipMemcpyHostToDevice, stream) !=
@@ -392,7 +426,8 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     const size_t o_huf = o_img + (size_t)round_up((int64_t)(ims.size() * sizeof(wicca::JpegImageDev)), 256);
     const size_t o_hsy = o_huf + (size_t)round_up((int64_t)(huff.size() * sizeof(wicca::HuffDev)), 256);
     const size_t meta_bytes = o_hsy + huff_sync.size() * sizeof(wicca::HuffDevSync);
-    HIP_TRY(ws->jmeta.reserve(meta_bytes));
+    const size_t o_dmg = (size_t)round_up((int64_t)meta_bytes, 256);  // per-image damage flags (not uploaded)
+    HIP_TRY(ws->jmeta.reserve(o_dmg + (size_t)n * sizeof(int32_t)));
     HIP_TRY(ws->jplanes.reserve((size_t)std::max<int64_t>(plane_bytes, 256)));
     HIP_TRY(ws->jscratch.reserve(wicca::jpeg_scratch_bytes((int64_t)sub_seg.size(), (int64_t)segs.size())));
     if (tmp_bytes) HIP_TRY(ws->jtmp.reserve((size_t)tmp_bytes));
@@ -412,7 +447,19 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     memcpy(packed + o_huf, huff.data(), huff.size() * sizeof(wicca::HuffDev));
     memcpy(packed + o_hsy, huff_sync.data(), huff_sync.size() * sizeof(wicca::HuffDevSync));
     HIP_TRY(hipMemcpyAsync(m, packed, meta_bytes, hipMemcpyHostToDevice, stream));
+    int32_t* damage = (int32_t*)(m + o_dmg);
+    HIP_TRY(hipMemsetAsync(damage, 0, (size_t)n * sizeof(int32_t), stream));
+    for (int64_t i = 0; i < n; ++i) {  // markers out of sequence or missing: damaged before the decode starts
+        const wicca::JpegInfo& f = info[(size_t)i];
+        if (f.host_scans) continue;
+        const int64_t mcus = (int64_t)f.mcux * f.mcuy;
+        const int64_t ri = f.restart_interval > 0 ? f.restart_interval : mcus;
+        const int64_t nseg = std::max<int64_t>(1, (mcus + ri - 1) / ri);
+        if (!rst_ok[(size_t)i] || (int64_t)seg_off[(size_t)i].size() - 1 < nseg)
+            HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(damage + i), 1, 1, stream));
+    }
     wicca::JpegPlan P{};
+    P.damage = damage;
     P.stream = stream_d;
     P.segs = (const wicca::JpegSegDev*)(m + o_seg);
     P.sub_seg = (const int32_t*)(m + o_sub);
@@ -458,12 +505,34 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
                                          info[(size_t)i].H, info[(size_t)i].orientation, dst[i], dpitch[i],
                                          stream));
     if (async_rounds > 0 && t_async_done) (void)hipEventRecord(t_async_done, stream);
+    if (damage_out) *damage_out = damage;
     if (async_rounds > 0) {  // the caller holds the workspace (and its pinned staging) until it waits
         sync_on_exit.active = false;
         return WICCA_OK;
     }
     // the pinned staging (streams, tables) is reused by the next call
     HIP_TRY(hipStreamSynchronize(stream));
+    if (!force_host) {  // damaged files: again, through the host entropy decoder
+        std::vector<int32_t> dmg((size_t)n, 0);
+        HIP_TRY(hipMemcpyAsync(dmg.data(), damage, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        std::vector<const uint8_t*> rd;
+        std::vector<int64_t> rs, rp;
+        std::vector<uint8_t*> ro;
+        for (int64_t i = 0; i < n; ++i)
+            if (dmg[(size_t)i] && !info[(size_t)i].host_scans) {
+                rd.push_back(data[i]);
+                rs.push_back(sizes[i]);
+                ro.push_back(dst[i]);
+                rp.push_back(dpitch[i]);
+            }
+        if (!rd.empty()) {
+            int redo_rounds = 0;
+            const int rc = jpeg_decode_to_device(ws, rd.data(), rs.data(), (int64_t)rd.size(), ro.data(), rp.data(),
+                                                 orient, stream, &redo_rounds, 0, nullptr, true);
+            if (rc) return rc;
+        }
+    }
     if (jpeg_timing())
         fprintf(stderr, "[wicca jpeg] %lld files: parse+destuff %.2f ms, tables+upload issue %.2f ms, "
                 "device decode %.2f ms (%d sync passes), sub_bits %lld\n", (long long)n, t_destuffed - t_start,
@@ -662,6 +731,7 @@ struct AsyncDecode {
     int device = 0;
     hipStream_t stream = nullptr;
     const int* flags = nullptr;  // device ring of per-round "changed" flags
+    const int32_t* damage = nullptr;  // device per-image damage flags (redone with the host decoder)
     std::vector<const uint8_t*> data;  // for the synchronous redo if the rounds launched did not converge
     std::vector<int64_t> sizes, pitches;
     std::vector<uint8_t*> dsts;
@@ -681,6 +751,7 @@ struct AsyncStage {
     int device = 0;
     hipStream_t stream = nullptr;
     const int* flags = nullptr;
+    const int32_t* damage = nullptr;
     std::vector<const uint8_t*> data;
     std::vector<int64_t> sizes;
     int depth = 0, border = 1, k = 0, interpolation = 3;
@@ -763,7 +834,7 @@ int wicca_jpeg_decode_u8_async(const uint8_t* const* data, const int64_t* sizes,
     const double t0 = now_ms();
     t_async_ready = t_async_done = nullptr;
     if ((rc = jpeg_decode_to_device(st->lease.ws, data, sizes, n, dsts, dst_pitches, apply_orientation != 0,
-                                    st->stream, &rounds, kAsyncRounds, &st->flags)))
+                                    st->stream, &rounds, kAsyncRounds, &st->flags, false, &st->damage)))
         return rc;
     st->ready = t_async_ready;
     st->done = t_async_done;
@@ -827,6 +898,30 @@ int wicca_jpeg_wait(int64_t ticket)
             if ((rc = jpeg_decode_to_device(st->lease.ws, st->data.data(), st->sizes.data(),
                                             (int64_t)st->data.size(), st->dsts.data(), st->pitches.data(),
                                             st->orient, st->stream, &rounds)))
+                return rc;
+            return WICCA_OK;  // the synchronous decode redid its damaged files itself
+        }
+    }
+    if (st->damage) {  // damaged files: again, through the host entropy decoder
+        const int64_t n = (int64_t)st->data.size();
+        std::vector<int32_t> dmg((size_t)n, 0);
+        HIP_TRY(hipMemcpyAsync(dmg.data(), st->damage, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost,
+                               st->stream));
+        HIP_TRY(hipStreamSynchronize(st->stream));
+        std::vector<const uint8_t*> rd;
+        std::vector<int64_t> rs, rp;
+        std::vector<uint8_t*> ro;
+        for (int64_t i = 0; i < n; ++i)
+            if (dmg[(size_t)i]) {
+                rd.push_back(st->data[(size_t)i]);
+                rs.push_back(st->sizes[(size_t)i]);
+                ro.push_back(st->dsts[(size_t)i]);
+                rp.push_back(st->pitches[(size_t)i]);
+            }
+        if (!rd.empty()) {
+            int rounds = 0;
+            if ((rc = jpeg_decode_to_device(st->lease.ws, rd.data(), rs.data(), (int64_t)rd.size(), ro.data(),
+                                            rp.data(), st->orient, st->stream, &rounds, 0, nullptr, true)))
                 return rc;
         }
     }
@@ -967,22 +1062,7 @@ int wicca_jpeg_host_coefficients(const uint8_t* data, int64_t size, int force_ho
                                     (long long)b);
     if (!f.host_scans) {
         if (!force_host) return fail(WICCA_ERR_ARG, "a single-scan sequential file is decoded on the device");
-        // the file's one interleaved scan as a host scan
-        wicca::JpegScan sc;
-        sc.ns = f.ncomp;
-        // the scan's component order is the order of the MCU slots
-        int order = 0;
-        for (int k = 0; k < f.bpm && order < f.ncomp; ++k)
-            if (k == 0 || f.slot_comp[k] != f.slot_comp[k - 1]) sc.comp[order++] = f.slot_comp[k];
-        for (int i = 0; i < sc.ns; ++i) {
-            sc.dc[i] = f.dc[f.comp[sc.comp[i]].td];
-            sc.ac[i] = f.ac[f.comp[sc.comp[i]].ta];
-        }
-        sc.restart_interval = f.restart_interval;
-        sc.data = f.scan;
-        sc.len = wicca::scan_data_end(f.scan, f.scan_len, 0);
-        f.scans.push_back(sc);
-        f.host_scans = true;
+        make_host_scan(f);  // the file's one interleaved scan as a host scan
     }
     memset(out, 0, (size_t)b * 128);
     int64_t rel[wicca::kJpegMaxComp] = {0, 0, 0};
@@ -1250,7 +1330,7 @@ int wicca_image_icon_stage_async(const uint8_t* const* data, const int64_t* size
     int rounds = 0;
     t_async_ready = t_async_done = nullptr;
     if ((rc = jpeg_decode_to_device(ws, data, sizes, n, d.data(), p.data(), true, cs, &rounds, kAsyncRounds,
-                                    &st->flags)))
+                                    &st->flags, false, &st->damage)))
         return rc;
     for (hipEvent_t* e : {&t_async_ready, &t_async_done})  // the decode's timing events: not reported here
         if (*e) {
@@ -1312,8 +1392,15 @@ int wicca_image_stage_wait(int64_t ticket)
     bool converged = false;
     for (int r = 1; r <= kAsyncRounds; ++r) converged |= h[r % 16] == 0;
     const int64_t n = (int64_t)st->data.size();
+    if (converged && st->damage) {  // a damaged file: the synchronous stage redoes it with the host decoder
+        std::vector<int32_t> dmg((size_t)n, 0);
+        HIP_TRY(hipMemcpyAsync(dmg.data(), st->damage, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost,
+                               st->stream));
+        HIP_TRY(hipStreamSynchronize(st->stream));
+        for (int64_t i = 0; i < n && converged; ++i) converged = dmg[(size_t)i] == 0;
+    }
     if (!converged) {  // rare: the whole stage again, synchronously, with the host looking at every round
-        const AsyncStage a = {WorkspaceLease(), st->device, nullptr, nullptr, st->data, st->sizes, st->depth,
+        const AsyncStage a = {WorkspaceLease(), st->device, nullptr, nullptr, nullptr, st->data, st->sizes, st->depth,
                               st->border, st->k, st->interpolation, st->out_w, st->out_h, st->resized, st->icons};
         st.reset();  // the workspace goes back to the pool before the synchronous call leases one
         return icon_stage_impl(a.data.data(), a.sizes.data(), n, a.depth, a.border, a.k, a.out_w, a.out_h,

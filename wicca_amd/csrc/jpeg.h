@@ -83,7 +83,7 @@ int jpeg_parse(const uint8_t* data, size_t size, JpegInfo* info, std::string* er
 void jpeg_host_decode(const JpegInfo& info, int16_t* coef, const int64_t* comp_block0);
 
 // End of entropy-coded data starting at d[pos]: the first marker other than
-// stuffing, fill bytes or RSTn (its 0xFF), or n.
+// stuffing, fill bytes, RSTn or a code below SOF0 (its 0xFF), or n.
 size_t scan_data_end(const uint8_t* d, size_t n, size_t pos);
 
 // Remove byte stuffing (FF 00 -> FF) and split at RSTn markers: `out` gets the
@@ -91,8 +91,10 @@ size_t scan_data_end(const uint8_t* d, size_t n, size_t pos);
 // first byte of segment s (seg_off.back() = out.size()).
 void jpeg_destuff(const JpegInfo& info, std::vector<uint8_t>& out, std::vector<int64_t>& seg_off);
 // The same into out[0 .. info.scan_len) (the de-stuffed data is never longer);
-// returns the de-stuffed length.
-size_t jpeg_destuff_into(const JpegInfo& info, uint8_t* out, std::vector<int64_t>& seg_off);
+// returns the de-stuffed length.  *rst_in_order (if given): every RSTn
+// carries the number the sequence expects (false: libjpeg resynchronises).
+size_t jpeg_destuff_into(const JpegInfo& info, uint8_t* out, std::vector<int64_t>& seg_off,
+                         bool* rst_in_order = nullptr);
 
 // ---------------------------------------------------------------------------
 // Device plan (built on the host, uploaded once per decode call).
@@ -147,6 +149,9 @@ struct JpegPlan {
     int32_t sub_bits;        // subsequence length
     const int32_t* sub_img;  // per workgroup of kJpegLanes subsequences: its image (uniform)
     int32_t max_tabs;        // most Huffman tables one image of the batch uses (<= 2 * kJpegMaxComp)
+    int32_t* damage;         // per image: set by the write pass where the data is damaged (a code no
+                             // table has, a run past coefficient 63, a segment whose data ends before
+                             // its blocks do); the host redoes those images with the host decoder
 };
 
 // Lanes per decode workgroup; an image's subsequences are padded to whole

@@ -126,8 +126,9 @@ struct BitReader {
 };
 
 // (code length << 8) | symbol of the codeword at the top of `look` (the next
-// 32 bits); a bit string that is no code (only off the true decode path)
-// reads as symbol 0 after 16 bits, as in jdhuff.
+// 32 bits); a bit string that is no code reads as symbol 0 after 17 bits, as
+// in jdhuff.c (jpeg_huff_decode / HUFF_DECODE_FAST: the search runs to the
+// maxcode[17] sentinel).
 template <typename HT>
 __device__ __forceinline__ uint32_t huff_lookup(const HT& t, uint32_t look)
 {
@@ -144,7 +145,7 @@ __device__ __forceinline__ uint32_t huff_lookup(const HT& t, uint32_t look)
             l = m ? L : l;
             vo = m ? t.valoff[L] : vo;
         }
-        e = l ? ((uint32_t)l << 8) | t.vals[(vo + (int32_t)(look >> (32 - l))) & 255] : 16u << 8;
+        e = l ? ((uint32_t)l << 8) | t.vals[(vo + (int32_t)(look >> (32 - l))) & 255] : 17u << 8;
     }
     return e;
 }
@@ -308,8 +309,9 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BitReader& br, int6
                           DecState& st, int64_t& started, int32_t (&dc)[kJpegMaxComp], int64_t g,
                           int64_t block_lo, int64_t block_end, int16_t* coef, const WaveStage* ws = nullptr,
                           bool seg_last = false, SyncCk* ck = nullptr, int n_ck = 0, int64_t ck_base = 0,
-                          SyncCk* hit_ck = nullptr, int ck_step = 0)
+                          SyncCk* hit_ck = nullptr, int ck_step = 0, int32_t* damage = nullptr)
 {
+    bool bad = false;  // WRITE: the true decode path meets damaged data (see JpegPlan::damage)
     int nck = 0, hit = -1;
     uint32_t cur = 0;  // CK 2: pos_slot of checkpoint nck
     if (CK == 2 && n_ck > 0) cur = ck[0].pos_slot;
@@ -363,6 +365,7 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BitReader& br, int6
         const bool isdc = st.k == 0;
         const uint32_t e = huff_lookup(*(isdc ? tdc : tac), look);
         const int len = (int)(e >> 8), sym = (int)(e & 255);
+        if (WRITE) bad |= len > 16;
         const int s = isdc ? min(sym, 16) : (sym & 15);  // a DC size > 11 only in corrupt streams
         const int v = s ? extend((look << len) >> (32 - s), s) : 0;
         br.skip(len + s);
@@ -388,6 +391,7 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BitReader& br, int6
             const int r = sym >> 4;
             if (s) {
                 st.k += r;
+                if (WRITE) bad |= st.k > 63;  // libjpeg writes these to coefficient 63
                 if (WRITE && blk >= 0 && st.k < 64) {
                     const int n = ws->nat[st.k];
                     if (staged) {
@@ -422,6 +426,10 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BitReader& br, int6
         // call against 3.0 ms
         if (WRITE && WICCA_JPEG_STAGE) flush_blocks(done, blk, *ws, coef);
     }
+    // the segment's data ends before its last block does: libjpeg-turbo then
+    // decodes the running MCU on from zero bits (jdhuff.c jpeg_fill_bit_buffer)
+    if (WRITE && seg_last) bad |= g < block_end - 1 || (g == block_end - 1 && st.k != 0);
+    if (WRITE && bad && damage) atomicOr(damage, 1);
     if (WRITE && blk >= 0 && st.k > 0) {  // the range ends inside block blk: this lane's part [.., st.k)
         const int kend = min(st.k, 64);
         if (staged) {
@@ -729,7 +737,8 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 4 : 1) void jpeg_write_kernel(
 #endif
     // the block in progress at the start was started by an earlier lane
     decode_run<true>(im, tabs.t, br, b1, st, started, dc, sg.block0 + b.block - 1, sg.block0,
-                     sg.block_end, P.coef, &ws, j == sg.n_sub - 1);
+                     sg.block_end, P.coef, &ws, j == sg.n_sub - 1, nullptr, 0, 0, nullptr, 0,
+                     P.damage ? P.damage + sg.img : nullptr);
 }
 
 // ---------------------------------------------------------------------------

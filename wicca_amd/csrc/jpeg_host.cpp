@@ -86,7 +86,10 @@ size_t scan_data_end(const uint8_t* d, size_t n, size_t pos)
         while (j < n && d[j] == 0xFF) ++j;  // fill bytes
         if (j >= n) return n;
         const uint8_t m = d[j];
-        if (m == 0x00 || (m >= 0xD0 && m <= 0xD7)) {
+        // stuffing, RSTn, and codes below SOF0 (no valid marker: libjpeg's
+        // resync skips them, read_markers takes 0x01 TEM as parameterless)
+        // stay inside the scan; the bit reader stops at them by itself
+        if (m < 0xC0 || (m >= 0xD0 && m <= 0xD7)) {
             i = j;
             continue;
         }
@@ -340,7 +343,12 @@ namespace {
 // One 0xFF at s[*i] (i + 1 < n): a stuffed data byte, a fill byte, an RSTn
 // (the next restart segment starts at the current output length) or the end
 // of the scan.  Returns false at the end of the scan.
-inline bool destuff_marker(const uint8_t* s, size_t& i, uint8_t* out, size_t& o, std::vector<int64_t>& seg_off)
+// An RSTn out of sequence (not RST(k mod 8) for the k-th marker) sets
+// rst_bad: libjpeg resynchronises there (jdmarker.c read_restart_marker /
+// jpeg_resync_to_restart), which the device's one-segment-per-marker split
+// does not follow.
+inline bool destuff_marker(const uint8_t* s, size_t& i, uint8_t* out, size_t& o, std::vector<int64_t>& seg_off,
+                           bool& rst_bad)
 {
     const uint8_t nx = s[i + 1];
     if (nx == 0x00) {  // stuffed data byte
@@ -349,6 +357,7 @@ inline bool destuff_marker(const uint8_t* s, size_t& i, uint8_t* out, size_t& o,
     } else if (nx == 0xFF) {  // fill byte
         i += 1;
     } else if (nx >= 0xD0 && nx <= 0xD7) {  // RSTn: next segment starts byte-aligned
+        rst_bad |= (size_t)(nx - 0xD0) != ((seg_off.size() - 1) & 7);
         seg_off.push_back((int64_t)o);
         i += 2;
     } else {
@@ -358,7 +367,8 @@ inline bool destuff_marker(const uint8_t* s, size_t& i, uint8_t* out, size_t& o,
 }
 
 // Scalar tail / fallback: memchr to the next 0xFF, memcpy the run.
-size_t destuff_scalar(const uint8_t* s, size_t n, size_t i, uint8_t* out, size_t o, std::vector<int64_t>& seg_off)
+size_t destuff_scalar(const uint8_t* s, size_t n, size_t i, uint8_t* out, size_t o, std::vector<int64_t>& seg_off,
+                      bool& rst_bad)
 {
     while (i < n) {
         const uint8_t* ff = (const uint8_t*)memchr(s + i, 0xFF, n - i);
@@ -367,7 +377,7 @@ size_t destuff_scalar(const uint8_t* s, size_t n, size_t i, uint8_t* out, size_t
         o += run;
         i += run;
         if (i + 1 >= n) break;  // end of data (a lone trailing 0xFF is dropped)
-        if (!destuff_marker(s, i, out, o, seg_off)) break;
+        if (!destuff_marker(s, i, out, o, seg_off, rst_bad)) break;
     }
     seg_off.push_back((int64_t)o);
     return o;
@@ -379,7 +389,7 @@ size_t destuff_scalar(const uint8_t* s, size_t n, size_t i, uint8_t* out, size_t
 // ahead of the input (o <= i), so a full 32-byte store at out + o stays inside
 // the caller's n-byte region.
 __attribute__((target("avx2"))) size_t destuff_avx2(const uint8_t* s, size_t n, uint8_t* out,
-                                                    std::vector<int64_t>& seg_off)
+                                                    std::vector<int64_t>& seg_off, bool& rst_bad)
 {
     size_t i = 0, o = 0;
     const __m256i ff = _mm256_set1_epi8((char)0xFF);
@@ -399,22 +409,25 @@ __attribute__((target("avx2"))) size_t destuff_avx2(const uint8_t* s, size_t n, 
             seg_off.push_back((int64_t)o);
             return o;
         }
-        if (!destuff_marker(s, i, out, o, seg_off)) {
+        if (!destuff_marker(s, i, out, o, seg_off, rst_bad)) {
             seg_off.push_back((int64_t)o);
             return o;
         }
     }
-    return destuff_scalar(s, n, i, out, o, seg_off);
+    return destuff_scalar(s, n, i, out, o, seg_off, rst_bad);
 }
 
 }  // namespace
 
-size_t jpeg_destuff_into(const JpegInfo& info, uint8_t* out, std::vector<int64_t>& seg_off)
+size_t jpeg_destuff_into(const JpegInfo& info, uint8_t* out, std::vector<int64_t>& seg_off, bool* rst_in_order)
 {
     seg_off.assign(1, 0);
+    bool rst_bad = false;
     static const bool avx2 = __builtin_cpu_supports("avx2");
-    if (avx2) return destuff_avx2(info.scan, info.scan_len, out, seg_off);
-    return destuff_scalar(info.scan, info.scan_len, 0, out, 0, seg_off);
+    const size_t got = avx2 ? destuff_avx2(info.scan, info.scan_len, out, seg_off, rst_bad)
+                            : destuff_scalar(info.scan, info.scan_len, 0, out, 0, seg_off, rst_bad);
+    if (rst_in_order) *rst_in_order = !rst_bad;
+    return got;
 }
 
 void jpeg_destuff(const JpegInfo& info, std::vector<uint8_t>& out, std::vector<int64_t>& seg_off)
@@ -544,21 +557,55 @@ struct HostBits {
         skip(k);
         return v;
     }
-    // process_restart: drop the bits left, consume the RSTn marker
-    void restart()
+    // jdmarker.c next_marker: skip to the next marker, past non-0xFF bytes,
+    // fill bytes and stuffed FF00 pairs; pos ends on the 0xFF in front of it.
+    // The end of the data reads as an EOI (the fake one a truncated decode gets).
+    int next_marker()
+    {
+        size_t j = pos;
+        for (;;) {
+            while (j < n && d[j] != 0xFF) ++j;
+            while (j < n && d[j] == 0xFF) ++j;
+            if (j >= n) {
+                pos = n;
+                return 0xD9;
+            }
+            if (d[j] != 0x00) {
+                pos = j - 1;
+                return d[j];
+            }
+            ++j;
+        }
+    }
+    // process_restart: drop the bits left, then read_restart_marker for RST
+    // number `want` (next_restart_num), resynchronising as
+    // jpeg_resync_to_restart does when the marker found is another one
+    void restart(int want)
     {
         buf = 0;
         cnt = zeros = 0;
-        size_t j = pos;
-        while (j < n && d[j] != 0xFF) ++j;  // bytes the encoder left before the marker (corrupt streams)
-        while (j < n && d[j] == 0xFF) ++j;
-        if (j < n && d[j] >= 0xD0 && d[j] <= 0xD7) {
-            pos = j + 1;
-            at_marker = false;
-            insufficient = false;
-        } else {
-            pos = j > 0 ? j - 1 : j;
-            at_marker = true;  // no restart marker where one was due: the segment reads as empty
+        int m = at_marker ? (pos + 1 < n ? d[pos + 1] : 0xD9) : next_marker();
+        for (;;) {
+            int action;
+            const auto rst = [](int k) { return 0xD0 + (k & 7); };
+            if (m == rst(want)) action = 1;
+            else if (m < 0xC0) action = 2;                                   // not a valid marker
+            else if (m < 0xD0 || m > 0xD7) action = 3;                       // a marker but no RSTn
+            else if (m == rst(want + 1) || m == rst(want + 2)) action = 3;   // one of the next two
+            else if (m == rst(want - 1) || m == rst(want - 2)) action = 2;   // a prior one: advance
+            else action = 1;                                                 // too far away: accept
+            if (action == 1) {  // consume it; the segment decodes from here
+                pos = std::min(n, pos + 2);
+                at_marker = false;
+                insufficient = false;
+                return;
+            }
+            if (action == 3) {  // leave it: the segment reads as empty
+                at_marker = pos < n;
+                return;
+            }
+            pos = std::min(n, pos + 2);
+            m = next_marker();
         }
     }
 };
@@ -696,11 +743,12 @@ void jpeg_host_decode(const JpegInfo& info, int16_t* coef, const int64_t* comp_b
                 --eobrun;
             }
         };
-        int restarts_to_go = sc.restart_interval;
+        int restarts_to_go = sc.restart_interval, next_restart_num = 0;
         auto before_mcu = [&]() {
             if (sc.restart_interval) {
                 if (restarts_to_go == 0) {  // process_restart
-                    br.restart();
+                    br.restart(next_restart_num);
+                    next_restart_num = (next_restart_num + 1) & 7;
                     for (int c = 0; c < kJpegMaxComp; ++c) last_dc[c] = 0;
                     eobrun = 0;
                     restarts_to_go = sc.restart_interval;
