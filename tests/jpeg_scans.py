@@ -184,3 +184,72 @@ def coefficients(data: bytes, force: int) -> np.ndarray:
                                           ctypes.byref(nb))
     assert rc == 0, _lib.last_error()
     return out
+
+
+def gray_file(coefs: np.ndarray, qt, W: int, H: int, restart: int = 0) -> bytes:
+    """A baseline one-component JPEG holding exactly `coefs` (bh x bw blocks
+    of 64 int16 quantised coefficients, natural order; bw = ceil(W/8)) and the
+    quantisation table `qt` (64 values, natural order; 16-bit precision when
+    any exceeds 255).  AC values within +-1023 and DC differences within
+    +-2047 (the T.81 K.3 / K.5 tables).  For IDCT parity probes."""
+    return coef_file([(coefs, qt)], W, H, restart)
+
+
+def coef_file(comps, W: int, H: int, restart: int = 0) -> bytes:
+    """gray_file for 1 or 3 components at 4:4:4 (interleaved MCUs of one
+    block per component): `comps` = [(coefs, qt), ...], table i for
+    component i."""
+    bw, bh = -(-W // 8), -(-H // 8)
+    nc = len(comps)
+    blocks = [np.asarray(c).reshape(bh * bw, 64) for c, _ in comps]
+    dqt = bytearray()
+    for i, (_, qt) in enumerate(comps):
+        qt = [int(q) for q in qt]
+        wide = max(qt) > 255
+        zq = [qt[_ZIGZAG[k]] for k in range(64)]
+        dqt += bytes([(0x10 if wide else 0x00) | i]) + (b"".join(q.to_bytes(2, "big") for q in zq) if wide
+                                                        else bytes(zq))
+    out = bytearray(b"\xff\xd8")
+    out += _seg(0xDB, bytes(dqt))
+    out += _seg(0xC0, bytes([8, H >> 8, H & 255, W >> 8, W & 255, nc]) +
+                b"".join(bytes([i + 1, 0x11, i]) for i in range(nc)))
+    out += _seg(0xC4, bytes([0x00]) + bytes(_DC_L_BITS) + bytes(_DC_VALS) + bytes([0x10]) + bytes(_AC_L_BITS) +
+                _AC_L_VALS)
+    if restart:
+        out += _seg(0xDD, bytes([restart >> 8, restart & 255]))
+    out += _seg(0xDA, bytes([nc]) + b"".join(bytes([i + 1, 0x00]) for i in range(nc)) + bytes([0, 63, 0]))
+    dc_t, ac_t = _codes(_DC_L_BITS, _DC_VALS), _codes(_AC_L_BITS, _AC_L_VALS)
+    bits = _Bits()
+    pred = [0] * nc
+    for i in range(bh * bw):
+        if restart and i and i % restart == 0:
+            out += bits.flush() + bytes([0xFF, 0xD0 + (i // restart - 1) % 8])
+            bits = _Bits()
+            pred = [0] * nc
+        for c in range(nc):
+            zz = [int(blocks[c][i][_ZIGZAG[k]]) for k in range(64)]
+            diff = zz[0] - pred[c]
+            pred[c] = zz[0]
+            s = _size(diff)
+            assert s <= 11, "DC difference outside +-2047"
+            bits.put(*dc_t[s])
+            if s:
+                bits.put(_vbits(diff, s), s)
+            run = 0
+            for k in range(1, 64):
+                v = zz[k]
+                if v == 0:
+                    run += 1
+                    continue
+                while run > 15:
+                    bits.put(*ac_t[0xF0])
+                    run -= 16
+                s = _size(v)
+                assert s <= 10, "AC value outside +-1023"
+                bits.put(*ac_t[(run << 4) | s])
+                bits.put(_vbits(v, s), s)
+                run = 0
+            if run:
+                bits.put(*ac_t[0x00])
+    out += bits.flush() + b"\xff\xd9"
+    return bytes(out)

@@ -382,6 +382,18 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
             }
             memcpy(im.qt[c], f.qt[k.tq], sizeof(im.qt[c]));
         }
+        im.fmt = wicca::kJpegFmtOther;  // the fused kernel's chroma path
+        if (f.ncomp == 1) {
+            im.fmt = wicca::kJpegFmtGray;
+        } else if (f.ncomp == 3) {
+            const wicca::JpegComponent &cb = f.comp[1], &cr = f.comp[2];
+            const bool alike = cb.h == cr.h && cb.v == cr.v && cb.bw == cr.bw && cb.bh == cr.bh && cb.dw == cr.dw &&
+                               cb.dh == cr.dh && (int64_t)cb.bw * 8 * cb.bh * 8 < ((int64_t)1 << 31);
+            if (alike && f.hmax == 2 * cb.h && f.vmax == 2 * cb.v && cb.dw > 2)
+                im.fmt = wicca::kJpegFmtH2V2;
+            else if (alike && f.hmax == cb.h && f.vmax == cb.v)
+                im.fmt = wicca::kJpegFmtH1V1;
+        }
         if (orient && f.orientation != 1) {  // decode into a temporary, then orient
             tmp_off[(size_t)i] = tmp_bytes;
             tmp_bytes += round_up((int64_t)f.W * 3, 128) * f.H;
@@ -526,6 +538,8 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
                 ro.push_back(dst[i]);
                 rp.push_back(dpitch[i]);
             }
+        if (jpeg_timing())
+            fprintf(stderr, "[wicca jpeg] %zu of %lld files damaged: redone on the host\n", rd.size(), (long long)n);
         if (!rd.empty()) {
             int redo_rounds = 0;
             const int rc = jpeg_decode_to_device(ws, rd.data(), rs.data(), (int64_t)rd.size(), ro.data(), rp.data(),

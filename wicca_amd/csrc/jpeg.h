@@ -114,8 +114,17 @@ struct HuffDevT {
 using HuffDev = HuffDevT<kHuffLutBits>;
 using HuffDevSync = HuffDevT<kHuffLutBitsSync>;
 
+// Chroma formats of the fused luma / colour kernel (JpegImageDev::fmt)
+enum : int32_t {
+    kJpegFmtGray = 0,   // one component
+    kJpegFmtH2V2 = 1,   // 4:2:0, Cb and Cr planes alike, wider than 2 samples, under 2^31 bytes
+    kJpegFmtH1V1 = 2,   // 4:4:4, planes under 2^31 bytes
+    kJpegFmtOther = 3,  // any other sampling: per-sample upsampling
+};
+
 struct JpegImageDev {
     int32_t W, H, ncomp, bpm, mcux, hmax, vmax;
+    int32_t fmt;  // kJpegFmt*
     int32_t slot_comp[kJpegMaxSlots], slot_h[kJpegMaxSlots], slot_v[kJpegMaxSlots];
     int32_t comp_h[kJpegMaxComp], comp_v[kJpegMaxComp], comp_bw[kJpegMaxComp], comp_bh[kJpegMaxComp];
     int32_t comp_dw[kJpegMaxComp], comp_dh[kJpegMaxComp];

@@ -742,128 +742,76 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 4 : 1) void jpeg_write_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// ISLOW IDCT (jidctint.c) — one lane per 8x8 block of one component.
+// ISLOW IDCT as libjpeg-turbo's x86-64 SIMD code computes it (jidctint-sse2 /
+// jidctint-avx2, the IDCT Pillow's and OpenCV's libjpeg-turbo builds run on
+// x86-64; third-party, not in the reference tree).  It is jidctint.c's
+// algorithm (CONST_BITS 13, PASS1_BITS 2) in 16-bit lanes, and for valid
+// coefficients equals it bit for bit; on damaged data it differs, and this
+// restates what it does there:
+//  - dequantisation keeps the low 16 bits of coefficient * quantiser (pmullw);
+//  - a block whose coefficient rows 1..7 are all zero takes pass 1's shortcut:
+//    every row of column c is the 16-bit (dequantised DC << PASS1_BITS) (psllw);
+//  - the butterfly pairs its products as pmaddwd does, (in0 + in4), (in0 - in4),
+//    (in7 + in3) and (in5 + in1) are 16-bit sums, the rest 32-bit modulo 2^32;
+//  - pass 1 and pass 2 results saturate to 16 bits (packssdw), pass 2's then
+//    to 8 bits (packsswb) before the +128 centring — a clamp, where
+//    jidctint.c's range-limit table wraps.
+// oracle/jpeg_idct.py restates it in NumPy, pinned against Pillow on files
+// built around extreme coefficients (tests/test_jpeg_idct.py).
 // ---------------------------------------------------------------------------
 struct IdctJob {
     int64_t block0, plane0;
     int32_t bw, bh, img, comp;
 };
 
-#define FIX_0_298631336 ((int64_t)2446)
-#define FIX_0_390180644 ((int64_t)3196)
-#define FIX_0_541196100 ((int64_t)4433)
-#define FIX_0_765366865 ((int64_t)6270)
-#define FIX_0_899976223 ((int64_t)7373)
-#define FIX_1_175875602 ((int64_t)9633)
-#define FIX_1_501321110 ((int64_t)12299)
-#define FIX_1_847759065 ((int64_t)15137)
-#define FIX_1_961570560 ((int64_t)16069)
-#define FIX_2_053119869 ((int64_t)16819)
-#define FIX_2_562915447 ((int64_t)20995)
-#define FIX_3_072711026 ((int64_t)25172)
+constexpr int kF0298 = 2446, kF0390 = 3196, kF0541 = 4433, kF0765 = 6270, kF0899 = 7373, kF1175 = 9633,
+              kF1501 = 12299, kF1847 = 15137, kF1961 = 16069, kF2053 = 16819, kF2562 = 20995, kF3072 = 25172;
 constexpr int kConstBits = 13, kPass1Bits = 2;
 
-__device__ __forceinline__ int64_t descale(int64_t x, int n) { return (x + ((int64_t)1 << (n - 1))) >> n; }
-__device__ __forceinline__ int32_t descale32(int32_t x, int n) { return (x + (1 << (n - 1))) >> n; }
+__device__ __forceinline__ int32_t sext16(int32_t x) { return (int32_t)(int16_t)x; }
 
-#ifndef WICCA_IDCT32
-#define WICCA_IDCT32 1  // 0: every chroma IDCT pass in 64-bit arithmetic
-#endif
-#ifndef WICCA_LUMA_IDCT32
-#define WICCA_LUMA_IDCT32 1  // 0: the fused luma IDCT always in 64-bit passes
-#endif
-constexpr int32_t kIdct32Max = 12600;  // 32-bit IDCT pass exact for inputs within +-kIdct32Max (with the descale rounding term)
-
-// The last pass's descale by 2^18 and idct_limit in one: bits 18..27 of the
-// rounded sum plus 512 << 18 (a 32-bit wrap does not touch them) are
-// (x + 512) & 1023 for x = the descaled value, and the table's four ranges
-// (x' < 128 -> x' + 128, < 512 -> 255, < 896 -> 0, else x' - 896, x' = x & 1023)
-// are clamp(((x + 512) & 1023) - 384, 0, 255).
-__device__ __forceinline__ uint8_t idct_limit_descale32(int32_t o)
+// a * c1 + b * c2 for 16-bit a, b and |c| < 2^15: pmaddwd's pair (exact in
+// int32), two full-rate 24-bit multiplies
+__device__ __forceinline__ uint32_t pmadd(int32_t a, int c1, int32_t b, int c2)
 {
-    constexpr int sh = kConstBits + kPass1Bits + 3;
-    const uint32_t w = ((uint32_t)o + (1u << (sh - 1)) + (512u << sh)) >> sh;
-    return (uint8_t)min(255, max(0, (int)(w & 1023u) - 384));
+    return (uint32_t)(__mul24(a, c1) + __mul24(b, c2));
 }
 
-// idct_sample_range_limit[x & 1023] of jdmaster.c's prepare_range_limit_table
-__device__ __forceinline__ uint8_t idct_limit(int64_t v)
+// The 1-D butterfly on 8 16-bit values (column r in pass 1, row r in pass 2);
+// `rnd` rides on the two even-part terms, so every output arrives with it
+// added once.  Sums modulo 2^32 (paddd).
+__device__ __forceinline__ void islow_simd(const int32_t (&v)[8], uint32_t rnd, uint32_t (&o)[8])
 {
-    const int x = (int)(v & 1023);
-    return (uint8_t)(x < 128 ? x + 128 : x < 512 ? 255 : x < 896 ? 0 : x - 896);
-}
-
-// jidctint.c's 1-D butterfly on 8 values (rows 0..7 of a column in pass 1,
-// columns 0..7 of a row in pass 2), JLONG = 64-bit products as libjpeg-turbo
-// computes them on LP64.  Returns the 8 outputs before descaling.  (A 32-bit
-// variant, exact while every input is below 2^13.5 — intermediates stay under
-// 2^17.45 times the input bound — ran slower: 1.81 vs 1.43 ms per 25 x 8K,
-// both paths taken within waves.)
-// x * c for the butterfly's constants: in the 32-bit passes both factors are
-// below 2^23 in magnitude (inputs <= kIdct32Max, sums of a few of them,
-// constants < 2^15), so the full-rate 24-bit multiply v_mul_i32_i24 gives the
-// exact product; a plain int32 multiply is the quarter-rate v_mul_lo_u32.
-template <typename T>
-__device__ __forceinline__ T mulk(T x, int64_t c);
-template <>
-__device__ __forceinline__ int32_t mulk<int32_t>(int32_t x, int64_t c) { return __mul24(x, (int)c); }
-template <>
-__device__ __forceinline__ int64_t mulk<int64_t>(int64_t x, int64_t c) { return x * c; }
-
-template <typename T>
-__device__ __forceinline__ void islow_1d(const T (&v)[8], T (&o)[8])
-{
-    T z2 = v[2], z3 = v[6];
-    T z1 = mulk<T>(z2 + z3, FIX_0_541196100);
-    T tmp2 = z1 + mulk<T>(z3, (-FIX_1_847759065));
-    T tmp3 = z1 + mulk<T>(z2, FIX_0_765366865);
-    z2 = v[0];
-    z3 = v[4];
-    T tmp0 = (z2 + z3) * ((T)1 << kConstBits);
-    T tmp1 = (z2 - z3) * ((T)1 << kConstBits);
-    const T tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
-    tmp0 = v[7];
-    tmp1 = v[5];
-    tmp2 = v[3];
-    tmp3 = v[1];
-    z1 = tmp0 + tmp3;
-    z2 = tmp1 + tmp2;
-    z3 = tmp0 + tmp2;
-    T z4 = tmp1 + tmp3;
-    const T z5 = mulk<T>(z3 + z4, FIX_1_175875602);
-    tmp0 = mulk<T>(tmp0, FIX_0_298631336);
-    tmp1 = mulk<T>(tmp1, FIX_2_053119869);
-    tmp2 = mulk<T>(tmp2, FIX_3_072711026);
-    tmp3 = mulk<T>(tmp3, FIX_1_501321110);
-    z1 = mulk<T>(z1, (-FIX_0_899976223));
-    z2 = mulk<T>(z2, (-FIX_2_562915447));
-    z3 = mulk<T>(z3, (-FIX_1_961570560));
-    z4 = mulk<T>(z4, (-FIX_0_390180644));
-    z3 += z5;
-    z4 += z5;
-    tmp0 += z1 + z3;
-    tmp1 += z2 + z4;
-    tmp2 += z2 + z3;
-    tmp3 += z1 + z4;
-    o[0] = tmp10 + tmp3;
-    o[7] = tmp10 - tmp3;
-    o[1] = tmp11 + tmp2;
-    o[6] = tmp11 - tmp2;
-    o[2] = tmp12 + tmp1;
-    o[5] = tmp12 - tmp1;
-    o[3] = tmp13 + tmp0;
-    o[4] = tmp13 - tmp0;
+    const uint32_t tmp3 = pmadd(v[2], kF0541 + kF0765, v[6], kF0541);
+    const uint32_t tmp2 = pmadd(v[2], kF0541, v[6], kF0541 - kF1847);
+    // (in0 +- in4) << CONST_BITS from the 16-bit sum: << 16 then arithmetic >> 3
+    const uint32_t tmp0 = (uint32_t)((int32_t)((uint32_t)(v[0] + v[4]) << 16) >> (16 - kConstBits)) + rnd;
+    const uint32_t tmp1 = (uint32_t)((int32_t)((uint32_t)(v[0] - v[4]) << 16) >> (16 - kConstBits)) + rnd;
+    const uint32_t tmp10 = tmp0 + tmp3, tmp13 = tmp0 - tmp3, tmp11 = tmp1 + tmp2, tmp12 = tmp1 - tmp2;
+    const int32_t z3 = sext16(v[7] + v[3]), z4 = sext16(v[5] + v[1]);
+    const uint32_t z3p = pmadd(z3, kF1175 - kF1961, z4, kF1175);
+    const uint32_t z4p = pmadd(z3, kF1175, z4, kF1175 - kF0390);
+    const uint32_t t0 = pmadd(v[7], kF0298 - kF0899, v[1], -kF0899) + z3p;
+    const uint32_t t3 = pmadd(v[7], -kF0899, v[1], kF1501 - kF0899) + z4p;
+    const uint32_t t1 = pmadd(v[5], kF2053 - kF2562, v[3], -kF2562) + z4p;
+    const uint32_t t2 = pmadd(v[5], -kF2562, v[3], kF3072 - kF2562) + z3p;
+    o[0] = tmp10 + t3;
+    o[7] = tmp10 - t3;
+    o[1] = tmp11 + t2;
+    o[6] = tmp11 - t2;
+    o[2] = tmp12 + t1;
+    o[5] = tmp12 - t1;
+    o[3] = tmp13 + t0;
+    o[4] = tmp13 - t0;
 }
 
 // Eight lanes per 8x8 block (a lane per row, then per column, then per row):
 // a block's 128 coefficient bytes are one coalesced read, every lane holds 8
 // values instead of 128 (one lane per block ran at 156 VGPRs, 3 waves per
-// SIMD), and the two transposes go through the wave's LDS.  The all-zero-AC
-// shortcuts of jidctint.c give the same values as the full butterfly, so
-// they are not needed for bit-exactness.
+// SIMD), and the two transposes go through the wave's LDS.
 constexpr int kIdctBlocksPerWg = 32;
 
-// Lane r of the 8 lanes of one block: dequantised row r in, row r of the
+// Lane r of the 8 lanes of one block: coefficient row r in (v), row r of the
 // block's samples out (px).  `t` is the block's LDS transpose area
 // (kTrBlock ints); every lane of the wave must call this (wave barriers),
 // `live` is uniform over the block's 8 lanes.
@@ -876,48 +824,40 @@ constexpr int kIdctBlocksPerWg = 32;
 // swizzle removed them at the price of per-access index arithmetic.
 constexpr int kTrPitch = 9, kTrBlock = 8 * kTrPitch;
 
-// I32: 32-bit passes where exact (else always 64-bit, as JLONG).
-template <bool I32>
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ void idct8_lane_v(uint4 v, const uint16_t* qt, int r, bool live, int32_t* t,
                                              uint8_t (&px)[8])
 {
     auto at = [&](int i, int j) { return i * kTrPitch + j; };
-    if (live) {
+    // pass 1's shortcut: the block's coefficient rows 1..7 all zero (lane r
+    // holds row r; a wave holds 8 blocks, 8 lanes each)
+    const bool nz = r != 0 && (v.x | v.y | v.z | v.w) != 0;
+    const uint64_t vote = __ballot(nz);
+    const bool ac_zero = ((vote >> (threadIdx.x & 56)) & 0xFFu) == 0;
+    if (live) {  // dequantised row r: the low 16 bits of each product, two per v_pk_mul_lo_u16
         const uint4 qv = *reinterpret_cast<const uint4*>(qt + r * 8);
         const uint32_t cw[4] = {v.x, v.y, v.z, v.w}, qw[4] = {qv.x, qv.y, qv.z, qv.w};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {  // dequantised row r (coefficient * quantiser fits in int32)
-            t[at(r, 2 * k)] = (int32_t)(int16_t)(cw[k] & 0xFFFF) * (int32_t)(qw[k] & 0xFFFF);
-            t[at(r, 2 * k + 1)] = (int32_t)(int16_t)(cw[k] >> 16) * (int32_t)(qw[k] >> 16);
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t pr = __builtin_bit_cast(uint32_t, __builtin_bit_cast(ushort2_t, cw[k]) *
+                                                                 __builtin_bit_cast(ushort2_t, qw[k]));
+            t[at(r, 2 * k)] = sext16((int32_t)pr);
+            t[at(r, 2 * k + 1)] = (int32_t)pr >> 16;
         }
     }
     wave_lds_sync();
-    // each pass in 32-bit arithmetic when every input of the wave is at most
-    // kIdct32Max (jidctint.c's butterfly grows a value by < 169,352 = 2^17.4:
-    // 12,600 * 169,352 + 2^17 < 2^31, so the products and sums equal the JLONG ones);
-    // otherwise in 64-bit (JLONG) as libjpeg-turbo computes on LP64
     int32_t in[8];
-    bool big = false;
-    if (live) {  // pass 1: column r
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            in[k] = t[at(k, r)];
-            big |= in[k] > kIdct32Max || in[k] < -kIdct32Max;
-        }
-    }
+    for (int k = 0; k < 8; ++k) in[k] = live ? t[at(k, r)] : 0;  // pass 1: column r
     int32_t p1[8];
-    if (I32 && !__any(big)) {
-        int32_t o[8];
-        if (live) islow_1d<int32_t>(in, o);
+    {
+        uint32_t o[8];
+        islow_simd(in, 1u << (kConstBits - kPass1Bits - 1), o);
+        const int32_t dc = sext16(in[0] << kPass1Bits);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) p1[k] = (int32_t)descale32(o[k], kConstBits - kPass1Bits);
-    } else {
-        int64_t c64[8], o[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) c64[k] = in[k];
-        if (live) islow_1d<int64_t>(c64, o);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) p1[k] = (int32_t)descale(o[k], kConstBits - kPass1Bits);
+        for (int k = 0; k < 8; ++k)
+            p1[k] = ac_zero ? dc : min(max((int32_t)o[k] >> (kConstBits - kPass1Bits), -32768), 32767);
     }
     wave_lds_sync();
     if (live) {
@@ -925,38 +865,21 @@ __device__ __forceinline__ void idct8_lane_v(uint4 v, const uint16_t* qt, int r,
         for (int k = 0; k < 8; ++k) t[at(k, r)] = p1[k];
     }
     wave_lds_sync();
-    // pass 2: row r -> samples
-    big = false;
-    if (live) {
+    if (!live) return;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            in[k] = t[at(r, k)];
-            big |= in[k] > kIdct32Max || in[k] < -kIdct32Max;
-        }
-    }
+    for (int k = 0; k < 8; ++k) in[k] = t[at(r, k)];  // pass 2: row r
     constexpr int sh = kConstBits + kPass1Bits + 3;
-    if (I32 && !__any(big)) {
-        int32_t o[8];
-        if (!live) return;
-        islow_1d<int32_t>(in, o);
+    uint32_t o[8];
+    islow_simd(in, 1u << (sh - 1), o);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) px[k] = idct_limit_descale32(o[k]);
-    } else {
-        int64_t r64[8], o[8];
-        if (!live) return;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) r64[k] = in[k];
-        islow_1d<int64_t>(r64, o);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) px[k] = idct_limit(descale(o[k], sh));
-    }
+    for (int k = 0; k < 8; ++k) px[k] = (uint8_t)(min(max((int32_t)o[k] >> sh, -128), 127) + 128);
 }
 
 __device__ __forceinline__ void idct8_lane(const int16_t* blk, const uint16_t* qt, int r, bool live, int32_t* t,
                                            uint8_t (&px)[8])
 {
     const uint4 v = live ? *reinterpret_cast<const uint4*>(blk + r * 8) : uint4{0, 0, 0, 0};
-    idct8_lane_v<WICCA_IDCT32 != 0>(v, qt, r, live, t, px);
+    idct8_lane_v(v, qt, r, live, t, px);
 }
 
 __device__ __forceinline__ uint2 pack8(const uint8_t (&px)[8])
@@ -1221,67 +1144,7 @@ __device__ __forceinline__ void chroma8_h2v2(const uint8_t* plane, int64_t pitch
     }
 }
 
-// The same for the fused kernel's lanes (c = x/2 a multiple of 4) away from
-// the plane's edges, two samples per 32-bit operation: the bytes of a chroma
-// row word split into even and odd 16-bit halves, 3 * near + far of two
-// columns in one integer multiply-add (each half <= 1020), then each pair of
-// outputs (3 * t[j+1] + t[j or j+2] + 8 or 7) >> 4 in one more (<= 4088 per
-// half, no carry between them).  One 12-byte load per chroma row (columns
-// c-4 .. c+7) instead of four unaligned 4-byte windows.  False: use chroma8_h2v2.
-__device__ __forceinline__ bool chroma8_h2v2_pair(const uint8_t* plane, int64_t pitch, int dw, int dh, int x, int y,
-                                                  int (&out)[8])
-{
-    const int c = x >> 1, iy = y >> 1;
-    if (c < 4 || c + 4 > dw - 1 || c + 8 > pitch) return false;
-    const int oy = (y & 1) ? min(iy + 1, dh - 1) : max(iy - 1, 0);
-    const uint3 a = *reinterpret_cast<const uint3*>(plane + (int64_t)iy * pitch + c - 4);
-    const uint3 b = *reinterpret_cast<const uint3*>(plane + (int64_t)oy * pitch + c - 4);
-    constexpr uint32_t kM = 0x00FF00FFu;
-    const uint32_t te = 3u * (a.y & kM) + (b.y & kM);                // (t3, t1): columns c+2, c
-    const uint32_t to = 3u * ((a.y >> 8) & kM) + ((b.y >> 8) & kM);  // (t4, t2): columns c+3, c+1
-    const uint32_t t0 = 3u * (a.x >> 24) + (b.x >> 24);              // column c-1
-    const uint32_t t5 = 3u * (a.z & 255u) + (b.z & 255u);            // column c+4
-    const uint32_t p04 = ((3u * te + ((to << 16) | t0) + 0x00080008u) >> 4) & kM;
-    const uint32_t p15 = ((3u * te + to + 0x00070007u) >> 4) & kM;
-    const uint32_t p26 = ((3u * to + te + 0x00080008u) >> 4) & kM;
-    const uint32_t p37 = ((3u * to + ((t5 << 16) | (te >> 16)) + 0x00070007u) >> 4) & kM;
-    out[0] = (int)(p04 & 255u);
-    out[4] = (int)(p04 >> 16);
-    out[1] = (int)(p15 & 255u);
-    out[5] = (int)(p15 >> 16);
-    out[2] = (int)(p26 & 255u);
-    out[6] = (int)(p26 >> 16);
-    out[3] = (int)(p37 & 255u);
-    out[7] = (int)(p37 >> 16);
-    return true;
-}
-
-// jdcolor.c: R = Y + ((91881 (Cr - 128) + 2^15) >> 16), B likewise with
-// 116130 Cb, G = Y + ((-46802 (Cr - 128) - 22554 (Cb - 128) + 2^15) >> 16),
-// each clamped.  Y << 16 and the -128 offsets fold into the addend of one
-// full-rate 24-bit multiply-add per product (the sums stay within +-2^26, and
-// adding a multiple of 2^16 before the arithmetic shift adds Y after it).
-__device__ __forceinline__ void ycc8_to_rgb(uint32_t ylo, uint32_t yhi, const int (&cbv)[8], const int (&crv)[8],
-                                            uint8_t (&o)[24])
-{
-    constexpr int kR = 32768 - 91881 * 128, kB = 32768 - 116130 * 128, kG = 32768 + (46802 + 22554) * 128;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int Y = (int)(((q < 4 ? ylo : yhi) >> (8 * (q & 3))) & 255);
-        const int y16 = Y << 16;
-        o[3 * q] = clamp255((__mul24(91881, crv[q]) + (y16 + kR)) >> 16);
-        o[3 * q + 1] = clamp255((__mul24(-46802, crv[q]) + (__mul24(-22554, cbv[q]) + (y16 + kG))) >> 16);
-        o[3 * q + 2] = clamp255((__mul24(116130, cbv[q]) + (y16 + kB)) >> 16);
-    }
-}
-
-// A workgroup walks kFuseRows tiles down one 256-pixel column strip: the next
-// tile's coefficients are loaded while the current one is transformed and
-// coloured, and each tile's chroma loads are issued before its IDCT.
-#ifndef WICCA_FUSE_ROWS
-#define WICCA_FUSE_ROWS 1
-#endif
-constexpr int kFuseRows = WICCA_FUSE_ROWS;
+constexpr int kFuseRows = 1;  // block rows per workgroup (the launch grid's y unit)
 
 __device__ __forceinline__ void chroma8(const JpegPlan& P, const JpegImageDev& im, int x, int y, int (&cbv)[8],
                                         int (&crv)[8])
@@ -1292,18 +1155,8 @@ __device__ __forceinline__ void chroma8(const JpegPlan& P, const JpegImageDev& i
     const uint8_t* pr = P.planes + im.comp_plane0[2];
     const int64_t sb = (int64_t)im.comp_bw[1] * 8, sr = (int64_t)im.comp_bw[2] * 8;
     if (fh1 == 2 && fv1 == 2 && fh2 == 2 && fv2 == 2 && im.comp_dw[1] > 2 && im.comp_dw[2] > 2) {
-        if (!chroma8_h2v2_pair(pb, sb, im.comp_dw[1], im.comp_dh[1], x, y, cbv))
-            chroma8_h2v2(pb, sb, im.comp_dw[1], im.comp_dh[1], x, y, cbv);
-        if (!chroma8_h2v2_pair(pr, sr, im.comp_dw[2], im.comp_dh[2], x, y, crv))
-            chroma8_h2v2(pr, sr, im.comp_dw[2], im.comp_dh[2], x, y, crv);
-    } else if (fh1 == 1 && fv1 == 1 && fh2 == 1 && fv2 == 1) {  // 4:4:4: x is 8-aligned in 8-B rows
-        const uint2 b8 = *reinterpret_cast<const uint2*>(pb + (int64_t)y * sb + x);
-        const uint2 r8 = *reinterpret_cast<const uint2*>(pr + (int64_t)y * sr + x);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            cbv[q] = (int)(((q < 4 ? b8.x : b8.y) >> (8 * (q & 3))) & 255);
-            crv[q] = (int)(((q < 4 ? r8.x : r8.y) >> (8 * (q & 3))) & 255);
-        }
+        chroma8_h2v2(pb, sb, im.comp_dw[1], im.comp_dh[1], x, y, cbv);
+        chroma8_h2v2(pr, sr, im.comp_dw[2], im.comp_dh[2], x, y, crv);
     } else {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -1314,84 +1167,229 @@ __device__ __forceinline__ void chroma8(const JpegPlan& P, const JpegImageDev& i
     }
 }
 
+
+// Two 16-bit additions in one v_pk_add_u16 (no carry between the halves).
+__device__ __forceinline__ uint32_t pk_add_u16(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(ushort2_t, a) + __builtin_bit_cast(ushort2_t, b));
+}
+
+// h2v2 fancy upsampling (jdsample.c) of output pixels x .. x+7 (c = x/2 a
+// multiple of 4, away from the plane's edges) from the 12-byte windows at
+// chroma column c-4 of the nearest (a) and the next-nearest (b) chroma row,
+// two samples per 32-bit operation: 3 * near + far of two columns per integer
+// multiply-add (each 16-bit half <= 1020), each output pair 3 * t[j+1] +
+// t[j or j+2] + 8 or 7 in one more (<= 4088 per half).  The rounding term and
+// the colour conversion's -128 go in as one v_pk_add_u16 of (r - 2048) per
+// half, so bits 4..11 of a half, sign-extended, are the sample minus 128.
+__device__ __forceinline__ void chroma8_h2v2_m128(uint3 a, uint3 b, int (&out)[8])
+{
+    constexpr uint32_t kM = 0x00FF00FFu;
+    const uint32_t te = 3u * (a.y & kM) + (b.y & kM);                // (t3, t1): columns c+2, c
+    const uint32_t to = 3u * ((a.y >> 8) & kM) + ((b.y >> 8) & kM);  // (t4, t2): columns c+3, c+1
+    const uint32_t t0 = 3u * (a.x >> 24) + (b.x >> 24);              // column c-1
+    const uint32_t t5 = 3u * (a.z & 255u) + (b.z & 255u);            // column c+4
+    const uint32_t s04 = pk_add_u16(3u * te + ((to << 16) | t0), 0xF808F808u);
+    const uint32_t s15 = pk_add_u16(3u * te + to, 0xF807F807u);
+    const uint32_t s26 = pk_add_u16(3u * to + te, 0xF808F808u);
+    const uint32_t s37 = pk_add_u16(3u * to + ((t5 << 16) | (te >> 16)), 0xF807F807u);
+    out[0] = __builtin_amdgcn_sbfe(s04, 4, 8);
+    out[4] = __builtin_amdgcn_sbfe(s04, 20, 8);
+    out[1] = __builtin_amdgcn_sbfe(s15, 4, 8);
+    out[5] = __builtin_amdgcn_sbfe(s15, 20, 8);
+    out[2] = __builtin_amdgcn_sbfe(s26, 4, 8);
+    out[6] = __builtin_amdgcn_sbfe(s26, 20, 8);
+    out[3] = __builtin_amdgcn_sbfe(s37, 4, 8);
+    out[7] = __builtin_amdgcn_sbfe(s37, 20, 8);
+}
+
+// Byte 2 of a, b, c, d as one word (three v_perm_b32-class operations).
+__device__ __forceinline__ uint32_t pack_b2(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
+{
+    return __builtin_amdgcn_perm(b, a, 0x0c0c0602u) | __builtin_amdgcn_perm(d, c, 0x06020c0cu);
+}
+
+// jdcolor.c for 8 pixels, cb / cr already minus 128: R = Y + ((91881 cr +
+// 2^15) >> 16), B likewise with 116130 cb, G = Y + ((-46802 cr - 22554 cb +
+// 2^15) >> 16), each clamped to 0..255.  Y << 16 | 2^15 comes from the Y word
+// in one v_perm_b32 (the 0x80 byte from a constant), each channel is one or
+// two 24-bit multiply-adds onto it, and clamping the sum to [0, 255 << 16]
+// (v_med3_i32) leaves the channel in byte 2: no shifts, and the 24 bytes are
+// picked out of byte 2 of their words by v_perm_b32.
+__device__ __forceinline__ void ycc8_pack(uint2 yv, const int (&cb)[8], const int (&cr)[8], uint32_t (&w)[6])
+{
+    uint32_t R[8], G[8], B[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        const int yh = (int)__builtin_amdgcn_perm(q < 4 ? yv.x : yv.y, 0x8000u, 0x0c000100u | ((4u + (q & 3)) << 16));
+        R[q] = (uint32_t)min(max(__mul24(91881, cr[q]) + yh, 0), 0xFF0000);
+        G[q] = (uint32_t)min(max(__mul24(-46802, cr[q]) + (__mul24(-22554, cb[q]) + yh), 0), 0xFF0000);
+        B[q] = (uint32_t)min(max(__mul24(116130, cb[q]) + yh, 0), 0xFF0000);
+    }
+    w[0] = pack_b2(R[0], G[0], B[0], R[1]);
+    w[1] = pack_b2(G[1], B[1], R[2], G[2]);
+    w[2] = pack_b2(B[2], R[3], G[3], B[3]);
+    w[3] = pack_b2(R[4], G[4], B[4], R[5]);
+    w[4] = pack_b2(G[5], B[5], R[6], G[6]);
+    w[5] = pack_b2(B[6], R[7], G[7], B[7]);
+}
+
+// One 256 x 8-pixel tile per workgroup, specialised per chroma format
+// (JpegImageDev::fmt, chosen on the host): the IDCT lanes (block lb of the
+// tile, row r) and the colour lanes (tile row rr, pixels cx .. cx+7) are the
+// same 256 threads.  Each lane's chroma loads are issued before the IDCT.
+template <int FMT>
+__device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegImageDev& im, int tx, int ty, int32_t* tr,
+                                                uint8_t* ytile, uint32_t* stage)
+{
+    const int x0 = tx * kFuseW, y0 = ty * 8;
+    const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;
+    const int bx = tx * kFuseBlocks + lb;
+    const bool blive = bx < im.comp_bw[0];
+    const uint4 cv = blive ? *reinterpret_cast<const uint4*>(
+                                 P.coef + (im.comp_block0[0] + (int64_t)ty * im.comp_bw[0] + bx) * 64 + r * 8)
+                           : uint4{0, 0, 0, 0};
+    const int rr = threadIdx.x >> 5, cx = (threadIdx.x & 31) * 8;
+    const int x = x0 + cx, y = y0 + rr;
+    const bool px_live = y < im.H && x < im.W;
+    // chroma: loads before the IDCT, arithmetic after it
+    uint3 ab{0, 0, 0}, bb{0, 0, 0}, ar{0, 0, 0}, br{0, 0, 0};
+    uint2 cb8{0, 0}, cr8{0, 0};
+    bool interior = false;
+    const uint8_t* pb = P.planes + im.comp_plane0[1];
+    const uint8_t* pr = P.planes + im.comp_plane0[2];
+    if constexpr (FMT == kJpegFmtH2V2) {
+        // Cb and Cr planes alike, under 2^31 bytes (the host's conditions)
+        const int dw = im.comp_dw[1], dh = im.comp_dh[1];
+        const uint32_t sb = (uint32_t)im.comp_bw[1] * 8u;
+        const int c = x >> 1, iy = y >> 1;
+        const int oy = (y & 1) ? min(iy + 1, dh - 1) : max(iy - 1, 0);
+        interior = px_live && c >= 4 && c + 5 <= dw;  // then c + 8 <= sb too (sb: a multiple of 8 >= dw)
+        if (interior) {
+            const uint32_t o0 = __umul24((uint32_t)iy, sb) + (uint32_t)(c - 4);
+            const uint32_t o1 = __umul24((uint32_t)oy, sb) + (uint32_t)(c - 4);
+            ab = *reinterpret_cast<const uint3*>(pb + o0);
+            bb = *reinterpret_cast<const uint3*>(pb + o1);
+            ar = *reinterpret_cast<const uint3*>(pr + o0);
+            br = *reinterpret_cast<const uint3*>(pr + o1);
+        }
+    } else if constexpr (FMT == kJpegFmtH1V1) {
+        if (px_live) {  // x is 8-aligned in rows of whole blocks
+            const uint32_t o = __umul24((uint32_t)y, (uint32_t)im.comp_bw[1] * 8u) + (uint32_t)x;
+            cb8 = *reinterpret_cast<const uint2*>(pb + o);
+            cr8 = *reinterpret_cast<const uint2*>(pr + o);
+        }
+    }
+    uint8_t px[8];
+    idct8_lane_v(cv, im.qt[0], r, blive, tr + lb * kTrBlock, px);
+    if (blive) *reinterpret_cast<uint2*>(ytile + r * kYPitch + lb * 8) = pack8(px);
+    __syncthreads();  // ytile complete
+    uint32_t w[6] = {0, 0, 0, 0, 0, 0};
+    if (px_live) {
+        const uint2 yv = *reinterpret_cast<const uint2*>(ytile + rr * kYPitch + cx);
+        if constexpr (FMT == kJpegFmtGray) {
+            w[0] = __builtin_amdgcn_perm(0u, yv.x, 0x01000000u);
+            w[1] = __builtin_amdgcn_perm(0u, yv.x, 0x02020101u);
+            w[2] = __builtin_amdgcn_perm(0u, yv.x, 0x03030302u);
+            w[3] = __builtin_amdgcn_perm(0u, yv.y, 0x01000000u);
+            w[4] = __builtin_amdgcn_perm(0u, yv.y, 0x02020101u);
+            w[5] = __builtin_amdgcn_perm(0u, yv.y, 0x03030302u);
+        } else {
+            int cbm[8], crm[8];
+            if constexpr (FMT == kJpegFmtH2V2) {
+                if (interior) {
+                    chroma8_h2v2_m128(ab, bb, cbm);
+                    chroma8_h2v2_m128(ar, br, crm);
+                } else {  // the plane's left and right edges
+                    chroma8_h2v2(pb, (int64_t)im.comp_bw[1] * 8, im.comp_dw[1], im.comp_dh[1], x, y, cbm);
+                    chroma8_h2v2(pr, (int64_t)im.comp_bw[2] * 8, im.comp_dw[2], im.comp_dh[2], x, y, crm);
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        cbm[q] -= 128;
+                        crm[q] -= 128;
+                    }
+                }
+            } else if constexpr (FMT == kJpegFmtH1V1) {
+                const uint32_t b0 = cb8.x ^ 0x80808080u, b1 = cb8.y ^ 0x80808080u;  // bytes as int8: sample - 128
+                const uint32_t r0 = cr8.x ^ 0x80808080u, r1 = cr8.y ^ 0x80808080u;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    cbm[q] = __builtin_amdgcn_sbfe(b0, 8 * q, 8);
+                    cbm[q + 4] = __builtin_amdgcn_sbfe(b1, 8 * q, 8);
+                    crm[q] = __builtin_amdgcn_sbfe(r0, 8 * q, 8);
+                    crm[q + 4] = __builtin_amdgcn_sbfe(r1, 8 * q, 8);
+                }
+            } else {  // other subsamplings: the per-sample path
+                chroma8(P, im, x, y, cbm, crm);
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    cbm[q] -= 128;
+                    crm[q] -= 128;
+                }
+            }
+            ycc8_pack(yv, cbm, crm, w);
+        }
+    }
+    uint2* srow = reinterpret_cast<uint2*>(stage + rr * (kFuseRowBytes / 4) + (cx * 3) / 4);  // 24 B per lane
+    srow[0] = uint2{w[0], w[1]};
+    srow[1] = uint2{w[2], w[3]};
+    srow[2] = uint2{w[4], w[5]};
+    __syncthreads();  // stage complete
+    const int rows = min(8, im.H - y0);
+    const int nbytes = min(kFuseW, im.W - x0) * 3;
+    const bool al16 = (((uintptr_t)im.dst | (uintptr_t)im.dst_pitch) & 15) == 0;  // uniform
+    const uint8_t* s8 = reinterpret_cast<const uint8_t*>(stage);
+    for (int q = threadIdx.x; q < 8 * (kFuseRowBytes / 16); q += 256) {
+        const int row = q / (kFuseRowBytes / 16), off = (q - row * (kFuseRowBytes / 16)) * 16;
+        if (row >= rows || off >= nbytes) continue;
+        uint8_t* d = im.dst + (int64_t)(y0 + row) * im.dst_pitch + (int64_t)x0 * 3 + off;
+        const uint8_t* sp = s8 + row * kFuseRowBytes + off;
+        if (al16 && off + 16 <= nbytes) {
+            *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(sp);
+        } else {
+            for (int i = 0; i < 16 && off + i < nbytes; ++i) d[i] = sp[i];
+        }
+    }
+}
+
+// XCD: tiles dealt to the 8 XCDs in contiguous runs (workgroup b runs on XCD
+// b mod 8 as observed; speed only): the tiles a chroma row serves (the block
+// rows above and below) and the neighbours' edge columns then meet in one
+// XCD's L2 instead of being fetched by several.
+template <bool XCD>
 __global__ __launch_bounds__(256) void jpeg_luma_color_kernel(JpegPlan P)
 {
     __shared__ int32_t tr[kFuseBlocks * kTrBlock];
     __shared__ __attribute__((aligned(16))) uint8_t ytile[8 * kYPitch];
     __shared__ __attribute__((aligned(16))) uint32_t stage[8 * kFuseRowBytes / 4];
-    const JpegImageDev& im = P.imgs[blockIdx.z];
-    const int x0 = blockIdx.x * kFuseW, by0 = blockIdx.y * kFuseRows;
-    if (x0 >= im.W || by0 * 8 >= im.H) return;  // uniform: the grid is sized for the batch's largest image
-    const int nby = min(kFuseRows, (im.H + 7) / 8 - by0);  // tiles of this workgroup
-    // IDCT lanes: block (blockIdx.x * 32 + lb, row), lane r = row r of the block
-    const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;
-    const int bx = blockIdx.x * kFuseBlocks + lb;
-    const bool blive = bx < im.comp_bw[0];
-    const int16_t* cbase = P.coef + (im.comp_block0[0] + bx) * 64 + r * 8;
-    const int64_t crow = (int64_t)im.comp_bw[0] * 64;  // coefficients per block row
-    // colour lanes: tile row rr, pixels cx .. cx+7
-    const int rr = threadIdx.x >> 5, cx = (threadIdx.x & 31) * 8;
-    const int x = x0 + cx;
-    const int rows_out = min(kFuseW, im.W - x0);
-    const int nbytes = rows_out * 3;
-    const bool al16 = (((uintptr_t)im.dst | (uintptr_t)im.dst_pitch) & 15) == 0;  // uniform
-    uint4 cnext = blive ? *reinterpret_cast<const uint4*>(cbase + by0 * crow) : uint4{0, 0, 0, 0};
-#pragma unroll 1
-    for (int g = 0; g < nby; ++g) {
-        const int y0 = (by0 + g) * 8, y = y0 + rr;
-        const bool px_live = y < im.H && x < im.W;
-        const uint4 ccur = cnext;
-        if (g + 1 < nby && blive) cnext = *reinterpret_cast<const uint4*>(cbase + (by0 + g + 1) * crow);
-        int cbv[8], crv[8];
-#ifndef WICCA_ABL_NOCOLOR
-        if (px_live && im.ncomp == 3) chroma8(P, im, x, y, cbv, crv);
-#endif
-        uint8_t px[8];
-#ifndef WICCA_ABL_NOIDCT
-        idct8_lane_v<WICCA_LUMA_IDCT32 != 0>(ccur, im.qt[0], r, blive, tr + lb * kTrBlock, px);
-#else  // ablation (timing only): the coefficients' low bytes instead of the IDCT
-        px[0] = ccur.x; px[1] = ccur.x >> 8; px[2] = ccur.y; px[3] = ccur.y >> 8;
-        px[4] = ccur.z; px[5] = ccur.z >> 8; px[6] = ccur.w; px[7] = ccur.w >> 8;
-#endif
-        if (blive) *reinterpret_cast<uint2*>(ytile + r * kYPitch + lb * 8) = pack8(px);
-        __syncthreads();  // ytile complete; the previous tile's stage has been stored
-        uint8_t o[24];
-#pragma unroll
-        for (int i = 0; i < 24; ++i) o[i] = 0;
-        if (px_live) {
-            const uint2 yv = *reinterpret_cast<const uint2*>(ytile + rr * kYPitch + cx);
-#ifdef WICCA_ABL_NOCOLOR  // ablation (timing only): every image coloured as grayscale
-            if (true) {
-#else
-            if (im.ncomp == 1) {
-#endif
-#pragma unroll
-                for (int q = 0; q < 8; ++q)
-                    o[3 * q] = o[3 * q + 1] = o[3 * q + 2] = (uint8_t)(((q < 4 ? yv.x : yv.y) >> (8 * (q & 3))) & 255);
-            } else {
-                ycc8_to_rgb(yv.x, yv.y, cbv, crv, o);
-            }
-        }
-        uint32_t* srow = stage + rr * (kFuseRowBytes / 4) + (cx * 3) / 4;  // 24 B = 6 dwords per lane
-#pragma unroll
-        for (int w = 0; w < 6; ++w)
-            srow[w] = (uint32_t)o[4 * w] | ((uint32_t)o[4 * w + 1] << 8) | ((uint32_t)o[4 * w + 2] << 16) |
-                      ((uint32_t)o[4 * w + 3] << 24);
-        __syncthreads();  // stage complete; ytile free for the next tile
-        const int rows = min(8, im.H - y0);
-        const uint8_t* s8 = reinterpret_cast<const uint8_t*>(stage);
-        for (int q = threadIdx.x; q < 8 * (kFuseRowBytes / 16); q += 256) {
-            const int row = q / (kFuseRowBytes / 16), off = (q - row * (kFuseRowBytes / 16)) * 16;
-            if (row >= rows || off >= nbytes) continue;
-            uint8_t* d = im.dst + (int64_t)(y0 + row) * im.dst_pitch + (int64_t)x0 * 3 + off;
-            const uint8_t* sp = s8 + row * kFuseRowBytes + off;
-            if (al16 && off + 16 <= nbytes) {
-                *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(sp);
-            } else {
-                for (int i = 0; i < 16 && off + i < nbytes; ++i) d[i] = sp[i];
-            }
-        }
+    int tx = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
+    if constexpr (XCD) {
+        const uint32_t gx = gridDim.x, gxy = gx * gridDim.y, n = gxy * gridDim.z;
+        const uint32_t L = blockIdx.x + gx * (blockIdx.y + gridDim.y * blockIdx.z);
+        const uint32_t per = n >> 3, rem = n & 7, x = L & 7;
+        const uint32_t T = x * per + min(x, rem) + (L >> 3);
+        tz = (int)(T / gxy);
+        const uint32_t t = T - (uint32_t)tz * gxy;
+        ty = (int)(t / gx);
+        tx = (int)(t - (uint32_t)ty * gx);
     }
+    const JpegImageDev& im = P.imgs[tz];
+    if (tx * kFuseW >= im.W || ty * 8 >= im.H) return;  // uniform: grid sized for the largest image
+    switch (im.fmt) {
+    case kJpegFmtGray: luma_color_tile<kJpegFmtGray>(P, im, tx, ty, tr, ytile, stage); break;
+    case kJpegFmtH2V2: luma_color_tile<kJpegFmtH2V2>(P, im, tx, ty, tr, ytile, stage); break;
+    case kJpegFmtH1V1: luma_color_tile<kJpegFmtH1V1>(P, im, tx, ty, tr, ytile, stage); break;
+    default: luma_color_tile<kJpegFmtOther>(P, im, tx, ty, tr, ytile, stage); break;
+    }
+}
+
+bool luma_xcd()
+{
+    static const bool on = [] {
+        const char* e = getenv("WICCA_JPEG_XCD");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
 }
 
 // EXIF orientation (tag 0x0112), as cv2.imread applies it for IMREAD_COLOR:
@@ -1627,8 +1625,11 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             const JpegImageDev& im = ims[(size_t)i0];
             const uint32_t x = (uint32_t)(batched ? gx : (im.W + kFuseW - 1) / kFuseW);
             const uint32_t y = (uint32_t)(batched ? gy : (im.H + 8 * kFuseRows - 1) / (8 * kFuseRows));
-            hipLaunchKernelGGL(jpeg_luma_color_kernel,
-                               dim3(x, y, (uint32_t)std::min<int64_t>(per_launch, n_images - i0)), dim3(256), 0, s, Q);
+            const dim3 grid(x, y, (uint32_t)std::min<int64_t>(per_launch, n_images - i0));
+            if (luma_xcd())
+                hipLaunchKernelGGL(jpeg_luma_color_kernel<true>, grid, dim3(256), 0, s, Q);
+            else
+                hipLaunchKernelGGL(jpeg_luma_color_kernel<false>, grid, dim3(256), 0, s, Q);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
         return hipSuccess;
