@@ -472,6 +472,11 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     }
     wicca::JpegPlan P{};
     P.damage = damage;
+    static const int abl = [] {  // timing-only ablations of the fused kernel (wrong pixels)
+        const char* e = getenv("WICCA_JPEG_ABL");
+        return e ? atoi(e) : 0;
+    }();
+    P.abl = abl;
     P.stream = stream_d;
     P.segs = (const wicca::JpegSegDev*)(m + o_seg);
     P.sub_seg = (const int32_t*)(m + o_sub);

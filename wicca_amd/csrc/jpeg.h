@@ -161,6 +161,7 @@ struct JpegPlan {
     int32_t* damage;         // per image: set by the write pass where the data is damaged (a code no
                              // table has, a run past coefficient 63, a segment whose data ends before
                              // its blocks do); the host redoes those images with the host decoder
+    int32_t abl;             // timing-only ablations of the fused kernel (WICCA_JPEG_ABL bits; 0 in use)
 };
 
 // Lanes per decode workgroup; an image's subsequences are padded to whole

@@ -1246,9 +1246,9 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
     const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;
     const int bx = tx * kFuseBlocks + lb;
     const bool blive = bx < im.comp_bw[0];
-    const uint4 cv = blive ? *reinterpret_cast<const uint4*>(
+    const uint4 cv = blive && !(P.abl & 8) ? *reinterpret_cast<const uint4*>(
                                  P.coef + (im.comp_block0[0] + (int64_t)ty * im.comp_bw[0] + bx) * 64 + r * 8)
-                           : uint4{0, 0, 0, 0};
+                           : uint4{(uint32_t)threadIdx.x, 0, 0, 0};
     const int rr = threadIdx.x >> 5, cx = (threadIdx.x & 31) * 8;
     const int x = x0 + cx, y = y0 + rr;
     const bool px_live = y < im.H && x < im.W;
@@ -1265,7 +1265,9 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
         const int c = x >> 1, iy = y >> 1;
         const int oy = (y & 1) ? min(iy + 1, dh - 1) : max(iy - 1, 0);
         interior = px_live && c >= 4 && c + 5 <= dw;  // then c + 8 <= sb too (sb: a multiple of 8 >= dw)
-        if (interior) {
+        if (P.abl & 2) {
+            ab = bb = ar = br = uint3{(uint32_t)x, (uint32_t)y, 7u};
+        } else if (interior) {
             const uint32_t o0 = __umul24((uint32_t)iy, sb) + (uint32_t)(c - 4);
             const uint32_t o1 = __umul24((uint32_t)oy, sb) + (uint32_t)(c - 4);
             ab = *reinterpret_cast<const uint3*>(pb + o0);
@@ -1281,7 +1283,12 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
         }
     }
     uint8_t px[8];
-    idct8_lane_v(cv, im.qt[0], r, blive, tr + lb * kTrBlock, px);
+    if (P.abl & 4) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) px[k] = (uint8_t)((k < 2 ? cv.x : k < 4 ? cv.y : k < 6 ? cv.z : cv.w) >> (16 * (k & 1)));
+    } else {
+        idct8_lane_v(cv, im.qt[0], r, blive, tr + lb * kTrBlock, px);
+    }
     if (blive) *reinterpret_cast<uint2*>(ytile + r * kYPitch + lb * 8) = pack8(px);
     __syncthreads();  // ytile complete
     uint32_t w[6] = {0, 0, 0, 0, 0, 0};
@@ -1344,7 +1351,10 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
         if (row >= rows || off >= nbytes) continue;
         uint8_t* d = im.dst + (int64_t)(y0 + row) * im.dst_pitch + (int64_t)x0 * 3 + off;
         const uint8_t* sp = s8 + row * kFuseRowBytes + off;
-        if (al16 && off + 16 <= nbytes) {
+        if (P.abl & 1) {
+            const uint4 v = *reinterpret_cast<const uint4*>(sp);
+            asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+        } else if (al16 && off + 16 <= nbytes) {
             *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(sp);
         } else {
             for (int i = 0; i < 16 && off + i < nbytes; ++i) d[i] = sp[i];
@@ -1383,11 +1393,14 @@ __global__ __launch_bounds__(256) void jpeg_luma_color_kernel(JpegPlan P)
     }
 }
 
+// Off by default: measured on one box, contiguous runs cut the kernel's
+// FETCH_SIZE 1.61 -> 1.01 GB per call but took 1.715 against 1.669 ms
+// (profiles/r04i_*): the fused kernel is not bound by its fetches.
 bool luma_xcd()
 {
     static const bool on = [] {
         const char* e = getenv("WICCA_JPEG_XCD");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) != 0;
     }();
     return on;
 }
