@@ -274,6 +274,24 @@ __global__ __launch_bounds__(256) void copy_flat(const u32x4* __restrict__ a, u3
     }
 }
 
+// Flat read:write ratio R:1 (the guide's flat form, one launch, no loop): each
+// lane reads R vectors 256 apart (nt) and writes their sum once (nt; R = 4 is
+// the D = 1 icon ratio, 16 the D = 2 one); W = false: no store (a read ceiling).
+template <int R, bool W>
+__global__ __launch_bounds__(256) void flat_ratio(const u32x4* __restrict__ a, u32x4* __restrict__ b, size_t n,
+                                                  unsigned* out)
+{
+    const size_t blk = blockIdx.x, i0 = blk * 256 * R + threadIdx.x;
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+        const size_t j = i0 + (size_t)u * 256;
+        if (j < n) acc += __builtin_nontemporal_load(a + j);
+    }
+    if constexpr (W) __builtin_nontemporal_store(acc, b + blk * 256 + threadIdx.x);
+    else sink(acc, out);
+}
+
 // Read n 16-B vectors, write n * NUM / DEN of them (a stream at the kernels'
 // write ratios): each block owns contiguous chunks of 256 * U vectors, loads
 // them U deep, and writes its share of the chunk contiguously.
@@ -339,6 +357,13 @@ int main(int argc, char** argv)
             float ms = timeit([&] { hipLaunchKernelGGL((copy_flat<V, A, B>), dim3(nb), dim3(256), 0, 0, p, qq, fn); }, reps); \
             printf("copy_flat V=%d ntl=%d nts=%d bytes=%zu  %.3f ms  %.1f GB/s (read+write)\n", V, (int)A, (int)B, sz, ms, 2.0 * sz / ms / 1e6); }
             CF(1, false, false) CF(1, true, true) CF(1, true, false) CF(2, false, false) CF(4, false, false) CF(4, true, true)
+        }
+        {
+#define FR(R, W) { const unsigned nb = (unsigned)((n + 256 * R - 1) / (256 * R)); \
+            float ms = timeit([&] { hipLaunchKernelGGL((flat_ratio<R, W>), dim3(nb), dim3(256), 0, 0, p, qq, n, out); }, reps); \
+            const double wb = W ? (double)nb * 256 * 16 : 0.0; \
+            printf("flat_ratio R=%d store=%d  %.3f ms  read %.1f GB/s  read+write %.1f GB/s\n", R, (int)W, ms, bytes / ms / 1e6, (bytes + wb) / ms / 1e6); }
+            FR(1, true) FR(2, true) FR(4, true) FR(8, true) FR(16, true) FR(4, false) FR(16, false)
         }
         for (int blocks : {1024, 2048, 4096}) {
 #define CU(U, A, B) { float ms = timeit([&] { hipLaunchKernelGGL((copyU<U, A, B>), dim3(blocks), dim3(256), 0, 0, p, qq, cn); }, reps); \

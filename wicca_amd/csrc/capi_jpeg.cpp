@@ -713,6 +713,11 @@ int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, c
     memcpy(ws->spin.ptr + o_rp, icon_rp.data(), sizeof(wicca::ResizeParams) * (size_t)n);
     HIP_TRY(hipMemcpyAsync(ws->smeta.ptr, ws->spin.ptr, bytes, hipMemcpyHostToDevice, cs));
     wicca::StageParams sp{};
+    static const int stage_abl = [] {  // timing-only ablations of stage_rows (wrong outputs)
+        const char* e = getenv("WICCA_STAGE_ABL");
+        return e ? atoi(e) : 0;
+    }();
+    sp.abl = stage_abl;
     sp.imgs = (const wicca::StageImageDev*)ws->smeta.ptr;
     sp.C = 3;
     sp.depth = depth;

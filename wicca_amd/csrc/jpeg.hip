@@ -825,6 +825,7 @@ constexpr int kIdctBlocksPerWg = 32;
 constexpr int kTrPitch = 9, kTrBlock = 8 * kTrPitch;
 
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void idct8_lane_v(uint4 v, const uint16_t* qt, int r, bool live, int32_t* t,
                                              uint8_t (&px)[8])
@@ -1145,6 +1146,12 @@ __device__ __forceinline__ void chroma8_h2v2(const uint8_t* plane, int64_t pitch
 }
 
 constexpr int kFuseRows = 1;  // block rows per workgroup (the launch grid's y unit)
+#ifndef WICCA_LUMA_NT
+#define WICCA_LUMA_NT 0  // 1: non-temporal coefficient loads and RGB stores
+#endif
+#ifndef WICCA_LUMA_WAVES
+#define WICCA_LUMA_WAVES 0  // > 0: amdgpu_waves_per_eu for the fused kernel
+#endif
 
 __device__ __forceinline__ void chroma8(const JpegPlan& P, const JpegImageDev& im, int x, int y, int (&cbv)[8],
                                         int (&crv)[8])
@@ -1246,9 +1253,16 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
     const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;
     const int bx = tx * kFuseBlocks + lb;
     const bool blive = bx < im.comp_bw[0];
-    const uint4 cv = blive && !(P.abl & 8) ? *reinterpret_cast<const uint4*>(
-                                 P.coef + (im.comp_block0[0] + (int64_t)ty * im.comp_bw[0] + bx) * 64 + r * 8)
-                           : uint4{(uint32_t)threadIdx.x, 0, 0, 0};
+    uint4 cv{(uint32_t)threadIdx.x, 0, 0, 0};
+    if (blive && !(P.abl & 8)) {
+        const int16_t* cp = P.coef + (im.comp_block0[0] + (int64_t)ty * im.comp_bw[0] + bx) * 64 + r * 8;
+#if WICCA_LUMA_NT
+        const u32x4_t c4 = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(cp));
+        cv = uint4{c4[0], c4[1], c4[2], c4[3]};
+#else
+        cv = *reinterpret_cast<const uint4*>(cp);
+#endif
+    }
     const int rr = threadIdx.x >> 5, cx = (threadIdx.x & 31) * 8;
     const int x = x0 + cx, y = y0 + rr;
     const bool px_live = y < im.H && x < im.W;
@@ -1355,7 +1369,11 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
             const uint4 v = *reinterpret_cast<const uint4*>(sp);
             asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
         } else if (al16 && off + 16 <= nbytes) {
+#if WICCA_LUMA_NT
+            __builtin_nontemporal_store(*reinterpret_cast<const u32x4_t*>(sp), reinterpret_cast<u32x4_t*>(d));
+#else
             *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(sp);
+#endif
         } else {
             for (int i = 0; i < 16 && off + i < nbytes; ++i) d[i] = sp[i];
         }
@@ -1367,7 +1385,11 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
 // rows above and below) and the neighbours' edge columns then meet in one
 // XCD's L2 instead of being fetched by several.
 template <bool XCD>
-__global__ __launch_bounds__(256) void jpeg_luma_color_kernel(JpegPlan P)
+__global__ __launch_bounds__(256)
+#if WICCA_LUMA_WAVES
+__attribute__((amdgpu_waves_per_eu(WICCA_LUMA_WAVES)))
+#endif
+void jpeg_luma_color_kernel(JpegPlan P)
 {
     __shared__ int32_t tr[kFuseBlocks * kTrBlock];
     __shared__ __attribute__((aligned(16))) uint8_t ytile[8 * kYPitch];

@@ -37,6 +37,7 @@ struct StageParams {
     const StageImageDev* imgs;
     int32_t C, depth, border, k;
     int32_t dw, dh;       // classifier input size
+    int32_t abl;          // timing-only ablations of stage_rows (WICCA_STAGE_ABL bits; 0 in use)
 };
 
 // Limits of the fused row kernel: a source row fits the LDS stage, at most

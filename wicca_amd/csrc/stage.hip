@@ -150,6 +150,7 @@ stage_rows_kernel(StageParams P)
         const int y = y0 + r;
 #pragma unroll
         for (int m = 0; m < kStChunks; ++m) {
+            if (P.abl & 2) break;
             const u32x4 a = v[m];
             lo[m][0] += a.x & 0x00FF00FFu;
             hi[m][0] += (a.x >> 8) & 0x00FF00FFu;
@@ -160,7 +161,7 @@ stage_rows_kernel(StageParams P)
             lo[m][3] += a.w & 0x00FF00FFu;
             hi[m][3] += (a.w >> 8) & 0x00FF00FFu;
         }
-        const bool hrow = hs && y < H;  // uniform
+        const bool hrow = hs && y < H && !(P.abl & 4);  // uniform
         if (hrow) {
 #pragma unroll
             for (int m = 0; m < kStChunks; ++m) {
@@ -173,7 +174,7 @@ stage_rows_kernel(StageParams P)
             __syncthreads();  // row y is in b; the other buffer was last read before this
 #pragma unroll
             for (int k = 0; k < (NT > 0 ? NT : 1); ++k) {
-                if (tk[k].n_el == 0) continue;
+                if (tk[k].n_el == 0 || (P.abl & 1)) continue;
                 area_task_row(b, tk[k], im.hsum + tk[k].out + (int64_t)y * tk[k].n_el);
             }
         }
