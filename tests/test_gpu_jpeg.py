@@ -304,8 +304,10 @@ def test_file_caller_stage_fused_cases(tmp_path, depth, shape, interp, border, k
     sums and its icon, stage.hip) against cv2.resize restated (oracle) and the
     C oracle's icon: every depth class, both borders, the non-AREA
     interpolations (separate source resize), images smaller than the
-    classifier input (upscaled: no row sums) and odd sizes."""
-    sizes = [(480, 640), (1081, 1919), (133, 517), (77, 61), (300, 2050), (600, 401)]
+    classifier input (upscaled: no row sums), odd sizes, and rows split into
+    2 and 3 parts."""
+    # the last two rows span 2 and 3 of stage_rows' row parts
+    sizes = [(480, 640), (1081, 1919), (133, 517), (77, 61), (300, 2050), (600, 401), (96, 4000), (130, 7680)]
     paths, refs = [], []
     for i, (h, w) in enumerate(sizes):
         data = J.encode(J.test_image("scene" if i % 2 else "noise", h, w, 7 * i + depth), 85, i % 3)
