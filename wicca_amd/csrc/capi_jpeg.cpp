@@ -623,16 +623,6 @@ bool stage_fused()
     return on;
 }
 
-// WICCA_STAGE_PARTS=0: stage_rows takes whole rows (no row parts).
-bool stage_parts()
-{
-    static const bool on = [] {
-        const char* e = getenv("WICCA_STAGE_PARTS");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
-
 // The caller stage over n device-resident RGB images (img[i], pitch[i]):
 // one stage_rows launch reads every image once for its icon and, when its
 // source resize is the two-pass INTER_AREA, that resize's row sums; then the
@@ -665,13 +655,6 @@ int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, c
     bool any_copy = false;
     int rounds = 0;
     std::vector<std::vector<wicca::AreaTask>> tasks((size_t)n);
-    // rows split into parts (twice the workgroups at half the registers and
-    // LDS each) when some image's row spans 2 .. kStageMaxParts of them
-    const int part_bytes = wicca::stage_part_bytes(depth);
-    int max_parts = 1;
-    for (int64_t i = 0; i < n; ++i) max_parts = std::max<int>(max_parts, (int)((W[i] * 3 + part_bytes - 1) / part_bytes));
-    bool parts = stage_parts() && depth >= 1 && depth <= 8 && max_parts >= 2 && max_parts <= wicca::kStageMaxParts;
-    int halo = 0;
     for (int64_t i = 0; i < n; ++i) {
         wicca::StageImageDev& e = sd[(size_t)i];
         memset(&e, 0, sizeof(e));
@@ -695,22 +678,9 @@ int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, c
             e.ky = fast ? rp.ky : 0;
             e.kx = fast ? rp.kx : 0;
             e.area_scale = rp.area_scale;
-            if (parts) {
-                e.n_parts = (int32_t)((W[i] * 3 + part_bytes - 1) / part_bytes);
-                halo = std::max(halo, wicca::append_area_tasks_parts((int)W[i], (int)out_w, rp.scale_x, fast, rp.kx, 0,
-                                                                     part_bytes, e.n_parts, tasks[(size_t)i],
-                                                                     e.part_task0));
-                for (int p = 0; p < e.n_parts; ++p)
-                    rounds = std::max(rounds, (e.part_task0[p + 1] - e.part_task0[p] + 255) / 256);
-            } else {
-                wicca::append_area_tasks((int)W[i], (int)out_w, rp.scale_x, fast, rp.kx, 0, tasks[(size_t)i]);
-                rounds = std::max(rounds, (int)((tasks[(size_t)i].size() + 255) / 256));
-            }
+            wicca::append_area_tasks((int)W[i], (int)out_w, rp.scale_x, fast, rp.kx, 0, tasks[(size_t)i]);
             e.n_tasks = (int32_t)tasks[(size_t)i].size();
-        }
-        if (parts && !e.hsum) {  // icon only: one part per part_bytes of the row
-            e.n_parts = (int32_t)((W[i] * 3 + part_bytes - 1) / part_bytes);
-            for (int p = 0; p <= e.n_parts; ++p) e.part_task0[p] = 0;
+            rounds = std::max(rounds, (int)((e.n_tasks + 255) / 256));
         }
         wicca::ResizeParams& q = icon_rp[(size_t)i];
         q.src = e.icon;
@@ -721,21 +691,6 @@ int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, c
         q.dst_stride = 0;
         // copies and cubic / Lanczos-4 (host tables per image) take the per-image path
         any_copy = any_copy || q.mode == wicca::RS_COPY || q.mode == wicca::RS_KERNEL;
-    }
-    if (parts && (!wicca::stage_parts_fit(part_bytes, halo) || rounds > 2)) {  // windows too wide: whole rows
-        parts = false;
-        rounds = 0;
-        for (int64_t i = 0; i < n; ++i) {
-            wicca::StageImageDev& e = sd[(size_t)i];
-            e.n_parts = 0;
-            tasks[(size_t)i].clear();
-            if (!e.hsum) continue;
-            const wicca::ResizeParams& rp = src_rp[(size_t)i];
-            wicca::append_area_tasks((int)W[i], (int)out_w, rp.scale_x, rp.mode == wicca::RS_AREA_FAST, rp.kx, 0,
-                                     tasks[(size_t)i]);
-            e.n_tasks = (int32_t)tasks[(size_t)i].size();
-            rounds = std::max(rounds, (int)((e.n_tasks + 255) / 256));
-        }
     }
     // descriptors: [StageImageDev x n | ResizeParams x n | task tables], pinned,
     // one upload (the caller synchronises before the staging is reused)
@@ -770,11 +725,6 @@ int fused_stage(Workspace* ws, hipStream_t cs, int64_t n, uint8_t* const* img, c
     sp.k = (int32_t)saturate_k(k);
     sp.dw = (int32_t)out_w;
     sp.dh = (int32_t)out_h;
-    if (parts) {
-        sp.part_bytes = part_bytes;
-        sp.halo = halo;
-        sp.max_parts = max_parts;
-    }
     HIP_TRY(wicca::launch_stage_rows(sp, n, max_oh, rounds, cs));
     if (rounds > 0) HIP_TRY(wicca::launch_stage_vsum(sp, n, cs));
     for (int64_t i = 0; i < n; ++i) {  // source resizes the row kernel did not prepare

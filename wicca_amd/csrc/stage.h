@@ -17,10 +17,6 @@ namespace wicca {
 
 struct AreaTask;
 
-// A row of an image may be split into parts (workgroups) of part_bytes bytes
-// (StageParams): at most kStageMaxParts per row.
-constexpr int kStageMaxParts = 4;
-
 // One image of the stage (device array).
 struct StageImageDev {
     const uint8_t* src;   // HWC uint8, rows 16-B aligned, pitch >= round_up(W * C, 16)
@@ -35,8 +31,6 @@ struct StageImageDev {
     int32_t ky, kx;       // ky > 0: integer scale (RS_AREA_FAST), exact integer sums
     float area_scale;
     double scale_x, scale_y;  // W / dw, H / dh (computeResizeAreaTab geometry)
-    int32_t n_parts;          // row parts (1 .. kStageMaxParts)
-    int32_t part_task0[kStageMaxParts + 1];  // tasks of part p: [part_task0[p], part_task0[p + 1])
 };
 
 struct StageParams {
@@ -44,9 +38,6 @@ struct StageParams {
     int32_t C, depth, border, k;
     int32_t dw, dh;       // classifier input size
     int32_t abl;          // timing-only ablations of stage_rows (WICCA_STAGE_ABL bits; 0 in use)
-    int32_t part_bytes;   // row bytes per part (a multiple of lcm(16, C * 2^depth)); 0: whole rows
-    int32_t halo;         // bytes loaded past a part for its row-sum windows (a multiple of 16)
-    int32_t max_parts;    // grid.x = largest icon height * max_parts
 };
 
 // Limits of the fused row kernel: a source row fits the LDS stage, at most
@@ -110,26 +101,6 @@ inline AreaTabHost area_tab_host(int d, int ssize, double scale)
 // 8K -> 224 scale) on one bank).
 void append_area_tasks(int W, int dw, double scale_x, bool fast, int kx, uint32_t out0, std::vector<AreaTask>& tasks);
 
-// The same split by row part: a task goes to the part holding the first byte
-// of its window (3 * max(s1 - 1, 0) / part_bytes), the parts' tasks appended
-// in part order, each part bank-ordered as above; part_task0[p] (n_parts + 1
-// entries) gets the running task offsets (relative to tasks.size() on entry),
-// and the result is the halo (bytes past its part, rounded up to 16, that
-// some part's windows read, their 16-B over-read included).
-int append_area_tasks_parts(int W, int dw, double scale_x, bool fast, int kx, uint32_t out0, int part_bytes,
-                            int n_parts, std::vector<AreaTask>& tasks, int32_t* part_task0);
-
-// Row parts of the fused stage: part bytes for depth D (RGB), a multiple of
-// lcm(16, 3 * 2^D) near kStagePartTarget; images whose rows need one part keep
-// whole rows.
-constexpr int kStagePartTarget = 11 * 1024;
-constexpr int kStagePartChunks = 3;  // 16-B chunks per lane of a part plus its halo (<= 12 KiB)
-inline int stage_part_bytes(int D)
-{
-    const int a = 3 << D, l = a % 16 == 0 ? a : (a % 8 == 0 ? 2 * a : (a % 4 == 0 ? 4 * a : (a % 2 == 0 ? 8 * a : 16 * a)));
-    return std::max(l, kStagePartTarget / l * l);
-}
-
 struct PlanImageDev {
     const uint8_t* src;   // HWC uint8 RGB, rows 16-B aligned, pitch >= round_up(W * 3, 16)
     int64_t src_pitch;
@@ -164,8 +135,6 @@ hipError_t launch_plan_vsum(const PlanParams& p, int64_t n, hipStream_t s);
 // grid = (largest icon height, n); rounds = ceil(most tasks / 256) (0: no
 // image has row sums).  Then the vertical pass of those images.
 hipError_t launch_stage_rows(const StageParams& p, int64_t n, int max_oh, int rounds, hipStream_t s);
-// Whether the parts form takes this launch (halo and part fit kStagePartChunks).
-inline bool stage_parts_fit(int part_bytes, int halo) { return part_bytes + halo <= kStagePartChunks * 256 * 16; }
 hipError_t launch_stage_vsum(const StageParams& p, int64_t n, hipStream_t s);
 
 }  // namespace wicca

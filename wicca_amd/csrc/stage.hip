@@ -97,64 +97,48 @@ __device__ __forceinline__ void area_task_row(const uint8_t* b, const AreaTask& 
     out[2] = a2;
 }
 
-// NT = the row-sum task rounds per lane: ceil(tasks / 256) of the image (or
-// row part) with the most (0: no image of the launch takes its source resize
-// from row sums).  KC = 16-B chunks per lane of what a workgroup loads of a
-// row.  PARTS: a workgroup takes one part of part_bytes of each row of its
-// band (plus a halo for the row-sum windows that start in it), so its
-// registers and LDS are half the whole-row form's and twice as many
-// workgroups share the CUs; the icon columns of a part are whole 2^D blocks.
-template <int NT, int KC, bool PARTS>
-__global__ __attribute__((amdgpu_flat_work_group_size(1, kStThreads),
-                          amdgpu_waves_per_eu(PARTS ? (NT <= 1 ? 5 : 4) : (NT <= 1 ? 3 : 2)))) void
+// NT = the row-sum task rounds per lane: ceil(tasks / 256) of the image with
+// the most (0: no image of the launch takes its source resize from row sums)
+template <int NT>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kStThreads), amdgpu_waves_per_eu(NT <= 1 ? 3 : 2))) void
 stage_rows_kernel(StageParams P)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t buf[2][KC * kStThreads * 16 + 64];
+    __shared__ __attribute__((aligned(16))) uint8_t buf[2][kStageRowMax + 64];
     const StageImageDev& im = P.imgs[blockIdx.y];
-    int band = blockIdx.x, part = 0;
-    if constexpr (PARTS) {
-        band = (int)(blockIdx.x / (uint32_t)P.max_parts);
-        part = (int)blockIdx.x - band * P.max_parts;
-        if (part >= im.n_parts) return;  // uniform
-    }
+    const int band = blockIdx.x;
     if (band >= im.oh) return;  // uniform: the grid is sized for the largest icon
     const int C = P.C, D = P.depth, R = 1 << D;
     const int H = im.H, W = im.W;
     const int y0 = band * R;
-    const int row_bytes = W * C;
-    const int b0 = PARTS ? part * P.part_bytes : 0;                               // first byte of the part
-    const int b1 = PARTS ? min(row_bytes, b0 + P.part_bytes) : row_bytes;        // its column-sum bytes end
-    const int q0 = b0 >> 4;                                                      // first 16-B chunk
-    const int nq = (PARTS ? min(row_bytes + 15, b1 + P.halo + 15) : row_bytes + 15) / 16 - q0;  // chunks loaded
+    const int nq = (W * C + 15) >> 4;  // 16-B chunks of a row (the pitch covers them)
     const bool replicate = P.border == 1;
     const bool hs = NT > 0 && im.hsum != nullptr;  // uniform
     const int t = threadIdx.x;
 
     // this lane's row-sum tasks (output columns), for every row of the band
-    const int task0 = PARTS ? im.part_task0[part] : 0, task1 = PARTS ? im.part_task0[part + 1] : im.n_tasks;
     AreaTask tk[NT > 0 ? NT : 1];
 #pragma unroll
     for (int r = 0; r < (NT > 0 ? NT : 1); ++r) {
-        const int k = task0 + t + r * kStThreads;
-        if (hs && k < task1) {
+        const int k = t + r * kStThreads;
+        if (hs && k < im.n_tasks) {
             tk[r] = im.tasks[k];
         } else {
             tk[r].s1len = 0;
             tk[r].n_el = 0;  // no task
         }
     }
-    uint32_t lo[KC][4], hi[KC][4];
+    uint32_t lo[kStChunks][4], hi[kStChunks][4];
 #pragma unroll
-    for (int m = 0; m < KC; ++m)
+    for (int m = 0; m < kStChunks; ++m)
 #pragma unroll
         for (int w = 0; w < 4; ++w) lo[m][w] = hi[m][w] = 0;
     // two rows in flight: row y + 2's loads go out as soon as row y is summed
     // and staged (its registers are free again)
-    u32x4 va[KC], vb[KC];
-    auto load_row = [&](u32x4 (&v)[KC], int y) {
-        const u32x4* row = reinterpret_cast<const u32x4*>(im.src + (int64_t)min(y, H - 1) * im.src_pitch) + q0;
+    u32x4 va[kStChunks], vb[kStChunks];
+    auto load_row = [&](u32x4 (&v)[kStChunks], int y) {
+        const u32x4* row = reinterpret_cast<const u32x4*>(im.src + (int64_t)min(y, H - 1) * im.src_pitch);
 #pragma unroll
-        for (int m = 0; m < KC; ++m) {
+        for (int m = 0; m < kStChunks; ++m) {
             const int q = t + m * kStThreads;
             v[m] = q < nq ? __builtin_nontemporal_load(row + q) : u32x4{0, 0, 0, 0};
         }
@@ -162,10 +146,10 @@ stage_rows_kernel(StageParams P)
     // rows the block sums take: real rows, and under REPLICATE the clamped
     // copies of row H-1 below the image
     const int rows_in = replicate ? R : max(0, min(R, H - y0));
-    auto row_step = [&](u32x4 (&v)[KC], int r, uint8_t* b) {
+    auto row_step = [&](u32x4 (&v)[kStChunks], int r, uint8_t* b) {
         const int y = y0 + r;
 #pragma unroll
-        for (int m = 0; m < KC; ++m) {
+        for (int m = 0; m < kStChunks; ++m) {
             if (P.abl & 2) break;
             const u32x4 a = v[m];
             lo[m][0] += a.x & 0x00FF00FFu;
@@ -180,7 +164,7 @@ stage_rows_kernel(StageParams P)
         const bool hrow = hs && y < H && !(P.abl & 4);  // uniform
         if (hrow) {
 #pragma unroll
-            for (int m = 0; m < KC; ++m) {
+            for (int m = 0; m < kStChunks; ++m) {
                 const int q = t + m * kStThreads;
                 if (q < nq) reinterpret_cast<u32x4*>(b)[q] = v[m];
             }
@@ -188,11 +172,16 @@ stage_rows_kernel(StageParams P)
         if (r + 2 < rows_in) load_row(v, y + 2);  // in flight during the next two rows
         if (hrow) {
             __syncthreads();  // row y is in b; the other buffer was last read before this
-            const uint8_t* bb = b - b0;  // the row's byte x at bb[x] (x within the part and its halo)
 #pragma unroll
             for (int k = 0; k < (NT > 0 ? NT : 1); ++k) {
                 if (tk[k].n_el == 0 || (P.abl & 1)) continue;
-                area_task_row(bb, tk[k], im.hsum + tk[k].out + (int64_t)y * tk[k].n_el);
+                if (P.abl & 8) {  // timing only: the sums without their stores
+                    float o3[3];
+                    area_task_row(b, tk[k], o3);
+                    asm volatile("" ::"v"(o3[0]), "v"(o3[1]), "v"(o3[2]));
+                    continue;
+                }
+                area_task_row(b, tk[k], im.hsum + tk[k].out + (int64_t)y * tk[k].n_el);
             }
         }
     };
@@ -203,10 +192,10 @@ stage_rows_kernel(StageParams P)
         if (r + 1 < rows_in) row_step(vb, r + 1, buf[1]);
     }
     __syncthreads();  // the row buffers are free: they take the column sums
-    // column sums as u16 per loaded byte (2 * KC * 4 KiB <= both row buffers)
+    // column sums as u16 per row byte (2 * W * C <= 48 KiB)
     uint16_t* cs = reinterpret_cast<uint16_t*>(&buf[0][0]);
 #pragma unroll
-    for (int m = 0; m < KC; ++m) {
+    for (int m = 0; m < kStChunks; ++m) {
         const int q = t + m * kStThreads;
         if (q < nq) {
 #pragma unroll
@@ -219,22 +208,18 @@ stage_rows_kernel(StageParams P)
         }
     }
     __syncthreads();
-    // the part's icon columns (whole 2^D blocks): (ow, C) block sums over 2^D
-    // columns of the column sums, cs[x - b0] for row byte x
+    // icon row `band`: (ow, C) block sums over 2^D columns of the column sums
     const uint32_t kpad = replicate ? 0u : (uint32_t)P.k * (uint32_t)max(0, y0 + R - H);  // CONSTANT rows below
     uint8_t* icon = im.icon + (int64_t)band * im.icon_pitch;
-    const int blk = C << D;  // row bytes of one icon column
-    const int e0 = PARTS ? b0 / blk * C : 0;
-    const int e1 = PARTS ? min(im.ow, (b1 + blk - 1) / blk) * C : im.ow * C;
-    for (int e = e0 + t; e < e1; e += kStThreads) {
+    for (int e = t; e < im.ow * C; e += kStThreads) {
         const int ox = e / C, c = e - ox * C;
         const int col0 = ox << D;
         const int ncol = min(R, W - col0);  // real columns of the block
         uint32_t S = 0;
-        for (int j = 0; j < ncol; ++j) S += cs[(col0 + j) * C + c - b0];
+        for (int j = 0; j < ncol; ++j) S += cs[(col0 + j) * C + c];
         S += kpad * (uint32_t)ncol;
         if (ncol < R)  // right padding
-            S += replicate ? (uint32_t)(R - ncol) * cs[(W - 1) * C + c - b0] : (uint32_t)(R - ncol) * (uint32_t)P.k * R;
+            S += replicate ? (uint32_t)(R - ncol) * cs[(W - 1) * C + c] : (uint32_t)(R - ncol) * (uint32_t)P.k * R;
         icon[e] = (uint8_t)(S >> (2 * D));
     }
 }
@@ -424,30 +409,6 @@ void append_area_tasks(int W, int dw, double scale_x, bool fast, int kx, uint32_
     }
 }
 
-int append_area_tasks_parts(int W, int dw, double scale_x, bool fast, int kx, uint32_t out0, int part_bytes,
-                            int n_parts, std::vector<AreaTask>& tasks, int32_t* part_task0)
-{
-    std::vector<AreaTask> all;
-    append_area_tasks(W, dw, scale_x, fast, kx, out0, all);  // bank-ordered; split by part, order kept
-    const int64_t base = (int64_t)tasks.size();
-    int halo = 0;
-    for (int p = 0; p < n_parts; ++p) {
-        part_task0[p] = (int32_t)((int64_t)tasks.size() - base);
-        for (const AreaTask& k : all) {
-            const int s1 = (int)(k.s1len & 0xFFFFu), len = (int)(k.s1len >> 16);
-            const int first = 3 * std::max(s1 - 1, 0);
-            if (std::min(first / part_bytes, n_parts - 1) != p) continue;
-            tasks.push_back(k);
-            // bytes read: up to the last partial cell (pixel s1 + len), and the
-            // aligned loop's dwords up to 16 B past the full cells
-            const int end = std::max(3 * (s1 + len) + 3, ((3 * s1) & ~3) + 12 * (len / 4) + 16);
-            halo = std::max(halo, end - (p + 1) * part_bytes);
-        }
-    }
-    part_task0[n_parts] = (int32_t)((int64_t)tasks.size() - base);
-    return (std::max(halo, 0) + 15) / 16 * 16;
-}
-
 hipError_t launch_plan_rows(const PlanParams& p, int64_t n, int max_h, int rounds, hipStream_t s)
 {
     if (n <= 0 || max_h <= 0) return hipSuccess;
@@ -483,25 +444,13 @@ hipError_t launch_stage_rows(const StageParams& p, int64_t n, int max_oh, int ro
 {
     if (n <= 0 || max_oh <= 0) return hipSuccess;
     if (n > 65535 || p.depth < 1 || p.depth > 8 || rounds < 0 || rounds > kStageRounds) return hipErrorInvalidValue;
-    if (p.part_bytes > 0) {  // row parts
-        if (p.max_parts < 1 || p.max_parts > kStageMaxParts || !stage_parts_fit(p.part_bytes, p.halo) ||
-            (int64_t)max_oh * p.max_parts > 0x7FFFFFFF || rounds > 2)
-            return hipErrorInvalidValue;
-        const dim3 grid((uint32_t)(max_oh * p.max_parts), (uint32_t)n);
-        switch (rounds) {
-        case 0: hipLaunchKernelGGL((stage_rows_kernel<0, kStagePartChunks, true>), grid, dim3(kStThreads), 0, s, p); break;
-        case 1: hipLaunchKernelGGL((stage_rows_kernel<1, kStagePartChunks, true>), grid, dim3(kStThreads), 0, s, p); break;
-        default: hipLaunchKernelGGL((stage_rows_kernel<2, kStagePartChunks, true>), grid, dim3(kStThreads), 0, s, p); break;
-        }
-        return hipGetLastError();
-    }
     const dim3 grid((uint32_t)max_oh, (uint32_t)n);
     switch (rounds) {
-    case 0: hipLaunchKernelGGL((stage_rows_kernel<0, kStChunks, false>), grid, dim3(kStThreads), 0, s, p); break;
-    case 1: hipLaunchKernelGGL((stage_rows_kernel<1, kStChunks, false>), grid, dim3(kStThreads), 0, s, p); break;
-    case 2: hipLaunchKernelGGL((stage_rows_kernel<2, kStChunks, false>), grid, dim3(kStThreads), 0, s, p); break;
-    case 3: hipLaunchKernelGGL((stage_rows_kernel<3, kStChunks, false>), grid, dim3(kStThreads), 0, s, p); break;
-    default: hipLaunchKernelGGL((stage_rows_kernel<4, kStChunks, false>), grid, dim3(kStThreads), 0, s, p); break;
+    case 0: hipLaunchKernelGGL(stage_rows_kernel<0>, grid, dim3(kStThreads), 0, s, p); break;
+    case 1: hipLaunchKernelGGL(stage_rows_kernel<1>, grid, dim3(kStThreads), 0, s, p); break;
+    case 2: hipLaunchKernelGGL(stage_rows_kernel<2>, grid, dim3(kStThreads), 0, s, p); break;
+    case 3: hipLaunchKernelGGL(stage_rows_kernel<3>, grid, dim3(kStThreads), 0, s, p); break;
+    default: hipLaunchKernelGGL(stage_rows_kernel<4>, grid, dim3(kStThreads), 0, s, p); break;
     }
     return hipGetLastError();
 }
