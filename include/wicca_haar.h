@@ -355,7 +355,7 @@ int wicca_jpeg_icon_stage_multi_gpu(const uint8_t* const* data, const int64_t* s
  */
 
 /* Decoded size of a file (EXIF orientation applied to JPEG when
- * apply_orientation); kind: 1 JPEG, 2 PNG, 3 BMP, 4 TIFF, 5 GIF. */
+ * apply_orientation); kind: 1 JPEG, 2 PNG, 3 BMP, 4 TIFF, 5 GIF, 6 PNM. */
 int wicca_image_info(const uint8_t* data, int64_t size, int apply_orientation,
                      int64_t* height, int64_t* width, int* kind);
 

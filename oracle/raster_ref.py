@@ -328,6 +328,82 @@ def encode_bmp(img: np.ndarray, bpp: int = 24, palette: np.ndarray | None = None
     return b"BM" + struct.pack("<IHHI", total, 0, 0, off) + hdr + pal + px.tobytes()
 
 
+def encode_bmp_rle(idx: np.ndarray, palette: np.ndarray, rle4: bool = False, absolute: bool = True,
+                   skips: bool = False, end_early: bool = False):
+    """A BI_RLE8 / BI_RLE4 BMP of an (H, W) index array (bottom-up) and the
+    indices a decoder must produce: rows as encoded runs (a repeated index, or
+    for RLE4 an alternating pair) and, with `absolute`, absolute runs of 3..64
+    indices (padded to 16 bits; even counts for RLE4); end of line after every row; `skips` ends
+    some rows early (end of line) and opens others with a delta escape over
+    their first two pixels -- skipped pixels decode as index 0; `end_early`
+    stops with end of bitmap halfway (OpenCV fills the rest with palette
+    entry 0, Pillow refuses such a file).  Returns (file bytes, indices)."""
+    idx = np.asarray(idx, np.uint8)
+    h, w = idx.shape
+    want = idx.copy()
+    out = bytearray()
+    stop = max(1, h // 2) if end_early else h
+    for ys, r in enumerate(range(h - 1, -1, -1)):  # stored bottom-up
+        if ys >= stop:
+            want[r, :] = 0
+            continue
+        row = [int(v) for v in idx[r]]
+        end, x = w, 0
+        if skips and ys % 5 == 3:  # end of line before the row's end
+            end = w // 2
+            want[r, end:] = 0
+        if skips and ys % 7 == 2 and w > 4:  # a delta escape over the first two pixels
+            out += bytes([0, 2, 2, 0])
+            want[r, :2] = 0
+            x = 2
+        while x < end:
+            if rle4:
+                a = row[x]
+                bb = row[x + 1] if x + 1 < end else 0
+                n = 1
+                while x + n < end and n < 255 and row[x + n] == (a if n % 2 == 0 else bb):
+                    n += 1
+                if absolute and n < 3 and end - x >= 4:
+                    m = min(end - x, 64) & ~1  # even: Pillow reads odd RLE4 absolute runs one pixel short
+                    vals = row[x:x + m] + [0]
+                    packed = bytes((vals[i] << 4) | vals[i + 1] for i in range(0, m, 2))
+                    out += bytes([0, m]) + packed + (b"\0" if len(packed) % 2 else b"")
+                    x += m
+                    continue
+                out += bytes([n, (a << 4) | (bb if n > 1 else 0)])
+                x += n
+            else:
+                v = row[x]
+                n = 1
+                while x + n < end and n < 255 and row[x + n] == v:
+                    n += 1
+                if absolute and n < 3 and end - x >= 3:
+                    m = min(end - x, 64)
+                    out += bytes([0, m]) + bytes(row[x:x + m]) + (b"\0" if m % 2 else b"")
+                    x += m
+                    continue
+                out += bytes([n, v])
+                x += n
+        out += bytes([0, 0])  # end of line
+    out += bytes([0, 1])  # end of bitmap
+    p = np.asarray(palette, np.uint8)
+    q = np.zeros((len(p), 4), np.uint8)
+    q[:, :3] = p[:, ::-1]
+    pal = q.tobytes()
+    hdr = struct.pack("<IiiHHIIiiII", 40, w, h, 1, 4 if rle4 else 8, 2 if rle4 else 1, len(out), 2835, 2835, len(p), 0)
+    off = 14 + len(hdr) + len(pal)
+    return b"BM" + struct.pack("<IHHI", off + len(out), 0, 0, off) + hdr + pal + bytes(out), want
+
+
+def encode_pnm(img: np.ndarray, comment: bool = True) -> bytes:
+    """Binary PGM (P5, an (H, W) array) or PPM (P6, (H, W, 3)) at maxval 255."""
+    img = np.asarray(img, np.uint8)
+    magic = b"P5" if img.ndim == 2 else b"P6"
+    h, w = img.shape[:2]
+    head = magic + b"\n" + (b"# written by the test suite\n" if comment else b"") + f"{w} {h}\n255\n".encode()
+    return head + img.tobytes()
+
+
 # ----------------------------------------------------------------------------- TIFF
 def _packbits(b: bytes) -> bytes:
     out = bytearray()

@@ -379,3 +379,64 @@ def test_gif_oversized_frame_descriptor_is_cheap():
     got = WJ.decode(bytes(data))
     assert time.perf_counter() - t0 < 5.0
     assert got.shape == (1, 1, 3) and got[0, 0].tolist() == [200, 100, 50]
+
+
+@pytest.mark.parametrize("rle4", [False, True], ids=["rle8", "rle4"])
+def test_rle_bmp_vs_pillow(rle4):
+    """BI_RLE8 / BI_RLE4 BMPs (encoded and absolute runs, end of line, delta
+    escapes; skipped pixels take palette entry 0) against Pillow, batched with
+    an uncompressed BMP."""
+    rng = np.random.default_rng(21 + rle4)
+    pal = rng.integers(0, 256, (16 if rle4 else 256, 3)).astype(np.uint8)
+    blobs, wants = [], []
+    for absolute, skips, shape in [(False, False, (37, 53)), (True, False, (64, 300)), (True, True, (120, 257)),
+                                   (True, True, (1, 1))]:
+        idx = rng.integers(0, len(pal), shape).astype(np.uint8)
+        idx[:, : shape[1] // 3] = idx[:, :1]
+        data, want = rr.encode_bmp_rle(idx, pal, rle4, absolute, skips)
+        blobs.append(data)
+        wants.append(pal[want])
+    plain = rr.encode_bmp(rng.integers(0, 256, (30, 41, 3), dtype=np.uint8), 24)
+    got = WJ.decode_batch(blobs + [plain])
+    for i, data in enumerate(blobs):
+        assert np.array_equal(got[i], wants[i]), i
+        assert np.array_equal(got[i], rr.pillow_rgb(data)), i
+    assert np.array_equal(got[-1], rr.decode_bmp(plain))
+
+
+def test_rle_bmp_opencv_rules():
+    """Where Pillow refuses: end of bitmap before the last row (OpenCV fills the
+    rest with palette entry 0; parity unpinned, restated from OpenCV's
+    BmpDecoder), and a run past a row's end, which fails the file's slot."""
+    rng = np.random.default_rng(5)
+    pal = rng.integers(0, 256, (256, 3)).astype(np.uint8)
+    idx = rng.integers(0, 256, (20, 33)).astype(np.uint8)
+    early, want = rr.encode_bmp_rle(idx, pal, False, True, False, end_early=True)
+    assert np.array_equal(WJ.decode(early), pal[want])
+    good, _ = rr.encode_bmp_rle(idx, pal)
+    hdr = 14 + 40 + 4 * 256
+    over = good[:hdr] + bytes([200, 9]) + good[hdr:]  # a 200-pixel run in a 33-pixel row
+    got = WJ.decode_batch([over, good], errors="none")
+    assert got[0] is None and np.array_equal(got[1], pal[idx])
+
+
+def test_pnm_vs_pillow(tmp_path, capsys):
+    """Binary PGM / PPM at maxval 255 (load_image, file stage); other PNM
+    kinds fail their slot as unsupported."""
+    rng = np.random.default_rng(8)
+    gray = rng.integers(0, 256, (61, 93), dtype=np.uint8)
+    rgb = rng.integers(0, 256, (480, 640, 3), dtype=np.uint8)
+    blobs = [rr.encode_pnm(gray), rr.encode_pnm(rgb, comment=False)]
+    got = WJ.decode_batch(blobs)
+    assert np.array_equal(got[0], np.repeat(gray[..., None], 3, axis=2))
+    assert np.array_equal(got[1], rgb)
+    for i, data in enumerate(blobs):
+        assert np.array_equal(got[i], rr.pillow_rgb(data))
+    ascii_pgm = b"P2\n2 2\n255\n0 1 2 3\n"
+    wide = b"P5\n2 2\n65535\n" + bytes(8)
+    assert WJ.decode_batch([ascii_pgm, wide, blobs[0]], errors="none")[:2] == [None, None]
+    p = tmp_path / "x.ppm"
+    p.write_bytes(blobs[1])
+    imgs, icons = wicca_amd.get_img_batch([str(p)], (224, 224), 3)
+    assert np.array_equal(imgs[0], R.resize(rgb, (224, 224), R.INTER_AREA))
+    assert np.array_equal(icons[0], R.resize(c_oracle.ll_int_block(rgb, 3)[0], (224, 224), R.INTER_AREA))

@@ -184,3 +184,25 @@ def test_gif_writer_and_expected_vs_pillow(h, w, npal, interlace):
     pal = rng.integers(0, 256, (npal, 3), dtype=np.uint8)
     data = rr.encode_gif(idx, pal, interlace=interlace)
     np.testing.assert_array_equal(rr.gif_expected(idx, pal), rr.pillow_rgb(data))
+
+
+@pytest.mark.parametrize("rle4", [False, True])
+@pytest.mark.parametrize("absolute,skips", [(False, False), (True, False), (True, True)])
+def test_rle_bmp_writer_matches_pillow(rle4, absolute, skips):
+    """oracle encode_bmp_rle's files and expected indices against Pillow's
+    decode (encoded and absolute runs, end of line, delta escapes)."""
+    rng = np.random.default_rng(11 + 2 * rle4 + skips)
+    pal = rng.integers(0, 256, (16 if rle4 else 256, 3)).astype(np.uint8)
+    for shape in ((37, 53), (1, 1), (2, 255), (64, 300)):
+        idx = rng.integers(0, len(pal), shape).astype(np.uint8)
+        idx[:, : shape[1] // 3] = idx[:, :1]  # long runs too
+        data, want = rr.encode_bmp_rle(idx, pal, rle4, absolute, skips)
+        assert np.array_equal(rr.pillow_rgb(data), pal[want]), shape
+
+
+def test_pnm_writer_matches_pillow():
+    rng = np.random.default_rng(3)
+    for img in (rng.integers(0, 256, (17, 29), dtype=np.uint8), rng.integers(0, 256, (8, 5, 3), dtype=np.uint8)):
+        got = rr.pillow_rgb(rr.encode_pnm(img))
+        want = np.repeat(img[..., None], 3, axis=2) if img.ndim == 2 else img
+        assert np.array_equal(got, want)

@@ -77,11 +77,11 @@ int probe_file(const uint8_t* data, int64_t size, int64_t i, bool any, bool orie
             if (rc) return fail(WICCA_ERR_DECODE, "image %lld: %s", (long long)i, err.c_str());
             *H = r.H;
             *W = r.W;
-            if (kind) *kind = rk == wicca::RK_PNG ? 2 : rk == wicca::RK_BMP ? 3 : rk == wicca::RK_TIFF ? 4 : 5;
+            if (kind) *kind = rk == wicca::RK_PNG ? 2 : rk == wicca::RK_BMP ? 3 : rk == wicca::RK_TIFF ? 4 : rk == wicca::RK_GIF ? 5 : 6;
             return WICCA_OK;
         }
         if (size < 2 || data[0] != 0xFF || data[1] != 0xD8)
-            return fail(WICCA_ERR_DECODE, "image %lld: unrecognised image format (JPEG, PNG, BMP, TIFF and GIF are decoded)",
+            return fail(WICCA_ERR_DECODE, "image %lld: unrecognised image format (JPEG, PNG, BMP, TIFF, GIF and PNM are decoded)",
                         (long long)i);
     }
     wicca::JpegInfo f;

@@ -15,7 +15,10 @@
 //       fail the file.
 //   BMP (OpenCV's BmpDecoder): 1/4/8-bit palettes (BGRx entries), 16-bit
 //       5-5-5 / 5-6-5 (component << 3 / << 2, no bit replication), 24-bit
-//       BGR, 32-bit BGRx (alpha dropped), bottom-up or top-down rows.
+//       BGR, 32-bit BGRx (alpha dropped), bottom-up or top-down rows; RLE8 /
+//       RLE4 decoded on the host (pixels a delta or end-of-line skips take
+//       palette entry 0; a run past the row's end fails the file).
+//   PNM (OpenCV's PxMDecoder): binary P5 gray / P6 RGB at maxval 255.
 //
 // Why the row reconstruction is on the host: deflate is a serial bit stream
 // (no resynchronisation points), so inflate runs on host threads, one file
@@ -35,7 +38,7 @@
 
 namespace wicca {
 
-enum RasterKind { RK_NONE = 0, RK_PNG = 1, RK_BMP = 2, RK_TIFF = 3, RK_GIF = 4 };
+enum RasterKind { RK_NONE = 0, RK_PNG = 1, RK_BMP = 2, RK_TIFF = 3, RK_GIF = 4, RK_PNM = 5 };
 
 // RasterImageDev::flags
 constexpr int kRasterInvert = 1;   // TIFF WhiteIsZero gray: 255 - v
@@ -70,10 +73,13 @@ struct RasterInfo {
         uint32_t crc;
     };
     std::vector<Chunk> idat;
-    // BMP: pixel array offset, stored row stride, bottom-up storage
+    // BMP: pixel array offset, stored row stride, bottom-up storage; RLE8 /
+    // RLE4 (rle = 1 / 2: decoded on the host into 8-bit index rows);
+    // PNM: raster offset and row stride (top-down)
     size_t data_off = 0;
     int64_t stride = 0;
     bool bottom_up = false;
+    int rle = 0;
     // TIFF (first IFD): strips or tiles (offset, byte count), layout, coding
     int flags = 0;                 // kRasterInvert / kRasterPremul
     int spp = 1;                   // samples per pixel

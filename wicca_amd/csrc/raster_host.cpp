@@ -190,8 +190,10 @@ int parse_bmp(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
         return bad(err, -1, "BMP: unknown header size");
     }
     if (w <= 0 || h == 0) return bad(err, -1, "BMP: invalid image size");
-    if (comp == 1 || comp == 2) return bad(err, -2, "BMP: RLE compression is not decoded");
-    const bool rgb = comp == 0, fields = comp == 3;
+    const bool rle8 = comp == 1 && bpp == 8, rle4 = comp == 2 && bpp == 4;
+    if ((comp == 1 || comp == 2) && !(rle8 || rle4)) return bad(err, -1, "BMP: RLE with a wrong bit count");
+    if ((rle8 || rle4) && h < 0) return bad(err, -1, "BMP: top-down RLE bitmap");
+    const bool rgb = comp == 0 || rle8 || rle4, fields = comp == 3;
     if (!((rgb && (bpp == 1 || bpp == 4 || bpp == 8 || bpp == 16 || bpp == 24 || bpp == 32)) ||
           (fields && (bpp == 16 || bpp == 32))))
         return bad(err, -2, "BMP: unsupported compression / bit count");
@@ -227,10 +229,112 @@ int parse_bmp(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
         info->fmt = bpp == 24 ? RF_BGR : RF_BGRX;
     }
     if (info->W > kMaxDim || info->H > kMaxDim) return bad(err, -2, "BMP: image larger than 65535 pixels");
-    info->stride = (info->W * bpp + 31) / 32 * 4;
     info->data_off = off;
+    if (rle8 || rle4) {  // decoded to 8-bit index rows (raster_unpack)
+        info->rle = rle8 ? 1 : 2;
+        info->bits = 8;
+        info->stride = info->W;
+        if ((uint64_t)off >= n) return bad(err, -1, "BMP: truncated pixel data");
+        return 0;
+    }
+    info->stride = (info->W * bpp + 31) / 32 * 4;
     if ((uint64_t)off > n || (uint64_t)(n - off) < (uint64_t)info->stride * (uint64_t)info->H)
         return bad(err, -1, "BMP: truncated pixel data");
+    return 0;
+}
+
+// BMP RLE8 / RLE4 (BI_RLE8 / BI_RLE4) into W-byte index rows, stored order
+// (bottom row first, as the device conversion reads bottom-up BMPs): encoded
+// runs (count, colour; RLE4 alternates the two nibbles), absolute runs
+// (escape count >= 3, padded to 16 bits), end of line, end of bitmap and
+// delta escapes; pixels a skip passes over keep index 0 (OpenCV fills them
+// with palette entry 0, Pillow leaves index 0).  A run past the row's end is
+// corrupt data (OpenCV's BmpDecoder fails the file); data that ends early
+// leaves the rest 0.
+int unpack_bmp_rle(const uint8_t* d, size_t n, const RasterInfo& f, uint8_t* out, std::string* err)
+{
+    const int64_t W = f.W, H = f.H;
+    memset(out, 0, (size_t)(W * H));
+    const bool four = f.rle == 2;
+    size_t p = f.data_off;
+    int64_t x = 0, y = 0;  // y: stored row (0 = the bottom row)
+    while (p + 1 < n && y < H) {
+        const int c0 = d[p], c1 = d[p + 1];
+        p += 2;
+        if (c0 > 0) {  // encoded run
+            if (x + c0 > W) return bad(err, -1, "BMP: RLE run past the end of a row");
+            uint8_t* r = out + y * W + x;
+            for (int i = 0; i < c0; ++i) r[i] = four ? (uint8_t)((i & 1) ? (c1 & 15) : (c1 >> 4)) : (uint8_t)c1;
+            x += c0;
+        } else if (c1 == 0) {  // end of line
+            x = 0;
+            ++y;
+        } else if (c1 == 1) {  // end of bitmap
+            break;
+        } else if (c1 == 2) {  // delta
+            if (p + 1 >= n) break;
+            x += d[p];
+            y += d[p + 1];
+            p += 2;
+            if (x > W) return bad(err, -1, "BMP: RLE delta past the end of a row");
+        } else {  // absolute run of c1 pixels
+            const int cnt = c1;
+            const size_t bytes = four ? (size_t)((cnt + 1) / 2) : (size_t)cnt;
+            if (x + cnt > W) return bad(err, -1, "BMP: RLE run past the end of a row");
+            if (p + bytes > n) break;
+            uint8_t* r = out + y * W + x;
+            for (int i = 0; i < cnt; ++i) r[i] = four ? (uint8_t)((i & 1) ? (d[p + i / 2] & 15) : (d[p + i / 2] >> 4)) : d[p + i];
+            x += cnt;
+            p += (bytes + 1) & ~(size_t)1;  // absolute runs are padded to 16 bits
+        }
+    }
+    return 0;
+}
+
+// ----------------------------------------------------------------------------- PNM
+// Binary PGM (P5) / PPM (P6) at maxval 255: the header's whitespace and '#'
+// comments, then the raster (one whitespace byte after maxval).
+int parse_pnm(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
+{
+    info->kind = RK_PNM;
+    if (n < 3 || d[0] != 'P') return bad(err, -1, "PNM: bad magic");
+    const int type = d[1] - '0';
+    if (type < 1 || type > 6) return bad(err, -1, "PNM: bad magic");
+    if (type != 5 && type != 6) return bad(err, -2, "PNM: only binary P5 / P6 are decoded");
+    size_t p = 2;
+    int64_t v[3];
+    for (int k = 0; k < 3; ++k) {
+        for (;;) {  // whitespace and comments
+            if (p >= n) return bad(err, -1, "PNM: truncated header");
+            if (d[p] == '#') {
+                while (p < n && d[p] != '\n' && d[p] != '\r') ++p;
+            } else if (d[p] == ' ' || d[p] == '\t' || d[p] == '\n' || d[p] == '\r' || d[p] == '\v' || d[p] == '\f') {
+                ++p;
+            } else {
+                break;
+            }
+        }
+        if (d[p] < '0' || d[p] > '9') return bad(err, -1, "PNM: bad header number");
+        int64_t x = 0;
+        while (p < n && d[p] >= '0' && d[p] <= '9') {
+            x = x * 10 + (d[p] - '0');
+            if (x > (1 << 24)) return bad(err, -1, "PNM: header number too large");
+            ++p;
+        }
+        v[k] = x;
+    }
+    if (p >= n) return bad(err, -1, "PNM: truncated header");
+    ++p;  // the single whitespace byte before the raster
+    if (v[0] <= 0 || v[1] <= 0) return bad(err, -1, "PNM: invalid image size");
+    if (v[2] != 255) return bad(err, -2, "PNM: only maxval 255 is decoded");
+    if (v[0] > kMaxDim || v[1] > kMaxDim) return bad(err, -2, "PNM: image larger than 65535 pixels");
+    info->W = v[0];
+    info->H = v[1];
+    info->bits = 8;
+    info->fmt = type == 5 ? RF_GRAY : RF_RGB;
+    info->stride = info->W * (type == 5 ? 1 : 3);
+    info->data_off = p;
+    if ((uint64_t)(n - p) < (uint64_t)info->stride * (uint64_t)info->H) return bad(err, -1, "PNM: truncated raster");
     return 0;
 }
 
@@ -833,6 +937,9 @@ int raster_kind(const uint8_t* data, size_t size)
     if (size >= 2 && data[0] == 'B' && data[1] == 'M') return RK_BMP;
     if (size >= 4 && (memcmp(data, kTiffLE, 4) == 0 || memcmp(data, kTiffBE, 4) == 0)) return RK_TIFF;
     if (size >= 6 && (memcmp(data, "GIF87a", 6) == 0 || memcmp(data, "GIF89a", 6) == 0)) return RK_GIF;
+    if (size >= 3 && data[0] == 'P' && data[1] >= '1' && data[1] <= '6' &&
+        (data[2] == ' ' || data[2] == '\t' || data[2] == '\n' || data[2] == '\r' || data[2] == '#'))
+        return RK_PNM;
     return RK_NONE;
 }
 
@@ -844,8 +951,9 @@ int raster_parse(const uint8_t* data, size_t size, RasterInfo* info, std::string
     case RK_BMP: return parse_bmp(data, size, info, err);
     case RK_TIFF: return parse_tiff(data, size, info, err);
     case RK_GIF: return parse_gif(data, size, info, err);
+    case RK_PNM: return parse_pnm(data, size, info, err);
     }
-    return bad(err, -1, "not a PNG, BMP, TIFF or GIF file");
+    return bad(err, -1, "not a PNG, BMP, TIFF, GIF or PNM file");
 }
 
 void raster_layout(const RasterInfo& info, RasterLayout* lay)
@@ -865,7 +973,7 @@ void raster_layout(const RasterInfo& info, RasterLayout* lay)
         lay->bytes = lay->pass_pitch[0] * info.H;
         return;
     }
-    if (info.kind == RK_BMP) {
+    if (info.kind == RK_BMP || info.kind == RK_PNM) {
         lay->pass_pitch[0] = info.stride;
         lay->pass_w[0] = info.W;
         lay->pass_h[0] = info.H;
@@ -896,7 +1004,8 @@ void raster_layout(const RasterInfo& info, RasterLayout* lay)
 int raster_unpack(const uint8_t* data, size_t size, const RasterInfo& info, const RasterLayout& lay, uint8_t* out,
                   std::string* err)
 {
-    if (info.kind == RK_BMP) {
+    if (info.kind == RK_BMP && info.rle) return unpack_bmp_rle(data, size, info, out, err);
+    if (info.kind == RK_BMP || info.kind == RK_PNM) {
         memcpy(out, data + info.data_off, (size_t)lay.bytes);
         return 0;
     }

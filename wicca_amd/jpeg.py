@@ -5,9 +5,10 @@
 the GPU (``wicca_amd/csrc/jpeg.hip``), restating libjpeg-turbo's default
 arithmetic bit for bit (checked against Pillow 12.2.0 / libjpeg-turbo
 3.1.4.1, ``tests/test_gpu_jpeg.py``), EXIF orientation applied as
-``cv2.imread`` does; PNG, BMP, TIFF and GIF files (the other formats
-``ClassifierProcessor`` counts, ``classifying_tools.py:162``) are inflated /
-copied on host threads and converted to RGB on the GPU
+``cv2.imread`` does; PNG, BMP (RLE included), TIFF and GIF files (the other
+formats ``ClassifierProcessor`` counts, ``classifying_tools.py:162``) and
+binary PGM / PPM are inflated / copied on host threads and converted to RGB
+on the GPU
 (``wicca_amd/csrc/raster.hip``, ``tests/test_gpu_raster.py``).  The entry
 points sniff each file (``wicca_image_*``), so a batch may mix formats.
 
@@ -17,8 +18,8 @@ points sniff each file (``wicca_image_*``), so a batch may mix formats.
 (``cv2.imread`` returns None for every file it cannot read and
 ``validate_image`` then raises that message, validation.py:94-95) and
 returns ``None``; ``WICCA_LOAD_DETAIL=1`` prints the decoder's own reason
-instead.  Files no decoder here handles (RLE BMP, JPEG-compressed TIFF,
-...) fail that way too — there is no CPU fallback behind it.
+instead.  Files no decoder here handles (CMYK JPEG, JPEG-compressed TIFF,
+ASCII PNM, ...) fail that way too — there is no CPU fallback behind it.
 """
 from __future__ import annotations
 
@@ -49,12 +50,12 @@ def info(data: bytes, apply_orientation: bool = True) -> tuple[int, int, int, in
     return h.value, w.value, c.value, o.value
 
 
-KINDS = {1: "jpeg", 2: "png", 3: "bmp", 4: "tiff", 5: "gif"}
+KINDS = {1: "jpeg", 2: "png", 3: "bmp", 4: "tiff", 5: "gif", 6: "pnm"}
 
 
 def image_info(data: bytes, apply_orientation: bool = True) -> tuple[int, int, str]:
-    """(height, width, format) of a JPEG, PNG, BMP, TIFF or GIF file's bytes
-    (format "jpeg" / "png" / "bmp" / "tiff" / "gif"; JPEG sizes after EXIF
+    """(height, width, format) of a JPEG, PNG, BMP, TIFF, GIF or PNM file's bytes
+    (format "jpeg" / "png" / "bmp" / "tiff" / "gif" / "pnm"; JPEG sizes after EXIF
     orientation)."""
     arr = np.frombuffer(data, np.uint8)
     h, w = ctypes.c_int64(), ctypes.c_int64()
