@@ -58,11 +58,14 @@ def test_bmp_header_errors():
     bad565 = rr.encode_bmp(img, 16, fields565=True)
     k = bad565.index(struct.pack("<III", 0xF800, 0x7E0, 0x1F))
     bad_masks = bad565[:k] + struct.pack("<III", 0xFF00, 0xF0, 0xF) + bad565[k + 12:]
-    for unsup in (rle, bpp2, bad_masks):
+    for unsup in (bpp2, bad_masks):
         with pytest.raises(NotImplementedError):
             WJ.image_info(unsup)
+    rle_ok, _ = rr.encode_bmp_rle(np.zeros((5, 6), np.uint8), np.zeros((4, 3), np.uint8))
+    assert WJ.image_info(rle_ok)[:3] == (5, 6, "bmp")
     neg_w = good[:18] + struct.pack("<i", -6) + good[22:]
-    for bad in (good[:-1], good[:20], neg_w, good[:14] + struct.pack("<I", 20) + good[18:]):
+    # rle: BI_RLE8 on a 24-bit header is no valid BMP
+    for bad in (good[:-1], good[:20], neg_w, good[:14] + struct.pack("<I", 20) + good[18:], rle):
         with pytest.raises(ValueError):
             WJ.image_info(bad)
 
