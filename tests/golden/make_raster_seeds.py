@@ -1,7 +1,7 @@
 """Writes tests/golden/raster/: small PNG / BMP / TIFF files (every PNG
 colour type family, Adam7, each filter, BMP palette / 16 / 24 / 32-bit,
-top-down, TIFF LZW / Deflate + predictor + tiles + big-endian / PackBits /
-WhiteIsZero / unassociated alpha) and
+top-down, RLE8 / RLE4, TIFF LZW / Deflate + predictor + tiles + big-endian /
+PackBits / WhiteIsZero / unassociated alpha, binary PGM / PPM) and
 cases.json with each file's expected RGB SHA-256 from Pillow 12.2.0 (the pin;
 the parity-unpinned kinds, 16-bit gray PNG, 16-bit BMP and unassociated-alpha
 TIFF, from the restatement oracle/raster_ref.py).  They seed the ASan/UBSan mutation fuzz
@@ -69,6 +69,13 @@ def main():
     files["full.gif"] = rr.encode_gif(gidx, gpal)
     files["partial_transparent_interlaced.gif"] = rr.encode_gif(gidx, gpal, screen=(25, 20), pos=(3, 4),
                                                                 transparent=5, interlace=True)
+    ridx = rng.integers(0, 256, (17, 23), dtype=np.uint8)
+    ridx[:, :9] = ridx[:, :1]
+    files["pal8_rle8.bmp"], _ = rr.encode_bmp_rle(ridx, rng.integers(0, 256, (256, 3), dtype=np.uint8))
+    files["pal4_rle4_skips.bmp"], _ = rr.encode_bmp_rle(ridx & 15, rng.integers(0, 256, (16, 3), dtype=np.uint8),
+                                                         rle4=True, skips=True)
+    files["gray.pgm"] = rr.encode_pnm(rng.integers(0, 256, (9, 13), dtype=np.uint8))
+    files["rgb.ppm"] = rr.encode_pnm(img, comment=False)
     cases = []
     for name, data in sorted(files.items()):
         with open(os.path.join(OUT, name), "wb") as f:
@@ -77,6 +84,8 @@ def main():
         if name.endswith(".gif"):
             rgb = (rr.gif_expected(gidx, gpal) if name == "full.gif" else
                    rr.gif_expected(gidx, gpal, screen=(25, 20), pos=(3, 4), transparent=5))
+        elif name.endswith((".pgm", ".ppm")) or "_rle" in name:
+            rgb = rr.pillow_rgb(data)
         else:
             rgb = rr.decode_rgb(data)
         if not unpinned:

@@ -23,7 +23,7 @@ def test_golden_info(case):
     h, w, kind = WJ.image_info(data)
     assert (h, w) == (case["height"], case["width"])
     ext = case["file"].rsplit(".", 1)[1]
-    assert kind == {"tif": "tiff"}.get(ext, ext)
+    assert kind == {"tif": "tiff", "pgm": "pnm", "ppm": "pnm"}.get(ext, ext)
 
 
 def _ihdr_png(w=4, h=3, bits=8, ct=2, il=0, crc_ok=True, idat=True, iend=True):
