@@ -191,7 +191,7 @@ def test_corrupt_png_and_bmp_fail_their_slot(tmp_path, capsys):
     assert np.array_equal(outs[0], s.astype(np.uint8)) and np.array_equal(outs[2], img)
     with pytest.raises((ValueError, NotImplementedError)):
         WJ.decode_batch(blobs)
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(ValueError):  # BI_RLE8 on a 24-bit header: no valid BMP
         WJ.decode(rle_bmp)
     paths = []
     for i, b in enumerate(blobs):

@@ -477,6 +477,11 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         return e ? atoi(e) : 0;
     }();
     P.abl = abl;
+    static const int direct_rgb = [] {  // the fused kernel's lane-own colour and direct stores (0: LDS tile / stage)
+        const char* e = getenv("WICCA_JPEG_DIRECT_RGB");
+        return e ? atoi(e) : 1;
+    }();
+    P.direct_rgb = direct_rgb;
     P.stream = stream_d;
     P.segs = (const wicca::JpegSegDev*)(m + o_seg);
     P.sub_seg = (const int32_t*)(m + o_sub);

@@ -162,6 +162,7 @@ struct JpegPlan {
                              // table has, a run past coefficient 63, a segment whose data ends before
                              // its blocks do); the host redoes those images with the host decoder
     int32_t abl;             // timing-only ablations of the fused kernel (WICCA_JPEG_ABL bits; 0 in use)
+    int32_t direct_rgb;      // fused kernel: lanes store their 24 RGB bytes directly (no LDS stage)
 };
 
 // Lanes per decode workgroup; an image's subsequences are padded to whole

@@ -1245,7 +1245,12 @@ __device__ __forceinline__ void ycc8_pack(uint2 yv, const int (&cb)[8], const in
 // (JpegImageDev::fmt, chosen on the host): the IDCT lanes (block lb of the
 // tile, row r) and the colour lanes (tile row rr, pixels cx .. cx+7) are the
 // same 256 threads.  Each lane's chroma loads are issued before the IDCT.
-template <int FMT>
+// SAME: each lane colours the 8 pixels its own IDCT produced (block lb, row
+// r) and stores its 24 RGB bytes directly: no luma tile in LDS, no workgroup
+// barrier (the destination must be 8-B aligned).  Otherwise the colour lanes
+// take tile rows (32 lanes per row) from the LDS luma tile and the RGB leaves
+// through an LDS stage as 16-B stores.
+template <int FMT, bool SAME>
 __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegImageDev& im, int tx, int ty, int32_t* tr,
                                                 uint8_t* ytile, uint32_t* stage)
 {
@@ -1263,7 +1268,7 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
         cv = *reinterpret_cast<const uint4*>(cp);
 #endif
     }
-    const int rr = threadIdx.x >> 5, cx = (threadIdx.x & 31) * 8;
+    const int rr = SAME ? r : threadIdx.x >> 5, cx = SAME ? lb * 8 : (threadIdx.x & 31) * 8;
     const int x = x0 + cx, y = y0 + rr;
     const bool px_live = y < im.H && x < im.W;
     // chroma: loads before the IDCT, arithmetic after it
@@ -1303,11 +1308,13 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
     } else {
         idct8_lane_v(cv, im.qt[0], r, blive, tr + lb * kTrBlock, px);
     }
-    if (blive) *reinterpret_cast<uint2*>(ytile + r * kYPitch + lb * 8) = pack8(px);
-    __syncthreads();  // ytile complete
+    if (!SAME) {
+        if (blive) *reinterpret_cast<uint2*>(ytile + r * kYPitch + lb * 8) = pack8(px);
+        __syncthreads();  // ytile complete
+    }
     uint32_t w[6] = {0, 0, 0, 0, 0, 0};
     if (px_live) {
-        const uint2 yv = *reinterpret_cast<const uint2*>(ytile + rr * kYPitch + cx);
+        const uint2 yv = SAME ? pack8(px) : *reinterpret_cast<const uint2*>(ytile + rr * kYPitch + cx);
         if constexpr (FMT == kJpegFmtGray) {
             w[0] = __builtin_amdgcn_perm(0u, yv.x, 0x01000000u);
             w[1] = __builtin_amdgcn_perm(0u, yv.x, 0x02020101u);
@@ -1350,6 +1357,25 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
             }
             ycc8_pack(yv, cbm, crm, w);
         }
+    }
+    if (SAME) {
+        if (P.abl & 1) {  // timing only: no stores
+            asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]));
+            return;
+        }
+        if (px_live) {
+            uint8_t* d = im.dst + (int64_t)y * im.dst_pitch + (int64_t)x * 3;
+            if (x + 8 <= im.W) {
+                uint2* d2 = reinterpret_cast<uint2*>(d);
+                d2[0] = uint2{w[0], w[1]};
+                d2[1] = uint2{w[2], w[3]};
+                d2[2] = uint2{w[4], w[5]};
+            } else {  // the row's last pixels
+                const int nb = (im.W - x) * 3;
+                for (int i = 0; i < nb; ++i) d[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+            }
+        }
+        return;
     }
     uint2* srow = reinterpret_cast<uint2*>(stage + rr * (kFuseRowBytes / 4) + (cx * 3) / 4);  // 24 B per lane
     srow[0] = uint2{w[0], w[1]};
@@ -1407,11 +1433,20 @@ void jpeg_luma_color_kernel(JpegPlan P)
     }
     const JpegImageDev& im = P.imgs[tz];
     if (tx * kFuseW >= im.W || ty * 8 >= im.H) return;  // uniform: grid sized for the largest image
+    if (P.direct_rgb && (((uintptr_t)im.dst | (uintptr_t)im.dst_pitch) & 7) == 0) {  // uniform
+        switch (im.fmt) {
+        case kJpegFmtGray: luma_color_tile<kJpegFmtGray, true>(P, im, tx, ty, tr, ytile, stage); break;
+        case kJpegFmtH2V2: luma_color_tile<kJpegFmtH2V2, true>(P, im, tx, ty, tr, ytile, stage); break;
+        case kJpegFmtH1V1: luma_color_tile<kJpegFmtH1V1, true>(P, im, tx, ty, tr, ytile, stage); break;
+        default: luma_color_tile<kJpegFmtOther, true>(P, im, tx, ty, tr, ytile, stage); break;
+        }
+        return;
+    }
     switch (im.fmt) {
-    case kJpegFmtGray: luma_color_tile<kJpegFmtGray>(P, im, tx, ty, tr, ytile, stage); break;
-    case kJpegFmtH2V2: luma_color_tile<kJpegFmtH2V2>(P, im, tx, ty, tr, ytile, stage); break;
-    case kJpegFmtH1V1: luma_color_tile<kJpegFmtH1V1>(P, im, tx, ty, tr, ytile, stage); break;
-    default: luma_color_tile<kJpegFmtOther>(P, im, tx, ty, tr, ytile, stage); break;
+    case kJpegFmtGray: luma_color_tile<kJpegFmtGray, false>(P, im, tx, ty, tr, ytile, stage); break;
+    case kJpegFmtH2V2: luma_color_tile<kJpegFmtH2V2, false>(P, im, tx, ty, tr, ytile, stage); break;
+    case kJpegFmtH1V1: luma_color_tile<kJpegFmtH1V1, false>(P, im, tx, ty, tr, ytile, stage); break;
+    default: luma_color_tile<kJpegFmtOther, false>(P, im, tx, ty, tr, ytile, stage); break;
     }
 }
 
