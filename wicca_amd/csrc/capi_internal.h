@@ -283,6 +283,8 @@ int raster_decode_to_device(Workspace* ws, const uint8_t* const* data, const int
 int image_file_probe(const uint8_t* data, int64_t size, int64_t i, int64_t* H, int64_t* W);
 int image_files_screen(const uint8_t* const* data, const int64_t* sizes, int64_t n, int* status,
                        std::vector<int64_t>* good);
+bool timing_on();      // WICCA_JPEG_TIMING set: per-call phase timings on stderr
+double timing_now_ms();
 int image_files_decode(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
                        uint8_t* const* dst, const int64_t* dpitch, hipStream_t stream, int* late);
 

@@ -1463,4 +1463,7 @@ int image_files_decode(Workspace* ws, const uint8_t* const* data, const int64_t*
     return decode_files_to_device(ws, data, sizes, n, dst, dpitch, true, stream, true, late);
 }
 
+bool timing_on() { return jpeg_timing(); }
+double timing_now_ms() { return now_ms(); }
+
 }  // namespace wicca_capi

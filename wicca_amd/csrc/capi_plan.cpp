@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <vector>
 
@@ -103,9 +104,15 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         }
     }
     std::vector<int> late((size_t)n, 0);
+    const double t0 = timing_now_ms();
     if ((rc = image_files_decode(ws, data, sizes, n, img.data(), pitch.data(), cs,
                                  late_status ? late.data() : nullptr)))
         return rc;
+    double t_decoded = 0;
+    if (timing_on()) {
+        HIP_TRY(hipStreamSynchronize(cs));
+        t_decoded = timing_now_ms();
+    }
 
     // icon planes (device): image i, depth slot u at ipitch = round_up(iw * 3, 16)
     std::vector<int64_t> ico_off((size_t)n * U), ico_pitch((size_t)n * U);
@@ -404,6 +411,11 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                 if ((rc = run_resize(q, q.src, q.src_pitch, 0, q.dst, q.dst_pitch, 0, 1, cs, ws))) return rc;
             }
     }
+    double t_kernels = 0;
+    if (timing_on()) {
+        HIP_TRY(hipStreamSynchronize(cs));
+        t_kernels = timing_now_ms();
+    }
     // 5. the np.stack of :323 for every (shape, depth), to the caller's arrays
     for (int s = 0; s < S; ++s) {
         const size_t bytes = (size_t)(n * ob[(size_t)s]);
@@ -413,6 +425,9 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                                    bytes, hipMemcpyDeviceToHost, cs));
     }
     HIP_TRY(hipStreamSynchronize(cs));
+    if (timing_on())
+        fprintf(stderr, "[wicca plan] %lld files: decode %.2f ms, plan kernels %.2f ms, outputs to host %.2f ms\n",
+                (long long)n, t_decoded - t0, t_kernels - t_decoded, timing_now_ms() - t_kernels);
     for (int64_t i = 0; i < n && late_status; ++i) {  // data found corrupt during the decode: zero outputs
         late_status[i] = late[(size_t)i];
         if (!late[(size_t)i]) continue;
