@@ -264,8 +264,9 @@ def test_batch_larger_than_one_device_pass():
         assert np.array_equal(got[i], J.decode_rgb(blobs[i])), i
 
 
-@pytest.mark.parametrize("env", [{"WICCA_JPEG_WRITE_SLOTS": "6"}, {"WICCA_JPEG_SYNC_CK": "0"}],
-                         ids=["slots6", "no-checkpoints"])
+@pytest.mark.parametrize("env", [{"WICCA_JPEG_WRITE_SLOTS": "6"}, {"WICCA_JPEG_SYNC_CK": "0"},
+                                 {"WICCA_JPEG_SYNC_CK": "1"}],
+                         ids=["slots6", "no-checkpoints", "round0-checkpoints"])
 def test_write_and_sync_variants_subprocess(env):
     """The sync and write passes have 4-table builds (every baseline file) and
     6-table ones (extended-sequential files with separate tables per

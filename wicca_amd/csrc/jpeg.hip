@@ -73,7 +73,10 @@ struct SubResult {
 // state and counts, minus the checkpoint's prefix.  Huffman codes resynchronise
 // within a few codewords, so round 1 (which had decoded every subsequence in
 // full) costs a few blocks per lane.
-constexpr int kSyncCk = 8;
+#ifndef WICCA_JPEG_SYNC_CKS
+#define WICCA_JPEG_SYNC_CKS 8
+#endif
+constexpr int kSyncCk = WICCA_JPEG_SYNC_CKS;
 struct SyncCk {
     uint32_t pos_slot;  // (p - lane start) | slot << 24
     int32_t started;    // blocks started before it
@@ -304,17 +307,22 @@ __device__ __forceinline__ void zero_zig(int16_t* coef, const uint8_t* nat, int6
 // 2 stops at the first of the n_ck checkpoints in ck the decode reaches
 // (returns its index, -1 if none; *hit_ck gets it).  ck_base = the lane's
 // start bit.
+// CK 3 (sync rounds >= 1 with refresh): CK 2's stop at a checkpoint in ck,
+// and meanwhile CK 1's recording into ck_rec (*n_rec gets the count).
 template <bool WRITE, int CK = 0, typename HT = HuffDev>
 __device__ int decode_run(const DecGeom& im, const HT* tabs, BitReader& br, int64_t stop,
                           DecState& st, int64_t& started, int32_t (&dc)[kJpegMaxComp], int64_t g,
                           int64_t block_lo, int64_t block_end, int16_t* coef, const WaveStage* ws = nullptr,
                           bool seg_last = false, SyncCk* ck = nullptr, int n_ck = 0, int64_t ck_base = 0,
-                          SyncCk* hit_ck = nullptr, int ck_step = 0, int32_t* damage = nullptr)
+                          SyncCk* hit_ck = nullptr, int ck_step = 0, int32_t* damage = nullptr,
+                          SyncCk* ck_rec = nullptr, int* n_rec = nullptr)
 {
+    constexpr bool REC = CK == 1 || CK == 3, CMP = CK == 2 || CK == 3;
     bool bad = false;  // WRITE: the true decode path meets damaged data (see JpegPlan::damage)
-    int nck = 0, hit = -1;
-    uint32_t cur = 0;  // CK 2: pos_slot of checkpoint nck
-    if (CK == 2 && n_ck > 0) cur = ck[0].pos_slot;
+    int nck = 0, hit = -1, nrec = 0;
+    SyncCk* rec = CK == 3 ? ck_rec : ck;
+    uint32_t cur = 0;  // CMP: pos_slot of checkpoint nck
+    if (CMP && n_ck > 0) cur = ck[0].pos_slot;
     int64_t blk = -1;
     bool staged = false;
     int zk = 0;  // next zigzag position of a block written position by position (not staged)
@@ -337,15 +345,15 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BitReader& br, int6
     const int32_t ck_off = (int32_t)(br.base - ck_base);  // reader-relative -> checkpoint-relative
     int32_t nstart = 0;  // blocks started in this run
     while (br.pr < stop_r) {
-        if (CK == 1 && st.k == 0 && nck < kSyncCk && br.pr + ck_off >= nck * ck_step) {
+        if (REC && st.k == 0 && nrec < kSyncCk && br.pr + ck_off >= nrec * ck_step) {
             SyncCk e;
             e.pos_slot = (uint32_t)(br.pr + ck_off) | ((uint32_t)st.slot << 24);
             e.started = (int32_t)started + nstart;
             for (int q = 0; q < kJpegMaxComp; ++q) e.dc[q] = dc[q];
             e.pad_ = 0;
-            ck[nck++] = e;
+            rec[nrec++] = e;
         }
-        if (CK == 2 && st.k == 0 && nck < n_ck) {
+        if (CMP && st.k == 0 && nck < n_ck) {
             const uint32_t here = (uint32_t)(br.pr + ck_off);
             while ((cur & 0xFFFFFFu) < here) {  // checkpoints are in increasing bit order
                 if (++nck == n_ck) break;
@@ -454,7 +462,8 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BitReader& br, int6
     }
     st.p = br.p();
     started += nstart;
-    return CK == 1 ? nck : hit;
+    if (CK == 3) *n_rec = nrec;
+    return CK == 1 ? nrec : hit;
 }
 
 // The image's Huffman tables, staged in LDS: the host stores an image's
@@ -534,7 +543,7 @@ template <int CK, int NS>
 __global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(JpegPlan P, const SubResult* prev,
                                                              SubResult* next, int round, int* changed,
                                                              const SubResult* older, SyncCk* cks, int* stats,
-                                                             const SubResult* r0res, const int* prev_changed)
+                                                             SubResult* r0res, const int* prev_changed)
 {
     // launched ahead of the host's look at the flags: once a round moved no
     // end state, every later round repeats its results
@@ -594,23 +603,38 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(J
     int32_t dc[kJpegMaxComp] = {0, 0, 0};
     BitReader br;
     br.reset(P.stream, st.p);
+    // checkpoints: two sets per lane (cks, then cks + n_sub * kSyncCk), the
+    // one in use named by bit 16 of r0res[i].n_ck (r0res: the result of the
+    // decode that recorded them)
     SyncCk* ck = cks + i * kSyncCk;
     if (CK == 1) {
         r.n_ck = decode_run<false, 1, HuffDevSync>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr, nullptr, false, ck,
                                       0, b0, nullptr, P.sub_bits / kSyncCk);
-    } else if (CK == 2) {
-        const SubResult& o = r0res[i];  // this lane's round-0 result and checkpoints
+    } else if (CK == 2 || CK == 3) {
+        const int o_nck = r0res[i].n_ck;  // checkpoints of this lane's last full decode (its result: r0res[i])
+        const int set = (o_nck >> 16) & 1;
+        SyncCk* cur_ck = ck + (set ? P.n_sub * kSyncCk : 0);
+        SyncCk* new_ck = ck + (set ? 0 : P.n_sub * kSyncCk);
         SyncCk h;
-        const int hit = decode_run<false, 2, HuffDevSync>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr, nullptr,
-                                             false, ck, o.n_ck, b0, &h);
-        if (hit >= 0) {  // the rest is round 0's decode from checkpoint `hit`
+        int n_rec = 0;
+        const int hit = decode_run<false, CK, HuffDevSync>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr,
+                                                           nullptr, false, cur_ck, o_nck & 0xFFFF, b0, &h,
+                                                           P.sub_bits / kSyncCk, nullptr, new_ck, &n_rec);
+        if (hit >= 0) {  // the rest is that decode's from checkpoint `hit`
             if (stats) {
                 const uint64_t m = __ballot(true);
                 if (__ffsll((long long)m) - 1 == (int)(threadIdx.x & 63)) atomicAdd(stats + 1, (int)__popcll(m));
             }
+            const SubResult& o = r0res[i];  // read after the decode: fewer live registers in it
             st = o.end;
             r.started += o.started - h.started;
             for (int c = 0; c < kJpegMaxComp; ++c) dc[c] += o.dc[c] - h.dc[c];
+        } else if (CK == 3) {  // a full decode from a new start: its checkpoints replace the old ones
+            SubResult f = r;
+            f.end = st;
+            for (int c = 0; c < kJpegMaxComp; ++c) f.dc[c] = dc[c];
+            f.n_ck = n_rec | ((set ^ 1) << 16);
+            r0res[i] = f;
         }
     } else {
         decode_run<false, 0, HuffDevSync>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr);
@@ -1517,7 +1541,7 @@ size_t jpeg_jobs_bytes() { return kJpegMaxJobs * sizeof(IdctJob); }
 size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg)
 {
     (void)n_seg;
-    return (size_t)n_sub * (4 * sizeof(SubResult) + sizeof(SubBase) + kSyncCk * sizeof(SyncCk)) + 256 +
+    return (size_t)n_sub * (5 * sizeof(SubResult) + sizeof(SubBase) + 2 * kSyncCk * sizeof(SyncCk)) + 256 +
            kJpegMaxJobs * sizeof(IdctJob);
 }
 
@@ -1530,8 +1554,9 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     SubResult* ra = (SubResult*)base;
     SubResult* rb = ra + P.n_sub;
     SubResult* rc = rb + P.n_sub;
-    SubResult* r0 = rc + P.n_sub;  // round 0's results: kept for every later round's checkpoint hits
-    SubBase* sb = (SubBase*)(r0 + P.n_sub);
+    SubResult* r0 = rc + P.n_sub;  // round 0's results
+    SubResult* ckres = r0 + P.n_sub;  // per lane: the result of the decode that recorded its checkpoints
+    SubBase* sb = (SubBase*)(ckres + P.n_sub);
     int* flags = (int*)(sb + P.n_sub);  // [0, kFlagRing): per-round "an end state changed"; then stats
     IdctJob* jobs = (IdctJob*)((uint8_t*)flags + 256);
     SyncCk* cks = (SyncCk*)(jobs + kJpegMaxJobs);
@@ -1569,11 +1594,16 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
         // first round-0 checkpoint its decode reaches: a lane re-decoded in
         // round 2 or 3 (its predecessor's end moved) usually meets its own
         // round-0 decode within a few blocks.
+        // A lane that finds no checkpoint decodes its whole subsequence from its
+        // new start; its decode's checkpoints then replace the old ones (two
+        // sets per lane, ckres holds the decode they belong to), so the next
+        // round can stop it on the path it just took.
         // WICCA_JPEG_SYNC_CK=0: no checkpoints (every round-1 lane decodes its whole subsequence);
+        // 1: round 0's checkpoints only; 2 (default): refreshed by full decodes;
         // WICCA_JPEG_TIMING: per-round counts of decoding lanes and checkpoint hits to stderr
         static const int ck_mode = [] {
             const char* e = getenv("WICCA_JPEG_SYNC_CK");
-            return e ? atoi(e) : 1;
+            return e ? atoi(e) : 2;
         }();
         static const bool stats_on = getenv("WICCA_JPEG_TIMING") != nullptr;
         constexpr int kStatRounds = 6;
@@ -1594,14 +1624,16 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             const int* prev_changed = round >= 2 ? flags + (round - 1) % kFlagRing : nullptr;
 #define WICCA_SYNC_LAUNCH(CKV, NSV)                                                                        \
     hipLaunchKernelGGL((jpeg_sync_kernel<CKV, NSV>), dim3(grid), dim3(kJThreads), 0, s, P, prev, next, round, \
-                       changed, older, cks, st, (const SubResult*)r0, prev_changed)
+                       changed, older, cks, st, ckres, prev_changed)
             if (ns4) {
                 if (ck == 1) WICCA_SYNC_LAUNCH(1, 4);
                 else if (ck == 2) WICCA_SYNC_LAUNCH(2, 4);
+                else if (ck == 3) WICCA_SYNC_LAUNCH(3, 4);
                 else WICCA_SYNC_LAUNCH(0, 4);
             } else {
                 if (ck == 1) WICCA_SYNC_LAUNCH(1, 2 * kJpegMaxComp);
                 else if (ck == 2) WICCA_SYNC_LAUNCH(2, 2 * kJpegMaxComp);
+                else if (ck == 3) WICCA_SYNC_LAUNCH(3, 2 * kJpegMaxComp);
                 else WICCA_SYNC_LAUNCH(0, 2 * kJpegMaxComp);
             }
 #undef WICCA_SYNC_LAUNCH
@@ -1609,6 +1641,10 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
         };
         e = sync(ck_mode ? 1 : 0, r0, r0, 0, nullptr, stats_on ? stats : nullptr);
         if (e != hipSuccess) return e;
+        // the checkpoints' results start as round 0's (checkpoint set 0)
+        if (ck_mode && (e = hipMemcpyAsync(ckres, r0, (size_t)P.n_sub * sizeof(SubResult), hipMemcpyDeviceToDevice,
+                                           s)) != hipSuccess)
+            return e;
         // rounds go out kSpec at a time with one host look per batch (a round
         // whose predecessor changed nothing copies its results and exits), so
         // the usual three rounds cost one host round trip instead of three
@@ -1631,7 +1667,7 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             for (int r = launched + 1; r <= launched + batch; ++r) {
                 SubResult* nxt = bufs[(r - 1) % 3];
                 int* st_r = stats_on && r < kStatRounds ? stats + 2 * r : nullptr;
-                if ((e = sync(ck_mode ? 2 : 0, cur, nxt, r, older, st_r)) != hipSuccess) return e;
+                if ((e = sync(ck_mode == 0 ? 0 : ck_mode == 1 ? 2 : 3, cur, nxt, r, older, st_r)) != hipSuccess) return e;
                 older = cur;
                 cur = nxt;
             }
