@@ -323,6 +323,28 @@ def test_file_caller_stage_fused_cases(tmp_path, depth, shape, interp, border, k
         assert np.array_equal(icons[i], R.resize(icon, shape, interp)), i
 
 
+@pytest.mark.parametrize("depth", [1, 2])
+def test_icon_area_resize_window(tmp_path, depth):
+    """INTER_AREA icon resizes through resize_desc_kernel's LDS window (the
+    rows and columns a workgroup's 256 output bytes read) and, where the
+    window exceeds 32 KB (depth 1 of a 3840-wide image to 100 x 60), the
+    per-lane path: both against cv2.resize restated on the C oracle's icon."""
+    sizes = [(2160, 3840), (1500, 2602), (999, 1777), (641, 479)]
+    paths = []
+    refs = []
+    for i, (h, w) in enumerate(sizes):
+        data = J.encode(J.test_image("noise" if i % 2 else "scene", h, w, 31 * i + depth), 80, 2)
+        p = tmp_path / f"w{i}.jpg"
+        p.write_bytes(data)
+        paths.append(str(p))
+        refs.append(J.decode_rgb(data))
+    for shape in [(224, 224), (331, 299), (100, 60)]:
+        _, icons = wicca_amd.get_img_batch(paths, shape, depth, 3, 1, 0)
+        for i, rgb in enumerate(refs):
+            icon = c_oracle.ll_int_block(rgb, depth, 1, 0)[0]
+            assert np.array_equal(icons[i], R.resize(icon, shape, 3)), (shape, i)
+
+
 def test_file_caller_stage_fused_equals_unfused(tmp_path):
     """WICCA_STAGE_FUSED=0 (per-image resize, icon and icon-resize launches)
     in a child process gives the same bytes as the fused stage."""
