@@ -325,10 +325,10 @@ def test_file_caller_stage_fused_cases(tmp_path, depth, shape, interp, border, k
 
 @pytest.mark.parametrize("depth", [1, 2])
 def test_icon_area_resize_window(tmp_path, depth):
-    """INTER_AREA icon resizes through resize_desc_kernel's LDS window (the
-    rows and columns a workgroup's 256 output bytes read) and, where the
-    window exceeds 32 KB (depth 1 of a 3840-wide image to 100 x 60), the
-    per-lane path: both against cv2.resize restated on the C oracle's icon."""
+    """INTER_AREA icon resizes of the file stage (resize_desc_kernel) at
+    downscales from under 2x to 38x (depth 1 of a 3840-wide image to 100 x
+    60), non-integer and ragged, against cv2.resize restated on the C
+    oracle's icon."""
     sizes = [(2160, 3840), (1500, 2602), (999, 1777), (641, 479)]
     paths = []
     refs = []
