@@ -374,6 +374,25 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                 return rc;
         }
     }
+    // icon resizes (classifying_tools.py:318), one launch per shape over (depth, image)
+    for (int s = 0; s < S; ++s) {
+        if (!shape_per_image[(size_t)s]) {
+            HIP_TRY(wicca::launch_resize_desc(
+                (const wicca::ResizeParams*)(dp + o_irp) + (size_t)s * U * n, (int64_t)U * n,
+                (int)shapes[(size_t)s].h, (int)(shapes[(size_t)s].w * 3), cs));
+            continue;
+        }
+        for (int u = 0; u < U; ++u)
+            for (int64_t i = 0; i < n; ++i) {
+                const wicca::ResizeParams& q = irp[(size_t)((s * U + u) * n + i)];
+                if ((rc = run_resize(q, q.src, q.src_pitch, 0, q.dst, q.dst_pitch, 0, 1, cs, ws))) return rc;
+            }
+    }
+    // the icons' copies to the caller (5/6 of the output bytes at 5 depths)
+    // leave on the copy stream while the source resizes below run
+    HIP_TRY(ws->ensure_pipeline());
+    hipEvent_t icons_done = ws->slot_ready[0];  // the workspace is this call's alone
+    HIP_TRY(hipEventRecord(icons_done, cs));
     // source resizes (classifying_tools.py:315), every shape
     for (AreaGroup& g : groups) {
         wicca::PlanParams pp{};
@@ -397,33 +416,31 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                                  ws)))
                 return rc;
         }
-    // icon resizes (classifying_tools.py:318), one launch per shape over (depth, image)
+    // 5. the np.stack of :323 for every (shape, depth), to the caller's arrays:
+    // the icons from the copy stream (every kernel is already queued on cs, so
+    // a copy that holds the host thread does not hold the GPU), then the
+    // resized sources behind their kernels
+    HIP_TRY(hipStreamWaitEvent(ws->copy_stream, icons_done, 0));
+    struct CopyDrain {  // an error return below still waits for copies into the caller's arrays
+        hipStream_t s;
+        ~CopyDrain() { (void)hipStreamSynchronize(s); }
+    } drain{ws->copy_stream};
     for (int s = 0; s < S; ++s) {
-        if (!shape_per_image[(size_t)s]) {
-            HIP_TRY(wicca::launch_resize_desc(
-                (const wicca::ResizeParams*)(dp + o_irp) + (size_t)s * U * n, (int64_t)U * n,
-                (int)shapes[(size_t)s].h, (int)(shapes[(size_t)s].w * 3), cs));
-            continue;
-        }
-        for (int u = 0; u < U; ++u)
-            for (int64_t i = 0; i < n; ++i) {
-                const wicca::ResizeParams& q = irp[(size_t)((s * U + u) * n + i)];
-                if ((rc = run_resize(q, q.src, q.src_pitch, 0, q.dst, q.dst_pitch, 0, 1, cs, ws))) return rc;
-            }
+        const size_t bytes = (size_t)(n * ob[(size_t)s]);
+        for (int d = 0; d < n_depths; ++d)
+            HIP_TRY(hipMemcpyAsync(icons[s * n_depths + d], dout + ico_out_off[(size_t)(s * U + slot_of[(size_t)d])],
+                                   bytes, hipMemcpyDeviceToHost, ws->copy_stream));
     }
     double t_kernels = 0;
     if (timing_on()) {
         HIP_TRY(hipStreamSynchronize(cs));
         t_kernels = timing_now_ms();
     }
-    // 5. the np.stack of :323 for every (shape, depth), to the caller's arrays
     for (int s = 0; s < S; ++s) {
         const size_t bytes = (size_t)(n * ob[(size_t)s]);
         HIP_TRY(hipMemcpyAsync(resized[s], dout + res_off[(size_t)s], bytes, hipMemcpyDeviceToHost, cs));
-        for (int d = 0; d < n_depths; ++d)
-            HIP_TRY(hipMemcpyAsync(icons[s * n_depths + d], dout + ico_out_off[(size_t)(s * U + slot_of[(size_t)d])],
-                                   bytes, hipMemcpyDeviceToHost, cs));
     }
+    HIP_TRY(hipStreamSynchronize(ws->copy_stream));
     HIP_TRY(hipStreamSynchronize(cs));
     if (timing_on())
         fprintf(stderr, "[wicca plan] %lld files: decode %.2f ms, plan kernels %.2f ms, outputs to host %.2f ms\n",
