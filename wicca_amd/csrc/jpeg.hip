@@ -37,6 +37,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "jpeg.h"
@@ -91,6 +92,9 @@ struct SyncCk {
 // the serial decode chain.  Positions inside the loop are 32-bit, relative to
 // `base` (the lane's first word).  The host pads the stream with 64 zero bytes
 // past its end (the reader looks at most 12 bytes ahead of its position).
+#ifndef WICCA_JPEG_READER
+#define WICCA_JPEG_READER 2  // 32-bit words per chunk of the sync passes' reader: 2 or 4 (0: word reader)
+#endif
 struct BitReader {
     const uint32_t* w;  // stream words from base
     int64_t base;       // absolute bit position of w[0]
@@ -127,6 +131,83 @@ struct BitReader {
         pr += k;
     }
 };
+
+// The guess pass's reader: the stream in 8-B chunks (16-B with
+// WICCA_JPEG_READER=4), one chunk consumed word by word, the next in flight.
+// A lane's subsequence is ~512 contiguous bytes and a wave's lanes are that
+// far apart, so every load touches its own 128-B line; with one 4-B load per
+// refill the lines were evicted between a lane's refills and fetched again for
+// every word (guess pass FETCH_SIZE 29x the stream's bytes, profiles/r04ab_*;
+// 8-B chunks: 15x, guess pass 1.24 -> 1.00 ms, r04ac_*, r04ae_*).  16-B
+// chunks fetch less (7.5x) but were no faster and spill in the later rounds'
+// kernels.  The write pass keeps the word reader: its block stores share the
+// load counter, so waiting for a chunk loaded refills earlier also waited for
+// the stores issued since (write pass 2.79 -> 3.04 ms with chunks).
+struct BitReaderC {
+    static constexpr int CW = WICCA_JPEG_READER == 4 ? 4 : 2;  // words per chunk
+    typedef uint32_t chunk_t __attribute__((ext_vector_type(CW)));
+    const chunk_t* q;   // chunks from base
+    int64_t base;       // absolute bit position of q[0] (a multiple of 32 * CW)
+    int32_t pr;         // next unconsumed bit, relative to base
+    int32_t qi;         // index of the chunk in nxt
+    int32_t left;       // words of cur not yet appended
+    uint64_t buf;       // n valid bits, MSB-aligned
+    int n;
+    chunk_t cur, nxt;   // raw words; cur[0] is the next to append
+    __device__ __forceinline__ static uint32_t be(uint32_t x) { return __builtin_bswap32(x); }
+    __device__ __forceinline__ void advance()
+    {
+#pragma unroll
+        for (int k = 0; k + 1 < CW; ++k) cur[k] = cur[k + 1];
+        if (--left == 0) {
+            cur = nxt;
+            nxt = q[++qi];
+            left = CW;
+        }
+    }
+    __device__ __forceinline__ void append()
+    {
+        buf |= (uint64_t)be(cur[0]) << (32 - n);
+        n += 32;
+        advance();
+    }
+    __device__ void reset(const uint8_t* stream, int64_t bitpos)
+    {
+        base = bitpos & ~(int64_t)(32 * CW - 1);
+        q = reinterpret_cast<const chunk_t*>(stream) + (base / (32 * CW));
+        pr = (int32_t)(bitpos - base);
+        cur = q[0];
+        nxt = q[1];
+        qi = 1;
+        left = CW;
+        const int sw = pr >> 5;
+#pragma unroll
+        for (int k = 0; k + 1 < CW; ++k)
+            if (k < sw) advance();
+        buf = 0;
+        n = 0;
+        append();
+        append();
+        buf <<= (pr & 31);
+        n = 64 - (pr & 31);
+    }
+    __device__ __forceinline__ int64_t p() const { return base + pr; }
+    __device__ __forceinline__ void refill()
+    {
+        if (n <= 32) append();
+    }
+    __device__ __forceinline__ void skip(int k)
+    {
+        buf <<= k;
+        n -= k;
+        pr += k;
+    }
+};
+// the guess pass (CK 1) reads through chunks; the later rounds, whose lanes
+// mostly stop within S/8 bits, keep the word reader (1.79 against 1.85 ms of
+// rounds per call with chunks, profiles/r04ad_*)
+template <int CK>
+using SyncReader = typename std::conditional<CK == 1 && WICCA_JPEG_READER != 0, BitReaderC, BitReader>::type;
 
 // (code length << 8) | symbol of the codeword at the top of `look` (the next
 // 32 bits); a bit string that is no code reads as symbol 0 after 17 bits, as
@@ -309,8 +390,8 @@ __device__ __forceinline__ void zero_zig(int16_t* coef, const uint8_t* nat, int6
 // start bit.
 // CK 3 (sync rounds >= 1 with refresh): CK 2's stop at a checkpoint in ck,
 // and meanwhile CK 1's recording into ck_rec (*n_rec gets the count).
-template <bool WRITE, int CK = 0, typename HT = HuffDev>
-__device__ int decode_run(const DecGeom& im, const HT* tabs, BitReader& br, int64_t stop,
+template <bool WRITE, int CK = 0, typename HT = HuffDev, typename BR = BitReader>
+__device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t stop,
                           DecState& st, int64_t& started, int32_t (&dc)[kJpegMaxComp], int64_t g,
                           int64_t block_lo, int64_t block_end, int16_t* coef, const WaveStage* ws = nullptr,
                           bool seg_last = false, SyncCk* ck = nullptr, int n_ck = 0, int64_t ck_base = 0,
@@ -601,14 +682,14 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(J
     r.started = 0;
     r.n_ck = 0;
     int32_t dc[kJpegMaxComp] = {0, 0, 0};
-    BitReader br;
+    SyncReader<CK> br;
     br.reset(P.stream, st.p);
     // checkpoints: two sets per lane (cks, then cks + n_sub * kSyncCk), the
     // one in use named by bit 16 of r0res[i].n_ck (r0res: the result of the
     // decode that recorded them)
     SyncCk* ck = cks + i * kSyncCk;
     if (CK == 1) {
-        r.n_ck = decode_run<false, 1, HuffDevSync>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr, nullptr, false, ck,
+        r.n_ck = decode_run<false, 1, HuffDevSync, SyncReader<CK>>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr, nullptr, false, ck,
                                       0, b0, nullptr, P.sub_bits / kSyncCk);
     } else if (CK == 2 || CK == 3) {
         const int o_nck = r0res[i].n_ck;  // checkpoints of this lane's last full decode (its result: r0res[i])
@@ -617,7 +698,7 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(J
         SyncCk* new_ck = ck + (set ? 0 : P.n_sub * kSyncCk);
         SyncCk h;
         int n_rec = 0;
-        const int hit = decode_run<false, CK, HuffDevSync>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr,
+        const int hit = decode_run<false, CK, HuffDevSync, SyncReader<CK>>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr,
                                                            nullptr, false, cur_ck, o_nck & 0xFFFF, b0, &h,
                                                            P.sub_bits / kSyncCk, nullptr, new_ck, &n_rec);
         if (hit >= 0) {  // the rest is that decode's from checkpoint `hit`
@@ -637,7 +718,7 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(J
             r0res[i] = f;
         }
     } else {
-        decode_run<false, 0, HuffDevSync>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr);
+        decode_run<false, 0, HuffDevSync, SyncReader<CK>>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr);
     }
     r.end = st;
     for (int c = 0; c < kJpegMaxComp; ++c) r.dc[c] = dc[c];
