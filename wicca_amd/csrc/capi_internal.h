@@ -109,7 +109,7 @@ struct Workspace {
     hipEvent_t slot_ready[2] = {nullptr, nullptr}, slot_free[2] = {nullptr, nullptr};
     DevBuf slot[2], icon[2];
     // JPEG decode (wicca_jpeg_*): stream + tables, coefficients, planes, scratch, RGB images
-    DevBuf jstream, jmeta, jcoef, jplanes, jscratch, jrgb, jtmp;
+    DevBuf jstream, jmeta, jcoef, jplanes, jscratch, jrgb, jtmp, jilv;
     DevBuf rscratch;  // two-pass INTER_AREA row sums (float)
     DevBuf smeta;     // fused caller stage: image descriptors + icon resize parameters
     DevBuf rtab;      // INTER_CUBIC / INTER_LANCZOS4 coefficient tables
@@ -130,7 +130,7 @@ struct Workspace {
     {
         return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
                slot[0].cap + slot[1].cap + icon[0].cap + icon[1].cap + jstream.cap + jmeta.cap + jcoef.cap +
-               jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap + rscratch.cap + smeta.cap + rtab.cap + rraw.cap +
+               jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap + jilv.cap + rscratch.cap + smeta.cap + rtab.cap + rraw.cap +
                rmeta.cap + pmeta.cap + picons.cap + phsum.cap;
     }
     hipError_t ensure_pipeline()
@@ -174,6 +174,7 @@ struct Workspace {
         jscratch.release();
         jrgb.release();
         jtmp.release();
+        jilv.release();
         jhost.release();
         jtab.release();
         jhcoef.release();

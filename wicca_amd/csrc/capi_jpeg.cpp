@@ -442,6 +442,8 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     HIP_TRY(ws->jmeta.reserve(o_dmg + (size_t)n * sizeof(int32_t)));
     HIP_TRY(ws->jplanes.reserve((size_t)std::max<int64_t>(plane_bytes, 256)));
     HIP_TRY(ws->jscratch.reserve(wicca::jpeg_scratch_bytes((int64_t)sub_seg.size(), (int64_t)segs.size())));
+    const size_t ilv_bytes = wicca::jpeg_ilv_bytes((int64_t)sub_seg.size(), (int32_t)S);
+    if (ilv_bytes) HIP_TRY(ws->jilv.reserve(ilv_bytes));
     if (tmp_bytes) HIP_TRY(ws->jtmp.reserve((size_t)tmp_bytes));
     for (int64_t i = 0; i < n; ++i)
         if (tmp_off[(size_t)i] >= 0) ims[(size_t)i].dst = (uint8_t*)ws->jtmp.ptr + tmp_off[(size_t)i];
@@ -483,6 +485,9 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     }();
     P.direct_rgb = direct_rgb;
     P.stream = stream_d;
+    P.stream_bytes = (int64_t)stream_bytes;
+    P.ilv = ilv_bytes ? (const uint32_t*)ws->jilv.ptr : nullptr;
+    P.ilv_sw = wicca::jpeg_ilv_words((int32_t)S);
     P.segs = (const wicca::JpegSegDev*)(m + o_seg);
     P.sub_seg = (const int32_t*)(m + o_sub);
     P.sub_img = (const int32_t*)(m + o_sim);

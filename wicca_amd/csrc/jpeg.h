@@ -161,6 +161,13 @@ struct JpegPlan {
     int32_t* damage;         // per image: set by the write pass where the data is damaged (a code no
                              // table has, a run past coefficient 63, a segment whose data ends before
                              // its blocks do); the host redoes those images with the host decoder
+    // lane-interleaved copy of the streams (nullptr: read `stream`): word j of
+    // subsequence i at ilv[((i / 64) * ilv_sw + j) * 64 + i % 64], word 0 the
+    // subsequence's first byte (jpeg_interleave_kernel); a wave's refills then
+    // read neighbouring words instead of one 128-B line per lane
+    const uint32_t* ilv;
+    int64_t stream_bytes;    // bytes of `stream` (the copy reads none past them)
+    int32_t ilv_sw;          // words per slot: sub_bits / 32 + 8
     int32_t abl;             // timing-only ablations of the fused kernel (WICCA_JPEG_ABL bits; 0 in use)
     int32_t direct_rgb;      // fused kernel: lanes store their 24 RGB bytes directly (no LDS stage)
 };
@@ -174,6 +181,10 @@ constexpr int kJpegLanes = 256;
 // jpeg_scratch_bytes).  *sync_rounds receives the synchronisation passes run.
 constexpr int kJpegMaxJobs = 4096;  // (image, component) pairs per call
 size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg);
+// Bytes of the lane-interleaved stream copy (JpegPlan::ilv), 0 when it is off
+// (WICCA_JPEG_ILV=0).
+size_t jpeg_ilv_bytes(int64_t n_sub, int32_t sub_bits);
+inline int32_t jpeg_ilv_words(int32_t sub_bits) { return sub_bits / 32 + 8; }
 // async_rounds > 0: launch exactly that many synchronisation rounds (<= 15)
 // without reading their flags on the host (nothing in the call waits for
 // the device); *async_flags then points at the device ring of per-round

@@ -95,11 +95,14 @@ struct SyncCk {
 #ifndef WICCA_JPEG_READER
 #define WICCA_JPEG_READER 2  // 32-bit words per chunk of the sync passes' reader: 2 or 4 (0: word reader)
 #endif
+#ifndef WICCA_JPEG_ILV
+#define WICCA_JPEG_ILV 1  // the lane-interleaved stream copy (runtime switch WICCA_JPEG_ILV=0: the plain stream)
+#endif
 struct BitReader {
-    const uint32_t* w;  // stream words from base
-    int64_t base;       // absolute bit position of w[0]
+    const uint32_t* w;  // the word in nx
+    int64_t base;       // absolute bit position of the first word read
     int32_t pr;         // next unconsumed bit, relative to base
-    int32_t wi;         // index of the word in nx
+    int32_t st;         // words between consecutive stream words (1, or 64 interleaved)
     uint64_t buf;       // n valid bits, MSB-aligned
     int n;
     uint32_t nx;
@@ -107,11 +110,28 @@ struct BitReader {
     __device__ void reset(const uint8_t* stream, int64_t bitpos)
     {
         base = bitpos & ~(int64_t)31;
-        w = reinterpret_cast<const uint32_t*>(stream) + (base >> 5);
-        pr = (int32_t)(bitpos - base);
-        buf = ((uint64_t)be(w[0]) << 32) | be(w[1]);
-        wi = 2;
-        nx = w[2];
+        start(reinterpret_cast<const uint32_t*>(stream) + (base >> 5), 1, (int32_t)(bitpos - base));
+    }
+    // lane `i` of the interleaved copy (JpegPlan::ilv); s_i = the bit its
+    // subsequence starts at, bitpos >= s_i inside its slot
+    __device__ void reset(const JpegPlan& P, int64_t i, int64_t s_i, int64_t bitpos)
+    {
+        if (!P.ilv) {
+            reset(P.stream, bitpos);
+            return;
+        }
+        const int64_t j0 = (bitpos - s_i) >> 5;
+        base = s_i + 32 * j0;
+        start(P.ilv + (((i >> 6) * P.ilv_sw + j0) << 6) + (i & 63), 64, (int32_t)(bitpos - base));
+    }
+    __device__ __forceinline__ void start(const uint32_t* w0, int stride, int32_t off)
+    {
+        st = stride;
+        w = w0;
+        pr = off;
+        buf = ((uint64_t)be(w[0]) << 32) | be(w[st]);
+        w += 2 * st;
+        nx = *w;
         buf <<= pr;
         n = 64 - pr;
     }
@@ -121,7 +141,8 @@ struct BitReader {
         if (n <= 32) {
             buf |= (uint64_t)be(nx) << (32 - n);
             n += 32;
-            nx = w[++wi];
+            w += st;
+            nx = *w;
         }
     }
     __device__ __forceinline__ void skip(int k)
@@ -191,6 +212,7 @@ struct BitReaderC {
         buf <<= (pr & 31);
         n = 64 - (pr & 31);
     }
+    __device__ void reset(const JpegPlan& P, int64_t, int64_t, int64_t bitpos) { reset(P.stream, bitpos); }
     __device__ __forceinline__ int64_t p() const { return base + pr; }
     __device__ __forceinline__ void refill()
     {
@@ -207,7 +229,8 @@ struct BitReaderC {
 // mostly stop within S/8 bits, keep the word reader (1.79 against 1.85 ms of
 // rounds per call with chunks, profiles/r04ad_*)
 template <int CK>
-using SyncReader = typename std::conditional<CK == 1 && WICCA_JPEG_READER != 0, BitReaderC, BitReader>::type;
+using SyncReader = typename std::conditional<CK == 1 && WICCA_JPEG_READER != 0 && !WICCA_JPEG_ILV, BitReaderC,
+                                             BitReader>::type;
 
 // (code length << 8) | symbol of the codeword at the top of `look` (the next
 // 32 bits); a bit string that is no code reads as symbol 0 after 17 bits, as
@@ -683,7 +706,7 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(J
     r.n_ck = 0;
     int32_t dc[kJpegMaxComp] = {0, 0, 0};
     SyncReader<CK> br;
-    br.reset(P.stream, st.p);
+    br.reset(P, i, b0, st.p);
     // checkpoints: two sets per lane (cks, then cks + n_sub * kSyncCk), the
     // one in use named by bit 16 of r0res[i].n_ck (r0res: the result of the
     // decode that recorded them)
@@ -833,7 +856,7 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 4 : 1) void jpeg_write_kernel(
     int32_t dc[kJpegMaxComp] = {b.dc[0], b.dc[1], b.dc[2]};
     int64_t started = 0;
     BitReader br;
-    br.reset(P.stream, st.p);
+    br.reset(P, i, sg.bit0 + j * P.sub_bits, st.p);
 #if WICCA_JPEG_STAGE
     const int w0 = (int)(threadIdx.x & ~63u);  // the wave's first lane
     const WaveStage ws{lanes + w0 * kLaneBlock, s_owner + w0, s_nat};
@@ -1619,6 +1642,74 @@ bool jpeg_fused()
 
 size_t jpeg_jobs_bytes() { return kJpegMaxJobs * sizeof(IdctJob); }
 
+// The lane-interleaved copy (JpegPlan::ilv).  A workgroup takes 64
+// subsequences (one output group) x 32 words: each slot's 128 bytes (plus
+// the alignment) come in as 16-B loads into LDS, and the words leave in output
+// order, 64 consecutive words per row (coalesced both ways; one thread per
+// output word read the stream 512 B apart per lane: 420 us per call).  Word j
+// of subsequence i = stream bytes [b_i + 4j, b_i + 4j + 4), b_i = its first
+// byte (segments start on bytes, S is a multiple of 256 bits); bytes past the
+// stream read as zero; padding lanes' slots are zeros.
+constexpr int kIlvWords = 32, kIlvSlotBytes = 160;  // words per workgroup row block; staged bytes per slot
+
+__global__ __launch_bounds__(256) void jpeg_interleave_kernel(JpegPlan P)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t st[64 * kIlvSlotBytes];
+    __shared__ int64_t sb[64];  // slot's first byte of this block, -1: padding
+    const int64_t g = blockIdx.x;
+    const int jb = (int)blockIdx.y, t = (int)threadIdx.x;
+    if (t < 64) {
+        const int64_t i = g * 64 + t;
+        int64_t b = -1;
+        if (i < P.n_sub && P.sub_seg[i] >= 0) {
+            const JpegSegDev sg = P.segs[P.sub_seg[i]];
+            b = ((sg.bit0 + (i - sg.sub0) * (int64_t)P.sub_bits) >> 3) + 4 * (int64_t)kIlvWords * jb;
+        }
+        sb[t] = b;
+    }
+    __syncthreads();
+    constexpr int kChunks = kIlvSlotBytes / 16;
+    for (int c = t; c < 64 * kChunks; c += 256) {
+        const int l = c / kChunks, q = c - l * kChunks;
+        const int64_t b = sb[l];
+        uint4 v{0, 0, 0, 0};
+        if (b >= 0) {
+            const int64_t a = (b & ~(int64_t)15) + 16 * q;
+            if (a + 16 <= P.stream_bytes) v = *reinterpret_cast<const uint4*>(P.stream + a);
+        }
+        *reinterpret_cast<uint4*>(st + l * kIlvSlotBytes + 16 * q) = v;
+    }
+    __syncthreads();
+    for (int o = t; o < 64 * kIlvWords; o += 256) {
+        const int jj = o >> 6, l = o & 63;
+        const int j = kIlvWords * jb + jj;
+        if (j >= P.ilv_sw) break;  // rows ascend with o
+        const int64_t b = sb[l];
+        uint32_t v = 0;
+        if (b >= 0) {
+            const int off = (int)(b & 15) + 4 * jj;
+            const uint32_t* w = reinterpret_cast<const uint32_t*>(st + l * kIlvSlotBytes + (off & ~3));
+            v = __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(off & 3));
+        }
+        const_cast<uint32_t*>(P.ilv)[((g * P.ilv_sw + j) << 6) + l] = v;
+    }
+}
+
+bool jpeg_ilv_on()
+{
+    static const bool on = [] {
+        const char* e = getenv("WICCA_JPEG_ILV");
+        return WICCA_JPEG_ILV && !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+size_t jpeg_ilv_bytes(int64_t n_sub, int32_t sub_bits)
+{
+    if (!jpeg_ilv_on()) return 0;
+    return (size_t)((n_sub + 63) & ~(int64_t)63) * (size_t)jpeg_ilv_words(sub_bits) * 4;
+}
+
 size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg)
 {
     (void)n_seg;
@@ -1669,6 +1760,11 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     // the device Huffman decode (every image not decoded on the host)
     if (P.n_sub > 0) {
         const uint32_t grid = (uint32_t)((P.n_sub + kJThreads - 1) / kJThreads);
+        if (P.ilv) {
+            const dim3 ig((uint32_t)((P.n_sub + 63) / 64), (uint32_t)((P.ilv_sw + kIlvWords - 1) / kIlvWords));
+            hipLaunchKernelGGL(jpeg_interleave_kernel, ig, dim3(256), 0, s, P);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
         // round 0 (into r0, kept) + rounds until no end state changes; later
         // results rotate through three buffers (older = round - 2, cur =
         // round - 1, nxt = this round).  Every later round stops a lane at the
