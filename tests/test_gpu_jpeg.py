@@ -265,14 +265,15 @@ def test_batch_larger_than_one_device_pass():
 
 
 @pytest.mark.parametrize("env", [{"WICCA_JPEG_WRITE_SLOTS": "6"}, {"WICCA_JPEG_SYNC_CK": "0"},
-                                 {"WICCA_JPEG_SYNC_CK": "1"}],
-                         ids=["slots6", "no-checkpoints", "round0-checkpoints"])
+                                 {"WICCA_JPEG_SYNC_CK": "1"}, {"WICCA_JPEG_ILV": "0"}],
+                         ids=["slots6", "no-checkpoints", "round0-checkpoints", "plain-stream"])
 def test_write_and_sync_variants_subprocess(env):
     """The sync and write passes have 4-table builds (every baseline file) and
     6-table ones (extended-sequential files with separate tables per
     component; WICCA_JPEG_WRITE_SLOTS=6 forces them); the sync passes run with
-    or without checkpoints.  Each variant in a child process on the golden
-    files."""
+    or without checkpoints; every pass reads the lane-interleaved stream copy
+    or (WICCA_JPEG_ILV=0) the plain de-stuffed stream.  Each variant in a child
+    process on the golden files."""
     import subprocess
     import sys
     code = (
