@@ -486,7 +486,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     P.direct_rgb = direct_rgb;
     P.stream = stream_d;
     P.stream_bytes = (int64_t)stream_bytes;
-    P.ilv = ilv_bytes ? (const uint32_t*)ws->jilv.ptr : nullptr;
+    P.ilv = ilv_bytes ? (uint32_t*)ws->jilv.ptr : nullptr;
     P.ilv_sw = wicca::jpeg_ilv_words((int32_t)S);
     P.segs = (const wicca::JpegSegDev*)(m + o_seg);
     P.sub_seg = (const int32_t*)(m + o_sub);

@@ -165,7 +165,7 @@ struct JpegPlan {
     // subsequence i at ilv[((i / 64) * ilv_sw + j) * 64 + i % 64], word 0 the
     // subsequence's first byte (jpeg_interleave_kernel); a wave's refills then
     // read neighbouring words instead of one 128-B line per lane
-    const uint32_t* ilv;
+    uint32_t* ilv;
     int64_t stream_bytes;    // bytes of `stream` (the copy reads none past them)
     int32_t ilv_sw;          // words per slot: sub_bits / 32 + 8
     int32_t abl;             // timing-only ablations of the fused kernel (WICCA_JPEG_ABL bits; 0 in use)

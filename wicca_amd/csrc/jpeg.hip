@@ -1691,7 +1691,7 @@ __global__ __launch_bounds__(256) void jpeg_interleave_kernel(JpegPlan P)
             const uint32_t* w = reinterpret_cast<const uint32_t*>(st + l * kIlvSlotBytes + (off & ~3));
             v = __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(off & 3));
         }
-        const_cast<uint32_t*>(P.ilv)[((g * P.ilv_sw + j) << 6) + l] = v;
+        P.ilv[((g * P.ilv_sw + j) << 6) + l] = v;
     }
 }
 
