@@ -45,6 +45,26 @@ def decode_rgb(data: bytes, apply_orientation: bool = True, truncated: bool = Fa
     return np.asarray(im.convert("RGB")).copy()
 
 
+_FAKE_EOI_TAIL = b"\xff\xd9" * 32769  # covers a 65535-byte marker segment read from the tail
+
+
+def decode_rgb_imread(data: bytes) -> np.ndarray | None:
+    """What ``cv2.imread`` returns for a file's bytes, damaged ones included:
+    OpenCV reads files through libjpeg's stdio source manager, whose
+    ``fill_input_buffer`` (jdatasrc.c) hands the decoder a fake EOI (FF D9)
+    every time the file has no more bytes -- so a file cut inside a marker
+    segment is read on from FF D9 FF D9 ... (mostly a libjpeg error: imread
+    gives None), and a file cut inside entropy-coded data ends at an EOI.
+    Restated by feeding Pillow's libjpeg-turbo the bytes followed by that
+    tail (Pillow's own LOAD_TRUNCATED_IMAGES appends ONE EOI, and a decoder
+    that suspends inside a segment leaves a black image instead).  None where
+    libjpeg refuses the file."""
+    try:
+        return decode_rgb(bytes(data) + _FAKE_EOI_TAIL)
+    except Exception:  # noqa: BLE001 -- libjpeg error_exit: imread returns an empty Mat
+        return None
+
+
 def encode(img: np.ndarray, quality: int = 75, subsampling: int = 2, restart_blocks: int = 0,
            restart_rows: int = 0, optimize: bool = False, progressive: bool = False,
            orientation: int = 1) -> bytes:

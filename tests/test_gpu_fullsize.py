@@ -67,6 +67,63 @@ def test_8k_plane_checksum_all_depths(coder, D):
             assert got == _padded_sum(view, D, border, k), (i, D, border)
 
 
+def _block_icons(imgs, D, border, k):
+    """floor(S / 4^D) per 2^D x 2^D block of the padded images (n, H, W, C),
+    formed with torch on device (int32 sums): an independent restatement of
+    wavelet_coder.py:56-67 for D <= 8."""
+    n, H, W, C = imgs.shape
+    r = 1 << D
+    ar, ac = (-H) % r, (-W) % r
+    x = imgs
+    if ar:
+        pad = x[:, H - 1:H].expand(n, ar, W, C) if border == 1 else torch.full(
+            (n, ar, W, C), k, dtype=torch.uint8, device=x.device)
+        x = torch.cat([x, pad], 1)
+    if ac:
+        pad = x[:, :, W - 1:W].expand(n, x.shape[1], ac, C) if border == 1 else torch.full(
+            (n, x.shape[1], ac, C), k, dtype=torch.uint8, device=x.device)
+        x = torch.cat([x, pad], 2)
+    Hp, Wp = x.shape[1], x.shape[2]
+    s = x.reshape(n, Hp // r, r, Wp // r, r, C).sum((2, 4), dtype=torch.int32)
+    return (s >> (2 * D)).to(torch.uint8)
+
+
+def test_headline_batch_every_image_all_depths(coder):
+    """The exact launch bench.py times (BASELINE.json configs[2]): 128 x
+    7680x4320x3 images synthesised on device with the bench's seed, one
+    wicca_haar_ll_u8_uniform call per depth 1..6 (REPLICATE; CONSTANT 77 at
+    D = 6, where 32 rows are padded).  EVERY image of every launch against
+    torch block sums on device; the first, a middle and the last image at the
+    metric's depth against the C oracle on host-regenerated pixels."""
+    n, H, W, C = 128, 4320, 7680, 3
+    imgs, pitch = _synth_batch(n, H, W, C, 0)  # bench.py: seed 0 * 1000003 + rank 0
+    assert pitch == W * C
+    lib = _lib.load()
+    for D, border, k in [(1, 1, 0), (2, 1, 0), (3, 1, 0), (4, 1, 0), (5, 1, 0), (6, 1, 0), (6, 0, 77)]:
+        r = 1 << D
+        oh, ow = -(-H // r), -(-W // r)
+        op = (ow * C + 15) // 16 * 16
+        out = torch.empty((n, oh, op), dtype=torch.uint8, device="cuda")
+        out.fill_(0xA5)
+        _lib.check(lib.wicca_haar_ll_u8_uniform(
+            ctypes.c_void_p(imgs.data_ptr()), n, H, W, C, pitch, H * pitch, D, border, k,
+            ctypes.c_void_p(out.data_ptr()), op, oh * op, -1, None))
+        torch.cuda.synchronize()
+        for i0 in range(0, n, 16):
+            view = imgs[i0:i0 + 16].view(-1, H, W, C)
+            want = _block_icons(view, D, border, k)
+            got = out[i0:i0 + 16, :, :ow * C].reshape(-1, oh, ow, C)
+            bad = (got != want).flatten(1).any(1)
+            assert not bad.any(), (D, border, [i0 + int(j) for j in torch.nonzero(bad).flatten()])
+        if D == 5:
+            for i in (0, n // 2, n - 1):
+                ref = c_oracle.ll_int_block(synth_image(0, i, H, W, C), D)[0]
+                assert np.array_equal(out[i, :, :ow * C].cpu().numpy().reshape(oh, ow, C), ref), i
+        del out
+    del imgs
+    torch.cuda.empty_cache()
+
+
 def test_4k_batch_uniform_equals_single_and_checksum(coder):
     """configs[1]: 32 x 4K RGB at depth 3, one launch == per-image results."""
     n, H, W, C, D = 32, 2160, 3840, 3, 3

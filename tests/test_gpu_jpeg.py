@@ -474,35 +474,33 @@ DAMAGE = [(kind, sub, rb, prog) for kind, sub, rb, prog in
 @pytest.mark.parametrize("kind,sub,rb,prog", DAMAGE, ids=[f"{k}-s{s}-r{r}-p{int(p)}" for k, s, r, p in DAMAGE])
 @pytest.mark.parametrize("cut", [0.3, 0.5, 0.7, 0.95])
 def test_truncated_file_whole_decode_matches_libjpeg(kind, sub, rb, prog, cut):
-    """cv2.imread returns a truncated JPEG (libjpeg-turbo warns, inserts a fake
-    EOI and finishes the image: missing blocks all-zero, i.e. grey), so the
-    classifiers see every pixel of it (data_loader.py:53-63): the whole decode
-    against libjpeg-turbo's through Pillow with LOAD_TRUNCATED_IMAGES, bit for
-    bit, with and without restart markers, progressive files included."""
+    """cv2.imread returns a truncated JPEG (libjpeg-turbo's stdio source feeds
+    a fake EOI at the end of the file: missing blocks all-zero, i.e. grey;
+    progressive images whose first AC coefficients are not all final are
+    block-smoothed, jdcoefct.c decompress_smooth_data), so the classifiers see
+    every pixel of it (data_loader.py:53-63): the whole decode against
+    libjpeg-turbo's (oracle.jpeg_pil.decode_rgb_imread), bit for bit, with
+    and without restart markers, progressive files included; where libjpeg
+    refuses the cut file (imread: None) the engine fails that slot."""
     img = J.test_image(kind, 200, 344, 17 + sub + rb)
     if kind == "gray":
         img = img[..., 0] if img.ndim == 3 else img
     data = J.encode(img, 88, sub, rb, progressive=prog)
     short = data[:int(len(data) * cut)]
-    want = J.decode_rgb(short, truncated=True)
-    got = WJ.decode(short)
-    if prog and not np.array_equal(got, want):
-        # libjpeg-turbo smooths the blocks of a progressive image whose AC
-        # coefficients are not all final (jdcoefct.c decompress_smooth_data);
-        # the engine decodes the coefficients libjpeg holds (test_jpeg_host.py
-        # re-encodes them and compares) but does not restate the smoothing
-        from test_jpeg_host import host_coefs_as_libjpeg_pixels
-        assert np.array_equal(got, host_coefs_as_libjpeg_pixels(short, img, 88, sub))
-        pytest.skip("truncated progressive file: libjpeg's block smoothing (parity unpinned)")
-    assert np.array_equal(got, want)
+    want = J.decode_rgb_imread(short)
+    got = WJ.decode_batch([short], errors="none")[0]
+    if want is None:
+        assert got is None
+    else:
+        assert got is not None and np.array_equal(got, want)
 
 
 @pytest.mark.parametrize("seed", range(6))
 def test_corrupted_entropy_whole_decode_matches_libjpeg(seed):
     """Bytes flipped inside the entropy-coded data (markers untouched):
     libjpeg-turbo decodes on (a bad Huffman code decodes as a zero symbol,
-    jdhuff.c), so does cv2.imread; the whole image against Pillow's decode.
-    Where Pillow itself refuses the file the case is skipped (parity unpinned)."""
+    jdhuff.c), so does cv2.imread; the whole image against libjpeg's decode,
+    and where libjpeg refuses the file the engine fails its slot."""
     rng = np.random.default_rng(100 + seed)
     kind = ("scene", "noise", "smooth")[seed % 3]
     img = J.test_image(kind, 160, 232, seed)
@@ -514,11 +512,12 @@ def test_corrupted_entropy_whole_decode_matches_libjpeg(seed):
             nv = data[pos] ^ int(rng.integers(1, 255))
             if nv != 0xFF:
                 data[pos] = nv
-    try:
-        want = J.decode_rgb(bytes(data), truncated=True)
-    except Exception as e:  # noqa: BLE001 — Pillow refuses: nothing to pin against
-        pytest.skip(f"Pillow refuses this file ({e}): parity unpinned")
-    assert np.array_equal(WJ.decode(bytes(data)), want)
+    want = J.decode_rgb_imread(bytes(data))
+    got = WJ.decode_batch([bytes(data)], errors="none")[0]
+    if want is None:
+        assert got is None
+    else:
+        assert got is not None and np.array_equal(got, want)
 
 
 def _rst_damaged(how):

@@ -380,7 +380,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
                 im.comp_plane0[c] = plane_bytes;
                 plane_bytes += round_up((int64_t)k.bw * 8 * k.bh * 8, 256);
             }
-            memcpy(im.qt[c], f.qt[k.tq], sizeof(im.qt[c]));
+            memcpy(im.qt[c], k.q, sizeof(im.qt[c]));
         }
         im.fmt = wicca::kJpegFmtOther;  // the fused kernel's chroma path
         if (f.ncomp == 1) {

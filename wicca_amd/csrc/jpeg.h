@@ -34,6 +34,10 @@ struct JpegComponent {
     int id, h, v, tq, td, ta;
     int bw, bh;          // blocks per row / column (padded to whole MCUs)
     int dw, dh;          // downsampled (real) sample width / height
+    // quantisation table latched at the component's first scan (jdinput.c
+    // latch_quant_tables: a DQT between scans does not change it), natural order
+    uint16_t q[64];
+    bool latched;
 };
 
 // One scan of a multi-scan file (progressive, or sequential with a scan per

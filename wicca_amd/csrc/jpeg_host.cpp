@@ -108,11 +108,19 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
     size_t pos = 2;
     bool have_sof = false;
     int scan_ids[kJpegMaxComp] = {0, 1, 2};
+    for (int c = 0; c < kJpegMaxComp; ++c) info->comp[c].latched = false;
+    // A file cut inside a marker segment after its first scan: cv2.imread
+    // reads through libjpeg's stdio source manager, which feeds a fake EOI
+    // (FF D9) each time the file has no more bytes (jdatasrc.c
+    // fill_input_buffer), so the segment is read on from FF D9 FF D9 ...
+    // (a table index of 0xFF, a scan of 255 components: mostly an error,
+    // i.e. no image) and the marker after it is an EOI.
+    std::vector<uint8_t> fake;
     for (;;) {
         while (pos < n && d[pos] != 0xFF) ++pos;  // tolerate garbage between segments
         while (pos < n && d[pos] == 0xFF) ++pos;  // fill bytes
         if (pos >= n) {
-            if (info->host_scans && !info->scans.empty()) break;  // truncated after a scan: decode what is there
+            if (info->host_scans && !info->scans.empty()) break;  // truncated after a scan: the fake EOI
             return bad(-1, "truncated JPEG (no SOS)");
         }
         const int m = d[pos++];
@@ -121,18 +129,19 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
             if (info->host_scans && !info->scans.empty()) break;  // EOI after the last scan
             return bad(-1, "EOI before SOS");
         }
-        if (pos + 2 > n) {
-            if (info->host_scans && !info->scans.empty()) break;
-            return bad(-1, "truncated marker segment");
+        const uint8_t* seg = d + pos;  // length field and payload
+        const bool cut = pos + 2 > n || pos + (size_t)u16be(d + pos) > n;
+        if (cut) {
+            if (!(info->host_scans && !info->scans.empty())) return bad(-1, "truncated marker segment");
+            fake.assign(d + pos, d + n);
+            for (size_t i = n; fake.size() < 65537; ++i) fake.push_back(((i - n) & 1) ? 0xD9 : 0xFF);
+            seg = fake.data();
         }
-        const int len = u16be(d + pos);
-        if (len < 2 || pos + (size_t)len > n) {
-            if (info->host_scans && !info->scans.empty()) break;
-            return bad(-1, "truncated marker segment");
-        }
-        const uint8_t* s = d + pos + 2;
+        const int len = u16be(seg);
+        if (len < 2) return bad(-1, "bad marker segment length");
+        const uint8_t* s = seg + 2;
         const int sl = len - 2;
-        pos += (size_t)len;
+        pos = cut ? n : pos + (size_t)len;
         if (m == 0xC0 || m == 0xC1 || m == 0xC2) {  // baseline / extended sequential / progressive, Huffman
             if (have_sof) return bad(-1, "duplicate SOF");
             if (sl < 6) return bad(-1, "bad SOF");
@@ -214,6 +223,13 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
                 info->comp[c].td = td;
                 info->comp[c].ta = ta;
             }
+            for (int i = 0; i < ns; ++i) {
+                JpegComponent& k = info->comp[sc.comp[i]];
+                if (k.latched) continue;
+                if (!info->qt_present[k.tq]) return bad(-1, "missing quantisation table");
+                memcpy(k.q, info->qt[k.tq], sizeof(k.q));
+                k.latched = true;
+            }
             sc.Ss = s[1 + 2 * ns];
             sc.Se = s[2 + 2 * ns];
             sc.Ah = s[3 + 2 * ns] >> 4;
@@ -276,6 +292,8 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
         for (int c = 0; c < info->ncomp; ++c)
             if (!info->qt_present[info->comp[c].tq]) return bad(-1, "missing quantisation table");
     }
+    for (int c = 0; c < info->ncomp; ++c)  // a component no scan reached: its data is all zero anyway
+        if (!info->comp[c].latched) memcpy(info->comp[c].q, info->qt[info->comp[c].tq], sizeof(info->comp[c].q));
     // geometry
     if (info->ncomp == 1) {
         JpegComponent& k = info->comp[0];
@@ -633,15 +651,178 @@ int host_huff(const HuffDev& t, HostBits& br)
 
 inline int host_extend(uint32_t v, int s) { return (int)v < (1 << (s - 1)) ? (int)v - (1 << s) + 1 : (int)v; }
 
+// ---------------------------------------------------------------------------
+// Interblock smoothing of a progressive image whose low AC coefficients are
+// not all final (libjpeg-turbo >= 2.1 jdcoefct.c smoothing_ok /
+// decompress_smooth_data, on by default: do_block_smoothing, which cv2.imread
+// and Pillow leave set).  Third-party algorithm restated from its published
+// behaviour; pinned against libjpeg-turbo 3.1.4.1 (Pillow) on truncated
+// progressive files (tests/test_jpeg_smooth.py).
+//
+// The first nine AC coefficients (zigzag 1..9) of a block that are still zero
+// and not known to full precision are estimated from the quantised DC values
+// of the block's 5 x 5 neighbourhood (edges replicated); when no AC data at
+// all has arrived for the component ("change_dc") a Gaussian-like 5 x 5
+// kernel also replaces the DC.  Which progression state applies is chosen per
+// iMCU row: rows past the last one decoded with data in the final pass use
+// the component's state from before its latest scan.
+// ---------------------------------------------------------------------------
+
+// Kernels: estimate k (1..9 = zigzag position, 0 = the DC) = sum of weight x DC
+// over rows -2..2, columns -2..2 of the neighbourhood.
+struct SmoothKernel {
+    int16_t w[5][5];
+};
+// change_dc == false (some AC data present): 5-tap K.8-style gradients
+constexpr SmoothKernel kSmoothAc[6] = {
+    {},
+    {{{0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}, {-7, 50, 0, -50, 7}, {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}}},       // (0,1)
+    {{{0, 0, -7, 0, 0}, {0, 0, 50, 0, 0}, {0, 0, 0, 0, 0}, {0, 0, -50, 0, 0}, {0, 0, 7, 0, 0}}},       // (1,0)
+    {{{0, 0, -1, 0, 0}, {0, 0, 13, 0, 0}, {0, 0, -24, 0, 0}, {0, 0, 13, 0, 0}, {0, 0, -1, 0, 0}}},     // (2,0)
+    {{{0, -1, 0, 1, 0}, {-1, 10, 0, -10, 1}, {0, 0, 0, 0, 0}, {1, -10, 0, 10, -1}, {0, 1, 0, -1, 0}}}, // (1,1)
+    {{{0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}, {-1, 13, -24, 13, -1}, {0, 0, 0, 0, 0}, {0, 0, 0, 0, 0}}},     // (0,2)
+};
+// change_dc == true (DC only): the nine AC estimates and the new DC
+constexpr SmoothKernel kSmoothDc[10] = {
+    {{{-2, -6, -8, -6, -2}, {-6, 6, 42, 6, -6}, {-8, 42, 152, 42, -8}, {-6, 6, 42, 6, -6}, {-2, -6, -8, -6, -2}}},
+    {{{-1, -1, 0, 1, 1}, {-3, 13, 0, -13, 3}, {-3, 38, 0, -38, 3}, {-3, 13, 0, -13, 3}, {-1, -1, 0, 1, 1}}},
+    {{{-1, -3, -3, -3, -1}, {-1, 13, 38, 13, -1}, {0, 0, 0, 0, 0}, {1, -13, -38, -13, 1}, {1, 3, 3, 3, 1}}},
+    {{{0, 0, 1, 0, 0}, {0, 2, 7, 2, 0}, {0, -5, -14, -5, 0}, {0, 2, 7, 2, 0}, {0, 0, 1, 0, 0}}},
+    {{{-1, 0, 0, 0, 1}, {0, 9, 0, -9, 0}, {0, 0, 0, 0, 0}, {0, -9, 0, 9, 0}, {1, 0, 0, 0, -1}}},
+    {{{0, 0, 0, 0, 0}, {0, 2, -5, 2, 0}, {1, 7, -14, 7, 1}, {0, 2, -5, 2, 0}, {0, 0, 0, 0, 0}}},
+    {{{0, 0, 0, 0, 0}, {0, 1, 0, -1, 0}, {0, 2, 0, -2, 0}, {0, 1, 0, -1, 0}, {0, 0, 0, 0, 0}}},
+    {{{0, 0, 0, 0, 0}, {0, 1, -3, 1, 0}, {0, 0, 0, 0, 0}, {0, -1, 3, -1, 0}, {0, 0, 0, 0, 0}}},
+    {{{0, 0, 0, 0, 0}, {0, 1, 0, -1, 0}, {0, -3, 0, 3, 0}, {0, 1, 0, -1, 0}, {0, 0, 0, 0, 0}}},
+    {{{0, 0, 0, 0, 0}, {0, 1, 2, 1, 0}, {0, 0, 0, 0, 0}, {0, -1, -2, -1, 0}, {0, 0, 0, 0, 0}}},
+};
+// natural-order position of zigzag coefficient k = 0..9
+constexpr int kSmoothPos[10] = {0, 1, 8, 16, 9, 2, 3, 10, 17, 24};
+constexpr int kSmoothSaved = 10;
+
+// Progression status (jdphuff.c start_pass_phuff_decoder): coef_bits[c][k] =
+// the Al of the latest scan that carried coefficient k of component c (-1:
+// none yet); prev[c][k] = the same as it stood before component c's latest
+// scan; last_good = the last iMCU row that ended with data left (any pass).
+struct SmoothState {
+    int coef_bits[kJpegMaxComp][64];
+    int prev[kJpegMaxComp][64];
+    int scans = 0;
+    int64_t last_good = 0;
+    SmoothState()
+    {
+        for (auto& r : coef_bits)
+            for (int& x : r) x = -1;
+        for (auto& r : prev)
+            for (int& x : r) x = -1;
+    }
+    void start_scan(const JpegScan& sc)
+    {
+        ++scans;
+        for (int i = 0; i < sc.ns; ++i) {
+            const int c = sc.comp[i];
+            for (int k = std::min(sc.Ss, 1); k <= std::max(sc.Se, 9); ++k)
+                prev[c][k] = scans > 1 ? coef_bits[c][k] : 0;
+            for (int k = sc.Ss; k <= sc.Se; ++k) coef_bits[c][k] = sc.Al;
+        }
+    }
+};
+
+int64_t smooth_estimate(const SmoothKernel& K, const int* dc5)
+{
+    int64_t s = 0;
+    for (int r = 0; r < 5; ++r)
+        for (int c = 0; c < 5; ++c) s += (int64_t)K.w[r][c] * dc5[r * 5 + c];
+    return s;
+}
+
+// jdcoefct.c: pred = round(num / (Q << 8)) away from zero's half, clamped
+// below 2^Al when Al low bits are still unknown
+int smooth_pred(int64_t num, int64_t q, int al)
+{
+    const bool neg = num < 0;
+    int64_t p = ((q << 7) + (neg ? -num : num)) / (q << 8);
+    if (al > 0 && p >= (1 << al)) p = (1 << al) - 1;
+    return (int)(neg ? -p : p);
+}
+
+void block_smooth(const JpegInfo& info, const SmoothState& st, int16_t* coef, const int64_t* comp_block0)
+{
+    // smoothing_ok: every component's quantisers at the ten positions nonzero,
+    // its DC at least partly known; useful if any AC 1..9 is not final
+    bool useful = false;
+    for (int c = 0; c < info.ncomp; ++c) {
+        const uint16_t* q = info.comp[c].q;
+        for (int k = 0; k < kSmoothSaved; ++k)
+            if (q[kSmoothPos[k]] == 0) return;
+        if (st.coef_bits[c][0] < 0) return;
+        for (int k = 1; k < kSmoothSaved; ++k)
+            if (st.coef_bits[c][k] != 0) useful = true;
+    }
+    if (!useful) return;
+    const int64_t T = info.mcuy;  // total iMCU rows
+    std::vector<int> dc;
+    for (int c = 0; c < info.ncomp; ++c) {
+        const JpegComponent& k = info.comp[c];
+        const int64_t bw = k.bw, bh = k.bh, v = k.v;
+        const int64_t wib = (k.dw + 7) / 8, hib = (k.dh + 7) / 8;
+        int16_t* base = coef + comp_block0[c] * 64;
+        dc.resize((size_t)(bw * bh));
+        for (int64_t i = 0; i < bw * bh; ++i) dc[(size_t)i] = base[i * 64];  // the unsmoothed DCs
+        const uint16_t* qt = k.q;
+        int latch[2][kSmoothSaved];  // [0] current, [1] before the latest scan
+        for (int j = 0; j < kSmoothSaved; ++j) {
+            latch[0][j] = st.coef_bits[c][j];
+            latch[1][j] = st.scans > 1 ? st.prev[c][j] : -1;
+        }
+        const int64_t Q00 = qt[0];
+        for (int64_t R = 0; R < T; ++R) {
+            const int64_t block_rows = R < T - 1 ? v : (hib % v ? hib % v : v);
+            const int* bits = latch[R > st.last_good ? 1 : 0];
+            bool change_dc = true;
+            for (int j = 1; j < kSmoothSaved; ++j) change_dc = change_dc && bits[j] == -1;
+            const int64_t image_block_rows = block_rows * T;
+            for (int64_t r = 0; r < block_rows; ++r) {
+                const int64_t y = R * v + r, ibr = R * block_rows + r;
+                int64_t rows[5];
+                rows[2] = y;
+                rows[1] = ibr > 0 ? y - 1 : y;
+                rows[0] = ibr > 1 ? y - 2 : rows[1];
+                rows[3] = ibr < image_block_rows - 1 ? y + 1 : y;
+                rows[4] = ibr < image_block_rows - 2 ? y + 2 : rows[3];
+                for (int64_t b = 0; b < wib; ++b) {
+                    int dc5[25];
+                    for (int i = 0; i < 5; ++i)
+                        for (int j = 0; j < 5; ++j) {
+                            const int64_t x = std::min(std::max(b + j - 2, (int64_t)0), wib - 1);
+                            dc5[i * 5 + j] = dc[(size_t)(rows[i] * bw + x)];
+                        }
+                    int16_t* blk = base + (y * bw + b) * 64;
+                    const int nest = change_dc ? 9 : 5;
+                    for (int j = 1; j <= nest; ++j) {
+                        const int pos = kSmoothPos[j];
+                        const int al = bits[j];
+                        if (al == 0 || blk[pos] != 0) continue;
+                        const int64_t num = Q00 * smooth_estimate(change_dc ? kSmoothDc[j] : kSmoothAc[j], dc5);
+                        blk[pos] = (int16_t)smooth_pred(num, qt[pos], al);
+                    }
+                    if (change_dc) blk[0] = (int16_t)smooth_pred(Q00 * smooth_estimate(kSmoothDc[0], dc5), Q00, 0);
+                }
+            }
+        }
+    }
+}
+
 }  // namespace
 
 void jpeg_host_decode(const JpegInfo& info, int16_t* coef, const int64_t* comp_block0)
 {
     HostBits br;
     std::vector<HuffDev> dct(kJpegMaxComp), act(kJpegMaxComp);
+    SmoothState smooth;
     for (const JpegScan& sc : info.scans) {
         const bool prog = info.progressive;
         const bool dc_scan = sc.Ss == 0, first = sc.Ah == 0;
+        if (prog) smooth.start_scan(sc);
         for (int i = 0; i < sc.ns; ++i) {
             if (!prog || (dc_scan && first)) build_huff_dev(sc.dc[i], &dct[(size_t)i]);
             if (!prog || !dc_scan) build_huff_dev(sc.ac[i], &act[(size_t)i]);
@@ -757,10 +938,11 @@ void jpeg_host_decode(const JpegInfo& info, int16_t* coef, const int64_t* comp_b
             }
         };
         if (sc.ns > 1) {  // interleaved: MCUs of the frame
-            for (int64_t my = 0; my < info.mcuy; ++my)
+            for (int64_t my = 0; my < info.mcuy; ++my) {
                 for (int64_t mx = 0; mx < info.mcux; ++mx) {
                     before_mcu();
                     if (br.insufficient) continue;  // jdhuff / jdphuff: MCUs past the data are skipped
+                    smooth.last_good = my;
                     for (int i = 0; i < sc.ns; ++i) {
                         const JpegComponent& k = info.comp[sc.comp[i]];
                         for (int v = 0; v < k.v; ++v)
@@ -768,18 +950,22 @@ void jpeg_host_decode(const JpegInfo& info, int16_t* coef, const int64_t* comp_b
                                 decode_block(i, block_of(sc.comp[i], mx * k.h + h, my * k.v + v));
                     }
                 }
-        } else {  // one component: its own blocks, one per MCU
+            }
+        } else {  // one component: its own blocks, one per MCU; v block rows per iMCU row
             const int c = sc.comp[0];
             const JpegComponent& k = info.comp[c];
             const int64_t wb = (k.dw + 7) / 8, hb = (k.dh + 7) / 8;
-            for (int64_t by = 0; by < hb; ++by)
+            for (int64_t by = 0; by < hb; ++by) {
                 for (int64_t bx = 0; bx < wb; ++bx) {
                     before_mcu();
                     if (br.insufficient) continue;
+                    smooth.last_good = by / k.v;
                     decode_block(0, block_of(c, bx, by));
                 }
+            }
         }
     }
+    if (info.progressive) block_smooth(info, smooth, coef, comp_block0);
 }
 
 }  // namespace wicca
