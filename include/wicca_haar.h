@@ -286,6 +286,11 @@ int wicca_jpeg_decode_u8(const uint8_t* const* data, const int64_t* sizes, int64
 /* Synchronisation passes of the calling thread's last JPEG decode (diagnostic). */
 int wicca_jpeg_last_sync_rounds(void);
 
+/* Files (all threads, since load) that the device Huffman passes flagged as
+ * damaged and the host entropy decoder redid (diagnostic: a clean file never
+ * counts). */
+int64_t wicca_jpeg_damaged_redone(void);
+
 /* wicca_jpeg_decode_u8 into DEVICE buffers without waiting for the device: it
  * returns once the host's part is done (parse, de-stuffing, uploads issued,
  * kernels queued on a stream of its own) with *ticket set; the images are

@@ -15,6 +15,7 @@ import wicca_amd
 from oracle import c_oracle
 from oracle import jpeg_pil as J
 from oracle import resize_cv as R
+from wicca_amd import _lib
 from wicca_amd import jpeg as WJ
 
 pytestmark = pytest.mark.gpu
@@ -568,3 +569,46 @@ def test_damaged_restart_markers_batch_matches_libjpeg(tmp_path):
         assert np.array_equal(icons[i], R.resize(c_oracle.ll_int_block(rgb, 3)[0], (224, 224), R.INTER_AREA)), i
     m = wicca_amd.get_img_matrix(paths, [(224, 224)], (3, 4))
     assert np.array_equal(m[((224, 224), 3)][0], imgs) and np.array_equal(m[((224, 224), 3)][1], icons)
+
+
+def _low_entropy_files():
+    """Pillow optimize=True on flat / low-entropy content: Huffman tables with
+    one or two codes (a flat image's DC table has the single code '0'), with and
+    without restart intervals, colour and grayscale."""
+    flat = np.full((64, 96, 3), 128, np.uint8)
+    grad = np.tile(np.arange(200, dtype=np.uint8)[None, :, None], (120, 1, 3))
+    step = np.zeros((72, 72, 3), np.uint8)
+    step[:, 36:] = 255
+    out = []
+    for img in (flat, grad, step):
+        for rb in (0, 1, 3):
+            out.append(J.encode(img, 90, 2, rb, optimize=True))
+            out.append(J.encode(img[..., 0].copy(), 75, 0, rb, optimize=True))
+    return out
+
+
+def test_clean_low_entropy_files_are_not_flagged_damaged(tmp_path):
+    """the write pass's last lane of a segment used to decode the
+    encoder's fill bits after the final MCU; with a single-code DC table they
+    match no code, so a clean file was flagged damaged and redone on the host
+    (a silent throughput cliff).  Every path decodes these exactly and redoes
+    none of them (wicca_jpeg_damaged_redone does not move)."""
+    lib = _lib.load()
+    blobs = _low_entropy_files()
+    want = [J.decode_rgb(b) for b in blobs]
+    before = lib.wicca_jpeg_damaged_redone()
+    got = WJ.decode_batch(blobs)
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert np.array_equal(g, w), i
+    for i, g in enumerate(x for batch in WJ.decode_batches([blobs[:9], blobs[9:]]) for x in batch):
+        assert np.array_equal(g.cpu().numpy(), want[i]), i
+    paths = []
+    for i, b in enumerate(blobs):
+        p = tmp_path / f"{i}.jpg"
+        p.write_bytes(b)
+        paths.append(str(p))
+    imgs, _ = wicca_amd.get_img_batch(paths, (224, 224), 3)
+    for i, w in enumerate(want):
+        assert np.array_equal(imgs[i], R.resize(w, (224, 224), R.INTER_AREA)), i
+    list(wicca_amd.get_img_batches([paths[:9], paths[9:]], (224, 224), 3))
+    assert lib.wicca_jpeg_damaged_redone() == before

@@ -404,10 +404,13 @@ def test_rle_bmp_vs_pillow(rle4):
     assert np.array_equal(got[-1], rr.decode_bmp(plain))
 
 
-def test_rle_bmp_opencv_rules():
-    """Where Pillow refuses: end of bitmap before the last row (OpenCV fills the
-    rest with palette entry 0; parity unpinned, restated from OpenCV's
-    BmpDecoder), and a run past a row's end, which fails the file's slot."""
+def test_rle_bmp_corrupt_rules():
+    """Corrupt or unusual RLE data, PARITY UNPINNED (cv2 absent; restated from
+    OpenCV's BmpDecoder, where Pillow refuses or clips): end of bitmap before
+    the last row (the rest takes palette entry 0), a run past a row's end
+    (fails the file's slot; Pillow clips it), and a delta past the bottom row
+    (ends the bitmap: the rows it skips take palette entry 0).  Pinned here so
+    that a change of these rules is deliberate."""
     rng = np.random.default_rng(5)
     pal = rng.integers(0, 256, (256, 3)).astype(np.uint8)
     idx = rng.integers(0, 256, (20, 33)).astype(np.uint8)
@@ -418,6 +421,13 @@ def test_rle_bmp_opencv_rules():
     over = good[:hdr] + bytes([200, 9]) + good[hdr:]  # a 200-pixel run in a 33-pixel row
     got = WJ.decode_batch([over, good], errors="none")
     assert got[0] is None and np.array_equal(got[1], pal[idx])
+    # a delta escape of 50 rows after the first stored row (the bottom one)
+    runs, _ = rr.encode_bmp_rle(idx, pal, False, False)  # encoded runs only: the first 00 00 is an end of line
+    first_eol = next(i for i in range(hdr, len(runs) - 1, 2) if runs[i] == 0 and runs[i + 1] == 0)
+    deep = runs[:first_eol + 2] + bytes([0, 2, 0, 50]) + runs[first_eol + 2:]
+    want = np.zeros_like(idx)
+    want[-1] = idx[-1]
+    assert np.array_equal(WJ.decode(deep), pal[want])
 
 
 def test_pnm_vs_pillow(tmp_path, capsys):

@@ -15,17 +15,20 @@ from wicca_amd import plan as P
 
 
 class FakeMatrix:
-    def __init__(self, delay=0.0, fail_on=None):
+    def __init__(self, delay=0.0, fail_on=None, fail_times=None):
         self.calls = []
         self.delay = delay
         self.fail_on = fail_on
+        self.fail_times = fail_times  # None: always
         self.lock = threading.Lock()
 
     def __call__(self, paths, shapes, depths, interp, border, k, device, errors):
         with self.lock:
-            self.calls.append((tuple(paths), device))
+            self.calls.append((tuple(paths), device, tuple(depths)))
+            fail = self.fail_on is not None and self.fail_on in paths and (
+                self.fail_times is None or sum(self.fail_on in c[0] for c in self.calls) <= self.fail_times)
         time.sleep(self.delay)
-        if self.fail_on is not None and self.fail_on in paths:
+        if fail:
             raise ValueError("image 0: corrupt")
         n = len(paths)
         out = {}
@@ -84,11 +87,15 @@ def test_byte_cap_evicts_and_recomputes():
     assert plan.stats["evicted"] >= 1
 
 
-def test_failure_is_shared_by_every_requester():
-    plan, fake = _plan([(224, 224)] * 3, (2, 3), fake=FakeMatrix(delay=0.02, fail_on="/bad.jpg"))
+def test_failure_is_shared_by_waiting_requesters():
+    """The requesters waiting on a batch when its computation fails all see
+    that failure (one computation); the failure is not cached."""
+    plan, fake = _plan([(224, 224)] * 3, (2, 3), fake=FakeMatrix(delay=0.3, fail_on="/bad.jpg"))
     errs = []
+    go = threading.Barrier(6)
 
     def req():
+        go.wait()
         try:
             plan.get_img_batch(["/ok.jpg", "/bad.jpg"], (224, 224), 2)
         except ValueError as e:
@@ -99,6 +106,76 @@ def test_failure_is_shared_by_every_requester():
     for t in ts:
         t.join()
     assert len(errs) == 6 and len(fake.calls) == 1
+    assert plan.cached_batches() == 0
+
+
+def test_transient_failure_is_retried():
+    """a transient failure (e.g. a device OOM in the background
+    batch) is shared only with the requesters already waiting; the next
+    request computes the batch again and succeeds -- including a failure in
+    the prefetch thread, which the foreground then recomputes."""
+    plan, fake = _plan([(224, 224)] * 2, (2,), fake=FakeMatrix(fail_on="/t.jpg", fail_times=1))
+    with pytest.raises(ValueError):
+        plan.get_img_batch(["/t.jpg"], (224, 224), 2)
+    imgs, _ = plan.get_img_batch(["/t.jpg"], (224, 224), 2)
+    assert imgs.shape == (1, 224, 224, 3) and len(fake.calls) == 2
+    batches = [["/a.jpg"], ["/t.jpg"]]
+    plan, fake = _plan([(224, 224)], (2,), batches=batches, fake=FakeMatrix(fail_on="/t.jpg", fail_times=1))
+    plan.get_img_batch(batches[0], (224, 224), 2)  # starts /t.jpg in the background: it fails
+    plan._prefetch.join()
+    imgs, _ = plan.get_img_batch(batches[1], (224, 224), 2)
+    assert imgs.shape == (1, 224, 224, 3)
+    assert [c[0] for c in fake.calls] == [("/a.jpg",), ("/t.jpg",), ("/t.jpg",)]
+    assert plan.stats["failed"] == 1
+
+
+def _run_reference_loop(plan, classifiers, depths, batches):
+    """process_classifiers: depths outermost, a pool of classifier tasks per
+    depth, each walking the folder's batches (classifying_tools.py:546-551,
+    :414-419, :339-346)."""
+    for d in depths:
+        def classify(shape):
+            for b in batches:
+                imgs, icons = plan.get_img_batch(b, shape, d)
+                assert imgs.shape == (len(b), shape[1], shape[0], 3) and (icons == d).all()
+        with concurrent.futures.ThreadPoolExecutor(max_workers=len(classifiers)) as ex:
+            list(ex.map(classify, classifiers))
+
+
+@pytest.mark.parametrize("known", [True, False])
+def test_folder_larger_than_the_cache_runs_per_depth(known):
+    """a folder whose outputs for all depths exceed cache_bytes.
+    Keeping every depth of every batch until the last depth (the cyclic access
+    of the depth loop) would evict exactly the batch the next depth starts with
+    and recompute every batch at every depth for all depths.  The plan computes
+    per (batch, depth) instead: each batch once per depth -- one decode for all
+    14 classifiers -- with no more host memory than a few batches of one depth."""
+    depths = (2, 3, 4, 5, 6)
+    batches = [[f"/f/{i}_{j}.jpg" for j in range(3)] for i in range(12)]
+    per_batch_all = 3 * sum(w * h * 3 for (w, h) in set(CLASSIFIERS)) * (1 + len(depths))
+    cap = 4 * per_batch_all  # a third of the folder
+    plan, fake = _plan(CLASSIFIERS, depths, batches=batches if known else None, cache_bytes=cap)
+    assert plan.per_depth == known
+    _run_reference_loop(plan, CLASSIFIERS, depths, batches)
+    plan.close()
+    n = len(batches) * len(depths)
+    if known:
+        assert len(fake.calls) == n and all(len(c[2]) == 1 for c in fake.calls)
+        assert plan.stats["evicted"] == 0
+    else:  # found out at the first eviction: at most the batches computed before it were wasted
+        assert plan.per_depth
+        assert len(fake.calls) <= n + len(batches)
+    assert plan.cached_batches() == 0
+
+
+def test_folder_that_fits_computes_every_depth_at_once():
+    depths = (2, 3)
+    batches = [[f"/g/{i}.jpg"] for i in range(4)]
+    plan, fake = _plan(CLASSIFIERS, depths, batches=batches, cache_bytes=1 << 40)
+    assert not plan.per_depth
+    _run_reference_loop(plan, CLASSIFIERS, depths, batches)
+    plan.close()
+    assert len(fake.calls) == len(batches) and all(c[2] == depths for c in fake.calls)
 
 
 def test_unplanned_pair_uses_the_per_call_stage(monkeypatch):
@@ -118,6 +195,10 @@ def test_devices_round_robin_over_batches():
         plan.get_img_batch(b, (224, 224), 2)
     plan.close()
     assert {c[0][0]: c[1] for c in fake.calls} == {"/0.jpg": 0, "/1.jpg": 1, "/2.jpg": 0, "/3.jpg": 1}
+
+
+def test_default_cache_is_bounded():
+    assert 0 < P._default_cache_bytes() <= 32 << 30
 
 
 def test_depth_forms_and_validation():

@@ -79,6 +79,7 @@ SIGNATURES = {
     "wicca_jpeg_decode_u8": (_int, [ctypes.POINTER(_p), ctypes.POINTER(_i64), _i64, ctypes.POINTER(_p),
                                     ctypes.POINTER(_i64), _int, _int, _int, _p, ctypes.POINTER(_int)]),
     "wicca_jpeg_last_sync_rounds": (_int, []),
+    "wicca_jpeg_damaged_redone": (ctypes.c_int64, []),
     "wicca_jpeg_decode_u8_async": (_int, [ctypes.POINTER(_p), ctypes.POINTER(_i64), _i64, ctypes.POINTER(_p),
                                           ctypes.POINTER(_i64), _int, _int, ctypes.POINTER(_i64)]),
     "wicca_jpeg_wait": (_int, [_i64]),

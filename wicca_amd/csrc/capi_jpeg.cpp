@@ -216,6 +216,10 @@ void make_host_scan(wicca::JpegInfo& f)
 // libjpeg-turbo's rules for damaged data (a code no table has, runs past
 // coefficient 63, data that ends inside an MCU: that MCU decoded on from zero
 // bits, the rest of the segment grey).
+// Files the device passes flagged damaged and the host decoder redid, since
+// the library loaded (all threads): wicca_jpeg_damaged_redone().
+static std::atomic<int64_t> g_jpeg_redone{0};
+
 int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
                           uint8_t* const* dst, const int64_t* dpitch, bool orient, hipStream_t stream,
                           int* rounds_out, int async_rounds = 0, const int** async_flags = nullptr,
@@ -553,6 +557,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
                 ro.push_back(dst[i]);
                 rp.push_back(dpitch[i]);
             }
+        g_jpeg_redone += (int64_t)rd.size();
         if (jpeg_timing())
             fprintf(stderr, "[wicca jpeg] %zu of %lld files damaged: redone on the host\n", rd.size(), (long long)n);
         if (!rd.empty()) {
@@ -952,6 +957,7 @@ int wicca_jpeg_wait(int64_t ticket)
                 ro.push_back(st->dsts[(size_t)i]);
                 rp.push_back(st->pitches[(size_t)i]);
             }
+        g_jpeg_redone += (int64_t)rd.size();
         if (!rd.empty()) {
             int rounds = 0;
             if ((rc = jpeg_decode_to_device(st->lease.ws, rd.data(), rs.data(), (int64_t)rd.size(), ro.data(),
@@ -1081,6 +1087,8 @@ int wicca_image_info(const uint8_t* data, int64_t size, int apply_orientation, i
 }
 
 int wicca_jpeg_last_sync_rounds(void) { return t_jpeg_rounds; }
+
+int64_t wicca_jpeg_damaged_redone(void) { return g_jpeg_redone.load(); }
 
 int wicca_jpeg_host_coefficients(const uint8_t* data, int64_t size, int force_host, int16_t* out, int64_t cap_blocks,
                                  int64_t* blocks)
@@ -1431,6 +1439,7 @@ int wicca_image_stage_wait(int64_t ticket)
         HIP_TRY(hipMemcpyAsync(dmg.data(), st->damage, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost,
                                st->stream));
         HIP_TRY(hipStreamSynchronize(st->stream));
+        for (int64_t i = 0; i < n; ++i) g_jpeg_redone += dmg[(size_t)i] != 0;
         for (int64_t i = 0; i < n && converged; ++i) converged = dmg[(size_t)i] == 0;
     }
     if (!converged) {  // rare: the whole stage again, synchronously, with the host looking at every round

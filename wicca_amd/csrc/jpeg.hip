@@ -449,6 +449,11 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
     const int32_t ck_off = (int32_t)(br.base - ck_base);  // reader-relative -> checkpoint-relative
     int32_t nstart = 0;  // blocks started in this run
     while (br.pr < stop_r) {
+        // the segment's last block is complete: the bits left are the encoder's
+        // fill (1-bits up to the byte boundary), which libjpeg never decodes
+        // (a single-code table, e.g. optimize=True on flat content, reads them
+        // as a code no table has)
+        if (WRITE && seg_last && st.k == 0 && g >= block_end - 1) break;
         if (REC && st.k == 0 && nrec < kSyncCk && br.pr + ck_off >= nrec * ck_step) {
             SyncCk e;
             e.pos_slot = (uint32_t)(br.pr + ck_off) | ((uint32_t)st.slot << 24);

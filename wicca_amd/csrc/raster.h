@@ -17,7 +17,9 @@
 //       5-5-5 / 5-6-5 (component << 3 / << 2, no bit replication), 24-bit
 //       BGR, 32-bit BGRx (alpha dropped), bottom-up or top-down rows; RLE8 /
 //       RLE4 decoded on the host (pixels a delta or end-of-line skips take
-//       palette entry 0; a run past the row's end fails the file).
+//       palette entry 0; a run past the row's end fails the file, a delta
+//       past the bottom ends the bitmap -- corrupt-data rules restated from
+//       OpenCV's BmpDecoder, parity unpinned: Pillow clips such runs).
 //   PNM (OpenCV's PxMDecoder): binary P5 gray / P6 RGB at maxval 255.
 //
 // Why the row reconstruction is on the host: deflate is a serial bit stream

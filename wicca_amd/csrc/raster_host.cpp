@@ -249,8 +249,12 @@ int parse_bmp(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
 // (escape count >= 3, padded to 16 bits), end of line, end of bitmap and
 // delta escapes; pixels a skip passes over keep index 0 (OpenCV fills them
 // with palette entry 0, Pillow leaves index 0).  A run past the row's end is
-// corrupt data (OpenCV's BmpDecoder fails the file); data that ends early
-// leaves the rest 0.
+// corrupt data and fails the file; a delta past the bottom row ends the
+// bitmap; data that ends early leaves the rest 0.  Those three rules for
+// corrupt RLE data are PARITY UNPINNED: restated from OpenCV's BmpDecoder
+// (cv2 is absent here, and Pillow, the pinned checker, clips an over-long
+// run instead); tests/test_gpu_raster.py test_rle_bmp_corrupt_rules pins
+// the chosen behaviour so that a change is deliberate.
 int unpack_bmp_rle(const uint8_t* d, size_t n, const RasterInfo& f, uint8_t* out, std::string* err)
 {
     const int64_t W = f.W, H = f.H;

@@ -148,15 +148,23 @@ class StagePlan:
         classifiers' inference;
     devices: optional GPU ids; batch k of ``batches`` (or the k-th new batch)
         runs on ``devices[k % len(devices)]``;
-    cache_bytes: the most host memory the cached outputs may hold (least
-        recently used batches are dropped first, and recomputed if asked again);
+    cache_bytes: the most host memory the cached outputs may hold (default: a
+        quarter of the host's memory, at most 32 GiB).  ``process_classifiers``
+        runs the depths one after another over the whole folder
+        (classifying_tools.py:546-551), so a batch computed for every depth
+        stays cached until the last depth reaches it; when the folder's outputs
+        for all depths do not fit (known up front from ``batches``, or found
+        when the cap first forces an eviction), the plan computes each batch
+        per depth instead -- every shape of that depth from one decode, the
+        14x saving across classifiers kept -- and the working set is a few
+        batches of one depth;
     copy: hand each request its own arrays (the cached ones are never exposed).
     """
 
     def __init__(self, shapes: Iterable, depths, interpolation: int = 3, border_type: int = 1,
                  border_constant: int = 0, *, batches: Sequence[Sequence] | None = None,
                  device: int | None = None, devices: Sequence[int] | None = None, errors: str = "raise",
-                 cache_bytes: int = 32 << 30, copy: bool = True):
+                 cache_bytes: int | None = None, copy: bool = True):
         self.expected = collections.Counter(_norm_shape(s) for s in shapes)
         if not self.expected:
             raise ValueError("need at least one shape")
@@ -168,13 +176,17 @@ class StagePlan:
         self.device = device
         self.devices = list(devices) if devices else None
         self.errors = errors
-        self.cache_bytes = int(cache_bytes)
+        self.cache_bytes = int(cache_bytes) if cache_bytes is not None else _default_cache_bytes()
         self.copy = copy
         self._order = {}
         self._batches = [list(b) for b in batches] if batches is not None else None
+        # per_depth: entries are (batch, depth) -- see cache_bytes
+        self.per_depth = False
         if self._batches is not None:
             for i, b in enumerate(self._batches):
                 self._order.setdefault(self._key(b), i)
+            files = sum(len(b) for b in self._batches)
+            self.per_depth = files * self._file_bytes(len(self.depths)) > self.cache_bytes
         self._lock = threading.Lock()
         self._entries: collections.OrderedDict = collections.OrderedDict()
         self._bytes = 0
@@ -188,29 +200,39 @@ class StagePlan:
     def _key(paths) -> tuple:
         return tuple(str(p) for p in paths)
 
+    def _file_bytes(self, n_depths: int) -> int:
+        """Output bytes per file: each shape's resized image and its icons."""
+        return sum(w * h * 3 for (w, h) in self.shapes) * (1 + n_depths)
+
     def _device_for(self, key) -> int | None:
         if not self.devices:
             return self.device
-        idx = self._order.get(key)
+        idx = self._order.get(key[0])
         if idx is None:
             idx = self._new
             self._new += 1
         return self.devices[idx % len(self.devices)]
 
     def _compute(self, key, entry: _Entry, device) -> None:
+        paths, depth = key
         try:
-            entry.result = self._matrix(list(key), self.shapes, self.depths, self.interpolation,
-                                        self.border_type, self.border_constant, device, self.errors)
+            entry.result = self._matrix(list(paths), self.shapes, self.depths if depth is None else (depth,),
+                                        self.interpolation, self.border_type, self.border_constant, device,
+                                        self.errors)
             # a shape's resized images are shared by its depths: count each array once
             entry.nbytes = sum({id(a): a.nbytes for pair in entry.result.values() for a in pair}.values())
-        except BaseException as e:  # every requester of the batch sees the same failure
+        except BaseException as e:  # the requesters waiting now see the failure ...
             entry.error = e
         finally:
             with self._lock:
                 self.stats["computed"] += 1
-                if entry.result is not None and self._entries.get(key) is entry:
-                    self._bytes += entry.nbytes
-                    self._trim(keep=key)
+                if self._entries.get(key) is entry:
+                    if entry.error is not None:  # ... later ones compute the batch again
+                        del self._entries[key]
+                        self.stats["failed"] += 1
+                    else:
+                        self._bytes += entry.nbytes
+                        self._trim(keep=key)
             entry.event.set()
 
     def _trim(self, keep) -> None:
@@ -224,12 +246,15 @@ class StagePlan:
             del self._entries[k]
             self._bytes -= e.nbytes if e.result is not None else 0
             self.stats["evicted"] += 1
+            if not self.per_depth:  # the folder does not fit for every depth: one depth at a time from now
+                self.per_depth = True
+                self.stats["per_depth"] += 1
 
     def _start_prefetch(self, key) -> None:
-        idx = self._order.get(key)
+        idx = self._order.get(key[0])
         if idx is None or idx + 1 >= len(self._batches):
             return
-        nxt = self._key(self._batches[idx + 1])
+        nxt = (self._key(self._batches[idx + 1]), key[1])
         with self._lock:
             if nxt in self._entries or nxt in self._retired or (
                     self._prefetch is not None and self._prefetch.is_alive()):
@@ -242,11 +267,16 @@ class StagePlan:
         self.stats["prefetched"] += 1
         t.start()
 
-    def entry(self, file_paths) -> _Entry:
-        """The (computed) cache entry of a batch; computes it on first use."""
-        key = self._key(file_paths)
+    def entry(self, file_paths, depth=None) -> _Entry:
+        """The (computed) cache entry of a batch (of ``depth`` when the plan
+        runs per depth); computes it on first use."""
         with self._lock:
+            pk = self._key(file_paths)
+            key = (pk, None)  # a batch computed for every depth serves any of them
             entry = self._entries.get(key)
+            if entry is None and self.per_depth:
+                key = (pk, depth if depth is not None else self.depths[0])
+                entry = self._entries.get(key)
             owner = entry is None
             if owner:
                 entry = _Entry()
@@ -275,16 +305,18 @@ class StagePlan:
             self.stats["unplanned"] += 1
             return get_img_batch(list(file_paths), s, d, self.interpolation, self.border_type,
                                  self.border_constant, self.device, errors=self.errors)
-        key = self._key(file_paths)
-        entry = self.entry(file_paths)
+        entry = self.entry(file_paths, d)
         if entry.error is not None:
             raise entry.error
         images, icons = entry.result[(s, d)]
         out = (images.copy(), icons.copy()) if self.copy else (images, icons)
         with self._lock:
+            key = next((k for k in ((self._key(file_paths), d), (self._key(file_paths), None))
+                        if self._entries.get(k) is entry), None)
             entry.served[(s, d)] += 1
-            done = all(entry.served[(sh, dd)] >= self.expected[sh] for sh in self.expected for dd in self.depths)
-            if done and self._entries.get(key) is entry:
+            depths = self.depths if key is None or key[1] is None else (key[1],)
+            done = all(entry.served[(sh, dd)] >= self.expected[sh] for sh in self.expected for dd in depths)
+            if done and key is not None:
                 del self._entries[key]
                 self._bytes -= entry.nbytes
                 self._retired.add(key)
@@ -308,6 +340,16 @@ class StagePlan:
             self._entries.clear()
             self._retired.clear()
             self._bytes = 0
+
+
+def _default_cache_bytes() -> int:
+    """A quarter of the host's physical memory, at most 32 GiB."""
+    try:
+        import os
+        total = os.sysconf("SC_PAGE_SIZE") * os.sysconf("SC_PHYS_PAGES")
+    except (ValueError, OSError, AttributeError):
+        total = 16 << 30
+    return int(min(32 << 30, total // 4))
 
 
 def folder_batches(folder, batch_size: int = 25) -> list[list]:
