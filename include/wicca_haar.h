@@ -104,6 +104,16 @@ int64_t wicca_set_workspace_cap(int64_t bytes);
  * (-1: all devices).  Workspaces leased by running calls are unaffected. */
 int wicca_release_workspaces(int device);
 
+/* Pinned (page-locked) host memory from a pool kept by size: outputs the
+ * device writes there leave by DMA, where a copy into pageable memory runs
+ * as a blit kernel that shares the GPU with the compute kernels.  *out gets
+ * a block of at least `bytes`; wicca_host_free returns it to the pool (at most
+ * WICCA_HOST_POOL_MB, default 4096, stay idle); wicca_host_pool_bytes: idle
+ * pooled bytes. */
+int wicca_host_alloc(int64_t bytes, void** out);
+int wicca_host_free(void* p);
+int64_t wicca_host_pool_bytes(void);
+
 /* Output shape of get_small_copy for an (H, W) image at `depth`
  * (wicca/wavelet_coder.py:58 ratio = 2**depth; data_loader.py:107-110). */
 int wicca_icon_shape(int64_t H, int64_t W, int depth, int64_t* out_h, int64_t* out_w);

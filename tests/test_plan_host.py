@@ -122,10 +122,11 @@ def test_transient_failure_is_retried():
     batches = [["/a.jpg"], ["/t.jpg"]]
     plan, fake = _plan([(224, 224)], (2,), batches=batches, fake=FakeMatrix(fail_on="/t.jpg", fail_times=1))
     plan.get_img_batch(batches[0], (224, 224), 2)  # starts /t.jpg in the background: it fails
-    plan._prefetch.join()
+    for t in plan._prefetch:
+        t.join()
     imgs, _ = plan.get_img_batch(batches[1], (224, 224), 2)
     assert imgs.shape == (1, 224, 224, 3)
-    assert [c[0] for c in fake.calls] == [("/a.jpg",), ("/t.jpg",), ("/t.jpg",)]
+    assert sorted(c[0] for c in fake.calls) == [("/a.jpg",), ("/t.jpg",), ("/t.jpg",)]
     assert plan.stats["failed"] == 1
 
 
@@ -186,6 +187,30 @@ def test_unplanned_pair_uses_the_per_call_stage(monkeypatch):
     assert plan.get_img_batch(["/a.jpg"], (299, 299), 2) == ("imgs", "icons")
     assert plan.get_img_batch(["/a.jpg"], (224, 224), 5) == ("imgs", "icons")
     assert len(seen) == 2 and not fake.calls and plan.stats["unplanned"] == 2
+
+
+def test_next_batch_overlaps_the_requested_one():
+    """With batches known, the next batch starts computing when a batch is
+    first requested (not when it is done): two computations overlap."""
+    batches = [[f"/o/{i}.jpg"] for i in range(4)]
+    live, peak = [0], [0]
+    lock = threading.Lock()
+
+    class Probe(FakeMatrix):
+        def __call__(self, *a):
+            with lock:
+                live[0] += 1
+                peak[0] = max(peak[0], live[0])
+            try:
+                return super().__call__(*a)
+            finally:
+                with lock:
+                    live[0] -= 1
+    plan, fake = _plan([(224, 224)], (2,), batches=batches, fake=Probe(delay=0.1))
+    for b in batches:
+        plan.get_img_batch(b, (224, 224), 2)
+    plan.close()
+    assert peak[0] >= 2 and len(fake.calls) == len(batches)
 
 
 def test_devices_round_robin_over_batches():

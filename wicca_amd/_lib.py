@@ -47,6 +47,9 @@ SIGNATURES = {
     "wicca_balance_ranges": (_int, [ctypes.POINTER(_i64), _i64, _int, ctypes.POINTER(_i64)]),
     "wicca_workspace_bytes": (_i64, [_int]),
     "wicca_release_workspaces": (_int, [_int]),
+    "wicca_host_alloc": (_int, [_i64, ctypes.POINTER(_p)]),
+    "wicca_host_free": (_int, [_p]),
+    "wicca_host_pool_bytes": (_i64, []),
     "wicca_set_workspace_cap": (_i64, [_i64]),
     "wicca_icon_shape": (_int, [_i64, _i64, _int, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     "wicca_haar_ll_u8": (_int, [_p, _i64, _i64, _i64, _i64, _int, _int, _int, _p, _i64,
@@ -211,3 +214,24 @@ def built_source_hash() -> str:
 
 def device_count() -> int:
     return int(load().wicca_device_count())
+
+
+def pinned_empty(shape, dtype="uint8"):
+    """An uninitialised numpy array in pinned host memory (wicca_host_alloc):
+    device-to-host copies into it run by DMA.  The block goes back to the
+    library's pool when the array (and every view of it) is gone.  Where the
+    runtime cannot pin memory (no device) the array is ordinary memory."""
+    import weakref
+
+    import numpy as np
+    dt = np.dtype(dtype)
+    n = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+    if n == 0:
+        return np.empty(shape, dt)
+    lib = load()
+    p = ctypes.c_void_p()
+    if lib.wicca_host_alloc(n, ctypes.byref(p)) != WICCA_OK:  # no device / pinned memory exhausted:
+        return np.empty(shape, dt)                            # pageable (copies into it are staged)
+    buf = (ctypes.c_uint8 * n).from_address(p.value)
+    weakref.finalize(buf, lib.wicca_host_free, ctypes.c_void_p(p.value))
+    return np.frombuffer(buf, dt, count=n // dt.itemsize).reshape(shape)

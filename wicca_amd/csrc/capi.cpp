@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -603,6 +604,80 @@ int wicca_release_workspaces(int device)
     }
     for (auto& w : drop) w->destroy();
     return WICCA_OK;
+}
+
+// Pinned host memory for outputs the device writes by DMA: a hipMemcpyAsync
+// into pageable memory runs as a blit kernel into the runtime's staging
+// buffer plus a host copy (in the stage plan, 21 such kernels per 25 x 8K
+// call shared the GPU with plan_rows_kernel and doubled its time).  Blocks
+// are pooled by size (a batch's outputs have the same sizes every call) up
+// to WICCA_HOST_POOL_MB (default 4096) of idle bytes.
+namespace {
+std::mutex g_host_mu;
+std::multimap<size_t, void*> g_host_idle;  // size -> idle block
+std::map<void*, size_t> g_host_live;       // block -> size
+size_t g_host_idle_bytes = 0;
+size_t host_pool_cap()
+{
+    static const size_t cap = [] {
+        const char* e = getenv("WICCA_HOST_POOL_MB");
+        return (size_t)(e ? std::max(0L, atol(e)) : 4096L) << 20;
+    }();
+    return cap;
+}
+}  // namespace
+
+int wicca_host_alloc(int64_t bytes, void** out)
+{
+    if (!out || bytes <= 0) return fail(WICCA_ERR_ARG, "host_alloc: need bytes > 0 and an output pointer");
+    const size_t n = (size_t)(bytes + 4095) & ~(size_t)4095;
+    {
+        std::lock_guard<std::mutex> g(g_host_mu);
+        auto it = g_host_idle.find(n);
+        if (it != g_host_idle.end()) {
+            *out = it->second;
+            g_host_idle.erase(it);
+            g_host_idle_bytes -= n;
+            g_host_live[*out] = n;
+            return WICCA_OK;
+        }
+    }
+    void* p = nullptr;
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess || !p)
+        return fail(WICCA_ERR_NOMEM, "hipHostMalloc of %zu bytes failed", n);
+    std::lock_guard<std::mutex> g(g_host_mu);
+    g_host_live[p] = n;
+    *out = p;
+    return WICCA_OK;
+}
+
+int wicca_host_free(void* p)
+{
+    if (!p) return WICCA_OK;
+    std::vector<void*> drop;
+    {
+        std::lock_guard<std::mutex> g(g_host_mu);
+        auto it = g_host_live.find(p);
+        if (it == g_host_live.end()) return fail(WICCA_ERR_ARG, "host_free: not a wicca_host_alloc block");
+        const size_t n = it->second;
+        g_host_live.erase(it);
+        g_host_idle.emplace(n, p);
+        g_host_idle_bytes += n;
+        while (g_host_idle_bytes > host_pool_cap() && !g_host_idle.empty()) {  // largest idle blocks first
+            auto big = std::prev(g_host_idle.end());
+            g_host_idle_bytes -= big->first;
+            drop.push_back(big->second);
+            g_host_idle.erase(big);
+        }
+    }
+    for (void* q : drop) (void)hipHostFree(q);
+    return WICCA_OK;
+}
+
+int64_t wicca_host_pool_bytes(void)
+{
+    std::lock_guard<std::mutex> g(g_host_mu);
+    return (int64_t)g_host_idle_bytes;
 }
 
 int wicca_icon_shape(int64_t H, int64_t W, int depth, int64_t* out_h, int64_t* out_w)

@@ -232,8 +232,8 @@ def get_img_batch(file_paths: Sequence[str], shape, transform_depth: int, interp
         raise ValueError("need at least one array to stack")
     out_w, out_h = int(shape[0]), int(shape[1])
     n = len(blobs)
-    resized = np.empty((n, out_h, out_w, 3), np.uint8)
-    icons = np.empty((n, out_h, out_w, 3), np.uint8)
+    resized = _lib.pinned_empty((n, out_h, out_w, 3))  # DMA targets (wicca_host_alloc)
+    icons = _lib.pinned_empty((n, out_h, out_w, 3))
     if errors not in ("raise", "zero"):
         raise ValueError("errors must be 'raise' or 'zero'")
     keep, ptrs, sizes = _buffers(blobs)

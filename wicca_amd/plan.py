@@ -101,8 +101,10 @@ def get_img_matrix(file_paths: Sequence, shapes: Iterable, depths, interpolation
     keep = [np.frombuffer(b, np.uint8) for b in blobs]
     ptrs = (ctypes.c_void_p * n)(*[k.ctypes.data for k in keep])
     sizes = (ctypes.c_int64 * n)(*[k.size for k in keep])
-    resized = [np.empty((n, h, w, 3), np.uint8) for (w, h) in shp]
-    icons = [[np.empty((n, h, w, 3), np.uint8) for _ in dep] for (w, h) in shp]
+    # pinned host outputs: the device-to-host copies run by DMA, not as blit
+    # kernels sharing the GPU with the plan's kernels
+    resized = [_lib.pinned_empty((n, h, w, 3)) for (w, h) in shp]
+    icons = [[_lib.pinned_empty((n, h, w, 3)) for _ in dep] for (w, h) in shp]
     c_shapes = (ctypes.c_int64 * (2 * len(shp)))(*[v for s in shp for v in s])
     c_depths = (ctypes.c_int * len(dep))(*dep)
     c_res = (ctypes.c_void_p * len(shp))(*[r.ctypes.data for r in resized])
@@ -143,9 +145,11 @@ class StagePlan:
         and a batch is dropped once every expected request was served);
     depths: int / tuple / list / range (``normalize_depth``'s forms);
     batches: optional, the folder's batches in ``_classify``'s order
-        (``os.listdir`` in steps of ``batch_size``): after a batch is computed
-        the next one is computed in the background, so its decode overlaps the
-        classifiers' inference;
+        (``os.listdir`` in steps of ``batch_size``): when a batch is first
+        requested the next one starts computing in the background (at most
+        ``ahead`` of them at a time), so its host work and PCIe transfers
+        overlap the requested batch's device work and the classifiers'
+        inference;
     devices: optional GPU ids; batch k of ``batches`` (or the k-th new batch)
         runs on ``devices[k % len(devices)]``;
     cache_bytes: the most host memory the cached outputs may hold (default: a
@@ -164,7 +168,7 @@ class StagePlan:
     def __init__(self, shapes: Iterable, depths, interpolation: int = 3, border_type: int = 1,
                  border_constant: int = 0, *, batches: Sequence[Sequence] | None = None,
                  device: int | None = None, devices: Sequence[int] | None = None, errors: str = "raise",
-                 cache_bytes: int | None = None, copy: bool = True):
+                 cache_bytes: int | None = None, copy: bool = True, ahead: int = 2):
         self.expected = collections.Counter(_norm_shape(s) for s in shapes)
         if not self.expected:
             raise ValueError("need at least one shape")
@@ -178,6 +182,7 @@ class StagePlan:
         self.errors = errors
         self.cache_bytes = int(cache_bytes) if cache_bytes is not None else _default_cache_bytes()
         self.copy = copy
+        self.ahead = max(0, int(ahead))
         self._order = {}
         self._batches = [list(b) for b in batches] if batches is not None else None
         # per_depth: entries are (batch, depth) -- see cache_bytes
@@ -191,7 +196,7 @@ class StagePlan:
         self._entries: collections.OrderedDict = collections.OrderedDict()
         self._bytes = 0
         self._new = 0
-        self._prefetch = None
+        self._prefetch: list = []
         self._retired = set()  # batches every expected request was served from (never prefetched again)
         self._matrix = get_img_matrix  # the native call (tests inject a stand-in)
         self.stats = collections.Counter()
@@ -251,20 +256,23 @@ class StagePlan:
                 self.stats["per_depth"] += 1
 
     def _start_prefetch(self, key) -> None:
+        # the batch after `key` starts now, while `key` itself is still being
+        # computed: its host work (read, parse, de-stuffing, PCIe upload)
+        # overlaps the other's device work; at most `ahead` background batches
         idx = self._order.get(key[0])
         if idx is None or idx + 1 >= len(self._batches):
             return
         nxt = (self._key(self._batches[idx + 1]), key[1])
         with self._lock:
-            if nxt in self._entries or nxt in self._retired or (
-                    self._prefetch is not None and self._prefetch.is_alive()):
+            self._prefetch = [t for t in self._prefetch if t.is_alive()]
+            if nxt in self._entries or nxt in self._retired or len(self._prefetch) >= self.ahead:
                 return
             entry = _Entry()
             self._entries[nxt] = entry
             dev = self._device_for(nxt)
             t = threading.Thread(target=self._compute, args=(nxt, entry, dev), daemon=True)
-            self._prefetch = t
-        self.stats["prefetched"] += 1
+            self._prefetch.append(t)
+            self.stats["prefetched"] += 1
         t.start()
 
     def entry(self, file_paths, depth=None) -> _Entry:
@@ -286,12 +294,12 @@ class StagePlan:
             else:
                 self._entries.move_to_end(key)
                 self.stats["hits"] += 1
+        if self._batches is not None:
+            self._start_prefetch(key)
         if owner:
             self._compute(key, entry, dev)
         else:
             entry.event.wait()
-        if self._batches is not None:
-            self._start_prefetch(key)
         return entry
 
     def get_img_batch(self, file_paths, shape, transform_depth) -> tuple[np.ndarray, np.ndarray]:
@@ -333,9 +341,9 @@ class StagePlan:
 
     def close(self) -> None:
         """Wait for a background batch and drop the cache."""
-        t = self._prefetch
-        if t is not None:
+        for t in list(self._prefetch):
             t.join()
+        self._prefetch = []
         with self._lock:
             self._entries.clear()
             self._retired.clear()
