@@ -161,92 +161,164 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         for (int64_t i = 0; i < n; ++i)
             wicca::plan_resize((int)H[(size_t)i], (int)W[(size_t)i], (int)shapes[(size_t)s].h,
                                (int)shapes[(size_t)s].w, 3, interpolation, &src_rp[(size_t)(s * n + i)]);
-    auto rows_wanted = [&](int s, int64_t i) {
-        const wicca::ResizeParams& rp = src_rp[(size_t)(s * n + i)];
+    auto area_rows_ok = [&](const wicca::ResizeParams& rp, int s, int64_t h, int64_t w) {
         return (rp.mode == wicca::RS_AREA || rp.mode == wicca::RS_AREA_FAST) &&
-               wicca::plan_hsum_ok(shapes[(size_t)s].w, 3) && wicca::stage_row_ok(W[(size_t)i], 3) &&
-               H[(size_t)i] <= 65535;
+               wicca::plan_hsum_ok(shapes[(size_t)s].w, 3) && wicca::stage_row_ok(w, 3) && h <= 65535;
     };
-    // groups of at most kPlanShapes shapes and kPlanRounds * 256 pixel tasks
-    // (one launch each, one read of every image); per image one row-sum block
-    // with a plane per shape, and a task table
+    // 4. icon resizes: (shape s, depth slot u, image i)
+    std::vector<wicca::ResizeParams> irp((size_t)S * U * n);
+    for (int s = 0; s < S; ++s)
+        for (int u = 0; u < U; ++u)
+            for (int64_t i = 0; i < n; ++i) {
+                const size_t j = (size_t)(i * U + u);
+                wicca::ResizeParams& q = irp[(size_t)((s * U + u) * n + i)];
+                wicca::plan_resize((int)ih[j], (int)iw[j], (int)shapes[(size_t)s].h, (int)shapes[(size_t)s].w, 3,
+                                   interpolation, &q);
+                q.src = icon_ptr(i, u);
+                q.src_pitch = ico_pitch[j];
+                q.src_stride = 0;
+                q.dst = dout + ico_out_off[(size_t)(s * U + u)] + i * ob[(size_t)s];
+                q.dst_pitch = shapes[(size_t)s].w * 3;
+                q.dst_stride = 0;
+            }
+    // Images the row kernel reads -- the decoded sources, and the icons whose
+    // resize is an INTER_AREA downscale too (at depths 2-4 the icons of an 8K
+    // image are 1920..480 px wide: a per-lane resize kernel re-reads ~40 cells
+    // per output byte) -- in groups of at most kPlanShapes shapes and
+    // kPlanRounds * 256 pixel tasks (one launch each, one read of every image);
+    // per image one row-sum block with a plane per shape, and a task table
+    struct RowSrc {
+        const uint8_t* src;
+        int64_t pitch, H, W;
+    };
     struct AreaGroup {
         std::vector<int> shapes;
         std::vector<wicca::PlanImageDev> imgs;
         std::vector<std::vector<wicca::AreaTask>> tasks;
         std::vector<size_t> task_off;
         size_t off = 0;
-        int rounds = 0;
+        int rounds = 0, max_h = 0;
     };
-    std::vector<AreaGroup> groups;
-    {
+    int64_t hsum_total = 0;
+    // want(s, j): image j's resize to shape s comes from row sums; rp(s, j), dst(s, j)
+    auto make_groups = [&](const std::vector<RowSrc>& im, auto want, auto rp_of, auto dst_of) {
+        const int64_t m = (int64_t)im.size();
+        std::vector<AreaGroup> gs;
         AreaGroup g;
         int64_t cols = 0;
         for (int s = 0; s < S; ++s) {
             bool any = false;
-            for (int64_t i = 0; i < n && !any; ++i) any = rows_wanted(s, i);
+            for (int64_t j = 0; j < m && !any; ++j) any = want(s, j);
             if (!any) continue;
             const int64_t w = shapes[(size_t)s].w;
             if (!g.shapes.empty() &&
                 ((int)g.shapes.size() == wicca::kPlanShapes || cols + w > (int64_t)wicca::kPlanRounds * 256)) {
-                groups.push_back(std::move(g));
+                gs.push_back(std::move(g));
                 g = AreaGroup();
                 cols = 0;
             }
             g.shapes.push_back(s);
             cols += w;
         }
-        if (!g.shapes.empty()) groups.push_back(std::move(g));
-    }
-    std::vector<bool> by_rows((size_t)S * n, false);
-    int64_t hsum_total = 0;
-    std::vector<int64_t> hsum_img_off;
-    for (AreaGroup& g : groups) {
-        g.imgs.resize((size_t)n);
-        g.tasks.resize((size_t)n);
-        g.task_off.resize((size_t)n);
-        for (int64_t i = 0; i < n; ++i) {
-            wicca::PlanImageDev& e = g.imgs[(size_t)i];
-            memset(&e, 0, sizeof(e));
-            e.src = img[(size_t)i];
-            e.src_pitch = pitch[(size_t)i];
-            e.H = (int32_t)H[(size_t)i];
-            e.W = (int32_t)W[(size_t)i];
-            uint32_t plane = 0;  // floats into the image's row-sum block
-            const int64_t block0 = hsum_total;
-            for (size_t q = 0; q < g.shapes.size(); ++q) {
-                const int s = g.shapes[q];
-                if (!rows_wanted(s, i)) continue;
-                by_rows[(size_t)(s * n + i)] = true;
-                const wicca::ResizeParams& rp = src_rp[(size_t)(s * n + i)];
-                const bool fast = rp.mode == wicca::RS_AREA_FAST;
-                const int dw = (int)shapes[(size_t)s].w;
-                wicca::append_area_tasks((int)W[(size_t)i], dw, rp.scale_x, fast, rp.kx, plane, g.tasks[(size_t)i]);
-                e.dst[q] = dout + res_off[(size_t)s] + i * ob[(size_t)s];
-                e.scale_y[q] = rp.scale_y;
-                e.ky[q] = fast ? rp.ky : 0;
-                e.kx[q] = fast ? rp.kx : 0;
-                e.area_scale[q] = rp.area_scale;
-                e.hsum[q] = reinterpret_cast<float*>((intptr_t)(plane * sizeof(float)));  // relocated below
-                plane += (uint32_t)(H[(size_t)i] * 3 * dw);
+        if (!g.shapes.empty()) gs.push_back(std::move(g));
+        for (AreaGroup& gr : gs) {
+            gr.imgs.resize((size_t)m);
+            gr.tasks.resize((size_t)m);
+            gr.task_off.resize((size_t)m);
+            for (int64_t j = 0; j < m; ++j) {
+                wicca::PlanImageDev& e = gr.imgs[(size_t)j];
+                memset(&e, 0, sizeof(e));
+                e.src = im[(size_t)j].src;
+                e.src_pitch = im[(size_t)j].pitch;
+                e.H = (int32_t)im[(size_t)j].H;
+                e.W = (int32_t)im[(size_t)j].W;
+                uint32_t plane = 0;  // floats into the image's row-sum block
+                const int64_t block0 = hsum_total;
+                for (size_t q = 0; q < gr.shapes.size(); ++q) {
+                    const int s = gr.shapes[q];
+                    if (!want(s, j)) continue;
+                    const wicca::ResizeParams& rp = rp_of(s, j);
+                    const bool fast = rp.mode == wicca::RS_AREA_FAST;
+                    const int dw = (int)shapes[(size_t)s].w;
+                    wicca::append_area_tasks((int)im[(size_t)j].W, dw, rp.scale_x, fast, rp.kx, plane,
+                                             gr.tasks[(size_t)j]);
+                    e.dst[q] = dst_of(s, j);
+                    e.scale_y[q] = rp.scale_y;
+                    e.ky[q] = fast ? rp.ky : 0;
+                    e.kx[q] = fast ? rp.kx : 0;
+                    e.area_scale[q] = rp.area_scale;
+                    e.hsum[q] = reinterpret_cast<float*>((intptr_t)(plane * sizeof(float)));  // relocated below
+                    plane += (uint32_t)(im[(size_t)j].H * 3 * dw);
+                }
+                e.hsum_base = reinterpret_cast<float*>((intptr_t)(block0 * (int64_t)sizeof(float)));
+                hsum_total += round_up((int64_t)plane, 64);
+                e.n_tasks = (int32_t)gr.tasks[(size_t)j].size();
+                gr.rounds = std::max(gr.rounds, (int)((e.n_tasks + 255) / 256));
+                gr.max_h = std::max(gr.max_h, (int)im[(size_t)j].H);
             }
-            e.hsum_base = reinterpret_cast<float*>((intptr_t)(block0 * (int64_t)sizeof(float)));  // relocated below
-            hsum_total += round_up((int64_t)plane, 64);
-            e.n_tasks = (int32_t)g.tasks[(size_t)i].size();
-            g.rounds = std::max(g.rounds, (int)((e.n_tasks + 255) / 256));
         }
+        return gs;
+    };
+    std::vector<RowSrc> srcs((size_t)n);
+    for (int64_t i = 0; i < n; ++i) srcs[(size_t)i] = {img[(size_t)i], pitch[(size_t)i], H[(size_t)i], W[(size_t)i]};
+    std::vector<bool> by_rows((size_t)S * n, false);
+    for (int s = 0; s < S; ++s)
+        for (int64_t i = 0; i < n; ++i)
+            by_rows[(size_t)(s * n + i)] = area_rows_ok(src_rp[(size_t)(s * n + i)], s, H[(size_t)i], W[(size_t)i]);
+    std::vector<AreaGroup> groups = make_groups(
+        srcs, [&](int s, int64_t i) { return (bool)by_rows[(size_t)(s * n + i)]; },
+        [&](int s, int64_t i) -> const wicca::ResizeParams& { return src_rp[(size_t)(s * n + i)]; },
+        [&](int s, int64_t i) { return dout + res_off[(size_t)s] + i * ob[(size_t)s]; });
+    // icons by rows: the icon planes of every depth slot with an area downscale to some shape
+    std::vector<int64_t> row_icon;  // j -> i * U + u
+    std::vector<bool> icon_by_rows((size_t)S * U * n, false);
+    for (int64_t i = 0; i < n; ++i)
+        for (int u = 0; u < U; ++u) {
+            const size_t j = (size_t)(i * U + u);
+            bool any = false;
+            for (int s = 0; s < S; ++s) {
+                const size_t q = (size_t)((s * U + u) * n + i);
+                icon_by_rows[q] = area_rows_ok(irp[q], s, ih[j], iw[j]) && ico_pitch[j] % 16 == 0;
+                any = any || icon_by_rows[q];
+            }
+            if (any) row_icon.push_back((int64_t)j);
+        }
+    std::vector<RowSrc> isrcs(row_icon.size());
+    for (size_t j = 0; j < row_icon.size(); ++j) {
+        const int64_t ij = row_icon[j];
+        isrcs[j] = {icon_ptr(ij / U, (int)(ij % U)), ico_pitch[(size_t)ij], ih[(size_t)ij], iw[(size_t)ij]};
     }
+    auto irp_at = [&](int s, int64_t j) -> size_t {
+        const int64_t ij = row_icon[(size_t)j];
+        return (size_t)((s * U + (int)(ij % U)) * n + ij / U);
+    };
+    std::vector<AreaGroup> icon_groups = make_groups(
+        isrcs, [&](int s, int64_t j) { return (bool)icon_by_rows[irp_at(s, j)]; },
+        [&](int s, int64_t j) -> const wicca::ResizeParams& { return irp[irp_at(s, j)]; },
+        [&](int s, int64_t j) { return irp[irp_at(s, j)].dst; });
     if (hsum_total * (int64_t)sizeof(float) > ((int64_t)1 << 35))
         return fail(WICCA_ERR_NOMEM, "stage plan: %lld bytes of row sums", (long long)(hsum_total * 4));
     if (hsum_total) HIP_TRY(ws->phsum.reserve((size_t)hsum_total * sizeof(float)));
-    for (AreaGroup& g : groups)
-        for (int64_t i = 0; i < n; ++i) {
-            wicca::PlanImageDev& e = g.imgs[(size_t)i];
-            uint8_t* base = (uint8_t*)ws->phsum.ptr + (intptr_t)e.hsum_base;
-            e.hsum_base = (float*)base;
-            for (size_t q = 0; q < g.shapes.size(); ++q)
-                if (by_rows[(size_t)(g.shapes[q] * n + i)]) e.hsum[q] = (float*)(base + (intptr_t)e.hsum[q]);
-        }
+    for (std::vector<AreaGroup>* gv : {&groups, &icon_groups})
+        for (AreaGroup& g : *gv)
+            for (wicca::PlanImageDev& e : g.imgs) {
+                uint8_t* base = (uint8_t*)ws->phsum.ptr + (intptr_t)e.hsum_base;
+                e.hsum_base = (float*)base;
+                for (size_t q = 0; q < g.shapes.size(); ++q)
+                    if (e.dst[q]) e.hsum[q] = (float*)(base + (intptr_t)e.hsum[q]);
+            }
+    // the other icon resizes: per shape, a compact descriptor list for the
+    // per-lane kernel (or per image, for copies and cubic / Lanczos)
+    std::vector<std::vector<wicca::ResizeParams>> irp_rest((size_t)S);
+    std::vector<bool> shape_per_image((size_t)S, false);  // a copy / cubic / Lanczos icon resize in the shape
+    for (int s = 0; s < S; ++s)
+        for (int u = 0; u < U; ++u)
+            for (int64_t i = 0; i < n; ++i) {
+                const size_t q = (size_t)((s * U + u) * n + i);
+                if (icon_by_rows[q]) continue;
+                irp_rest[(size_t)s].push_back(irp[q]);
+                if (irp[q].mode == wicca::RS_COPY || irp[q].mode == wicca::RS_KERNEL) shape_per_image[(size_t)s] = true;
+            }
     // descriptors, packed into one pinned buffer and uploaded once:
     //   [MultiImageDev x n | block map | ResizeParams x (S * U * n) | per row
     //    group: PlanImageDev x n, then each image's task table]
@@ -293,29 +365,13 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         o_md = take(sizeof(wicca::MultiImageDev) * (size_t)n);
         o_map = take(sizeof(uint32_t) * bmap.size());
     }
-    // 4. icon resizes: (shape s, depth slot u, image i)
-    std::vector<wicca::ResizeParams> irp((size_t)S * U * n);
-    std::vector<bool> shape_per_image((size_t)S, false);  // a copy / cubic / Lanczos icon resize in the shape
-    for (int s = 0; s < S; ++s)
-        for (int u = 0; u < U; ++u)
-            for (int64_t i = 0; i < n; ++i) {
-                const size_t j = (size_t)(i * U + u);
-                wicca::ResizeParams& q = irp[(size_t)((s * U + u) * n + i)];
-                wicca::plan_resize((int)ih[j], (int)iw[j], (int)shapes[(size_t)s].h, (int)shapes[(size_t)s].w, 3,
-                                   interpolation, &q);
-                q.src = icon_ptr(i, u);
-                q.src_pitch = ico_pitch[j];
-                q.src_stride = 0;
-                q.dst = dout + ico_out_off[(size_t)(s * U + u)] + i * ob[(size_t)s];
-                q.dst_pitch = shapes[(size_t)s].w * 3;
-                q.dst_stride = 0;
-                if (q.mode == wicca::RS_COPY || q.mode == wicca::RS_KERNEL) shape_per_image[(size_t)s] = true;
-            }
-    for (AreaGroup& g : groups) {
-        g.off = take(sizeof(wicca::PlanImageDev) * (size_t)n);
-        for (int64_t i = 0; i < n; ++i) g.task_off[(size_t)i] = take(sizeof(wicca::AreaTask) * g.tasks[(size_t)i].size());
-    }
-    const size_t o_irp = take(sizeof(wicca::ResizeParams) * irp.size());
+    for (std::vector<AreaGroup>* gv : {&groups, &icon_groups})
+        for (AreaGroup& g : *gv) {
+            g.off = take(sizeof(wicca::PlanImageDev) * g.imgs.size());
+            for (size_t j = 0; j < g.imgs.size(); ++j) g.task_off[j] = take(sizeof(wicca::AreaTask) * g.tasks[j].size());
+        }
+    std::vector<size_t> o_irp((size_t)S);
+    for (int s = 0; s < S; ++s) o_irp[(size_t)s] = take(sizeof(wicca::ResizeParams) * irp_rest[(size_t)s].size());
     const size_t meta_bytes = off;
     HIP_TRY(ws->ppin.reserve(meta_bytes, 64 << 10));
     HIP_TRY(ws->pmeta.reserve(meta_bytes));
@@ -325,15 +381,17 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         memcpy(hp + o_md, md.data(), sizeof(wicca::MultiImageDev) * md.size());
         memcpy(hp + o_map, bmap.data(), sizeof(uint32_t) * bmap.size());
     }
-    for (AreaGroup& g : groups) {
-        for (int64_t i = 0; i < n; ++i) {
-            const auto& tk = g.tasks[(size_t)i];
-            memcpy(hp + g.task_off[(size_t)i], tk.data(), sizeof(wicca::AreaTask) * tk.size());
-            g.imgs[(size_t)i].tasks = (const wicca::AreaTask*)(dp + g.task_off[(size_t)i]);
+    for (std::vector<AreaGroup>* gv : {&groups, &icon_groups})
+        for (AreaGroup& g : *gv) {
+            for (size_t j = 0; j < g.imgs.size(); ++j) {
+                const auto& tk = g.tasks[j];
+                memcpy(hp + g.task_off[j], tk.data(), sizeof(wicca::AreaTask) * tk.size());
+                g.imgs[j].tasks = (const wicca::AreaTask*)(dp + g.task_off[j]);
+            }
+            memcpy(hp + g.off, g.imgs.data(), sizeof(wicca::PlanImageDev) * g.imgs.size());
         }
-        memcpy(hp + g.off, g.imgs.data(), sizeof(wicca::PlanImageDev) * g.imgs.size());
-    }
-    memcpy(hp + o_irp, irp.data(), sizeof(wicca::ResizeParams) * irp.size());
+    for (int s = 0; s < S; ++s)
+        memcpy(hp + o_irp[(size_t)s], irp_rest[(size_t)s].data(), sizeof(wicca::ResizeParams) * irp_rest[(size_t)s].size());
     // the decode's staging was waited for (synchronous decode); the pinned
     // descriptors stay untouched until this call's final synchronise
     HIP_TRY(hipMemcpyAsync(dp, hp, meta_bytes, hipMemcpyHostToDevice, cs));
@@ -374,19 +432,37 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                 return rc;
         }
     }
-    // icon resizes (classifying_tools.py:318), one launch per shape over (depth, image)
+    // row sums + vertical pass of a group of images (plan_rows / plan_vsum)
+    auto run_groups = [&](const std::vector<AreaGroup>& gv) -> hipError_t {
+        for (const AreaGroup& g : gv) {
+            wicca::PlanParams pp{};
+            pp.imgs = (const wicca::PlanImageDev*)(dp + g.off);
+            pp.n_shapes = (int32_t)g.shapes.size();
+            pp.C = 3;
+            for (size_t q = 0; q < g.shapes.size(); ++q) {
+                pp.dw[q] = (int32_t)shapes[(size_t)g.shapes[q]].w;
+                pp.dh[q] = (int32_t)shapes[(size_t)g.shapes[q]].h;
+            }
+            const int64_t m = (int64_t)g.imgs.size();
+            hipError_t e = wicca::launch_plan_rows(pp, m, g.max_h, g.rounds, cs);
+            if (e == hipSuccess) e = wicca::launch_plan_vsum(pp, m, cs);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    };
+    // icon resizes (classifying_tools.py:318): the INTER_AREA downscales from
+    // row sums, the rest one launch per shape over its (depth, image) list
+    HIP_TRY(run_groups(icon_groups));
     for (int s = 0; s < S; ++s) {
+        const auto& rest = irp_rest[(size_t)s];
+        if (rest.empty()) continue;
         if (!shape_per_image[(size_t)s]) {
-            HIP_TRY(wicca::launch_resize_desc(
-                (const wicca::ResizeParams*)(dp + o_irp) + (size_t)s * U * n, (int64_t)U * n,
-                (int)shapes[(size_t)s].h, (int)(shapes[(size_t)s].w * 3), cs));
+            HIP_TRY(wicca::launch_resize_desc((const wicca::ResizeParams*)(dp + o_irp[(size_t)s]), (int64_t)rest.size(),
+                                              (int)shapes[(size_t)s].h, (int)(shapes[(size_t)s].w * 3), cs));
             continue;
         }
-        for (int u = 0; u < U; ++u)
-            for (int64_t i = 0; i < n; ++i) {
-                const wicca::ResizeParams& q = irp[(size_t)((s * U + u) * n + i)];
-                if ((rc = run_resize(q, q.src, q.src_pitch, 0, q.dst, q.dst_pitch, 0, 1, cs, ws))) return rc;
-            }
+        for (const wicca::ResizeParams& q : rest)
+            if ((rc = run_resize(q, q.src, q.src_pitch, 0, q.dst, q.dst_pitch, 0, 1, cs, ws))) return rc;
     }
     // the icons' copies to the caller (5/6 of the output bytes at 5 depths)
     // leave on the copy stream while the source resizes below run
@@ -394,20 +470,7 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
     hipEvent_t icons_done = ws->slot_ready[0];  // the workspace is this call's alone
     HIP_TRY(hipEventRecord(icons_done, cs));
     // source resizes (classifying_tools.py:315), every shape
-    for (AreaGroup& g : groups) {
-        wicca::PlanParams pp{};
-        pp.imgs = (const wicca::PlanImageDev*)(dp + g.off);
-        pp.n_shapes = (int32_t)g.shapes.size();
-        pp.C = 3;
-        int max_h = 0;
-        for (int64_t i = 0; i < n; ++i) max_h = std::max(max_h, (int)H[(size_t)i]);
-        for (size_t q = 0; q < g.shapes.size(); ++q) {
-            pp.dw[q] = (int32_t)shapes[(size_t)g.shapes[q]].w;
-            pp.dh[q] = (int32_t)shapes[(size_t)g.shapes[q]].h;
-        }
-        HIP_TRY(wicca::launch_plan_rows(pp, n, max_h, g.rounds, cs));
-        HIP_TRY(wicca::launch_plan_vsum(pp, n, cs));
-    }
+    HIP_TRY(run_groups(groups));
     for (int s = 0; s < S; ++s)
         for (int64_t i = 0; i < n; ++i) {
             if (by_rows[(size_t)(s * n + i)]) continue;

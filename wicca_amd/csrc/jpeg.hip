@@ -225,6 +225,96 @@ struct BitReaderC {
         pr += k;
     }
 };
+// The write pass's reader: chunks of 4 stream words, each word its own load
+// (stride `st` words: 64 in the lane-interleaved copy, where a wave's 64
+// lanes read neighbouring words of a few lines with every load), the next
+// chunk's 4 loads in flight.  The write pass's block stores share the vector
+// memory counter with these loads and their number between a load and its
+// use is not known at compile time, so every wait for stream data is a
+// vmcnt(0) that also waits for the stores issued since: the word reader
+// waited at every word, this one at every fourth.
+struct BitReaderS4 {
+    const uint32_t* w;  // the first word of the chunk in nxt
+    int64_t base;       // absolute bit position of the first word read
+    int32_t pr;         // next unconsumed bit, relative to base
+    int32_t st;         // words between consecutive stream words
+    int32_t left;       // words of cur not yet appended
+    uint64_t buf;       // n valid bits, MSB-aligned
+    int n;
+    uint32_t cur[4], nxt[4];
+    __device__ __forceinline__ static uint32_t be(uint32_t x) { return __builtin_bswap32(x); }
+    __device__ __forceinline__ void load_next()
+    {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) nxt[k] = w[k * st];
+    }
+    __device__ __forceinline__ void advance()
+    {
+        cur[0] = cur[1];
+        cur[1] = cur[2];
+        cur[2] = cur[3];
+        if (--left == 0) {
+            // real copies, ordered before the next chunk's loads (the memory
+            // clobber), so that those land in nxt's own registers: left to the
+            // scheduler, the loads were hoisted above the copies, went to
+            // temporaries and were waited for at once to be moved in
+#pragma unroll
+            for (int k = 0; k < 4; ++k) asm volatile("v_mov_b32 %0, %1" : "=v"(cur[k]) : "v"(nxt[k]) : "memory");
+            w += 4 * st;
+            load_next();
+            left = 4;
+        }
+    }
+    __device__ __forceinline__ void append()
+    {
+        buf |= (uint64_t)be(cur[0]) << (32 - n);
+        n += 32;
+        advance();
+    }
+    __device__ void start(const uint32_t* w0, int stride, int32_t off)
+    {
+        st = stride;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cur[k] = w0[k * st];
+        w = w0 + 4 * st;
+        load_next();
+        left = 4;
+        pr = off;
+        buf = 0;
+        n = 0;
+        append();
+        append();
+        buf <<= pr;
+        n = 64 - pr;
+    }
+    __device__ void reset(const JpegPlan& P, int64_t i, int64_t s_i, int64_t bitpos)
+    {
+        if (!P.ilv) {
+            base = bitpos & ~(int64_t)31;
+            start(reinterpret_cast<const uint32_t*>(P.stream) + (base >> 5), 1, (int32_t)(bitpos - base));
+            return;
+        }
+        const int64_t j0 = (bitpos - s_i) >> 5;
+        base = s_i + 32 * j0;
+        start(P.ilv + (((i >> 6) * P.ilv_sw + j0) << 6) + (i & 63), 64, (int32_t)(bitpos - base));
+    }
+    __device__ __forceinline__ int64_t p() const { return base + pr; }
+    __device__ __forceinline__ void refill()
+    {
+        if (n <= 32) append();
+    }
+    __device__ __forceinline__ void skip(int k)
+    {
+        buf <<= k;
+        n -= k;
+        pr += k;
+    }
+};
+#ifndef WICCA_JPEG_WRITE_S4
+#define WICCA_JPEG_WRITE_S4 1  // 0: the write pass keeps the word reader
+#endif
+using WriteReader = std::conditional<WICCA_JPEG_WRITE_S4 != 0, BitReaderS4, BitReader>::type;
+
 // the guess pass (CK 1) reads through chunks; the later rounds, whose lanes
 // mostly stop within S/8 bits, keep the word reader (1.79 against 1.85 ms of
 // rounds per call with chunks, profiles/r04ad_*)
@@ -860,7 +950,7 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 4 : 1) void jpeg_write_kernel(
     const SubBase b = base[i];
     int32_t dc[kJpegMaxComp] = {b.dc[0], b.dc[1], b.dc[2]};
     int64_t started = 0;
-    BitReader br;
+    WriteReader br;
     br.reset(P, i, sg.bit0 + j * P.sub_bits, st.p);
 #if WICCA_JPEG_STAGE
     const int w0 = (int)(threadIdx.x & ~63u);  // the wave's first lane
@@ -1712,7 +1802,8 @@ bool jpeg_ilv_on()
 size_t jpeg_ilv_bytes(int64_t n_sub, int32_t sub_bits)
 {
     if (!jpeg_ilv_on()) return 0;
-    return (size_t)((n_sub + 63) & ~(int64_t)63) * (size_t)jpeg_ilv_words(sub_bits) * 4;
+    // + 16 rows: the write pass's reader loads up to two 4-word chunks ahead
+    return ((size_t)((n_sub + 63) & ~(int64_t)63) * (size_t)jpeg_ilv_words(sub_bits) + 16 * 64) * 4;
 }
 
 size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg)
