@@ -110,11 +110,22 @@ constexpr int kHuffLutBitsSync = 11;  // the sync passes' tables: codes > 9 bits
 template <int B>
 struct HuffDevT {
     static constexpr int kBits = B;
-    uint16_t lut[1 << B];  // (len << 8) | symbol for codes <= B bits, 0 = longer
+    // Second-level lookups of the write pass's tables (B = 9) for the codes
+    // longer than B bits: a lut entry 0x8000 | k << 12 | off points at the 2^k
+    // entries sub[off ..] indexed by the next k bits (every long code under
+    // that 9-bit prefix; bit strings no code has read as 17 << 8).  A table
+    // whose sub-tables do not fit keeps lut = 0 there: the maxcode compare
+    // chain.  Sized so that the write pass's 4 tables keep its workgroup's LDS
+    // at 4 workgroups per CU (the standard AC tables need 144 entries).
+    static constexpr int kSub = B == 9 ? 232 : 2;
+    uint16_t lut[1 << B];  // (len << 8) | symbol for codes <= B bits, 0 = longer (compare chain)
     int32_t maxcode[18];   // largest code of length l, -1 if none (maxcode[17] sentinel)
     int32_t valoff[18];    // vals index of the first code of length l, minus that code
     uint8_t vals[256];
+    uint16_t sub[kSub];
 };
+constexpr uint32_t kHuffSubFlag = 0x8000u;
+constexpr uint32_t kHuffNoCode = 17u << 8;  // jdhuff.c: 17 bits consumed, symbol 0
 using HuffDev = HuffDevT<kHuffLutBits>;
 using HuffDevSync = HuffDevT<kHuffLutBitsSync>;
 

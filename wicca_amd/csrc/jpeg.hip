@@ -331,6 +331,12 @@ __device__ __forceinline__ uint32_t huff_lookup(const HT& t, uint32_t look)
 {
     constexpr int kHuffLutBits = HT::kBits;
     uint32_t e = t.lut[look >> (32 - kHuffLutBits)];
+    if constexpr (HT::kSub > 2) {
+        if (e & kHuffSubFlag) {  // a long code: one more lookup by the next k bits
+            const uint32_t k = (e >> 12) & 7u;
+            e = t.sub[(e & 0xFFFu) + ((look << kHuffLutBits) >> (32 - k))];
+        }
+    }
     if (e == 0) {
         // a code longer than the lookup: every length's maxcode / valoff read
         // at once and the shortest match selected, so the slow path costs two

@@ -9,6 +9,7 @@
 // OpenCV's IMREAD_COLOR does.
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 
 #include <immintrin.h>
@@ -479,6 +480,47 @@ static void build_huff_lut(const JpegHuffTable& t, HuffDevT<B>* d)
     d->maxcode[0] = -1;
     d->maxcode[17] = INT_MAX;  // sentinel
     memcpy(d->vals, t.vals, 256);
+    // WICCA_JPEG_HUFF_SUB=0: no second-level tables (the compare chain for
+    // every long code; A/B only)
+    static const bool sub_on = [] {
+        const char* e = getenv("WICCA_JPEG_HUFF_SUB");
+        return !(e && atoi(e) == 0);
+    }();
+    if (B != 9 || !sub_on) return;
+    // second-level tables (HuffDevT::sub): the longest code under each 9-bit prefix
+    int maxlen[1 << B] = {0};
+    code = 0;
+    for (int l = 1; l <= 16; ++l) {
+        for (int i = 0; i < t.bits[l]; ++i, ++code)
+            if (l > B) maxlen[code >> (l - B)] = std::max(maxlen[code >> (l - B)], l);
+        code <<= 1;
+    }
+    int total = 0;
+    for (int p = 0; p < (1 << B); ++p)
+        if (maxlen[p]) total += 1 << (maxlen[p] - B);
+    if (total > HuffDevT<B>::kSub) return;  // the compare chain serves this table
+    int off = 0;
+    for (int p = 0; p < (1 << B); ++p) {
+        if (!maxlen[p]) continue;
+        const int k = maxlen[p] - B;
+        d->lut[p] = (uint16_t)(kHuffSubFlag | (uint32_t)k << 12 | (uint32_t)off);
+        for (int e = 0; e < (1 << k); ++e) d->sub[off + e] = (uint16_t)kHuffNoCode;
+        off += 1 << k;
+    }
+    code = 0;
+    k = 0;
+    for (int l = 1; l <= 16; ++l) {
+        for (int i = 0; i < t.bits[l]; ++i, ++k, ++code) {
+            if (l <= B) continue;
+            const int p = code >> (l - B), kk = maxlen[p] - B;
+            const int base = d->lut[p] & 0xFFF, r = code & ((1 << (l - B)) - 1);
+            const int lo = r << (maxlen[p] - l), hi = (r + 1) << (maxlen[p] - l);
+            for (int e = lo; e < hi && e < (1 << kk); ++e) d->sub[base + e] = (uint16_t)((l << 8) | t.vals[k]);
+        }
+        code <<= 1;
+    }
+    for (int e = 0; e < (1 << B); ++e)  // no code at all under this prefix: 17 bits, symbol 0
+        if (d->lut[e] == 0) d->lut[e] = (uint16_t)kHuffNoCode;
 }
 
 void build_huff_dev(const JpegHuffTable& t, HuffDev* d) { build_huff_lut(t, d); }
@@ -631,10 +673,19 @@ struct HostBits {
 int host_huff(const HuffDev& t, HostBits& br)
 {
     const uint32_t look = br.peek(16);
-    const uint16_t e = t.lut[look >> (16 - kHuffLutBits)];
-    if (e) {
-        br.skip(e >> 8);
-        return e & 255;
+    uint32_t e = t.lut[look >> (16 - kHuffLutBits)];
+    if (e & kHuffSubFlag) {  // a code longer than 9 bits: the second-level table
+        const uint32_t k = (e >> 12) & 7u;
+        e = t.sub[(e & 0xFFFu) + ((look >> (16 - kHuffLutBits - k)) & ((1u << k) - 1))];
+    }
+    if (e && e != kHuffNoCode) {
+        br.skip((int)(e >> 8));
+        return (int)(e & 255);
+    }
+    if (e == kHuffNoCode) {  // jdhuff.c: not a code; 17 bits consumed, a zero returned
+        br.skip(16);
+        br.get(1);
+        return 0;
     }
     for (int l = kHuffLutBits + 1; l <= 16; ++l) {
         const int32_t code = (int32_t)(look >> (16 - l));
