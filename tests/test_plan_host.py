@@ -70,6 +70,15 @@ def test_each_batch_computed_once_and_retired(prefetch):
         assert plan.stats["prefetched"] >= 1
 
 
+def test_shared_outputs_are_read_only():
+    plan, _ = _plan([(224, 224)] * 2, (3,), copy=False)
+    a, _ = plan.get_img_batch(["/a.jpg"], (224, 224), 3)
+    b, _ = plan.get_img_batch(["/a.jpg"], (224, 224), 3)
+    assert a is b and not a.flags.writeable
+    with pytest.raises(ValueError):
+        a[:] = 0
+
+
 def test_requests_get_private_copies():
     plan, _ = _plan([(224, 224)] * 2, (3,))
     a, _ = plan.get_img_batch(["/a.jpg"], (224, 224), 3)

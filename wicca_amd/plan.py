@@ -162,7 +162,14 @@ class StagePlan:
         per depth instead -- every shape of that depth from one decode, the
         14x saving across classifiers kept -- and the working set is a few
         batches of one depth;
-    copy: hand each request its own arrays (the cached ones are never exposed).
+    copy: True (default) hands each request its own writable arrays, as the
+        reference's ``np.stack`` does; False hands every classifier the one
+        cached pair, READ-ONLY (a classifier writing into its batch raises
+        instead of corrupting the others' input) -- Keras' ``preprocess_input``
+        converts uint8 batches to new float arrays, so the demo's classifiers
+        never write into them.  The private copies are ~665 MB of host memcpy
+        per 25 x 8K batch of the demo (14 classifiers x 5 depths), more than
+        the GPU's work on the batch.
     """
 
     def __init__(self, shapes: Iterable, depths, interpolation: int = 3, border_type: int = 1,
@@ -224,6 +231,10 @@ class StagePlan:
             entry.result = self._matrix(list(paths), self.shapes, self.depths if depth is None else (depth,),
                                         self.interpolation, self.border_type, self.border_constant, device,
                                         self.errors)
+            if not self.copy:  # shared by every requester: read-only
+                for pair in entry.result.values():
+                    for a in pair:
+                        a.flags.writeable = False
             # a shape's resized images are shared by its depths: count each array once
             entry.nbytes = sum({id(a): a.nbytes for pair in entry.result.values() for a in pair}.values())
         except BaseException as e:  # the requesters waiting now see the failure ...
