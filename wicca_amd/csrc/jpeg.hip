@@ -311,7 +311,7 @@ struct BitReaderS4 {
     }
 };
 #ifndef WICCA_JPEG_WRITE_S4
-#define WICCA_JPEG_WRITE_S4 1  // 0: the write pass keeps the word reader
+#define WICCA_JPEG_WRITE_S4 0  // 1: the write pass reads 4-word chunks (measured 4 % slower, profiles/r05h_*)
 #endif
 using WriteReader = std::conditional<WICCA_JPEG_WRITE_S4 != 0, BitReaderS4, BitReader>::type;
 
@@ -1479,9 +1479,21 @@ __device__ __forceinline__ void ycc8_pack(uint2 yv, const int (&cb)[8], const in
 // barrier (the destination must be 8-B aligned).  Otherwise the colour lanes
 // take tile rows (32 lanes per row) from the LDS luma tile and the RGB leaves
 // through an LDS stage as 16-B stores.
+// The h2v2 chroma window of one wave of the direct-store path (8 blocks x 8
+// rows = 64 x 8 pixels): chroma rows iy0-1 .. iy0+4 (clamped), columns
+// c_w-4 .. c_w+35, both planes = 2 x 6 x 10 dwords.  The wave loads it with
+// one or two coalesced dword loads per lane and each lane reads its two
+// 12-byte windows per plane from LDS: the per-lane 12-byte loads (4 per lane,
+// each wave touching ~4 partial lines per instruction) ran at 0.78 TB/s on
+// their own in the probe (tools/luma_probe.hip chroma12, profiles/r05g_*).
+constexpr int kCwinRows = 6, kCwinWords = 10, kCwinPlane = kCwinRows * kCwinWords, kCwin = 2 * kCwinPlane;
+#ifndef WICCA_LUMA_CWIN
+#define WICCA_LUMA_CWIN 1  // 0: every lane loads its own 12-byte chroma windows (A/B)
+#endif
+
 template <int FMT, bool SAME>
 __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegImageDev& im, int tx, int ty, int32_t* tr,
-                                                uint8_t* ytile, uint32_t* stage)
+                                                uint8_t* ytile, uint32_t* stage, uint32_t* cwin)
 {
     const int x0 = tx * kFuseW, y0 = ty * 8;
     const int lb = threadIdx.x >> 3, r = threadIdx.x & 7;
@@ -1506,6 +1518,7 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
     bool interior = false;
     const uint8_t* pb = P.planes + im.comp_plane0[1];
     const uint8_t* pr = P.planes + im.comp_plane0[2];
+    uint32_t cw[2] = {0, 0};  // SAME: this lane's words of the wave's chroma window (loads in flight)
     if constexpr (FMT == kJpegFmtH2V2) {
         // Cb and Cr planes alike, under 2^31 bytes (the host's conditions)
         const int dw = im.comp_dw[1], dh = im.comp_dh[1];
@@ -1515,6 +1528,20 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
         interior = px_live && c >= 4 && c + 5 <= dw;  // then c + 8 <= sb too (sb: a multiple of 8 >= dw)
         if (P.abl & 2) {
             ab = bb = ar = br = uint3{(uint32_t)x, (uint32_t)y, 7u};
+        } else if (SAME && WICCA_LUMA_CWIN) {
+            // the wave's window: word q of 120 = plane q / 60, row (q % 60) / 10, column word q % 10
+            const int lane = (int)(threadIdx.x & 63);
+            const int cw0 = ((x0 >> 1) + ((int)(threadIdx.x >> 6) << 5)) - 4;  // first window byte
+            const int iy0 = y0 >> 1;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int q = lane + 64 * h;
+                const int pl = q >= kCwinPlane ? 1 : 0, rem = q - pl * kCwinPlane;
+                const int row = rem / kCwinWords, col = cw0 + 4 * (rem - row * kCwinWords);
+                const int ry = min(max(iy0 - 1 + row, 0), dh - 1);
+                if (q < kCwin && col >= 0 && col + 4 <= (int)sb)
+                    cw[h] = *reinterpret_cast<const uint32_t*>((pl ? pr : pb) + __umul24((uint32_t)ry, sb) + (uint32_t)col);
+            }
         } else if (interior) {
             const uint32_t o0 = __umul24((uint32_t)iy, sb) + (uint32_t)(c - 4);
             const uint32_t o1 = __umul24((uint32_t)oy, sb) + (uint32_t)(c - 4);
@@ -1541,6 +1568,14 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
         if (blive) *reinterpret_cast<uint2*>(ytile + r * kYPitch + lb * 8) = pack8(px);
         __syncthreads();  // ytile complete
     }
+    if constexpr (SAME && FMT == kJpegFmtH2V2 && WICCA_LUMA_CWIN) {
+        if (!(P.abl & 2)) {
+            const int lane = (int)(threadIdx.x & 63);
+            cwin[lane] = cw[0];
+            if (lane + 64 < kCwin) cwin[lane + 64] = cw[1];
+            wave_lds_sync();  // every lane reads words its wave's other lanes wrote
+        }
+    }
     uint32_t w[6] = {0, 0, 0, 0, 0, 0};
     if (px_live) {
         const uint2 yv = SAME ? pack8(px) : *reinterpret_cast<const uint2*>(ytile + rr * kYPitch + cx);
@@ -1555,6 +1590,17 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
             int cbm[8], crm[8];
             if constexpr (FMT == kJpegFmtH2V2) {
                 if (interior) {
+                    if (SAME && WICCA_LUMA_CWIN && !(P.abl & 2)) {  // this lane's windows from the wave's LDS copy
+                        const int iy0 = y0 >> 1, iy = y >> 1;
+                        const int oy = (y & 1) ? min(iy + 1, im.comp_dh[1] - 1) : max(iy - 1, 0);
+                        const int w0 = (lb & 7);  // the window's words c-4 .. c+7 start at word lb mod 8
+                        const uint32_t* n0 = cwin + (iy - iy0 + 1) * kCwinWords + w0;
+                        const uint32_t* f0 = cwin + (oy - iy0 + 1) * kCwinWords + w0;
+                        ab = uint3{n0[0], n0[1], n0[2]};
+                        bb = uint3{f0[0], f0[1], f0[2]};
+                        ar = uint3{n0[kCwinPlane], n0[kCwinPlane + 1], n0[kCwinPlane + 2]};
+                        br = uint3{f0[kCwinPlane], f0[kCwinPlane + 1], f0[kCwinPlane + 2]};
+                    }
                     chroma8_h2v2_m128(ab, bb, cbm);
                     chroma8_h2v2_m128(ar, br, crm);
                 } else {  // the plane's left and right edges
@@ -1649,6 +1695,8 @@ void jpeg_luma_color_kernel(JpegPlan P)
     __shared__ int32_t tr[kFuseBlocks * kTrBlock];
     __shared__ __attribute__((aligned(16))) uint8_t ytile[8 * kYPitch];
     __shared__ __attribute__((aligned(16))) uint32_t stage[8 * kFuseRowBytes / 4];
+    __shared__ uint32_t cwin_all[4 * kCwin];  // per wave: its h2v2 chroma window (direct-store path)
+    uint32_t* cwin = cwin_all + (threadIdx.x >> 6) * kCwin;
     int tx = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
     if constexpr (XCD) {
         const uint32_t gx = gridDim.x, gxy = gx * gridDim.y, n = gxy * gridDim.z;
@@ -1664,18 +1712,18 @@ void jpeg_luma_color_kernel(JpegPlan P)
     if (tx * kFuseW >= im.W || ty * 8 >= im.H) return;  // uniform: grid sized for the largest image
     if (P.direct_rgb && (((uintptr_t)im.dst | (uintptr_t)im.dst_pitch) & 7) == 0) {  // uniform
         switch (im.fmt) {
-        case kJpegFmtGray: luma_color_tile<kJpegFmtGray, true>(P, im, tx, ty, tr, ytile, stage); break;
-        case kJpegFmtH2V2: luma_color_tile<kJpegFmtH2V2, true>(P, im, tx, ty, tr, ytile, stage); break;
-        case kJpegFmtH1V1: luma_color_tile<kJpegFmtH1V1, true>(P, im, tx, ty, tr, ytile, stage); break;
-        default: luma_color_tile<kJpegFmtOther, true>(P, im, tx, ty, tr, ytile, stage); break;
+        case kJpegFmtGray: luma_color_tile<kJpegFmtGray, true>(P, im, tx, ty, tr, ytile, stage, cwin); break;
+        case kJpegFmtH2V2: luma_color_tile<kJpegFmtH2V2, true>(P, im, tx, ty, tr, ytile, stage, cwin); break;
+        case kJpegFmtH1V1: luma_color_tile<kJpegFmtH1V1, true>(P, im, tx, ty, tr, ytile, stage, cwin); break;
+        default: luma_color_tile<kJpegFmtOther, true>(P, im, tx, ty, tr, ytile, stage, cwin); break;
         }
         return;
     }
     switch (im.fmt) {
-    case kJpegFmtGray: luma_color_tile<kJpegFmtGray, false>(P, im, tx, ty, tr, ytile, stage); break;
-    case kJpegFmtH2V2: luma_color_tile<kJpegFmtH2V2, false>(P, im, tx, ty, tr, ytile, stage); break;
-    case kJpegFmtH1V1: luma_color_tile<kJpegFmtH1V1, false>(P, im, tx, ty, tr, ytile, stage); break;
-    default: luma_color_tile<kJpegFmtOther, false>(P, im, tx, ty, tr, ytile, stage); break;
+    case kJpegFmtGray: luma_color_tile<kJpegFmtGray, false>(P, im, tx, ty, tr, ytile, stage, cwin); break;
+    case kJpegFmtH2V2: luma_color_tile<kJpegFmtH2V2, false>(P, im, tx, ty, tr, ytile, stage, cwin); break;
+    case kJpegFmtH1V1: luma_color_tile<kJpegFmtH1V1, false>(P, im, tx, ty, tr, ytile, stage, cwin); break;
+    default: luma_color_tile<kJpegFmtOther, false>(P, im, tx, ty, tr, ytile, stage, cwin); break;
     }
 }
 

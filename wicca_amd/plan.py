@@ -63,16 +63,9 @@ def _norm_depths(depths) -> tuple[int, ...]:
     return (_depth_index(depths),)
 
 
-def _read(paths: Sequence) -> list[bytes]:
-    blobs = []
-    for p in paths:
-        if not p:
-            raise ValueError("File path cannot be empty")
-        with open(p, "rb") as f:
-            blobs.append(f.read())
-    if not blobs:
-        raise ValueError("need at least one array to stack")
-    return blobs
+def _read(paths: Sequence) -> list:
+    from .jpeg import read_files
+    return read_files(paths)
 
 
 def get_img_matrix(file_paths: Sequence, shapes: Iterable, depths, interpolation: int = 3, border_type: int = 1,
