@@ -298,16 +298,22 @@ def kernel_rooflines(stats, table):
     bytes per launch, what the bytes are)]; the duration is the mean over the
     launches whose name contains the substring (rocprofv3 kernel trace)."""
     out = []
-    for label, sub, alg, what in table:
+    for entry in table:
+        label, sub, alg, what = entry[:4]
+        per = entry[4] if len(entry) > 4 else 1  # launches per call: alg is then the call's bytes
         hits = [(n, us) for k, (n, us) in (stats or {}).items() if sub in k]
         if not hits:
             continue
         n = sum(h[0] for h in hits)
-        us = sum(h[0] * h[1] for h in hits) / n
+        us = sum(h[0] * h[1] for h in hits) / n * per
         gbs = alg / (us * 1e-6) / 1e9
-        out.append({"kernel": label, "launches": n, "avg_us": round(us, 1), "alg_bytes_per_launch": int(alg),
-                    "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes": what})
+        e = {"kernel": label, "launches": n, "avg_us": round(us, 1), "alg_bytes_per_launch": int(alg),
+             "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes": what}
+        if per > 1:
+            e["launches_per_call"] = per
+            e["note"] = f"avg_us and alg_bytes_per_launch are per call ({per} launches)"
+        out.append(e)
     return out
 
 
@@ -927,14 +933,19 @@ def run_plan(args, torch, rank):
                ",".join(map(str, depths))])
     img_b = B * H * W * 3
     icon_b = sum(B * -(-H >> d) * -(-W >> d) * 3 for d in depths)
-    row_sum_b = sum(B * H * 3 * w * 4 for (w, h) in shapes)  # float INTER_AREA row sums per shape
     out_src_b = sum(B * w * h * 3 for (w, h) in shapes)
+    # the icon planes the area kernel's icon launch reads (INTER_AREA downscales
+    # in both dimensions to some shape) and the icon resizes it writes
+    area_icons = [(d, sh) for d in depths for sh in shapes
+                  if sh[0] <= -(-W >> d) and sh[1] <= -(-H >> d)]
+    icon_read_b = sum(B * -(-H >> d) * -(-W >> d) * 3 for d in sorted({d for d, _ in area_icons}))
+    icon_out_b = sum(B * w * h * 3 for _, (w, h) in area_icons)
     kernels = kernel_rooflines(kstats, [
         ("haar_multi_ragged_kernel (icons, every depth)", "haar_multi_ragged_kernel", img_b + icon_b,
          "decoded images read once + every depth's icons written"),
-        ("plan_rows_kernel (source resize rows)", "plan_rows_kernel", img_b + row_sum_b,
-         "decoded images read once + float row sums of every shape written"),
-        ("plan_vsum_kernel", "plan_vsum_kernel", row_sum_b + out_src_b, "row sums read + resized sources written"),
+        ("plan_area_kernel (INTER_AREA resizes: icon launch + source launch)", "plan_area_kernel",
+         img_b + out_src_b + icon_read_b + icon_out_b,
+         "decoded images and the downscaled depths' icons read once, every area resize written", 2),
     ])
     dominant = max(kernels, key=lambda e: e["avg_us"], default=None)
     cpu = None if args.no_cpu_baseline else plan_cpu_baseline(args, blobs, shapes, depths)

@@ -90,7 +90,8 @@ const char* wicca_kernel_name(int depth, int64_t C, int ragged);
 int wicca_balance_ranges(const int64_t* weights, int64_t n, int n_ranges, int64_t* first);
 
 /* Device memory held by idle pooled workspaces of `device` (-1: all devices).
- * The pool keeps at most WICCA_WORKSPACE_CAP_MB (default 4096) idle per
+ * The pool keeps at most WICCA_WORKSPACE_CAP_MB (default: an eighth of device
+ * 0's memory, at least 4096; 36 GB on an MI355X) idle per
  * device: when a returned workspace takes the device above the cap, the least
  * recently used other workspaces free their buffers (the returned one keeps
  * its own, so a batch larger than the cap does not re-allocate every call). */
@@ -435,6 +436,29 @@ int wicca_image_stage_plan_u8(const uint8_t* const* data, const int64_t* sizes, 
                               const int64_t* shapes, int n_shapes, const int* depths, int n_depths,
                               int border_type, int border_constant, int interpolation,
                               uint8_t* const* resized, uint8_t* const* icons, int device, int* status);
+
+/* wicca_image_stage_plan_u8 without waiting for the device (a StagePlan's
+ * loop over a folder's batches): the call returns once the batch's parse,
+ * de-stuffing and uploads, its decode, plan kernels and the copies into the
+ * output arrays are queued; its kernels run on the device after the previous
+ * asynchronous call's, its host work and output copies overlap them.  The
+ * output arrays should be pinned (wicca_host_alloc), else the copies hold the
+ * host.  data[i] and the outputs must stay valid until
+ * wicca_image_stage_plan_wait(*ticket) returns 0: then the outputs hold what
+ * wicca_image_stage_plan_u8 (status NULL) gives -- a batch whose decode did
+ * not converge in the rounds queued, or with a damaged file, is redone
+ * synchronously by the wait.  Batches the asynchronous form does not take
+ * (files other than JPEG, more than one decode pass) run the synchronous plan
+ * on a host thread of its own.  No per-file status: a file that fails fails
+ * the batch. */
+int wicca_image_stage_plan_async(const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                                 const int64_t* shapes, int n_shapes, const int* depths, int n_depths,
+                                 int border_type, int border_constant, int interpolation,
+                                 uint8_t* const* resized, uint8_t* const* icons, int device,
+                                 int64_t* ticket);
+
+/* Wait for an asynchronous stage plan (ticket 0: no-op). */
+int wicca_image_stage_plan_wait(int64_t ticket);
 
 /*
  * Deterministic synthetic images on device (no PCIe in timed regions):

@@ -188,3 +188,59 @@ def test_stage_plan_under_classifier_threads(tmp_path):
     assert plan.stats["computed"] == len(batches)
     assert plan.cached_batches() == 0
     assert plan.stats["retired"] == len(batches)
+
+
+def _matrix_sync(paths, shapes, depths):
+    """The synchronous native call (status NULL, as errors="raise" was before
+    the asynchronous entry)."""
+    from wicca_amd import _lib
+    _, keep, args, out = P._matrix_args(paths, shapes, depths, 3, 1, 0, None)
+    _lib.check(_lib.load().wicca_image_stage_plan_u8(*args, None))
+    del keep
+    return out
+
+
+def test_plan_async_batches_overlapped(tmp_path):
+    """wicca_image_stage_plan_async: four batches issued back to back (their
+    kernels chained on the device, host work and output copies overlapping),
+    waited for in reverse order -- sequential JPEG, progressive, ragged sizes,
+    and a batch with PNG / BMP files (the worker-thread form) -- each equal to
+    the synchronous call's bytes."""
+    specs = [("scene", 480 + 8 * i, 640 - 16 * i, "jpg") for i in range(3)] + \
+        [("scene", 720, 1280, "jpg-prog"), ("noise", 77, 61, "jpg"), ("smooth", 1081, 1919, "jpg")] + \
+        [("scene", 333, 517, "png"), ("noise", 250, 301, "bmp"), ("scene", 600, 401, "jpg")]
+    paths, _ = _files(tmp_path, specs)
+    batches = [paths[0:3], paths[3:6], paths[6:9], paths[0:6]]
+    shapes, depths = DEMO_SHAPES, range(2, 7)
+    calls = [P.get_img_matrix_async(b, shapes, depths) for b in batches]
+    got = [c.wait() for c in reversed(calls)][::-1]
+    for b, g in zip(batches, got):
+        want = _matrix_sync(b, shapes, depths)
+        assert set(g) == set(want)
+        for key in want:
+            assert np.array_equal(g[key][0], want[key][0]), key
+            assert np.array_equal(g[key][1], want[key][1]), key
+
+
+def test_plan_async_damaged_file_redone(tmp_path):
+    """A JPEG whose entropy data was overwritten mid-scan: the asynchronous
+    plan's wait finds the device's damage flag (or a decode that did not
+    converge) and redoes the batch synchronously, so the outputs are the
+    synchronous call's (libjpeg-turbo's damaged-data rules on the host)."""
+    from wicca_amd import _lib
+    paths, _ = _files(tmp_path, [("scene", 480, 640, "jpg"), ("noise", 720, 960, "jpg"),
+                                 ("scene", 600, 401, "jpg")])
+    data = bytearray(open(paths[1], "rb").read())
+    rng = np.random.default_rng(5)
+    mid = len(data) // 2
+    junk = rng.integers(0, 255, 600, dtype=np.uint8)  # no 0xFF: markers stay where they were
+    data[mid:mid + 600] = junk.tobytes()
+    open(paths[1], "wb").write(bytes(data))
+    lib = _lib.load()
+    before = lib.wicca_jpeg_damaged_redone()
+    got = wicca_amd.get_img_matrix(paths, [(224, 224), (299, 299)], (2, 3, 4))
+    want = _matrix_sync(paths, [(224, 224), (299, 299)], (2, 3, 4))
+    for key in want:
+        assert np.array_equal(got[key][0], want[key][0]), key
+        assert np.array_equal(got[key][1], want[key][1]), key
+    assert lib.wicca_jpeg_damaged_redone() > before  # 600 random bytes: some code no table has

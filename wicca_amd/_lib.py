@@ -107,6 +107,10 @@ SIGNATURES = {
     "wicca_image_stage_plan_u8": (_int, [ctypes.POINTER(_p), ctypes.POINTER(_i64), _i64, ctypes.POINTER(_i64),
                                          _int, ctypes.POINTER(_int), _int, _int, _int, _int, ctypes.POINTER(_p),
                                          ctypes.POINTER(_p), _int, ctypes.POINTER(_int)]),
+    "wicca_image_stage_plan_async": (_int, [ctypes.POINTER(_p), ctypes.POINTER(_i64), _i64, ctypes.POINTER(_i64),
+                                            _int, ctypes.POINTER(_int), _int, _int, _int, _int, ctypes.POINTER(_p),
+                                            ctypes.POINTER(_p), _int, ctypes.POINTER(_i64)]),
+    "wicca_image_stage_plan_wait": (_int, [_i64]),
     "wicca_synth_u8": (_int, [_p, _i64, _i64, _i64, _i64, _i64, _i64, ctypes.c_uint64, _int,
                               _p]),
     "wicca_synth_band_u8": (_int, [_p, _i64, _i64, _i64, _i64, ctypes.c_uint64, _i64, _i64, _int,

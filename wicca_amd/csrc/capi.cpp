@@ -61,9 +61,14 @@ std::mutex g_pool_mu;
 std::vector<std::unique_ptr<Workspace>> g_pool;  // idle workspaces
 
 // Idle device memory the pool may keep per device (WICCA_WORKSPACE_CAP_MB,
-// default 4096 MiB): a workspace returned while its device's idle pool already
-// holds that much gives its buffers back first.  Thirty-two threads on 8K
-// inputs otherwise pin ~3 GB per device for the life of the process.
+// default an eighth of device 0's memory, at least 4096 MiB: 36 GB on an
+// MI355X): a workspace returned while its device's idle pool already holds
+// that much gives its buffers back first.  Thirty-two threads on 8K inputs
+// otherwise pin ~3 GB each for the life of the process.  The stage plan's
+// workspace for 25 8K JPEG files holds ~7 GB (RGB, coefficients, row sums):
+// with a 4 GB cap, a loop keeping two batches in flight had one of its two
+// workspaces trimmed whenever both were idle, and the next batch re-allocated
+// it (hipFree synchronises the device) inside its issue, 20-45 ms.
 std::atomic<int64_t> g_pool_cap{-1};  // bytes; -1 = not read from the environment yet
 
 size_t pool_cap_bytes()
@@ -71,7 +76,10 @@ size_t pool_cap_bytes()
     int64_t cap = g_pool_cap.load();
     if (cap < 0) {
         const char* e = getenv("WICCA_WORKSPACE_CAP_MB");
-        const long long mb = e ? atoll(e) : 4096;
+        size_t total = 0;
+        const long long dflt =
+            hipDeviceTotalMem(&total, 0) == hipSuccess ? std::max<long long>(4096, (long long)(total >> 23)) : 4096;
+        const long long mb = e ? atoll(e) : dflt;
         int64_t want = (int64_t)std::max<long long>(mb, 0) << 20;
         g_pool_cap.compare_exchange_strong(cap, want);
         cap = g_pool_cap.load();

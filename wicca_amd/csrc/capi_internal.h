@@ -123,15 +123,15 @@ struct Workspace {
     HostBuf rhost, rmeta_pin;
     HostBuf opin;   // pinned outputs of an asynchronous file stage (wicca_image_icon_stage_async)
     // stage plan (wicca_image_stage_plan_u8): descriptors (pinned + device),
-    // icon planes of every depth, INTER_AREA row sums of every shape
-    DevBuf pmeta, picons, phsum;
+    // icon planes of every depth
+    DevBuf pmeta, picons;
     HostBuf ppin;
     size_t bytes() const
     {
         return in.cap + out.cap + t0.cap + t1.cap + t2.cap + meta[0].cap + meta[1].cap +
                slot[0].cap + slot[1].cap + icon[0].cap + icon[1].cap + jstream.cap + jmeta.cap + jcoef.cap +
                jplanes.cap + jscratch.cap + jrgb.cap + jtmp.cap + jilv.cap + rscratch.cap + smeta.cap + rtab.cap + rraw.cap +
-               rmeta.cap + pmeta.cap + picons.cap + phsum.cap;
+               rmeta.cap + pmeta.cap + picons.cap;
     }
     hipError_t ensure_pipeline()
     {
@@ -185,7 +185,6 @@ struct Workspace {
         opin.release();
         pmeta.release();
         picons.release();
-        phsum.release();
         ppin.release();
     }
     void destroy()
@@ -288,5 +287,27 @@ bool timing_on();      // WICCA_JPEG_TIMING set: per-call phase timings on stder
 double timing_now_ms();
 int image_files_decode(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
                        uint8_t* const* dst, const int64_t* dpitch, hipStream_t stream, int* late);
+
+// The asynchronous JPEG decode the asynchronous stages share (capi_jpeg.cpp).
+//   image_file_is_jpeg: the file parses as a JPEG (others: PNG / BMP / TIFF);
+//   jpeg_async_max_files: the most files one asynchronous decode takes;
+//   jpeg_files_decode_async: the decode of every file queued on `stream`
+//     (its kernels behind the previous asynchronous call's on the device),
+//     returning at once; the caller keeps the workspace until the stream is
+//     done, then asks jpeg_async_result whether the fixed synchronisation
+//     rounds converged and no file was flagged damaged (*ok false: redo the
+//     call synchronously);
+//   jpeg_serial_record: marks the end of this call's kernels on `stream` for
+//     the next asynchronous call to wait for, and ends the call's launch
+//     section (the decode's first kernel to here: one call at a time per
+//     device); jpeg_serial_leave ends it without a mark (an error return).
+int image_file_is_jpeg(const uint8_t* data, int64_t size, int64_t i, bool* jpeg);
+int64_t jpeg_async_max_files();
+int jpeg_files_decode_async(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                            uint8_t* const* dst, const int64_t* dpitch, hipStream_t stream, const int** flags,
+                            const int32_t** damage);
+int jpeg_async_result(hipStream_t stream, const int* flags, const int32_t* damage, int64_t n, bool* ok);
+int jpeg_serial_record(int device, hipStream_t stream);
+void jpeg_serial_leave();
 
 }  // namespace wicca_capi

@@ -169,11 +169,41 @@ bool jpeg_serial_async()
 }
 std::mutex g_serial_mu;
 hipEvent_t g_serial_last[64] = {};  // per device: the last asynchronous call's kernels done
+// An asynchronous call's launch section -- from its first kernel's wait on the
+// previous call's end to its own end event -- excludes the other calls' on the
+// device: two calls whose parse / de-stuffing ran concurrently would otherwise
+// both take the same "previous" event (or none) and run their kernels side by
+// side.  Held by the issuing thread across the decode and the caller's stage
+// kernels; serial_record (or serial_leave, on an error) releases it.
+std::mutex g_launch_mu[64];
+thread_local int t_launch_dev = -1;
+
+int serial_enter(int device, hipStream_t stream)
+{
+    g_launch_mu[device].lock();
+    t_launch_dev = device;
+    std::lock_guard<std::mutex> g(g_serial_mu);
+    if (g_serial_last[device]) HIP_TRY(hipStreamWaitEvent(stream, g_serial_last[device], 0));
+    return WICCA_OK;
+}
+
+void serial_leave()
+{
+    if (t_launch_dev < 0) return;
+    g_launch_mu[t_launch_dev].unlock();
+    t_launch_dev = -1;
+}
+
+// Releases a launch section still held when an asynchronous entry returns
+struct SerialLeave {
+    ~SerialLeave() { serial_leave(); }
+};
 
 // The end of an asynchronous call's kernels (after the decode, or after the
 // file stage's kernels): the next asynchronous call's kernels wait for it.
 int serial_record(int device, hipStream_t stream)
 {
+    SerialLeave leave;
     if (!jpeg_serial_async() || device < 0 || device >= 64) return WICCA_OK;
     std::lock_guard<std::mutex> g(g_serial_mu);
     hipEvent_t& last = g_serial_last[device];
@@ -524,8 +554,8 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     }
     const bool serial = async_rounds > 0 && jpeg_serial_async() && ws->device < 64;
     if (serial) {
-        std::lock_guard<std::mutex> g(g_serial_mu);
-        if (g_serial_last[ws->device]) HIP_TRY(hipStreamWaitEvent(stream, g_serial_last[ws->device], 0));
+        int rc = serial_enter(ws->device, stream);
+        if (rc) return rc;
     }
     HIP_TRY(wicca::jpeg_decode_device(P, ims.data(), ws->jscratch.ptr, n, &rounds, stream, async_rounds,
                                       async_flags, ws->jtab.ptr + jobs_off));
@@ -854,6 +884,7 @@ int wicca_jpeg_decode_u8_async(const uint8_t* const* data, const int64_t* sizes,
     if (n > wicca::kJpegMaxJobs / wicca::kJpegMaxComp)  // more than one device pass: decode synchronously
         return wicca_jpeg_decode_u8(data, sizes, n, dsts, dst_pitches, apply_orientation, 1, device, nullptr,
                                     nullptr);
+    SerialLeave leave;  // an error return inside the launch section
     int rc;
     for (int64_t i = 0; i < n; ++i) {
         wicca::JpegInfo f;
@@ -1349,6 +1380,7 @@ int wicca_image_icon_stage_async(const uint8_t* const* data, const int64_t* size
         *ticket = id;
         return WICCA_OK;
     }
+    SerialLeave leave;  // an error return inside the launch section
     DeviceGuard dg;
     int dev, rc;
     if ((rc = select_device(device, &dev, dg))) return rc;
@@ -1479,5 +1511,55 @@ int image_files_decode(Workspace* ws, const uint8_t* const* data, const int64_t*
 
 bool timing_on() { return jpeg_timing(); }
 double timing_now_ms() { return now_ms(); }
+
+int image_file_is_jpeg(const uint8_t* data, int64_t size, int64_t i, bool* jpeg)
+{
+    int64_t H = 0, W = 0;
+    int kind = 0;
+    const int rc = probe_file(data, size, i, true, true, &H, &W, &kind);
+    *jpeg = rc == WICCA_OK && kind == 1;
+    return rc;
+}
+
+int64_t jpeg_async_max_files() { return wicca::kJpegMaxJobs / wicca::kJpegMaxComp; }
+
+int jpeg_files_decode_async(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
+                            uint8_t* const* dst, const int64_t* dpitch, hipStream_t stream, const int** flags,
+                            const int32_t** damage)
+{
+    if (n > jpeg_async_max_files()) return fail(WICCA_ERR_ARG, "asynchronous decode of %lld files", (long long)n);
+    int rounds = 0;
+    t_async_ready = t_async_done = nullptr;
+    const int rc = jpeg_decode_to_device(ws, data, sizes, n, dst, dpitch, true, stream, &rounds, kAsyncRounds, flags,
+                                         false, damage);
+    for (hipEvent_t* e : {&t_async_ready, &t_async_done})  // the decode's timing events: not reported here
+        if (*e) {
+            (void)hipEventDestroy(*e);
+            *e = nullptr;
+        }
+    return rc;
+}
+
+int jpeg_async_result(hipStream_t stream, const int* flags, const int32_t* damage, int64_t n, bool* ok)
+{
+    *ok = false;
+    int h[16];
+    HIP_TRY(hipMemcpyAsync(h, flags, sizeof(h), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    bool converged = false;
+    for (int r = 1; r <= kAsyncRounds; ++r) converged |= h[r % 16] == 0;
+    if (converged && damage) {
+        std::vector<int32_t> dmg((size_t)n, 0);
+        HIP_TRY(hipMemcpyAsync(dmg.data(), damage, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, stream));
+        HIP_TRY(hipStreamSynchronize(stream));
+        for (int64_t i = 0; i < n; ++i) g_jpeg_redone += dmg[(size_t)i] != 0;
+        for (int64_t i = 0; i < n && converged; ++i) converged = dmg[(size_t)i] == 0;
+    }
+    *ok = converged;
+    return WICCA_OK;
+}
+
+int jpeg_serial_record(int device, hipStream_t stream) { return serial_record(device, stream); }
+void jpeg_serial_leave() { serial_leave(); }
 
 }  // namespace wicca_capi

@@ -17,8 +17,8 @@
 //      gives each smaller depth's icon as the top-left crop of its level,
 //      SURVEY A5); depths <= 0 / > 8 per image as get_small_copy computes them;
 //   3. the INTER_AREA source resize of every classifier shape from ONE more
-//      read of each image (plan_rows_kernel: row sums of up to 4 shapes at a
-//      time, integer scales included, then plan_vsum_kernel); other interpolations per image;
+//      read of each image (plan_area_kernel: up to 4 shapes at a time, both
+//      passes fused, integer scales included); other interpolations per image;
 //   4. every icon resized to every shape (one launch per shape over the
 //      batch x depths);
 //   5. the dense (n, h, w, 3) outputs back to the caller's host arrays.
@@ -27,8 +27,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "capi_internal.h"
@@ -42,10 +49,65 @@ struct PlanShape {
     int64_t w, h;
 };
 
+// Where the icons' copies to the caller go (WICCA_PLAN_COPY; tuning): 0 = the
+// workspace's copy stream, overlapping the source resizes; 1 = the compute
+// stream, behind every kernel of the call
+int plan_copy_mode()
+{
+    static const int m = [] {
+        const char* e = getenv("WICCA_PLAN_COPY");
+        return e ? atoi(e) : 0;
+    }();
+    return m;
+}
+
+// Shapes per area-kernel launch (WICCA_PLAN_GROUP, 1..kPlanShapes; tuning)
+int plan_group_shapes()
+{
+    static const int n = [] {
+        const char* e = getenv("WICCA_PLAN_GROUP");
+        const int v = e ? atoi(e) : wicca::kPlanShapes;
+        return std::max(1, std::min(wicca::kPlanShapes, v));
+    }();
+    return n;
+}
+
+// An asynchronous plan call (wicca_image_stage_plan_async): the workspace
+// stays leased, and the caller's arrays receive their copies, until the wait;
+// the call's arguments for a synchronous redo (rounds not converged, a file
+// flagged damaged) or for the worker thread of a batch the asynchronous form
+// does not take (PNG / BMP / TIFF files, more files than one decode pass).
+struct PlanCall {
+    WorkspaceLease lease;
+    int device = 0;
+    hipStream_t stream = nullptr, copy_stream = nullptr;
+    const int* flags = nullptr;
+    const int32_t* damage = nullptr;
+    std::vector<const uint8_t*> data;
+    std::vector<int64_t> sizes;
+    std::vector<PlanShape> shapes;
+    std::vector<int> depths;
+    int border = 1, k = 0, interpolation = 3;
+    std::vector<uint8_t*> resized, icons;
+    std::thread worker;
+    int worker_rc = WICCA_OK;
+    std::string worker_err;
+    ~PlanCall()
+    {
+        if (worker.joinable()) worker.join();  // a ticket dropped without its wait (process exit)
+    }
+};
+
 // The call for a batch in which every file parses (status screening done).
+// as: NULL (synchronous), or an asynchronous call whose files are all JPEG, at
+// most jpeg_async_max_files() of them: everything is queued on the leased
+// workspace's streams -- decode, plan kernels, the copies into the caller's
+// arrays (pinned: DMA copies that do not hold the host) -- and the function
+// returns; its kernels run behind the previous asynchronous call's on the
+// device (jpeg_serial_record), its host work and copies overlap them.
 int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, const std::vector<PlanShape>& shapes,
                const int* depths, int n_depths, int border, int k, int interpolation, uint8_t* const* resized,
-               uint8_t* const* icons, int device, int* late_status)
+               uint8_t* const* icons, int device, int* late_status, PlanCall* as = nullptr)
 {
     const int S = (int)shapes.size();
     // distinct depths: each is computed once, repeated entries are copied out
@@ -84,7 +146,8 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
     DeviceGuard dg;
     int dev, rc;
     if ((rc = select_device(device, &dev, dg))) return rc;
-    WorkspaceLease lease;
+    WorkspaceLease local;
+    WorkspaceLease& lease = as ? as->lease : local;
     if ((rc = acquire(dev, lease))) return rc;
     Workspace* ws = lease.ws;
     hipStream_t cs = ws->stream;
@@ -104,12 +167,30 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         }
     }
     std::vector<int> late((size_t)n, 0);
+    struct Leave {  // an error return inside the asynchronous call's launch section
+        ~Leave() { jpeg_serial_leave(); }
+    } leave;
+    const bool timing = timing_on() && !as;
     const double t0 = timing_now_ms();
-    if ((rc = image_files_decode(ws, data, sizes, n, img.data(), pitch.data(), cs,
-                                 late_status ? late.data() : nullptr)))
-        return rc;
+    if (as)
+        rc = jpeg_files_decode_async(ws, data, sizes, n, img.data(), pitch.data(), cs, &as->flags, &as->damage);
+    else
+        rc = image_files_decode(ws, data, sizes, n, img.data(), pitch.data(), cs, late_status ? late.data() : nullptr);
+    if (rc) return rc;
+    // the pinned staging and descriptors, and the copies into the caller's
+    // arrays, are in use until both streams are done: an error return waits
+    struct Drain {
+        Workspace* ws;
+        bool active = true;
+        ~Drain()
+        {
+            if (!active) return;
+            (void)hipStreamSynchronize(ws->stream);
+            if (ws->copy_stream) (void)hipStreamSynchronize(ws->copy_stream);
+        }
+    } drain{ws};
     double t_decoded = 0;
-    if (timing_on()) {
+    if (timing) {
         HIP_TRY(hipStreamSynchronize(cs));
         t_decoded = timing_now_ms();
     }
@@ -155,15 +236,43 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
     }
 
     // 3. which (image, shape) pairs take their source resize from the plan's
-    // row sums: INTER_AREA downscales, general (RS_AREA) or integer (RS_AREA_FAST)
+    // area kernel: INTER_AREA downscales, general (RS_AREA) or integer (RS_AREA_FAST)
     std::vector<wicca::ResizeParams> src_rp((size_t)S * n);
     for (int s = 0; s < S; ++s)
         for (int64_t i = 0; i < n; ++i)
             wicca::plan_resize((int)H[(size_t)i], (int)W[(size_t)i], (int)shapes[(size_t)s].h,
                                (int)shapes[(size_t)s].w, 3, interpolation, &src_rp[(size_t)(s * n + i)]);
+    // the vertical tables of each distinct (source height, shape) geometry
+    // (plan_vertical; -1: not a plain downscale, per-image resize instead)
+    struct VTab {
+        int H, dh, ky;
+        double scale_y;
+        std::vector<wicca::PlanVRow> rows;
+        std::vector<wicca::PlanBand> bands;
+        bool ok = false;
+        size_t o_rows = 0, o_bands = 0;
+    };
+    std::vector<VTab> vtabs;
+    auto vtab_of = [&](const wicca::ResizeParams& rp, int s, int64_t h) -> int {
+        const int ky = rp.mode == wicca::RS_AREA_FAST ? rp.ky : 0;
+        const int dh = (int)shapes[(size_t)s].h;
+        for (size_t k = 0; k < vtabs.size(); ++k)
+            if (vtabs[k].H == (int)h && vtabs[k].dh == dh && vtabs[k].ky == ky && vtabs[k].scale_y == rp.scale_y)
+                return vtabs[k].ok ? (int)k : -1;
+        VTab v;
+        v.H = (int)h;
+        v.dh = dh;
+        v.ky = ky;
+        v.scale_y = rp.scale_y;
+        v.ok = wicca::plan_vertical((int)h, dh, rp.scale_y, ky, v.rows, v.bands);
+        vtabs.push_back(std::move(v));
+        return vtabs.back().ok ? (int)vtabs.size() - 1 : -1;
+    };
     auto area_rows_ok = [&](const wicca::ResizeParams& rp, int s, int64_t h, int64_t w) {
-        return (rp.mode == wicca::RS_AREA || rp.mode == wicca::RS_AREA_FAST) &&
-               wicca::plan_hsum_ok(shapes[(size_t)s].w, 3) && wicca::stage_row_ok(w, 3) && h <= 65535;
+        const bool fast = rp.mode == wicca::RS_AREA_FAST;
+        return (rp.mode == wicca::RS_AREA || fast) &&
+               wicca::plan_area_ok(shapes[(size_t)s].w, 3, fast ? rp.kx : 1, fast ? rp.ky : 1) &&
+               wicca::stage_row_ok(w, 3) && h <= 65535 && vtab_of(rp, s, h) >= 0;
     };
     // 4. icon resizes: (shape s, depth slot u, image i)
     std::vector<wicca::ResizeParams> irp((size_t)S * U * n);
@@ -181,12 +290,12 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                 q.dst_pitch = shapes[(size_t)s].w * 3;
                 q.dst_stride = 0;
             }
-    // Images the row kernel reads -- the decoded sources, and the icons whose
+    // Images the area kernel reads -- the decoded sources, and the icons whose
     // resize is an INTER_AREA downscale too (at depths 2-4 the icons of an 8K
     // image are 1920..480 px wide: a per-lane resize kernel re-reads ~40 cells
     // per output byte) -- in groups of at most kPlanShapes shapes and
-    // kPlanRounds * 256 pixel tasks (one launch each, one read of every image);
-    // per image one row-sum block with a plane per shape, and a task table
+    // kPlanRounds * 256 pixel tasks (64-padded per shape; one launch each, one
+    // read of every image); per image a task table
     struct RowSrc {
         const uint8_t* src;
         int64_t pitch, H, W;
@@ -194,13 +303,13 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
     struct AreaGroup {
         std::vector<int> shapes;
         std::vector<wicca::PlanImageDev> imgs;
-        std::vector<std::vector<wicca::AreaTask>> tasks;
+        std::vector<std::array<int, wicca::kPlanShapes>> vt;  // per image and shape slot: its vtabs entry
+        std::vector<std::vector<wicca::PlanTask>> tasks;
         std::vector<size_t> task_off;
         size_t off = 0;
         int rounds = 0, max_h = 0;
     };
-    int64_t hsum_total = 0;
-    // want(s, j): image j's resize to shape s comes from row sums; rp(s, j), dst(s, j)
+    // want(s, j): image j's resize to shape s comes from the area kernel; rp(s, j), dst(s, j)
     auto make_groups = [&](const std::vector<RowSrc>& im, auto want, auto rp_of, auto dst_of) {
         const int64_t m = (int64_t)im.size();
         std::vector<AreaGroup> gs;
@@ -210,9 +319,9 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
             bool any = false;
             for (int64_t j = 0; j < m && !any; ++j) any = want(s, j);
             if (!any) continue;
-            const int64_t w = shapes[(size_t)s].w;
+            const int64_t w = round_up(shapes[(size_t)s].w, 64);
             if (!g.shapes.empty() &&
-                ((int)g.shapes.size() == wicca::kPlanShapes || cols + w > (int64_t)wicca::kPlanRounds * 256)) {
+                ((int)g.shapes.size() == plan_group_shapes() || cols + w > (int64_t)wicca::kPlanRounds * 256)) {
                 gs.push_back(std::move(g));
                 g = AreaGroup();
                 cols = 0;
@@ -223,6 +332,7 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         if (!g.shapes.empty()) gs.push_back(std::move(g));
         for (AreaGroup& gr : gs) {
             gr.imgs.resize((size_t)m);
+            gr.vt.assign((size_t)m, {-1, -1, -1, -1});
             gr.tasks.resize((size_t)m);
             gr.task_off.resize((size_t)m);
             for (int64_t j = 0; j < m; ++j) {
@@ -232,26 +342,19 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                 e.src_pitch = im[(size_t)j].pitch;
                 e.H = (int32_t)im[(size_t)j].H;
                 e.W = (int32_t)im[(size_t)j].W;
-                uint32_t plane = 0;  // floats into the image's row-sum block
-                const int64_t block0 = hsum_total;
                 for (size_t q = 0; q < gr.shapes.size(); ++q) {
                     const int s = gr.shapes[q];
                     if (!want(s, j)) continue;
                     const wicca::ResizeParams& rp = rp_of(s, j);
                     const bool fast = rp.mode == wicca::RS_AREA_FAST;
-                    const int dw = (int)shapes[(size_t)s].w;
-                    wicca::append_area_tasks((int)im[(size_t)j].W, dw, rp.scale_x, fast, rp.kx, plane,
-                                             gr.tasks[(size_t)j]);
+                    wicca::append_plan_tasks((int)im[(size_t)j].W, (int)shapes[(size_t)s].w, rp.scale_x, fast, rp.kx,
+                                             (int)q, gr.tasks[(size_t)j]);
                     e.dst[q] = dst_of(s, j);
-                    e.scale_y[q] = rp.scale_y;
+                    gr.vt[(size_t)j][q] = vtab_of(rp, s, im[(size_t)j].H);
                     e.ky[q] = fast ? rp.ky : 0;
                     e.kx[q] = fast ? rp.kx : 0;
                     e.area_scale[q] = rp.area_scale;
-                    e.hsum[q] = reinterpret_cast<float*>((intptr_t)(plane * sizeof(float)));  // relocated below
-                    plane += (uint32_t)(im[(size_t)j].H * 3 * dw);
                 }
-                e.hsum_base = reinterpret_cast<float*>((intptr_t)(block0 * (int64_t)sizeof(float)));
-                hsum_total += round_up((int64_t)plane, 64);
                 e.n_tasks = (int32_t)gr.tasks[(size_t)j].size();
                 gr.rounds = std::max(gr.rounds, (int)((e.n_tasks + 255) / 256));
                 gr.max_h = std::max(gr.max_h, (int)im[(size_t)j].H);
@@ -296,17 +399,6 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         isrcs, [&](int s, int64_t j) { return (bool)icon_by_rows[irp_at(s, j)]; },
         [&](int s, int64_t j) -> const wicca::ResizeParams& { return irp[irp_at(s, j)]; },
         [&](int s, int64_t j) { return irp[irp_at(s, j)].dst; });
-    if (hsum_total * (int64_t)sizeof(float) > ((int64_t)1 << 35))
-        return fail(WICCA_ERR_NOMEM, "stage plan: %lld bytes of row sums", (long long)(hsum_total * 4));
-    if (hsum_total) HIP_TRY(ws->phsum.reserve((size_t)hsum_total * sizeof(float)));
-    for (std::vector<AreaGroup>* gv : {&groups, &icon_groups})
-        for (AreaGroup& g : *gv)
-            for (wicca::PlanImageDev& e : g.imgs) {
-                uint8_t* base = (uint8_t*)ws->phsum.ptr + (intptr_t)e.hsum_base;
-                e.hsum_base = (float*)base;
-                for (size_t q = 0; q < g.shapes.size(); ++q)
-                    if (e.dst[q]) e.hsum[q] = (float*)(base + (intptr_t)e.hsum[q]);
-            }
     // the other icon resizes: per shape, a compact descriptor list for the
     // per-lane kernel (or per image, for copies and cubic / Lanczos)
     std::vector<std::vector<wicca::ResizeParams>> irp_rest((size_t)S);
@@ -368,7 +460,12 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
     for (std::vector<AreaGroup>* gv : {&groups, &icon_groups})
         for (AreaGroup& g : *gv) {
             g.off = take(sizeof(wicca::PlanImageDev) * g.imgs.size());
-            for (size_t j = 0; j < g.imgs.size(); ++j) g.task_off[j] = take(sizeof(wicca::AreaTask) * g.tasks[j].size());
+            for (size_t j = 0; j < g.imgs.size(); ++j) g.task_off[j] = take(sizeof(wicca::PlanTask) * g.tasks[j].size());
+        }
+    for (VTab& v : vtabs)
+        if (v.ok) {
+            v.o_rows = take(sizeof(wicca::PlanVRow) * v.rows.size());
+            v.o_bands = take(sizeof(wicca::PlanBand) * v.bands.size());
         }
     std::vector<size_t> o_irp((size_t)S);
     for (int s = 0; s < S; ++s) o_irp[(size_t)s] = take(sizeof(wicca::ResizeParams) * irp_rest[(size_t)s].size());
@@ -385,15 +482,27 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         for (AreaGroup& g : *gv) {
             for (size_t j = 0; j < g.imgs.size(); ++j) {
                 const auto& tk = g.tasks[j];
-                memcpy(hp + g.task_off[j], tk.data(), sizeof(wicca::AreaTask) * tk.size());
-                g.imgs[j].tasks = (const wicca::AreaTask*)(dp + g.task_off[j]);
+                memcpy(hp + g.task_off[j], tk.data(), sizeof(wicca::PlanTask) * tk.size());
+                g.imgs[j].tasks = (const wicca::PlanTask*)(dp + g.task_off[j]);
             }
+            for (size_t j = 0; j < g.imgs.size(); ++j)
+                for (int q = 0; q < wicca::kPlanShapes; ++q) {
+                    const int k = g.vt[j][(size_t)q];
+                    if (k < 0) continue;
+                    g.imgs[j].vrows[q] = (const wicca::PlanVRow*)(dp + vtabs[(size_t)k].o_rows);
+                    g.imgs[j].bands[q] = (const wicca::PlanBand*)(dp + vtabs[(size_t)k].o_bands);
+                }
             memcpy(hp + g.off, g.imgs.data(), sizeof(wicca::PlanImageDev) * g.imgs.size());
         }
     for (int s = 0; s < S; ++s)
         memcpy(hp + o_irp[(size_t)s], irp_rest[(size_t)s].data(), sizeof(wicca::ResizeParams) * irp_rest[(size_t)s].size());
-    // the decode's staging was waited for (synchronous decode); the pinned
-    // descriptors stay untouched until this call's final synchronise
+    for (const VTab& v : vtabs)
+        if (v.ok) {
+            memcpy(hp + v.o_rows, v.rows.data(), sizeof(wicca::PlanVRow) * v.rows.size());
+            memcpy(hp + v.o_bands, v.bands.data(), sizeof(wicca::PlanBand) * v.bands.size());
+        }
+    // the pinned descriptors stay untouched until the streams are done (this
+    // call's final synchronise, or the asynchronous call's wait)
     HIP_TRY(hipMemcpyAsync(dp, hp, meta_bytes, hipMemcpyHostToDevice, cs));
 
     // icons (wavelet_coder.py:50-67 per depth)
@@ -432,7 +541,7 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                 return rc;
         }
     }
-    // row sums + vertical pass of a group of images (plan_rows / plan_vsum)
+    // the INTER_AREA resizes of a group of images (plan_area)
     auto run_groups = [&](const std::vector<AreaGroup>& gv) -> hipError_t {
         for (const AreaGroup& g : gv) {
             wicca::PlanParams pp{};
@@ -443,15 +552,14 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                 pp.dw[q] = (int32_t)shapes[(size_t)g.shapes[q]].w;
                 pp.dh[q] = (int32_t)shapes[(size_t)g.shapes[q]].h;
             }
-            const int64_t m = (int64_t)g.imgs.size();
-            hipError_t e = wicca::launch_plan_rows(pp, m, g.max_h, g.rounds, cs);
-            if (e == hipSuccess) e = wicca::launch_plan_vsum(pp, m, cs);
+            pp.bands = (g.max_h + wicca::kPlanBand - 1) / wicca::kPlanBand;
+            const hipError_t e = wicca::launch_plan_area(pp, (int64_t)g.imgs.size(), g.max_h, g.rounds, cs);
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
     };
-    // icon resizes (classifying_tools.py:318): the INTER_AREA downscales from
-    // row sums, the rest one launch per shape over its (depth, image) list
+    // icon resizes (classifying_tools.py:318): the INTER_AREA downscales by
+    // the area kernel, the rest one launch per shape over its (depth, image) list
     HIP_TRY(run_groups(icon_groups));
     for (int s = 0; s < S; ++s) {
         const auto& rest = irp_rest[(size_t)s];
@@ -483,19 +591,20 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
     // the icons from the copy stream (every kernel is already queued on cs, so
     // a copy that holds the host thread does not hold the GPU), then the
     // resized sources behind their kernels
-    HIP_TRY(hipStreamWaitEvent(ws->copy_stream, icons_done, 0));
-    struct CopyDrain {  // an error return below still waits for copies into the caller's arrays
-        hipStream_t s;
-        ~CopyDrain() { (void)hipStreamSynchronize(s); }
-    } drain{ws->copy_stream};
+    const int copy_mode = plan_copy_mode();
+    hipStream_t icon_stream = copy_mode == 0 ? ws->copy_stream : cs;
+    if (copy_mode == 0) HIP_TRY(hipStreamWaitEvent(ws->copy_stream, icons_done, 0));
+    // the next asynchronous call's kernels may start once these are done:
+    // the copies below overlap them
+    if (as && (rc = jpeg_serial_record(dev, cs))) return rc;
     for (int s = 0; s < S; ++s) {
         const size_t bytes = (size_t)(n * ob[(size_t)s]);
         for (int d = 0; d < n_depths; ++d)
             HIP_TRY(hipMemcpyAsync(icons[s * n_depths + d], dout + ico_out_off[(size_t)(s * U + slot_of[(size_t)d])],
-                                   bytes, hipMemcpyDeviceToHost, ws->copy_stream));
+                                   bytes, hipMemcpyDeviceToHost, icon_stream));
     }
     double t_kernels = 0;
-    if (timing_on()) {
+    if (timing) {
         HIP_TRY(hipStreamSynchronize(cs));
         t_kernels = timing_now_ms();
     }
@@ -503,9 +612,16 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         const size_t bytes = (size_t)(n * ob[(size_t)s]);
         HIP_TRY(hipMemcpyAsync(resized[s], dout + res_off[(size_t)s], bytes, hipMemcpyDeviceToHost, cs));
     }
+    if (as) {
+        as->device = dev;
+        as->stream = cs;
+        as->copy_stream = ws->copy_stream;
+        drain.active = false;
+        return WICCA_OK;
+    }
     HIP_TRY(hipStreamSynchronize(ws->copy_stream));
     HIP_TRY(hipStreamSynchronize(cs));
-    if (timing_on())
+    if (timing)
         fprintf(stderr, "[wicca plan] %lld files: decode %.2f ms, plan kernels %.2f ms, outputs to host %.2f ms\n",
                 (long long)n, t_decoded - t0, t_kernels - t_decoded, timing_now_ms() - t_kernels);
     for (int64_t i = 0; i < n && late_status; ++i) {  // data found corrupt during the decode: zero outputs
@@ -519,6 +635,62 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
     return WICCA_OK;
 }
 
+// The entry points' argument checks; *sh: the shapes.
+int plan_args(int64_t n, const uint8_t* const* data, const int64_t* sizes, const int64_t* shapes, int n_shapes,
+              const int* depths, int n_depths, uint8_t* const* resized, uint8_t* const* icons,
+              std::vector<PlanShape>* sh)
+{
+    if (n < 0 || (n > 0 && (!data || !sizes))) return fail(WICCA_ERR_ARG, "bad arrays");
+    if (n_shapes < 1 || n_shapes > 64 || !shapes || !resized) return fail(WICCA_ERR_ARG, "need 1..64 shapes");
+    if (n_depths < 1 || n_depths > 64 || !depths || !icons) return fail(WICCA_ERR_ARG, "need 1..64 depths");
+    sh->assign((size_t)n_shapes, PlanShape{});
+    for (int s = 0; s < n_shapes; ++s) {
+        PlanShape& e = (*sh)[(size_t)s];
+        e.w = shapes[2 * s];
+        e.h = shapes[2 * s + 1];
+        if (e.w <= 0 || e.h <= 0 || e.w > 65535 || e.h > 65535)
+            return fail(WICCA_ERR_ARG, "bad output size for shape %d", s);
+        if (!resized[s]) return fail(WICCA_ERR_ARG, "output buffer is NULL");
+        for (int d = 0; d < n_depths; ++d)
+            if (!icons[s * n_depths + d]) return fail(WICCA_ERR_ARG, "output buffer is NULL");
+    }
+    for (int d = 0; d < n_depths; ++d)
+        if (depths[d] > 30) return fail(WICCA_ERR_ARG, "depth %d too large", depths[d]);
+    return WICCA_OK;
+}
+
+std::mutex g_plan_mu;
+std::unordered_map<int64_t, std::unique_ptr<PlanCall>> g_plan;
+int64_t g_plan_next = 1;
+
+// Tickets never waited for (process exit): joined and drained from an atexit
+// handler registered after the HIP runtime loaded (so run before its teardown)
+void drain_plan_tickets()
+{
+    std::unordered_map<int64_t, std::unique_ptr<PlanCall>> left;
+    {
+        std::lock_guard<std::mutex> g(g_plan_mu);
+        left.swap(g_plan);
+    }
+    for (auto& kv : left) {
+        PlanCall* a = kv.second.get();
+        if (a->worker.joinable()) a->worker.join();
+        if (a->stream) (void)hipStreamSynchronize(a->stream);
+        if (a->copy_stream) (void)hipStreamSynchronize(a->copy_stream);
+    }
+    left.clear();
+}
+
+int64_t plan_ticket(std::unique_ptr<PlanCall> call)
+{
+    static std::once_flag once;
+    std::call_once(once, [] { std::atexit(drain_plan_tickets); });
+    std::lock_guard<std::mutex> g(g_plan_mu);
+    const int64_t id = g_plan_next++;
+    g_plan[id] = std::move(call);
+    return id;
+}
+
 }  // namespace
 
 extern "C" {
@@ -528,21 +700,9 @@ int wicca_image_stage_plan_u8(const uint8_t* const* data, const int64_t* sizes, 
                               int interpolation, uint8_t* const* resized, uint8_t* const* icons, int device,
                               int* status)
 {
-    if (n < 0 || (n > 0 && (!data || !sizes))) return fail(WICCA_ERR_ARG, "bad arrays");
-    if (n_shapes < 1 || n_shapes > 64 || !shapes || !resized) return fail(WICCA_ERR_ARG, "need 1..64 shapes");
-    if (n_depths < 1 || n_depths > 64 || !depths || !icons) return fail(WICCA_ERR_ARG, "need 1..64 depths");
-    std::vector<PlanShape> sh((size_t)n_shapes);
-    for (int s = 0; s < n_shapes; ++s) {
-        sh[(size_t)s].w = shapes[2 * s];
-        sh[(size_t)s].h = shapes[2 * s + 1];
-        if (sh[(size_t)s].w <= 0 || sh[(size_t)s].h <= 0 || sh[(size_t)s].w > 65535 || sh[(size_t)s].h > 65535)
-            return fail(WICCA_ERR_ARG, "bad output size for shape %d", s);
-        if (!resized[s]) return fail(WICCA_ERR_ARG, "output buffer is NULL");
-        for (int d = 0; d < n_depths; ++d)
-            if (!icons[s * n_depths + d]) return fail(WICCA_ERR_ARG, "output buffer is NULL");
-    }
-    for (int d = 0; d < n_depths; ++d)
-        if (depths[d] > 30) return fail(WICCA_ERR_ARG, "depth %d too large", depths[d]);
+    std::vector<PlanShape> sh;
+    int rc0 = plan_args(n, data, sizes, shapes, n_shapes, depths, n_depths, resized, icons, &sh);
+    if (rc0) return rc0;
     if (n == 0) return WICCA_OK;
     if (!status) return plan_batch(data, sizes, n, sh, depths, n_depths, border_type, border_constant, interpolation,
                                    resized, icons, device, nullptr);
@@ -597,6 +757,98 @@ int wicca_image_stage_plan_u8(const uint8_t* const* data, const int64_t* sizes, 
     }
     t_last_error = first_err;
     return WICCA_OK;
+}
+
+int wicca_image_stage_plan_async(const uint8_t* const* data, const int64_t* sizes, int64_t n, const int64_t* shapes,
+                                 int n_shapes, const int* depths, int n_depths, int border_type, int border_constant,
+                                 int interpolation, uint8_t* const* resized, uint8_t* const* icons, int device,
+                                 int64_t* ticket)
+{
+    if (!ticket) return fail(WICCA_ERR_ARG, "null ticket");
+    *ticket = 0;
+    std::vector<PlanShape> sh;
+    int rc = plan_args(n, data, sizes, shapes, n_shapes, depths, n_depths, resized, icons, &sh);
+    if (rc) return rc;
+    if (n == 0) return WICCA_OK;
+    bool async_ok = n <= jpeg_async_max_files();
+    for (int64_t i = 0; i < n && async_ok; ++i) {
+        bool jpeg = false;
+        if ((rc = image_file_is_jpeg(data[i], sizes[i], i, &jpeg))) return rc;
+        async_ok = jpeg;
+    }
+    std::unique_ptr<PlanCall> call(new PlanCall);
+    PlanCall* a = call.get();
+    a->data.assign(data, data + n);
+    a->sizes.assign(sizes, sizes + n);
+    a->shapes = sh;
+    a->depths.assign(depths, depths + n_depths);
+    a->border = border_type;
+    a->k = border_constant;
+    a->interpolation = interpolation;
+    a->resized.assign(resized, resized + n_shapes);
+    a->icons.assign(icons, icons + (size_t)n_shapes * n_depths);
+    if (!async_ok) {
+        // the whole synchronous plan on a thread of its own: its host work
+        // (PNG inflate, ...) overlaps the caller's next batch
+        DeviceGuard dg;
+        if ((rc = select_device(device, &a->device, dg))) return rc;  // "current device" is the caller's
+        a->worker = std::thread([a] {
+            try {  // no exception may leave the thread
+                a->worker_rc = plan_batch(a->data.data(), a->sizes.data(), (int64_t)a->data.size(), a->shapes,
+                                          a->depths.data(), (int)a->depths.size(), a->border, a->k, a->interpolation,
+                                          a->resized.data(), a->icons.data(), a->device, nullptr);
+                if (a->worker_rc) a->worker_err = t_last_error;
+            } catch (const std::exception& e) {
+                a->worker_rc = WICCA_ERR_NOMEM;
+                a->worker_err = e.what();
+            }
+        });
+        *ticket = plan_ticket(std::move(call));
+        return WICCA_OK;
+    }
+    if ((rc = plan_batch(data, sizes, n, sh, depths, n_depths, border_type, border_constant, interpolation, resized,
+                         icons, device, nullptr, a)))
+        return rc;
+    *ticket = plan_ticket(std::move(call));
+    return WICCA_OK;
+}
+
+int wicca_image_stage_plan_wait(int64_t ticket)
+{
+    if (ticket == 0) return WICCA_OK;
+    std::unique_ptr<PlanCall> call;
+    {
+        std::lock_guard<std::mutex> g(g_plan_mu);
+        auto it = g_plan.find(ticket);
+        if (it == g_plan.end()) return fail(WICCA_ERR_ARG, "unknown plan ticket %lld", (long long)ticket);
+        call = std::move(it->second);
+        g_plan.erase(it);
+    }
+    if (call->worker.joinable()) {  // a synchronous plan on its own thread
+        call->worker.join();
+        if (call->worker_rc) return fail(call->worker_rc, "%s", call->worker_err.c_str());
+        return WICCA_OK;
+    }
+    DeviceGuard dg;
+    int dev, rc;
+    if ((rc = select_device(call->device, &dev, dg))) return rc;
+    HIP_TRY(hipStreamSynchronize(call->copy_stream));
+    HIP_TRY(hipStreamSynchronize(call->stream));
+    bool ok = false;
+    if ((rc = jpeg_async_result(call->stream, call->flags, call->damage, (int64_t)call->data.size(), &ok))) return rc;
+    if (ok) return WICCA_OK;
+    // rare: the whole plan again, synchronously (the host decoder redoes a
+    // damaged file, the host watches every synchronisation round)
+    PlanCall* a = call.get();
+    const std::vector<const uint8_t*> d = a->data;
+    const std::vector<int64_t> sz = a->sizes;
+    const std::vector<PlanShape> sh = a->shapes;
+    const std::vector<int> dp = a->depths;
+    const std::vector<uint8_t*> res = a->resized, ico = a->icons;
+    const int border = a->border, k = a->k, interp = a->interpolation, device = a->device;
+    call.reset();  // the workspace goes back to the pool before the synchronous call leases one
+    return plan_batch(d.data(), sz.data(), (int64_t)d.size(), sh, dp.data(), (int)dp.size(), border, k, interp,
+                      res.data(), ico.data(), device, nullptr);
 }
 
 }  // extern "C"

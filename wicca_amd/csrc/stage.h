@@ -48,18 +48,18 @@ constexpr int kStageRounds = 4;
 inline bool stage_row_ok(int64_t W, int64_t C) { return W * C <= kStageRowMax && C >= 1 && C <= 4; }
 inline bool stage_hsum_ok(int64_t dw, int64_t C) { return C == 3 && dw >= 1 && dw <= 256 * kStageRounds; }
 
-// ---- the stage plan (wicca_image_stage_plan_u8): the source resizes of up
-// to kPlanShapes classifier shapes from ONE read of each decoded image.
+// ---- the stage plan (wicca_image_stage_plan_u8): the INTER_AREA resizes of
+// up to kPlanShapes classifier shapes from ONE read of each image, horizontal
+// and vertical passes in one kernel (plan_area_kernel, stage.hip).
 constexpr int kPlanShapes = 4;
-constexpr int kPlanRows = 16;    // source rows per workgroup of plan_rows
-constexpr int kPlanRounds = 6;   // task rounds per lane (<= 1536 pixel tasks per image)
+constexpr int kPlanBand = 64;    // source rows whose output rows one workgroup owns
+constexpr int kPlanRounds = 6;   // task rounds per lane (<= 1536 tasks per image, 64-padded per shape)
+constexpr int kPlanVRows = 2 * kPlanBand;  // source rows a band reads (windows of at most kPlanBand rows)
 
-// One output column dx of one shape, for every staged row: the three channel
-// sums of OpenCV's INTER_AREA horizontal pass (computeResizeAreaTab: first
+// The horizontal window of one output column (computeResizeAreaTab: first
 // partial cell s1 - 1 with weight wa, full cells s1 .. s1 + len - 1 with wm,
 // last partial cell s1 + len with wb; a weight of 0 stands for an absent
-// cell).  Integer scales (RS_AREA_FAST) are the same with wa = wb = 0, wm = 1:
-// exact integer sums.  A row's sums go to hsum + out + y * n_el.
+// cell).  Integer scales (RS_AREA_FAST): wa = wb = 0, wm = 1, exact sums.
 struct AreaTask {
     uint32_t s1len;  // s1 | len << 16
     uint32_t out;    // first float of the column within the image's row-sum block
@@ -101,16 +101,53 @@ inline AreaTabHost area_tab_host(int d, int ssize, double scale)
 // 8K -> 224 scale) on one bank).
 void append_area_tasks(int W, int dw, double scale_x, bool fast, int kx, uint32_t out0, std::vector<AreaTask>& tasks);
 
+// One output column of one shape of the plan's area kernel.  An image's tasks
+// come in chunks of 64 (one wave) of a single shape, padding tasks invalid.
+struct PlanTask {
+    uint32_t s1len;  // as AreaTask
+    float wa, wm, wb;
+    uint32_t meta;   // dx | shape << 16 | valid << 24 | rot << 25 (area_fast_row's first group)
+};
+
+// The tasks of shapes[q] (q-th shape of the group) for an image of width W,
+// 64-padded, appended to `out`.
+void append_plan_tasks(int W, int dw, double scale_x, bool fast, int kx, int q, std::vector<PlanTask>& out);
+
+// Source row y's part in the vertical pass of one shape (OpenCV's ytab): its
+// weight b1 in output row dy's window and, when the row is shared with the
+// next window (a partial cell at both ends), b2 in dy + 1's.  flags:
+// kVOpen1 (y opens dy's window: `sum = beta * buf`), kVClose1 (y ends it: the
+// output row is written), kVTwo (y is also dy + 1's first row), kVClose2
+// (and its last).
+struct PlanVRow {
+    int32_t dy;
+    float b1, b2;
+    uint32_t flags;
+};
+constexpr uint32_t kVOpen1 = 1, kVClose1 = 2, kVTwo = 4, kVClose2 = 8;
+
+// The output rows of one shape a workgroup's band owns (those whose window
+// starts in the band: [dlo, dhi)) and the source rows they read [ya, yb].
+struct PlanBand {
+    int32_t dlo, dhi, ya, yb;
+};
+
+// The vertical tables of a shape for images of height H (plan_resize's
+// geometry: scale_y, ky > 0 for integer scales), kPlanBand-row bands.
+// False when a row would sit in more than two windows, a window is empty (not
+// an INTER_AREA downscale) or spans more than kPlanBand rows (a downscale by
+// more than 64): the shape goes to the per-image resize.
+bool plan_vertical(int H, int dh, double scale_y, int ky, std::vector<PlanVRow>& rows, std::vector<PlanBand>& bands);
+
 struct PlanImageDev {
     const uint8_t* src;   // HWC uint8 RGB, rows 16-B aligned, pitch >= round_up(W * 3, 16)
     int64_t src_pitch;
     int32_t H, W;
-    const AreaTask* tasks;  // every shape's pixel tasks (device)
+    const PlanTask* tasks;  // every shape's pixel tasks (device), n_tasks a multiple of 64
     int32_t n_tasks, pad_;
-    float* hsum_base;       // the image's row-sum block (tasks' `out` is relative to it)
-    float* hsum[kPlanShapes];   // H x (dw_s * 3) row sums of shape s, or nullptr (resized otherwise)
-    uint8_t* dst[kPlanShapes];  // (dh_s, dw_s, 3) dense: cv2.resize(image, (dw_s, dh_s), INTER_AREA)
-    double scale_y[kPlanShapes];
+    uint8_t* dst[kPlanShapes];  // (dh_s, dw_s, 3) dense: cv2.resize(image, (dw_s, dh_s), INTER_AREA), or nullptr
+    const PlanVRow* vrows[kPlanShapes];  // H entries per shape
+    const PlanBand* bands[kPlanShapes];  // ceil(H / kPlanBand) entries per shape
     int32_t ky[kPlanShapes];    // > 0: integer scale (RS_AREA_FAST) ky rows per output row
     int32_t kx[kPlanShapes];
     float area_scale[kPlanShapes];
@@ -120,16 +157,19 @@ struct PlanParams {
     const PlanImageDev* imgs;
     int32_t n_shapes, C;
     int32_t dw[kPlanShapes], dh[kPlanShapes];
+    int32_t bands;              // kPlanBand-row bands of the tallest image
 };
 
-// A shape the plan's row kernel takes: RGB, at most kPlanRounds * 256 pixel
-// tasks per image over all shapes (checked by the caller), dw * 3 floats a row.
-inline bool plan_hsum_ok(int64_t dw, int64_t C) { return C == 3 && dw >= 1 && dw <= 1024; }
+// A shape the plan's area kernel takes: RGB, output rows of at most 1024
+// pixels, and under an integer scale exact float sums (255 kx ky < 2^24).
+inline bool plan_area_ok(int64_t dw, int64_t C, int64_t kx, int64_t ky)
+{
+    return C == 3 && dw >= 1 && dw <= 1024 && 255 * kx * ky < (1 << 24);
+}
 
-// Row sums of every image's tasks: grid = (ceil(max H / kPlanRows), n);
-// rounds = ceil(max tasks / 256).  Then the vertical pass into dst.
-hipError_t launch_plan_rows(const PlanParams& p, int64_t n, int max_h, int rounds, hipStream_t s);
-hipError_t launch_plan_vsum(const PlanParams& p, int64_t n, hipStream_t s);
+// Every (image, shape) of a group: grid = bands x n workgroups; rounds =
+// ceil(most tasks / 256).
+hipError_t launch_plan_area(const PlanParams& p, int64_t n, int max_h, int rounds, hipStream_t s);
 
 // Icons of every image (and the row sums of those with hsum != nullptr):
 // grid = (largest icon height, n); rounds = ceil(most tasks / 256) (0: no

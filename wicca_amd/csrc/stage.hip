@@ -53,14 +53,15 @@ __device__ __forceinline__ float ub(uint32_t v, int k) { return (float)((v >> (8
 // read touch 32 different banks), each byte converted by v_cvt_f32_ubyte{0..3},
 // the R and G chains advanced together by v_pk_mul_f32 / v_pk_add_f32 and B
 // alone: per term the same two roundings as OpenCV's `buf[dx] += S[sx] * alpha`.
-__device__ __forceinline__ void area_task_row(const uint8_t* b, const AreaTask& T, float* out)
+__device__ __forceinline__ void area_window_row(const uint8_t* b, uint32_t s1len, float wa, float wm, float wb,
+                                                float* out)
 {
-    const int s1 = (int)(T.s1len & 0xFFFFu), len = (int)(T.s1len >> 16);
-    const f32x2 wm2 = {T.wm, T.wm};
+    const int s1 = (int)(s1len & 0xFFFFu), len = (int)(s1len >> 16);
+    const f32x2 wm2 = {wm, wm};
     // first partial cell (pixel s1 - 1; s1 = 0 only without one)
     const int ia = max(3 * s1 - 3, 0);
-    f32x2 a01 = f32x2{0.f, 0.f} + f32x2{(float)b[ia], (float)b[ia + 1]} * f32x2{T.wa, T.wa};
-    float a2 = 0.f + (float)b[ia + 2] * T.wa;
+    f32x2 a01 = f32x2{0.f, 0.f} + f32x2{(float)b[ia], (float)b[ia + 1]} * f32x2{wa, wa};
+    float a2 = 0.f + (float)b[ia + 2] * wa;
     // full cells, four pixels (12 bytes) a step
     const int base = 3 * s1;
     const uint32_t* w = reinterpret_cast<const uint32_t*>(b + (base & ~3));
@@ -76,25 +77,79 @@ __device__ __forceinline__ void area_task_row(const uint8_t* b, const AreaTask& 
         d0 = d3;
         // pixel 0: r0.0 r0.1 r0.2 | 1: r0.3 r1.0 r1.1 | 2: r1.2 r1.3 r2.0 | 3: r2.1 r2.2 r2.3
         a01 = a01 + f32x2{ub(r0, 0), ub(r0, 1)} * wm2;
-        a2 = a2 + ub(r0, 2) * T.wm;
+        a2 = a2 + ub(r0, 2) * wm;
         a01 = a01 + f32x2{ub(r0, 3), ub(r1, 0)} * wm2;
-        a2 = a2 + ub(r1, 1) * T.wm;
+        a2 = a2 + ub(r1, 1) * wm;
         a01 = a01 + f32x2{ub(r1, 2), ub(r1, 3)} * wm2;
-        a2 = a2 + ub(r2, 0) * T.wm;
+        a2 = a2 + ub(r2, 0) * wm;
         a01 = a01 + f32x2{ub(r2, 1), ub(r2, 2)} * wm2;
-        a2 = a2 + ub(r2, 3) * T.wm;
+        a2 = a2 + ub(r2, 3) * wm;
     }
     // the rest of the full cells (0..3), then the last partial cell
     const int rem = len - 4 * G;
     const uint8_t* q = b + base + 12 * G;
     for (int i = 0; i <= rem; ++i, q += 3) {
-        const float wv = i < rem ? T.wm : T.wb;
+        const float wv = i < rem ? wm : wb;
         a01 = a01 + f32x2{(float)q[0], (float)q[1]} * f32x2{wv, wv};
         a2 = a2 + (float)q[2] * wv;
     }
     out[0] = a01.x;
     out[1] = a01.y;
     out[2] = a2;
+}
+
+// An integer-scale (RS_AREA_FAST) window: len whole pixels from s1, exact
+// integer channel sums, so in any order -- the 12-byte groups from group rot
+// round to rot - 1 (the host staggers the lanes whose windows start on one
+// LDS bank: at an 8K -> 240 scale every window is 24 dwords long and the 64
+// windows of a wave start on only 4 banks).  Per group three aligned dwords
+// realigned by v_alignbyte_b32 and three v_dot4_u32_u8 per channel (byte k of
+// a group is channel k mod 3).
+__device__ __forceinline__ void area_fast_row(const uint8_t* b, int s1, int len, int rot, float* out)
+{
+    const int base = 3 * s1;
+    const uint32_t* w0 = reinterpret_cast<const uint32_t*>(b + (base & ~3));
+    const uint32_t sh = (uint32_t)(base & 3);
+    const int G = len >> 2;
+    uint32_t R = 0, Gs = 0, B = 0;
+    int j = rot;
+    uint32_t d0 = w0[3 * j];
+    for (int k = 0; k < G; ++k) {
+        const uint32_t* w = w0 + 3 * j;
+        const uint32_t d1 = w[1], d2 = w[2], d3 = w[3];
+        const uint32_t r0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+        const uint32_t r1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+        const uint32_t r2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+        // r0 = R0 G0 B0 R1 | r1 = G1 B1 R2 G2 | r2 = B2 R3 G3 B3 (byte 0 first)
+        R = __builtin_amdgcn_udot4(r0, 0x01000001u, R, false);
+        R = __builtin_amdgcn_udot4(r1, 0x00010000u, R, false);
+        R = __builtin_amdgcn_udot4(r2, 0x00000100u, R, false);
+        Gs = __builtin_amdgcn_udot4(r0, 0x00000100u, Gs, false);
+        Gs = __builtin_amdgcn_udot4(r1, 0x01000001u, Gs, false);
+        Gs = __builtin_amdgcn_udot4(r2, 0x00010000u, Gs, false);
+        B = __builtin_amdgcn_udot4(r0, 0x00010000u, B, false);
+        B = __builtin_amdgcn_udot4(r1, 0x00000100u, B, false);
+        B = __builtin_amdgcn_udot4(r2, 0x01000001u, B, false);
+        d0 = d3;
+        if (++j == G) {  // wrap to the window's first group
+            j = 0;
+            d0 = w0[0];
+        }
+    }
+    const uint8_t* q = b + base + 12 * G;
+    for (int i = 4 * G; i < len; ++i, q += 3) {
+        R += q[0];
+        Gs += q[1];
+        B += q[2];
+    }
+    out[0] = (float)R;
+    out[1] = (float)Gs;
+    out[2] = (float)B;
+}
+
+__device__ __forceinline__ void area_task_row(const uint8_t* b, const AreaTask& T, float* out)
+{
+    area_window_row(b, T.s1len, T.wa, T.wm, T.wb, out);
 }
 
 // NT = the row-sum task rounds per lane: ceil(tasks / 256) of the image with
@@ -258,115 +313,190 @@ __global__ __launch_bounds__(kStThreads) void stage_vsum_kernel(StageParams P)
 }
 
 // ---------------------------------------------------------------------------
-// The stage plan's source resizes (wicca_image_stage_plan_u8): each decoded
-// image is read ONCE for the INTER_AREA row sums of every classifier shape
-// (the reference resizes it once per classifier and depth,
-// classifying_tools.py:315 under the loops of :546-551 and :414-419).
+// The stage plan's INTER_AREA resizes (wicca_image_stage_plan_u8): each image
+// is read ONCE for every classifier shape of its group (the reference resizes
+// it once per classifier and depth, classifying_tools.py:315 under the loops
+// of :546-551 and :414-419), horizontal and vertical passes in one kernel.
 //
-// One workgroup per (image, kPlanRows source rows); each row is staged in LDS
-// as it is stored (RGB interleaved, two buffers, the next row's 16-B loads in
-// flight).  A lane owns up to NT pixel tasks (one output column of one shape,
-// its table entry in registers for all the rows) and forms the column's three
-// channel sums of each row in OpenCV's order: the first partial cell, the
-// full cells left to right, the last partial cell (a weight of 0 stands for
-// an absent cell: 0 + v * 0 = +0 and acc + 0 = acc exactly).  The full cells
-// stream as 12-byte groups of four pixels: three new aligned dwords per group
-// realigned with v_alignbyte_b32 (one LDS read per four bytes instead of one
-// per byte; the host orders the tasks so that the 32 lanes of a read touch 32
-// different banks), each byte converted by v_cvt_f32_ubyte{0..3}, the R and G
-// chains advanced together with v_pk_mul_f32 / v_pk_add_f32 and B alone: per
-// term the same two roundings as OpenCV's `buf[dx] += S[sx] * alpha`.
+// Output row dy of a shape belongs to the workgroup whose kPlanBand-row band
+// holds the first source row of its vertical window (computeResizeAreaTab:
+// partial row s1 - 1 with wa, full rows s1 .. s2 - 1 with wm, partial row s2
+// with wb); the workgroup streams the rows from the first window start of its
+// output rows (over all shapes) to the last window end, which runs at most one
+// window past the band.  Each row is staged in LDS (two buffers, the next
+// rows' 16-B loads in flight); a lane owns up to NT output columns (tasks, in
+// 64-task chunks of one shape: a wave's shape is uniform), forms each
+// column's three horizontal channel sums for the row in OpenCV's order
+// (area_window_row: the per-term roundings of `buf[dx] += S[sx] * alpha`),
+// and adds beta times them into its vertical sums in OpenCV's order (`sum =
+// beta * buf` for a window's first row, `sum += beta * buf` after), so no
+// row-sum plane goes through memory.  When a row ends a window the lane writes
+// its output bytes; a partial row that also opens the next window is added
+// into that one too.  Integer scales (RS_AREA_FAST): unit weights, exact
+// float sums (255 kx ky < 2^24), resizeAreaFast's rounding.
 // ---------------------------------------------------------------------------
+
+#ifndef WICCA_PLAN_AREA_OCC
+#define WICCA_PLAN_AREA_OCC 2  // workgroups per CU the register budget is sized for
+#endif
+#ifndef WICCA_PLAN_AREA_AHEAD
+#define WICCA_PLAN_AREA_AHEAD 2  // source rows in flight (registers): 2, or 1
+#endif
+
 template <int NT>
-__global__ __launch_bounds__(kStThreads, 3) void plan_rows_kernel(PlanParams P)
+__global__ __launch_bounds__(kStThreads, WICCA_PLAN_AREA_OCC) void plan_area_kernel(PlanParams P)
 {
-    __shared__ __attribute__((aligned(16))) uint8_t buf[2][kStageRowMax + 64];
-    const PlanImageDev& im = P.imgs[blockIdx.y];
+    // [two row buffers | the band's vertical table: kPlanShapes x kPlanVRows]
+    constexpr int kRowBuf = kStageRowMax + 64;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kRowBuf + kPlanShapes * kPlanVRows * sizeof(PlanVRow)];
+    uint8_t* const buf0 = lds;
+    uint8_t* const buf1 = lds + kRowBuf;
+    PlanVRow* const vtab = reinterpret_cast<PlanVRow*>(lds + 2 * kRowBuf);
+    // consecutive bands of an image on one XCD (workgroups are dealt to the 8
+    // XCDs round robin): a band re-reads up to one window of the next band's
+    // rows, from its XCD's L2 when the neighbour is resident there
+    uint32_t L = blockIdx.x;
+    const uint32_t per = gridDim.x / 8;
+    if (L < per * 8) L = (L % 8) * per + L / 8;
+    const PlanImageDev& im = P.imgs[L / (uint32_t)P.bands];
+    const int band = (int)(L % (uint32_t)P.bands);
     const int H = im.H, W = im.W;
-    const int y0 = blockIdx.x * kPlanRows;
-    if (y0 >= H) return;  // uniform: the grid is sized for the tallest image
-    const int y1 = min(H, y0 + kPlanRows);
+    if (band * kPlanBand >= H) return;  // uniform: the bands are counted for the tallest image
     const int t = threadIdx.x;
-    AreaTask tk[NT];
+    const int n_shapes = P.n_shapes;
+
+    // the band's source rows [ya, yb]: every shape's output rows' windows
+    int ya = H, yb = -1;
+    for (int q = 0; q < n_shapes; ++q) {
+        if (im.dst[q] == nullptr) continue;
+        const PlanBand b = im.bands[q][band];
+        if (b.dlo < b.dhi) {
+            ya = min(ya, b.ya);
+            yb = max(yb, b.yb);
+        }
+    }
+    if (yb < ya) return;  // uniform: no output row starts in this band
+    // their vertical table entries into LDS (at most kPlanVRows rows: a window
+    // spans at most kPlanBand rows, plan_vertical)
+    const int nrows = yb - ya + 1;
+    for (int e = t; e < n_shapes * nrows; e += kStThreads) {
+        const int q = e / nrows, j = e - q * nrows;
+        if (im.dst[q] != nullptr) vtab[q * kPlanVRows + j] = im.vrows[q][ya + j];
+    }
+
+    // this lane's tasks; per round the wave's shape, band entry and output (uniform)
+    PlanTask tk[NT];
+    float acc[NT][3];
+    int sq[NT];
+    PlanBand bq[NT];
+    uint8_t* dq[NT];
+    int dwq[NT], kyq[NT];
+    float asq[NT];
+    bool halfq[NT];
 #pragma unroll
     for (int r = 0; r < NT; ++r) {
         const int k = t + r * kStThreads;
-        if (k < im.n_tasks) {
-            tk[r] = im.tasks[k];
-        } else {
-            tk[r].s1len = 0;
-            tk[r].n_el = 0;  // marks no task
+        const bool on = (k & ~63) < im.n_tasks;
+        tk[r] = on ? im.tasks[k] : PlanTask{0u, 0.f, 0.f, 0.f, 0u};
+        acc[r][0] = acc[r][1] = acc[r][2] = 0.f;
+        const int q = on ? __builtin_amdgcn_readfirstlane((int)((tk[r].meta >> 16) & 0xFu)) : -1;
+        sq[r] = q;
+        bq[r] = PlanBand{0, 0, H, -1};
+        dq[r] = nullptr;
+        dwq[r] = kyq[r] = 0;
+        asq[r] = 0.f;
+        halfq[r] = false;
+        if (q >= 0) {
+            bq[r] = im.bands[q][band];
+            dq[r] = im.dst[q];
+            dwq[r] = P.dw[q];
+            kyq[r] = im.ky[q];
+            asq[r] = im.area_scale[q];
+            halfq[r] = im.kx[q] == 2 && im.ky[q] == 2;
         }
     }
+
+    // output row dy of round r's shape: the lane's three bytes
+    auto emit = [&](int r, int dy) {
+        if (!((tk[r].meta >> 24) & 1u)) return;
+        const int dx = (int)(tk[r].meta & 0xFFFFu);
+        // a global (not flat) store: flat operations also count on the LDS
+        // counter, and every LDS wait of the row loop would wait for them too
+        __attribute__((address_space(1))) uint8_t* o =
+            (__attribute__((address_space(1))) uint8_t*)(dq[r] + ((int64_t)dy * dwq[r] + dx) * 3);
+        if (kyq[r] > 0) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int isum = (int)acc[r][c];
+                o[c] = halfq[r] ? (uint8_t)((isum + 2) >> 2) : sat_u8(round_f32((float)isum * asq[r]));
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) o[c] = sat_u8(round_f32(acc[r][c]));
+        }
+    };
+
+    const uint8_t* const src = im.src;
+    const int64_t src_pitch = im.src_pitch;
     const int nq = (W * 3 + 15) >> 4;
-    // two rows in flight: row y + 2's loads go out as soon as row y is staged
-    // (its registers are free again), so a row's load latency overlaps two
-    // rows of sums instead of one
-    u32x4 va[kStChunks], vb[kStChunks];
-    auto load_row = [&](u32x4 (&v)[kStChunks], int y) {
-        const u32x4* row = reinterpret_cast<const u32x4*>(im.src + (int64_t)y * im.src_pitch);
+    constexpr int kAhead = WICCA_PLAN_AREA_AHEAD;
+    u32x4 va[kStChunks], vb[kAhead == 2 ? kStChunks : 1];
+    auto load_row = [&](auto& v, int y) {
+        const u32x4* row = reinterpret_cast<const u32x4*>(src + (int64_t)y * src_pitch);
 #pragma unroll
         for (int m = 0; m < kStChunks; ++m) {
             const int q = t + m * kStThreads;
             v[m] = q < nq ? __builtin_nontemporal_load(row + q) : u32x4{0, 0, 0, 0};
         }
     };
-    auto row_step = [&](u32x4 (&v)[kStChunks], int y, uint8_t* b) {
+    auto row_step = [&](auto& v, int y, uint8_t* b) {
 #pragma unroll
         for (int m = 0; m < kStChunks; ++m) {
             const int q = t + m * kStThreads;
             if (q < nq) reinterpret_cast<u32x4*>(b)[q] = v[m];
         }
-        if (y + 2 < y1) load_row(v, y + 2);  // in flight during the next two rows' sums
+        // the next row's loads (kAhead rows in flight) run during this row's sums
+        if (y + kAhead <= yb) load_row(v, y + kAhead);
         __syncthreads();  // row y staged; the other buffer was last read before this
 #pragma unroll
         for (int r = 0; r < NT; ++r) {
-            if (tk[r].n_el == 0) continue;
-            area_task_row(b, tk[r], im.hsum_base + tk[r].out + (int64_t)y * tk[r].n_el);
+            const int q = sq[r];
+            if (q < 0 || y < bq[r].ya || y > bq[r].yb) continue;  // uniform from here on
+            const PlanVRow vr = vtab[q * kPlanVRows + (y - ya)];
+            const bool w1 = vr.dy >= bq[r].dlo && vr.dy < bq[r].dhi;
+            const bool w2 = (vr.flags & kVTwo) && vr.dy + 1 >= bq[r].dlo && vr.dy + 1 < bq[r].dhi;
+            if (!w1 && !w2) continue;
+            float h[3];
+            if (kyq[r] > 0)
+                area_fast_row(b, (int)(tk[r].s1len & 0xFFFFu), (int)(tk[r].s1len >> 16), (int)(tk[r].meta >> 25), h);
+            else
+                area_window_row(b, tk[r].s1len, tk[r].wa, tk[r].wm, tk[r].wb, h);
+            if (w1) {  // the row's term in dy's window
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const float v1 = vr.b1 * h[c];
+                    acc[r][c] = (vr.flags & kVOpen1) ? v1 : acc[r][c] + v1;
+                }
+                if (vr.flags & kVClose1) emit(r, vr.dy);
+            }
+            if (w2) {  // ... and the first term of dy + 1's
+#pragma unroll
+                for (int c = 0; c < 3; ++c) acc[r][c] = vr.b2 * h[c];
+                if (vr.flags & kVClose2) emit(r, vr.dy + 1);
+            }
         }
     };
-    load_row(va, y0);
-    if (y0 + 1 < y1) load_row(vb, y0 + 1);
-    for (int y = y0; y < y1; y += 2) {
-        row_step(va, y, buf[0]);
-        if (y + 1 < y1) row_step(vb, y + 1, buf[1]);
+    if constexpr (kAhead == 2) {
+        load_row(va, ya);
+        if (ya + 1 <= yb) load_row(vb, ya + 1);
+        for (int y = ya; y <= yb; y += 2) {
+            row_step(va, y, buf0);
+            if (y + 1 <= yb) row_step(vb, y + 1, buf1);
+        }
+    } else {
+        load_row(va, ya);
+        for (int y = ya; y <= yb; ++y) row_step(va, y, ((y - ya) & 1) ? buf1 : buf0);
     }
-}
-
-// The vertical pass of every (image, shape) with row sums: blockIdx.z =
-// image * n_shapes + shape (stage_vsum_kernel's arithmetic; integer scales:
-// the exact integer block sum, then resizeAreaFast's rounding).
-__global__ __launch_bounds__(kStThreads) void plan_vsum_kernel(PlanParams P)
-{
-    const int s = (int)(blockIdx.z % (uint32_t)P.n_shapes);
-    const PlanImageDev& im = P.imgs[blockIdx.z / (uint32_t)P.n_shapes];
-    if (im.hsum[s] == nullptr) return;
-    const int n_el = P.dw[s] * P.C;
-    const int e = blockIdx.x * kStThreads + threadIdx.x;
-    const int dy = blockIdx.y;
-    if (e >= n_el || dy >= P.dh[s]) return;
-    const float* col = im.hsum[s] + e;
-    const int ky = im.ky[s];
-    if (ky > 0) {  // RS_AREA_FAST: every row sum is an exact integer, and so is their sum
-        int sum = 0;
-        for (int r = 0; r < ky; ++r) sum += (int)col[(int64_t)(dy * ky + r) * n_el];
-        const bool half = im.kx[s] == 2 && ky == 2 && P.C != 2;
-        im.dst[s][(int64_t)dy * n_el + e] =
-            half ? (uint8_t)((sum + 2) >> 2) : sat_u8(round_f32((float)sum * im.area_scale[s]));
-        return;
-    }
-    const AreaTab ty = area_tab(dy, im.H, im.scale_y[s]);
-    float sum = 0.f;
-    bool first = true;
-    auto term = [&](int sy, float beta) {
-        const float v = beta * col[(int64_t)sy * n_el];
-        sum = first ? v : sum + v;
-        first = false;
-    };
-    if (ty.has_a) term(ty.s1 - 1, ty.wa);
-    for (int sy = ty.s1; sy < ty.s2; ++sy) term(sy, ty.wm);
-    if (ty.has_b) term(ty.s2, ty.wb);
-    im.dst[s][(int64_t)dy * n_el + e] = sat_u8(round_f32(sum));
 }
 
 }  // namespace
@@ -409,34 +539,100 @@ void append_area_tasks(int W, int dw, double scale_x, bool fast, int kx, uint32_
     }
 }
 
-hipError_t launch_plan_rows(const PlanParams& p, int64_t n, int max_h, int rounds, hipStream_t s)
+void append_plan_tasks(int W, int dw, double scale_x, bool fast, int kx, int q, std::vector<PlanTask>& out)
 {
-    if (n <= 0 || max_h <= 0) return hipSuccess;
-    if (n > 65535 || p.C != 3 || rounds < 1 || rounds > kPlanRounds) return hipErrorInvalidValue;
-    const dim3 grid((uint32_t)((max_h + kPlanRows - 1) / kPlanRows), (uint32_t)n);
-    switch (rounds) {
-    case 1: hipLaunchKernelGGL(plan_rows_kernel<1>, grid, dim3(kStThreads), 0, s, p); break;
-    case 2: hipLaunchKernelGGL(plan_rows_kernel<2>, grid, dim3(kStThreads), 0, s, p); break;
-    case 3: hipLaunchKernelGGL(plan_rows_kernel<3>, grid, dim3(kStThreads), 0, s, p); break;
-    case 4: hipLaunchKernelGGL(plan_rows_kernel<4>, grid, dim3(kStThreads), 0, s, p); break;
-    case 5: hipLaunchKernelGGL(plan_rows_kernel<5>, grid, dim3(kStThreads), 0, s, p); break;
-    default: hipLaunchKernelGGL(plan_rows_kernel<6>, grid, dim3(kStThreads), 0, s, p); break;
+    std::vector<AreaTask> col;
+    append_area_tasks(W, dw, scale_x, fast, kx, 0, col);
+    const size_t first = out.size();  // a multiple of 64: lane groups of 32 start here
+    for (size_t i = 0; i < col.size(); ++i) {
+        const AreaTask& a = col[i];
+        uint32_t rot = 0;
+        if (fast) {  // area_fast_row's starting group: the first unused bank in the lane's group of 32
+            const int G = kx / 4, s = (3 * (int)(a.s1len & 0xFFFFu)) >> 2;
+            const size_t g0 = first + ((out.size() - first) & ~(size_t)31);
+            std::vector<bool> used(32, false);
+            for (size_t k = g0; k < out.size(); ++k) {
+                const int sk = (3 * (int)(out[k].s1len & 0xFFFFu)) >> 2;
+                used[(size_t)((sk + 3 * (int)(out[k].meta >> 25)) & 31)] = true;
+            }
+            for (int r = 0; r < std::min(G, 128); ++r)
+                if (!used[(size_t)((s + 3 * r) & 31)]) {
+                    rot = (uint32_t)r;
+                    break;
+                }
+        }
+        out.push_back(PlanTask{a.s1len, a.wa, a.wm, a.wb, (a.out / 3u) | (uint32_t)q << 16 | 1u << 24 | rot << 25});
     }
-    return hipGetLastError();
+    while (out.size() % 64) out.push_back(PlanTask{0u, 0.f, 0.f, 0.f, (uint32_t)q << 16});
 }
 
-hipError_t launch_plan_vsum(const PlanParams& p, int64_t n, hipStream_t s)
+bool plan_vertical(int H, int dh, double scale_y, int ky, std::vector<PlanVRow>& rows, std::vector<PlanBand>& bands)
 {
-    if (n <= 0) return hipSuccess;
-    int max_el = 0, max_dh = 0;
-    for (int i = 0; i < p.n_shapes; ++i) {
-        max_el = std::max(max_el, p.dw[i] * p.C);
-        max_dh = std::max(max_dh, p.dh[i]);
+    rows.assign((size_t)H, PlanVRow{-1, 0.f, 0.f, 0u});
+    std::vector<int> wfirst((size_t)dh), wlast((size_t)dh);
+    for (int dy = 0; dy < dh; ++dy) {
+        // the window's rows and weights in OpenCV's order (resize.hip's area_vsum)
+        int f, l;
+        AreaTabHost a{};
+        if (ky > 0) {
+            f = dy * ky;
+            l = f + ky - 1;
+        } else {
+            a = area_tab_host(dy, H, scale_y);
+            f = a.has_a ? a.s1 - 1 : a.s1;
+            l = a.has_b ? a.s2 : a.s2 - 1;
+        }
+        if (l < f || f < 0 || l >= H || l - f >= kPlanBand || (dy > 0 && f < wfirst[(size_t)dy - 1]))
+            return false;
+        wfirst[(size_t)dy] = f;
+        wlast[(size_t)dy] = l;
+        for (int y = f; y <= l; ++y) {
+            const float beta = ky > 0 ? 1.f : (a.has_a && y == a.s1 - 1) ? a.wa : (y < a.s2 ? a.wm : a.wb);
+            PlanVRow& e = rows[(size_t)y];
+            if (e.dy < 0) {
+                e.dy = dy;
+                e.b1 = beta;
+                e.flags = (y == f ? kVOpen1 : 0u) | (y == l ? kVClose1 : 0u);
+            } else if (!(e.flags & kVTwo) && e.dy == dy - 1 && y == f && (e.flags & kVClose1)) {
+                e.b2 = beta;
+                e.flags |= kVTwo | (y == l ? kVClose2 : 0u);
+            } else {
+                return false;  // a third window, or overlapping windows not of this shape
+            }
+        }
     }
-    if (n * p.n_shapes > 65535 || max_dh > 65535) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(plan_vsum_kernel, dim3((uint32_t)((max_el + kStThreads - 1) / kStThreads), (uint32_t)max_dh,
-                                              (uint32_t)(n * p.n_shapes)),
-                       dim3(kStThreads), 0, s, p);
+    const int nb = (H + kPlanBand - 1) / kPlanBand;
+    bands.assign((size_t)nb, PlanBand{0, 0, H, -1});
+    int dy = 0;
+    for (int b = 0; b < nb; ++b) {
+        const int y1 = std::min(H, (b + 1) * kPlanBand);
+        PlanBand& e = bands[(size_t)b];
+        e.dlo = dy;
+        while (dy < dh && (b == nb - 1 || wfirst[(size_t)dy] < y1)) ++dy;
+        e.dhi = dy;
+        if (e.dlo < e.dhi) {
+            e.ya = wfirst[(size_t)e.dlo];
+            e.yb = wlast[(size_t)e.dhi - 1];
+        }
+    }
+    return true;
+}
+
+hipError_t launch_plan_area(const PlanParams& p, int64_t n, int max_h, int rounds, hipStream_t s)
+{
+    if (n <= 0 || max_h <= 0) return hipSuccess;
+    if (p.C != 3 || rounds < 1 || rounds > kPlanRounds || p.n_shapes < 1 || p.n_shapes > kPlanShapes ||
+        p.bands != (max_h + kPlanBand - 1) / kPlanBand || n * p.bands > INT32_MAX)
+        return hipErrorInvalidValue;
+    const dim3 grid((uint32_t)(n * p.bands));
+    switch (rounds) {
+    case 1: hipLaunchKernelGGL(plan_area_kernel<1>, grid, dim3(kStThreads), 0, s, p); break;
+    case 2: hipLaunchKernelGGL(plan_area_kernel<2>, grid, dim3(kStThreads), 0, s, p); break;
+    case 3: hipLaunchKernelGGL(plan_area_kernel<3>, grid, dim3(kStThreads), 0, s, p); break;
+    case 4: hipLaunchKernelGGL(plan_area_kernel<4>, grid, dim3(kStThreads), 0, s, p); break;
+    case 5: hipLaunchKernelGGL(plan_area_kernel<5>, grid, dim3(kStThreads), 0, s, p); break;
+    default: hipLaunchKernelGGL(plan_area_kernel<6>, grid, dim3(kStThreads), 0, s, p); break;
+    }
     return hipGetLastError();
 }
 

@@ -68,17 +68,8 @@ def _read(paths: Sequence) -> list:
     return read_files(paths)
 
 
-def get_img_matrix(file_paths: Sequence, shapes: Iterable, depths, interpolation: int = 3, border_type: int = 1,
-                   border_constant: int = 0, device: int | None = None,
-                   errors: str = "raise") -> dict:
-    """``_get_img_batch(file_paths, shape)`` at ``self.depth = depth`` for every
-    (shape, depth) pair, from one native call: ``{(shape, depth): (batch_images,
-    batch_icons)}`` with ``shape = (width, height)``.  errors: as
-    :func:`wicca_amd.get_img_batch` ("raise" or "zero")."""
+def _matrix_args(file_paths, shapes, depths, interpolation, border_type, border_constant, device):
     from .coder import _border_value
-    from .jpeg import _load_error, _slot_error
-    if errors not in ("raise", "zero"):
-        raise ValueError("errors must be 'raise' or 'zero'")
     shp = []
     for s in shapes:
         s = _norm_shape(s)
@@ -92,30 +83,92 @@ def get_img_matrix(file_paths: Sequence, shapes: Iterable, depths, interpolation
     blobs = _read(file_paths)
     n = len(blobs)
     keep = [np.frombuffer(b, np.uint8) for b in blobs]
-    ptrs = (ctypes.c_void_p * n)(*[k.ctypes.data for k in keep])
-    sizes = (ctypes.c_int64 * n)(*[k.size for k in keep])
     # pinned host outputs: the device-to-host copies run by DMA, not as blit
-    # kernels sharing the GPU with the plan's kernels
+    # kernels sharing the GPU with the plan's kernels (and, asynchronously,
+    # without holding the host)
     resized = [_lib.pinned_empty((n, h, w, 3)) for (w, h) in shp]
     icons = [[_lib.pinned_empty((n, h, w, 3)) for _ in dep] for (w, h) in shp]
-    c_shapes = (ctypes.c_int64 * (2 * len(shp)))(*[v for s in shp for v in s])
-    c_depths = (ctypes.c_int * len(dep))(*dep)
-    c_res = (ctypes.c_void_p * len(shp))(*[r.ctypes.data for r in resized])
-    c_ico = (ctypes.c_void_p * (len(shp) * len(dep)))(*[a.ctypes.data for row in icons for a in row])
     k = _border_value(border_constant) if int(border_type) == 0 else 0
-    status = (ctypes.c_int * n)() if errors == "zero" else None
-    _lib.check(_lib.load().wicca_image_stage_plan_u8(
-        ptrs, sizes, n, c_shapes, len(shp), c_depths, len(dep), int(border_type), k, int(interpolation),
-        c_res, c_ico, -1 if device is None else int(device), status))
-    del keep
-    if status is not None:
-        for i in range(n):
-            if status[i] != 0:  # as load_image reports it (data_loader.py:61-63)
-                print(f"Error loading image {file_paths[i]}: {_load_error(_slot_error(blobs[i]))}")
+    args = ((ctypes.c_void_p * n)(*[b.ctypes.data for b in keep]), (ctypes.c_int64 * n)(*[b.size for b in keep]), n,
+            (ctypes.c_int64 * (2 * len(shp)))(*[v for s in shp for v in s]), len(shp),
+            (ctypes.c_int * len(dep))(*dep), len(dep), int(border_type), k, int(interpolation),
+            (ctypes.c_void_p * len(shp))(*[r.ctypes.data for r in resized]),
+            (ctypes.c_void_p * (len(shp) * len(dep)))(*[a.ctypes.data for row in icons for a in row]),
+            -1 if device is None else int(device))
     out = {}
     for si, s in enumerate(shp):
         for di, d in enumerate(dep):
             out[(s, d)] = (resized[si], icons[si][di])
+    return blobs, keep, args, out
+
+
+class MatrixCall:
+    """An issued :func:`get_img_matrix_async`; :meth:`wait` gives the matrix."""
+
+    def __init__(self, ticket: int, keep, out: dict):
+        self._ticket = ticket
+        self._keep = keep  # the file bytes and argument arrays, alive until the wait
+        self._out = out
+
+    def wait(self) -> dict:
+        if self._ticket is not None:
+            ticket, self._ticket = self._ticket, None
+            try:
+                _lib.check(_lib.load().wicca_image_stage_plan_wait(ticket))
+            finally:
+                self._keep = None
+        return self._out
+
+    def __del__(self):
+        if getattr(self, "_ticket", None) is not None:  # dropped unwaited: the native side must be done with the arrays
+            try:
+                _lib.load().wicca_image_stage_plan_wait(self._ticket)
+            except Exception:
+                pass
+
+
+def get_img_matrix_async(file_paths: Sequence, shapes: Iterable, depths, interpolation: int = 3,
+                         border_type: int = 1, border_constant: int = 0,
+                         device: int | None = None) -> MatrixCall:
+    """:func:`get_img_matrix` (errors "raise") without waiting for the device:
+    the batch's host work, decode, plan kernels and output copies are queued
+    (``wicca_image_stage_plan_async``) and its kernels run after the previous
+    asynchronous call's, so a loop that issues batch k+1 before waiting for
+    batch k overlaps k+1's host work and k's output copies with the kernels."""
+    blobs, keep, args, out = _matrix_args(file_paths, shapes, depths, interpolation, border_type,
+                                          border_constant, device)
+    if args[2] == 0:
+        return MatrixCall(None, None, out)
+    ticket = ctypes.c_int64(0)
+    _lib.check(_lib.load().wicca_image_stage_plan_async(*args, ctypes.byref(ticket)))
+    return MatrixCall(ticket.value, (blobs, keep, args), out)
+
+
+def get_img_matrix(file_paths: Sequence, shapes: Iterable, depths, interpolation: int = 3, border_type: int = 1,
+                   border_constant: int = 0, device: int | None = None,
+                   errors: str = "raise") -> dict:
+    """``_get_img_batch(file_paths, shape)`` at ``self.depth = depth`` for every
+    (shape, depth) pair, from one native call: ``{(shape, depth): (batch_images,
+    batch_icons)}`` with ``shape = (width, height)``.  errors: as
+    :func:`wicca_amd.get_img_batch` ("raise" or "zero").  With "raise" the call
+    goes through the asynchronous entry (issue, then wait): concurrent calls'
+    kernels then queue on the device one after another while their host work
+    overlaps, instead of contending for the GPU."""
+    from .jpeg import _load_error, _slot_error
+    if errors not in ("raise", "zero"):
+        raise ValueError("errors must be 'raise' or 'zero'")
+    if errors == "raise":
+        return get_img_matrix_async(file_paths, shapes, depths, interpolation, border_type, border_constant,
+                                    device).wait()
+    blobs, keep, args, out = _matrix_args(file_paths, shapes, depths, interpolation, border_type,
+                                          border_constant, device)
+    n = args[2]
+    status = (ctypes.c_int * n)()
+    _lib.check(_lib.load().wicca_image_stage_plan_u8(*args, status))
+    del keep
+    for i in range(n):
+        if status[i] != 0:  # as load_image reports it (data_loader.py:61-63)
+            print(f"Error loading image {file_paths[i]}: {_load_error(_slot_error(blobs[i]))}")
     return out
 
 
