@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--tiled-as-rank", default="", help=argparse.SUPPRESS)
     ap.add_argument("--plan-no-loop", action="store_true",
                     help="--config plan: skip the per-call loop and its check (profiling runs)")
-    ap.add_argument("--plan-batches", type=int, default=6,
+    ap.add_argument("--plan-batches", type=int, default=12,
                     help="--config plan: batches of distinct files the StagePlan loop walks")
     ap.add_argument("--kernel-only", action="store_true",
                     help="--config jpeg / plan: only the synchronous calls (the kernel-trace child run)")
@@ -873,6 +873,13 @@ def run_plan(args, torch, rank):
 
         def loop(ahead, copy=True):
             sp = StagePlan(DEMO_CLASSIFIERS, depths, args.interpolation, batches=batches, ahead=ahead, copy=copy)
+            done = []  # when each batch's computation finished (s from the loop start)
+            compute = sp._compute
+
+            def timed(*a, **kw):
+                compute(*a, **kw)
+                done.append(time.perf_counter() - t)
+            sp._compute = timed
 
             def classify(shape, d):
                 for paths in batches:
@@ -884,7 +891,12 @@ def run_plan(args, torch, rank):
                     list(ex.map(lambda shp: classify(shp, d), DEMO_CLASSIFIERS))
             wall = time.perf_counter() - t
             sp.close()
-            return wall, dict(sp.stats)
+            done.sort()
+            stats = dict(sp.stats)
+            stats["first_batch_ms"] = round(done[0] * 1e3, 2) if done else None
+            stats["steady_ms_per_batch"] = (round((done[-1] - done[0]) / (len(done) - 1) * 1e3, 3)
+                                            if len(done) > 1 else None)
+            return wall, stats
 
         loop(2, copy=False)  # warm: workspaces, the pinned pool, the page cache
         loop_wall, loop_stats = loop(2, copy=False)
@@ -962,6 +974,9 @@ def run_plan(args, torch, rank):
                    "images": B, "batches": NB, "classifiers": len(DEMO_CLASSIFIERS), "depths": depths,
                    "pairs": pairs},
         "loop_stats": loop_stats,
+        "steady_ms_per_batch": loop_stats.get("steady_ms_per_batch"),
+        "steady_what": "(last batch computed - first batch computed) / (batches - 1) in the timed loop: "
+                       "the pipeline's rate without its fill; value is the whole loop / batches",
         "outputs": "StagePlan(copy=False): every classifier of a (shape, depth) gets the batch's one cached "
                    "pair of arrays, read-only",
         "no_overlap": {"ms_per_batch": round(serial_wall / NB * 1e3, 3),

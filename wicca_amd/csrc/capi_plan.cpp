@@ -49,14 +49,18 @@ struct PlanShape {
     int64_t w, h;
 };
 
-// Where the icons' copies to the caller go (WICCA_PLAN_COPY; tuning): 0 = the
-// workspace's copy stream, overlapping the source resizes; 1 = the compute
-// stream, behind every kernel of the call
+// Where the icons' copies to the caller go (WICCA_PLAN_COPY): 1 (default) =
+// the compute stream, behind every kernel of the call, where the runtime
+// moves them by SDMA (~52 GB/s, no CU); 0 = the workspace's copy stream,
+// overlapping the source resizes -- a stream waiting on another's event gets
+// its device-to-host copies as blit kernels, 256 workgroups held for the
+// PCIe transfer, and the source launch beside them ran 2.5 ms instead of 0.9
+// (profiles/r05t_*, r05v_*)
 int plan_copy_mode()
 {
     static const int m = [] {
         const char* e = getenv("WICCA_PLAN_COPY");
-        return e ? atoi(e) : 0;
+        return e ? atoi(e) : 1;
     }();
     return m;
 }
@@ -572,8 +576,9 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         for (const wicca::ResizeParams& q : rest)
             if ((rc = run_resize(q, q.src, q.src_pitch, 0, q.dst, q.dst_pitch, 0, 1, cs, ws))) return rc;
     }
-    // the icons' copies to the caller (5/6 of the output bytes at 5 depths)
-    // leave on the copy stream while the source resizes below run
+    // the icons' copies to the caller (5/6 of the output bytes at 5 depths):
+    // on the copy stream (WICCA_PLAN_COPY=0) they leave while the source
+    // resizes below run
     HIP_TRY(ws->ensure_pipeline());
     hipEvent_t icons_done = ws->slot_ready[0];  // the workspace is this call's alone
     HIP_TRY(hipEventRecord(icons_done, cs));
@@ -588,9 +593,8 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                 return rc;
         }
     // 5. the np.stack of :323 for every (shape, depth), to the caller's arrays:
-    // the icons from the copy stream (every kernel is already queued on cs, so
-    // a copy that holds the host thread does not hold the GPU), then the
-    // resized sources behind their kernels
+    // the icons, then the resized sources, behind every kernel (see
+    // plan_copy_mode)
     const int copy_mode = plan_copy_mode();
     hipStream_t icon_stream = copy_mode == 0 ? ws->copy_stream : cs;
     if (copy_mode == 0) HIP_TRY(hipStreamWaitEvent(ws->copy_stream, icons_done, 0));

@@ -62,19 +62,18 @@ __device__ __forceinline__ void area_window_row(const uint8_t* b, uint32_t s1len
     const int ia = max(3 * s1 - 3, 0);
     f32x2 a01 = f32x2{0.f, 0.f} + f32x2{(float)b[ia], (float)b[ia + 1]} * f32x2{wa, wa};
     float a2 = 0.f + (float)b[ia + 2] * wa;
-    // full cells, four pixels (12 bytes) a step
+    // full cells, four pixels (12 bytes) a group: three aligned dwords
+    // realigned; sixteen pixels a step from 13 dwords read together (one LDS
+    // wait per 16 pixels: the compiler places a step's reads next to their
+    // first use, so a step of one group waited once per group)
     const int base = 3 * s1;
     const uint32_t* w = reinterpret_cast<const uint32_t*>(b + (base & ~3));
     const uint32_t sh = (uint32_t)(base & 3);
     const int G = len >> 2;
-    uint32_t d0 = w[0];
-    for (int g = 0; g < G; ++g) {
-        const uint32_t d1 = w[1], d2 = w[2], d3 = w[3];
-        w += 3;
+    auto group = [&](uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3) {
         const uint32_t r0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
         const uint32_t r1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
         const uint32_t r2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-        d0 = d3;
         // pixel 0: r0.0 r0.1 r0.2 | 1: r0.3 r1.0 r1.1 | 2: r1.2 r1.3 r2.0 | 3: r2.1 r2.2 r2.3
         a01 = a01 + f32x2{ub(r0, 0), ub(r0, 1)} * wm2;
         a2 = a2 + ub(r0, 2) * wm;
@@ -84,6 +83,19 @@ __device__ __forceinline__ void area_window_row(const uint8_t* b, uint32_t s1len
         a2 = a2 + ub(r2, 0) * wm;
         a01 = a01 + f32x2{ub(r2, 1), ub(r2, 2)} * wm2;
         a2 = a2 + ub(r2, 3) * wm;
+    };
+    int g = 0;
+    for (; g + 4 <= G; g += 4) {
+        const uint32_t* ww = w + 3 * g;
+        uint32_t e[13];
+#pragma unroll
+        for (int i = 0; i < 13; ++i) e[i] = ww[i];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) group(e[3 * k], e[3 * k + 1], e[3 * k + 2], e[3 * k + 3]);
+    }
+    for (; g < G; ++g) {
+        const uint32_t* ww = w + 3 * g;
+        group(ww[0], ww[1], ww[2], ww[3]);
     }
     // the rest of the full cells (0..3), then the last partial cell
     const int rem = len - 4 * G;
@@ -112,11 +124,7 @@ __device__ __forceinline__ void area_fast_row(const uint8_t* b, int s1, int len,
     const uint32_t sh = (uint32_t)(base & 3);
     const int G = len >> 2;
     uint32_t R = 0, Gs = 0, B = 0;
-    int j = rot;
-    uint32_t d0 = w0[3 * j];
-    for (int k = 0; k < G; ++k) {
-        const uint32_t* w = w0 + 3 * j;
-        const uint32_t d1 = w[1], d2 = w[2], d3 = w[3];
+    auto group = [&](uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3) {
         const uint32_t r0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
         const uint32_t r1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
         const uint32_t r2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
@@ -130,11 +138,28 @@ __device__ __forceinline__ void area_fast_row(const uint8_t* b, int s1, int len,
         B = __builtin_amdgcn_udot4(r0, 0x00010000u, B, false);
         B = __builtin_amdgcn_udot4(r1, 0x00000100u, B, false);
         B = __builtin_amdgcn_udot4(r2, 0x01000001u, B, false);
-        d0 = d3;
-        if (++j == G) {  // wrap to the window's first group
-            j = 0;
-            d0 = w0[0];
+    };
+    // four groups a step (their 16 dwords read together), from group rot round
+    int j = rot, k = 0;
+    for (; k + 4 <= G; k += 4) {
+        int jj[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            jj[i] = j;
+            j = j + 1 == G ? 0 : j + 1;
         }
+        uint32_t e[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int m = 0; m < 4; ++m) e[i][m] = w0[3 * jj[i] + m];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) group(e[i][0], e[i][1], e[i][2], e[i][3]);
+    }
+    for (; k < G; ++k) {
+        const uint32_t* w = w0 + 3 * j;
+        group(w[0], w[1], w[2], w[3]);
+        j = j + 1 == G ? 0 : j + 1;
     }
     const uint8_t* q = b + base + 12 * G;
     for (int i = 4 * G; i < len; ++i, q += 3) {

@@ -271,12 +271,27 @@ class StagePlan:
             self._new += 1
         return self.devices[idx % len(self.devices)]
 
-    def _compute(self, key, entry: _Entry, device) -> None:
+    def _compute(self, key, entry: _Entry, device, issued=None) -> None:
+        """Compute `entry`; `issued()` runs once the batch's native work is
+        queued (its host parse, de-stuffing and uploads done): the owner starts
+        the next batch's prefetch there, so the two batches' host work does
+        not compete and this batch's kernels go first."""
         paths, depth = key
+        depths = self.depths if depth is None else (depth,)
         try:
-            entry.result = self._matrix(list(paths), self.shapes, self.depths if depth is None else (depth,),
-                                        self.interpolation, self.border_type, self.border_constant, device,
-                                        self.errors)
+            if self._matrix is get_img_matrix and self.errors == "raise":
+                call = get_img_matrix_async(list(paths), self.shapes, depths, self.interpolation, self.border_type,
+                                            self.border_constant, device)
+                if issued is not None:
+                    issued()
+                    issued = None
+                entry.result = call.wait()
+            else:
+                if issued is not None:
+                    issued()
+                    issued = None
+                entry.result = self._matrix(list(paths), self.shapes, depths, self.interpolation,
+                                            self.border_type, self.border_constant, device, self.errors)
             if not self.copy:  # shared by every requester: read-only
                 for pair in entry.result.values():
                     for a in pair:
@@ -286,6 +301,11 @@ class StagePlan:
         except BaseException as e:  # the requesters waiting now see the failure ...
             entry.error = e
         finally:
+            if issued is not None:  # the issue failed: the prefetch still starts
+                try:
+                    issued()
+                except BaseException:
+                    pass
             with self._lock:
                 self.stats["computed"] += 1
                 if self._entries.get(key) is entry:
@@ -351,11 +371,12 @@ class StagePlan:
             else:
                 self._entries.move_to_end(key)
                 self.stats["hits"] += 1
-        if self._batches is not None:
-            self._start_prefetch(key)
+        prefetch = (lambda: self._start_prefetch(key)) if self._batches is not None else None
         if owner:
-            self._compute(key, entry, dev)
+            self._compute(key, entry, dev, issued=prefetch)
         else:
+            if prefetch is not None:
+                prefetch()
             entry.event.wait()
         return entry
 
