@@ -42,7 +42,26 @@ def decode_rgb(data: bytes, apply_orientation: bool = True, truncated: bool = Fa
         ImageFile.LOAD_TRUNCATED_IMAGES = prev
     if apply_orientation:
         im = ImageOps.exif_transpose(im)
+    if im.mode == "CMYK":
+        return cmyk_to_rgb_imread(np.asarray(im))
     return np.asarray(im.convert("RGB")).copy()
+
+
+def cmyk_to_rgb_imread(cmyk: np.ndarray) -> np.ndarray:
+    """What ``cv2.imread`` + ``cvtColor(BGR2RGB)`` makes of a four-component
+    JPEG whose libjpeg-turbo CMYK output Pillow returned as ``cmyk``.
+
+    Pillow reads every CMYK JPEG as rawmode ``CMYK;I`` ("assume adobe
+    conventions", JpegImagePlugin.py), so libjpeg's own output is ``255 -
+    cmyk``.  OpenCV's JpegDecoder asks libjpeg for JCS_CMYK and converts each
+    pixel with ``icvCvt_CMYK2BGR_8u_C4C3R``: c = k - ((255 - c) * k >> 8),
+    likewise m and y, BGR = (y, m, c), i.e. RGB = (c, m, y).  Restated from
+    OpenCV's published source (cv2 is absent here): this last step is parity
+    unpinned; libjpeg's CMYK / YCCK decode before it is pinned through
+    Pillow."""
+    raw = 255 - cmyk.astype(np.int32)
+    k = raw[..., 3:4]
+    return (k - (((255 - raw[..., :3]) * k) >> 8)).astype(np.uint8)
 
 
 _FAKE_EOI_TAIL = b"\xff\xd9" * 32769  # covers a 65535-byte marker segment read from the tail

@@ -612,3 +612,151 @@ def test_clean_low_entropy_files_are_not_flagged_damaged(tmp_path):
         assert np.array_equal(imgs[i], R.resize(w, (224, 224), R.INTER_AREA)), i
     list(wicca_amd.get_img_batches([paths[:9], paths[9:]], (224, 224), 3))
     assert lib.wicca_jpeg_damaged_redone() == before
+
+
+# --- colour spaces: libjpeg-turbo's default_decompress_parms (jdapimin.c) picks
+# YCbCr / RGB for three components from the JFIF and Adobe markers and the
+# component ids, CMYK / YCCK for four from the Adobe transform; cv2.imread
+# then converts CMYK to BGR (oracle/jpeg_pil.py cmyk_to_rgb_imread).
+
+def _segments(data):
+    """(marker, start, end) of every marker segment before the first SOS."""
+    out, pos = [], 2
+    while pos < len(data):
+        assert data[pos] == 0xFF
+        m = data[pos + 1]
+        ln = int.from_bytes(data[pos + 2:pos + 4], "big")
+        out.append((m, pos, pos + 2 + ln))
+        if m == 0xDA:
+            break
+        pos += 2 + ln
+    return out
+
+
+def _strip(data, marker):
+    for m, a, b in _segments(data):
+        if m == marker:
+            return data[:a] + data[b:]
+    raise AssertionError(f"no marker {marker:#x}")
+
+
+def _with_jfif(data):
+    app0 = b"\xff\xe0\x00\x10JFIF\x00\x01\x01\x00\x00\x01\x00\x01\x00\x00"
+    return data[:2] + app0 + data[2:]
+
+
+def _set_ids(data, ids):
+    """Component ids in SOF and SOS (a single-scan file)."""
+    d = bytearray(data)
+    for m, a, b in _segments(data):
+        if m in (0xC0, 0xC1, 0xC2):
+            for c, v in enumerate(ids):
+                d[a + 10 + 3 * c] = v
+        if m == 0xDA:
+            for c, v in enumerate(ids):
+                d[a + 5 + 2 * c] = v
+    return bytes(d)
+
+
+def _adobe_transform(data, t):
+    d = bytearray(data)
+    j = d.find(b"Adobe")
+    d[j + 11] = t
+    return bytes(d)
+
+
+def _rgb_jpeg(img, q=90):
+    import io
+
+    from PIL import Image
+    b = io.BytesIO()
+    Image.fromarray(img).save(b, "JPEG", quality=q, keep_rgb=True)
+    return b.getvalue()
+
+
+def _cmyk_jpeg(img, q=90, progressive=False):
+    import io
+
+    from PIL import Image
+    b = io.BytesIO()
+    Image.fromarray(img).convert("CMYK").save(b, "JPEG", quality=q, progressive=progressive)
+    return b.getvalue()
+
+
+def _colour_files():
+    files = []
+    for i, (H, W) in enumerate(((64, 80), (135, 241), (17, 33), (480, 640))):
+        img = J.test_image("scene" if i % 2 == 0 else "noise", H, W, 90 + i)
+        rgb = _rgb_jpeg(img, 85 + i)
+        files += [
+            ("rgb-adobe", rgb),                                    # Adobe transform 0, ids 'R' 'G' 'B'
+            ("rgb-ids", _strip(rgb, 0xEE)),                        # no marker, ids 'R' 'G' 'B'
+            ("rgb-as-ycc-ids", _set_ids(_strip(rgb, 0xEE), (1, 2, 3))),  # ids 1 2 3: YCbCr
+            ("rgb-jfif", _with_jfif(rgb)),                         # JFIF wins: YCbCr
+            ("cmyk", _cmyk_jpeg(img, 90)),                         # Adobe transform 0: CMYK
+            ("cmyk-prog", _cmyk_jpeg(img, 80, progressive=True)),  # host entropy decode, progressive
+            ("ycck", _adobe_transform(_cmyk_jpeg(img, 90), 2)),    # Adobe transform 2: YCCK
+            ("cmyk-nomarker", _strip(_cmyk_jpeg(img, 90), 0xEE)),  # no Adobe marker: plain CMYK
+        ]
+    return files
+
+
+def test_colour_spaces_match_imread():
+    """RGB-colour-space JPEGs (keep_rgb, with and without the Adobe marker,
+    under a JFIF marker), Adobe CMYK (baseline and progressive), YCCK and
+    marker-less CMYK, one batch with ordinary YCbCr files: every image as
+    cv2.imread gives it (libjpeg-turbo through Pillow, OpenCV's CMYK -> BGR
+    restated)."""
+    files = _colour_files()
+    plain = [J.encode(J.test_image("scene", 96, 128, 5), 90, 2), J.encode(J.test_image("gray", 40, 50, 6), 90)]
+    blobs = [d for _, d in files] + plain
+    outs = WJ.decode_batch(blobs)
+    for (name, d), got in zip(files, outs):
+        want = J.decode_rgb(d)
+        assert got.shape == want.shape, name
+        assert np.array_equal(got, want), name
+    for d, got in zip(plain, outs[len(files):]):
+        assert np.array_equal(got, J.decode_rgb(d))
+
+
+def test_colour_spaces_separate_backend(tmp_path):
+    """The same files through the separate IDCT / colour launches
+    (WICCA_JPEG_FUSED=0), in a child process."""
+    import subprocess
+    import sys
+    files = _colour_files()
+    want = {f"w{i}": J.decode_rgb(d) for i, (_, d) in enumerate(files)}
+    np.savez(tmp_path / "want.npz", **want)
+    for i, (_, d) in enumerate(files):
+        (tmp_path / f"f{i}.jpg").write_bytes(d)
+    code = (
+        "import sys, numpy as np\n"
+        "from wicca_amd import jpeg as WJ\n"
+        f"d = {str(tmp_path)!r}\n"
+        f"n = {len(files)}\n"
+        "want = np.load(d + '/want.npz')\n"
+        "outs = WJ.decode_batch([open(f'{d}/f{i}.jpg', 'rb').read() for i in range(n)])\n"
+        "bad = [i for i in range(n) if not np.array_equal(outs[i], want[f'w{i}'])]\n"
+        "print('BAD', bad)\n"
+        "sys.exit(1 if bad else 0)\n")
+    env = dict(os.environ, WICCA_JPEG_FUSED="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_cmyk_file_caller_stage(tmp_path):
+    """A CMYK and an RGB-colour-space file through the file caller stage
+    (_get_img_batch) equal the resize and icon of their imread decode."""
+    img = J.test_image("scene", 300, 400, 11)
+    paths = []
+    for name, d in (("c.jpg", _cmyk_jpeg(img)), ("r.jpg", _rgb_jpeg(img)), ("y.jpg", J.encode(img, 90, 2))):
+        p = tmp_path / name
+        p.write_bytes(d)
+        paths.append(str(p))
+    imgs, icons = wicca_amd.get_img_batch(paths, (224, 224), 3)
+    for i, p in enumerate(paths):
+        rgb = J.decode_rgb(open(p, "rb").read())
+        assert np.array_equal(imgs[i], R.resize(rgb, (224, 224), R.INTER_AREA)), p
+        icon = c_oracle.ll_int_block(rgb, 3, 1, 0)[0]
+        assert np.array_equal(icons[i], R.resize(icon, (224, 224), R.INTER_AREA)), p

@@ -271,7 +271,9 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     for (int64_t i = 0; i < n; ++i) {
         int rc = parse_one(data[i], sizes[i], &info[(size_t)i], i);
         if (rc) return rc;
-        if (force_host) make_host_scan(info[(size_t)i]);
+        // four-component files: the host entropy decoder (the device Huffman
+        // passes keep three components' DC predictors per lane)
+        if (force_host || info[(size_t)i].ncomp > wicca::kJpegDevComp) make_host_scan(info[(size_t)i]);
     }
     // coefficient layout: image i's components back to back from coef0[i]
     // blocks (component c: bw x bh blocks); multi-scan files (progressive,
@@ -410,13 +412,14 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
             }
             im.comp_block0[c] = coef_blocks;
             coef_blocks += (int64_t)k.bw * k.bh;  // == coef0[i] + the earlier components
-            if (c > 0 || !wicca::jpeg_fused()) {  // the fused back end keeps luma in LDS
+            if (c > 0 || !wicca::jpeg_fused() || f.ncomp == 4) {  // the fused back end keeps luma in LDS
                 im.comp_plane0[c] = plane_bytes;
                 plane_bytes += round_up((int64_t)k.bw * 8 * k.bh * 8, 256);
             }
             memcpy(im.qt[c], k.q, sizeof(im.qt[c]));
         }
         im.fmt = wicca::kJpegFmtOther;  // the fused kernel's chroma path
+        im.xform = f.xform;
         if (f.ncomp == 1) {
             im.fmt = wicca::kJpegFmtGray;
         } else if (f.ncomp == 3) {

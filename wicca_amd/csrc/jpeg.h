@@ -21,8 +21,19 @@
 
 namespace wicca {
 
-constexpr int kJpegMaxComp = 3;
+constexpr int kJpegMaxComp = 4;   // components of a file (gray, YCbCr / RGB, CMYK / YCCK)
+constexpr int kJpegDevComp = 3;   // components of a file the device Huffman decode takes (4: host)
 constexpr int kJpegMaxSlots = 10;  // blocks per MCU (baseline limit)
+
+// The file's colour space as libjpeg-turbo's default_decompress_parms
+// (jdapimin.c) decides it from the JFIF / Adobe markers and component ids,
+// and the conversion cv2.imread then applies (JpegImageDev::xform).
+enum : int32_t {
+    kJpegXformYcc = 0,   // YCbCr -> RGB (jdcolor.c), or gray
+    kJpegXformRgb = 1,   // RGB components as they are (Adobe transform 0, or ids 'R' 'G' 'B')
+    kJpegXformCmyk = 2,  // CMYK, then OpenCV's CMYK -> BGR
+    kJpegXformYcck = 3,  // YCCK -> CMYK (jdcolor.c ycck_cmyk_convert), then as CMYK
+};
 
 struct JpegHuffTable {
     uint8_t bits[17];  // bits[l] = number of codes of length l (1..16)
@@ -66,6 +77,9 @@ struct JpegInfo {
     bool dc_present[4] = {false, false, false, false}, ac_present[4] = {false, false, false, false};
     int restart_interval = 0;   // MCUs per restart segment (0: one segment)
     int orientation = 1;        // EXIF orientation tag (1 = as stored)
+    bool jfif = false, adobe = false;  // APP0 JFIF / APP14 Adobe markers seen (jdmarker.c)
+    int adobe_transform = 0;
+    int xform = kJpegXformYcc;  // kJpegXform*
     const uint8_t* scan = nullptr;  // entropy-coded data (stuffed, with RST markers)
     size_t scan_len = 0;
     int64_t total_blocks() const { return (int64_t)mcux * mcuy * bpm; }
@@ -76,7 +90,7 @@ struct JpegInfo {
 // sequential file is parsed to its end and its scans listed (host_scans).
 // Returns 0 or a negative code with *err set: -1 not a JPEG / corrupt /
 // truncated headers, -2 unsupported (lossless, hierarchical, arithmetic
-// coding, 12-bit, CMYK, unusual sampling).
+// coding, 12-bit, 2 components, unusual sampling).
 int jpeg_parse(const uint8_t* data, size_t size, JpegInfo* info, std::string* err);
 
 // Entropy-decode every scan of a host_scans file into coef (the image's
@@ -139,7 +153,9 @@ enum : int32_t {
 
 struct JpegImageDev {
     int32_t W, H, ncomp, bpm, mcux, hmax, vmax;
-    int32_t fmt;  // kJpegFmt*
+    int32_t fmt;    // kJpegFmt*
+    int32_t xform;  // kJpegXform*
+    int32_t pad_[3];
     int32_t slot_comp[kJpegMaxSlots], slot_h[kJpegMaxSlots], slot_v[kJpegMaxSlots];
     int32_t comp_h[kJpegMaxComp], comp_v[kJpegMaxComp], comp_bw[kJpegMaxComp], comp_bh[kJpegMaxComp];
     int32_t comp_dw[kJpegMaxComp], comp_dh[kJpegMaxComp];
@@ -172,7 +188,7 @@ struct JpegPlan {
     int64_t n_sub, n_seg;
     int32_t sub_bits;        // subsequence length
     const int32_t* sub_img;  // per workgroup of kJpegLanes subsequences: its image (uniform)
-    int32_t max_tabs;        // most Huffman tables one image of the batch uses (<= 2 * kJpegMaxComp)
+    int32_t max_tabs;        // most Huffman tables one image of the batch uses (<= 2 * kJpegDevComp)
     int32_t* damage;         // per image: set by the write pass where the data is damaged (a code no
                              // table has, a run past coefficient 63, a segment whose data ends before
                              // its blocks do); the host redoes those images with the host decoder

@@ -62,7 +62,7 @@ struct DecState {
 struct SubResult {
     DecState end;
     int64_t started;  // blocks whose DC codeword starts in the lane's range
-    int32_t dc[kJpegMaxComp];
+    int32_t dc[kJpegDevComp];
     int32_t n_ck;     // round 0: checkpoints recorded (SyncCk)
 };
 
@@ -81,7 +81,7 @@ constexpr int kSyncCk = WICCA_JPEG_SYNC_CKS;
 struct SyncCk {
     uint32_t pos_slot;  // (p - lane start) | slot << 24
     int32_t started;    // blocks started before it
-    int32_t dc[kJpegMaxComp];
+    int32_t dc[kJpegDevComp];
     int32_t pad_;
 };
 
@@ -362,11 +362,11 @@ __device__ __forceinline__ int extend(uint32_t v, int s)
 // What the Huffman passes need of an image, staged in LDS per workgroup (a
 // register copy of the whole JpegImageDev spilled 712 B per lane to scratch).
 struct DecGeom {
-    int64_t comp_block0[kJpegMaxComp];
+    int64_t comp_block0[kJpegDevComp];
     int32_t bpm, mcux;
     int32_t slot_comp[kJpegMaxSlots], slot_h[kJpegMaxSlots], slot_v[kJpegMaxSlots];
-    int32_t comp_h[kJpegMaxComp], comp_v[kJpegMaxComp], comp_bw[kJpegMaxComp];
-    int32_t dc_tab[kJpegMaxComp], ac_tab[kJpegMaxComp];  // LDS table slots
+    int32_t comp_h[kJpegDevComp], comp_v[kJpegDevComp], comp_bw[kJpegDevComp];
+    int32_t dc_tab[kJpegDevComp], ac_tab[kJpegDevComp];  // LDS table slots
     uint32_t slot_tab[kJpegMaxSlots];  // per MCU slot: dc_tab | ac_tab << 8 | component << 16
 };
 
@@ -511,7 +511,7 @@ __device__ __forceinline__ void zero_zig(int16_t* coef, const uint8_t* nat, int6
 // and meanwhile CK 1's recording into ck_rec (*n_rec gets the count).
 template <bool WRITE, int CK = 0, typename HT = HuffDev, typename BR = BitReader>
 __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t stop,
-                          DecState& st, int64_t& started, int32_t (&dc)[kJpegMaxComp], int64_t g,
+                          DecState& st, int64_t& started, int32_t (&dc)[kJpegDevComp], int64_t g,
                           int64_t block_lo, int64_t block_end, int16_t* coef, const WaveStage* ws = nullptr,
                           bool seg_last = false, SyncCk* ck = nullptr, int n_ck = 0, int64_t ck_base = 0,
                           SyncCk* hit_ck = nullptr, int ck_step = 0, int32_t* damage = nullptr,
@@ -554,7 +554,7 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
             SyncCk e;
             e.pos_slot = (uint32_t)(br.pr + ck_off) | ((uint32_t)st.slot << 24);
             e.started = (int32_t)started + nstart;
-            for (int q = 0; q < kJpegMaxComp; ++q) e.dc[q] = dc[q];
+            for (int q = 0; q < kJpegDevComp; ++q) e.dc[q] = dc[q];
             e.pad_ = 0;
             rec[nrec++] = e;
         }
@@ -708,7 +708,7 @@ __device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageD
             g.slot_h[k] = imp->slot_h[k];
             g.slot_v[k] = imp->slot_v[k];
         }
-        for (int c = 0; c < kJpegMaxComp; ++c) {
+        for (int c = 0; c < kJpegDevComp; ++c) {
             g.comp_block0[c] = imp->comp_block0[c];
             g.comp_h[c] = imp->comp_h[c];
             g.comp_v[c] = imp->comp_v[c];
@@ -717,7 +717,7 @@ __device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageD
             g.ac_tab[c] = c < ncomp ? imp->ac_tab[c] - first : 0;
         }
         for (int k = 0; k < kJpegMaxSlots; ++k) {
-            const int c = min(max(g.slot_comp[k], 0), kJpegMaxComp - 1);
+            const int c = min(max(g.slot_comp[k], 0), kJpegDevComp - 1);
             g.slot_tab[k] = (uint32_t)g.dc_tab[c] | ((uint32_t)g.ac_tab[c] << 8) | ((uint32_t)c << 16);
         }
     }
@@ -805,7 +805,7 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(J
     SubResult r;
     r.started = 0;
     r.n_ck = 0;
-    int32_t dc[kJpegMaxComp] = {0, 0, 0};
+    int32_t dc[kJpegDevComp] = {0, 0, 0};
     SyncReader<CK> br;
     br.reset(P, i, b0, st.p);
     // checkpoints: two sets per lane (cks, then cks + n_sub * kSyncCk), the
@@ -833,11 +833,11 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(J
             const SubResult& o = r0res[i];  // read after the decode: fewer live registers in it
             st = o.end;
             r.started += o.started - h.started;
-            for (int c = 0; c < kJpegMaxComp; ++c) dc[c] += o.dc[c] - h.dc[c];
+            for (int c = 0; c < kJpegDevComp; ++c) dc[c] += o.dc[c] - h.dc[c];
         } else if (CK == 3) {  // a full decode from a new start: its checkpoints replace the old ones
             SubResult f = r;
             f.end = st;
-            for (int c = 0; c < kJpegMaxComp; ++c) f.dc[c] = dc[c];
+            for (int c = 0; c < kJpegDevComp; ++c) f.dc[c] = dc[c];
             f.n_ck = n_rec | ((set ^ 1) << 16);
             r0res[i] = f;
         }
@@ -845,7 +845,7 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(J
         decode_run<false, 0, HuffDevSync, SyncReader<CK>>(im, tabs.t, br, b1, st, r.started, dc, 0, 0, 0, nullptr);
     }
     r.end = st;
-    for (int c = 0; c < kJpegMaxComp; ++c) r.dc[c] = dc[c];
+    for (int c = 0; c < kJpegDevComp; ++c) r.dc[c] = dc[c];
     if (round > 0 && !same_state(prev[i].end, st)) *changed = 1;
     next[i] = r;
 }
@@ -854,7 +854,7 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(J
 // subsequences: one workgroup of 256 lanes per segment.
 struct SubBase {
     int64_t block;
-    int32_t dc[kJpegMaxComp];
+    int32_t dc[kJpegDevComp];
     int32_t pad_;
 };
 
@@ -863,50 +863,50 @@ __global__ __launch_bounds__(256) void jpeg_scan_kernel(JpegPlan P, const SubRes
     const JpegSegDev sg = P.segs[blockIdx.x];
     const int64_t n = sg.n_sub;
     __shared__ int64_t sb[256];
-    __shared__ int32_t sd[kJpegMaxComp][256];
+    __shared__ int32_t sd[kJpegDevComp][256];
     __shared__ int64_t carry_b;
-    __shared__ int32_t carry_d[kJpegMaxComp];
+    __shared__ int32_t carry_d[kJpegDevComp];
     const int t = threadIdx.x;
     if (t == 0) {
         carry_b = 0;
-        for (int c = 0; c < kJpegMaxComp; ++c) carry_d[c] = 0;
+        for (int c = 0; c < kJpegDevComp; ++c) carry_d[c] = 0;
     }
     __syncthreads();
     for (int64_t c0 = 0; c0 < n; c0 += 256) {
         const int64_t i = c0 + t;
         int64_t vb = 0;
-        int32_t vd[kJpegMaxComp] = {0, 0, 0};
+        int32_t vd[kJpegDevComp] = {0, 0, 0};
         if (i < n) {
             const SubResult& r = res[sg.sub0 + i];
             vb = r.started;
-            for (int c = 0; c < kJpegMaxComp; ++c) vd[c] = r.dc[c];
+            for (int c = 0; c < kJpegDevComp; ++c) vd[c] = r.dc[c];
         }
         sb[t] = vb;
-        for (int c = 0; c < kJpegMaxComp; ++c) sd[c][t] = vd[c];
+        for (int c = 0; c < kJpegDevComp; ++c) sd[c][t] = vd[c];
         __syncthreads();
         for (int off = 1; off < 256; off <<= 1) {  // Hillis-Steele inclusive scan
             int64_t ab = 0;
-            int32_t ad[kJpegMaxComp] = {0, 0, 0};
+            int32_t ad[kJpegDevComp] = {0, 0, 0};
             if (t >= off) {
                 ab = sb[t - off];
-                for (int c = 0; c < kJpegMaxComp; ++c) ad[c] = sd[c][t - off];
+                for (int c = 0; c < kJpegDevComp; ++c) ad[c] = sd[c][t - off];
             }
             __syncthreads();
             sb[t] += ab;
-            for (int c = 0; c < kJpegMaxComp; ++c) sd[c][t] += ad[c];
+            for (int c = 0; c < kJpegDevComp; ++c) sd[c][t] += ad[c];
             __syncthreads();
         }
         if (i < n) {
             SubBase b;
             b.block = carry_b + sb[t] - vb;  // exclusive
-            for (int c = 0; c < kJpegMaxComp; ++c) b.dc[c] = carry_d[c] + sd[c][t] - vd[c];
+            for (int c = 0; c < kJpegDevComp; ++c) b.dc[c] = carry_d[c] + sd[c][t] - vd[c];
             b.pad_ = 0;
             base[sg.sub0 + i] = b;
         }
         __syncthreads();
         if (t == 255) {
             carry_b += sb[255];
-            for (int c = 0; c < kJpegMaxComp; ++c) carry_d[c] += sd[c][255];
+            for (int c = 0; c < kJpegDevComp; ++c) carry_d[c] += sd[c][255];
         }
         __syncthreads();
     }
@@ -954,7 +954,7 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 4 : 1) void jpeg_write_kernel(
         st = res[i - 1].end;
     }
     const SubBase b = base[i];
-    int32_t dc[kJpegMaxComp] = {b.dc[0], b.dc[1], b.dc[2]};
+    int32_t dc[kJpegDevComp] = {b.dc[0], b.dc[1], b.dc[2]};
     int64_t started = 0;
     WriteReader br;
     br.reset(P, i, sg.bit0 + j * P.sub_bits, st.p);
@@ -1205,6 +1205,7 @@ __device__ __forceinline__ void color_row(const JpegPlan& P, const JpegImageDev&
     uint8_t o[12];
 #pragma unroll
     for (int i = 0; i < 12; ++i) o[i] = 0;
+    if (im.ncomp == 4) return;  // uniform: jpeg_cmyk_kernel
     if (nx > 0) {
         // the Y plane is whole 8x8 blocks wide and 256-B aligned: x0..x0+3 is inside
         const uint32_t y4 = *reinterpret_cast<const uint32_t*>(
@@ -1261,6 +1262,14 @@ __device__ __forceinline__ void color_row(const JpegPlan& P, const JpegImageDev&
                     crv[q] = chroma_sample(pr, sr, im.comp_dw[2], im.comp_dh[2], fh2, fv2, x, y);
                 }
             }
+            if (im.xform == kJpegXformRgb) {  // components are R, G, B (uniform)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    o[3 * q] = (uint8_t)(y4 >> (8 * q));
+                    o[3 * q + 1] = (uint8_t)cbv[q];
+                    o[3 * q + 2] = (uint8_t)crv[q];
+                }
+            } else
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int Y = (int)((y4 >> (8 * q)) & 255);
@@ -1470,6 +1479,23 @@ __device__ __forceinline__ void ycc8_pack(uint2 yv, const int (&cb)[8], const in
     w[5] = pack_b2(B[6], R[7], G[7], B[7]);
 }
 
+// The same 24 bytes for an RGB-colour-space file (JpegImageDev::xform
+// kJpegXformRgb): the three components as they are (cb / cr minus 128).
+__device__ __forceinline__ void rgb8_pack(uint2 yv, const int (&g)[8], const int (&b)[8], uint32_t (&w)[6])
+{
+    uint8_t o[24];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        o[3 * q] = (uint8_t)((q < 4 ? yv.x : yv.y) >> (8 * (q & 3)));
+        o[3 * q + 1] = (uint8_t)(g[q] + 128);
+        o[3 * q + 2] = (uint8_t)(b[q] + 128);
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        w[k] = (uint32_t)o[4 * k] | (uint32_t)o[4 * k + 1] << 8 | (uint32_t)o[4 * k + 2] << 16 |
+               (uint32_t)o[4 * k + 3] << 24;
+}
+
 // One 256 x 8-pixel tile per workgroup, specialised per chroma format
 // (JpegImageDev::fmt, chosen on the host): the IDCT lanes (block lb of the
 // tile, row r) and the colour lanes (tile row rr, pixels cx .. cx+7) are the
@@ -1630,7 +1656,10 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
                     crm[q] -= 128;
                 }
             }
-            ycc8_pack(yv, cbm, crm, w);
+            if (im.xform == kJpegXformRgb)  // uniform
+                rgb8_pack(yv, cbm, crm, w);
+            else
+                ycc8_pack(yv, cbm, crm, w);
         }
     }
     if (SAME) {
@@ -1710,6 +1739,7 @@ void jpeg_luma_color_kernel(JpegPlan P)
     }
     const JpegImageDev& im = P.imgs[tz];
     if (tx * kFuseW >= im.W || ty * 8 >= im.H) return;  // uniform: grid sized for the largest image
+    if (im.ncomp == 4) return;                           // uniform: jpeg_cmyk_kernel
     if (P.direct_rgb && (((uintptr_t)im.dst | (uintptr_t)im.dst_pitch) & 7) == 0) {  // uniform
         switch (im.fmt) {
         case kJpegFmtGray: luma_color_tile<kJpegFmtGray, true>(P, im, tx, ty, tr, ytile, stage, cwin); break;
@@ -1725,6 +1755,39 @@ void jpeg_luma_color_kernel(JpegPlan P)
     case kJpegFmtH1V1: luma_color_tile<kJpegFmtH1V1, false>(P, im, tx, ty, tr, ytile, stage, cwin); break;
     default: luma_color_tile<kJpegFmtOther, false>(P, im, tx, ty, tr, ytile, stage, cwin); break;
     }
+}
+
+// Four-component files (Adobe CMYK / YCCK, rare in photo sets): every
+// component's plane comes from jpeg_idct_kernel; one lane per output pixel
+// upsamples each component as jdsample.c does (chroma_sample), converts YCCK
+// to CMYK as jdcolor.c ycck_cmyk_convert does (255 - the YCbCr -> RGB result,
+// K unchanged), and applies cv2.imread's CMYK -> BGR (OpenCV
+// icvCvt_CMYK2BGR_8u_C4C3R: c = k - ((255 - c) * k >> 8), likewise m, y; as
+// RGB after load_image's BGR2RGB).  grid = (ceil(W / 256), H, images).
+__global__ __launch_bounds__(256) void jpeg_cmyk_kernel(JpegPlan P)
+{
+    const JpegImageDev& im = P.imgs[blockIdx.z];
+    if (im.ncomp != 4 || (int)blockIdx.y >= im.H) return;  // uniform
+    const int x = (int)blockIdx.x * 256 + (int)threadIdx.x, y = (int)blockIdx.y;
+    if (x >= im.W) return;
+    int v[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+        v[c] = chroma_sample(P.planes + im.comp_plane0[c], (int64_t)im.comp_bw[c] * 8, im.comp_dw[c], im.comp_dh[c],
+                             im.hmax / im.comp_h[c], im.vmax / im.comp_v[c], x, y);
+    if (im.xform == kJpegXformYcck) {
+        const int Y = v[0], cb = v[1] - 128, cr = v[2] - 128;
+        const int crr = (__mul24(91881, cr) + 32768) >> 16;
+        const int cbb = (__mul24(116130, cb) + 32768) >> 16;
+        const int g = (__mul24(-46802, cr) + (__mul24(-22554, cb) + 32768)) >> 16;
+        v[0] = 255 - (int)clamp255(Y + crr);
+        v[1] = 255 - (int)clamp255(Y + g);
+        v[2] = 255 - (int)clamp255(Y + cbb);
+    }
+    const int k = v[3];
+    uint8_t* d = im.dst + (int64_t)y * im.dst_pitch + (int64_t)x * 3;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = (uint8_t)(k - (((255 - v[c]) * k) >> 8));
 }
 
 // Off by default: measured on one box, contiguous runs cut the kernel's
@@ -1889,8 +1952,10 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     const bool fused = jpeg_fused();
     std::vector<IdctJob> hj;
     int64_t max_blocks = 0;
-    for (int64_t i = 0; i < n_images; ++i)
-        for (int c = fused ? 1 : 0; c < ims[(size_t)i].ncomp; ++c) {
+    bool any_cmyk = false;
+    for (int64_t i = 0; i < n_images; ++i) {
+        any_cmyk = any_cmyk || ims[(size_t)i].ncomp == 4;
+        for (int c = fused && ims[(size_t)i].ncomp != 4 ? 1 : 0; c < ims[(size_t)i].ncomp; ++c) {
             IdctJob j;
             j.block0 = ims[(size_t)i].comp_block0[c];
             j.plane0 = ims[(size_t)i].comp_plane0[c];
@@ -1901,7 +1966,28 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             hj.push_back(j);
             max_blocks = std::max<int64_t>(max_blocks, (int64_t)j.bw * j.bh);
         }
+    }
     if (hj.size() > (size_t)kJpegMaxJobs) return hipErrorInvalidValue;
+    // the four-component images' colour pass (after the back end's other launches)
+    auto cmyk_pass = [&]() -> hipError_t {
+        if (!any_cmyk) return hipSuccess;
+        int max_w = 0, max_h = 0;
+        for (int64_t i = 0; i < n_images; ++i)
+            if (ims[(size_t)i].ncomp == 4) {
+                max_w = std::max(max_w, ims[(size_t)i].W);
+                max_h = std::max(max_h, ims[(size_t)i].H);
+            }
+        for (int64_t i0 = 0; i0 < n_images; i0 += 65535) {
+            JpegPlan Q = P;
+            Q.imgs = P.imgs + i0;
+            hipLaunchKernelGGL(jpeg_cmyk_kernel, dim3((uint32_t)((max_w + 255) / 256), (uint32_t)max_h,
+                                                      (uint32_t)std::min<int64_t>(65535, n_images - i0)),
+                               dim3(256), 0, s, Q);
+            const hipError_t e2 = hipGetLastError();
+            if (e2 != hipSuccess) return e2;
+        }
+        return hipSuccess;
+    };
     if (pinned_jobs && !hj.empty()) memcpy(pinned_jobs, hj.data(), sizeof(IdctJob) * hj.size());
     hipError_t e = hj.empty() ? hipSuccess
                               : hipMemcpyAsync(jobs, pinned_jobs ? pinned_jobs : hj.data(), sizeof(IdctJob) * hj.size(),
@@ -1958,10 +2044,10 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
                 else if (ck == 3) WICCA_SYNC_LAUNCH(3, 4);
                 else WICCA_SYNC_LAUNCH(0, 4);
             } else {
-                if (ck == 1) WICCA_SYNC_LAUNCH(1, 2 * kJpegMaxComp);
-                else if (ck == 2) WICCA_SYNC_LAUNCH(2, 2 * kJpegMaxComp);
-                else if (ck == 3) WICCA_SYNC_LAUNCH(3, 2 * kJpegMaxComp);
-                else WICCA_SYNC_LAUNCH(0, 2 * kJpegMaxComp);
+                if (ck == 1) WICCA_SYNC_LAUNCH(1, 2 * kJpegDevComp);
+                else if (ck == 2) WICCA_SYNC_LAUNCH(2, 2 * kJpegDevComp);
+                else if (ck == 3) WICCA_SYNC_LAUNCH(3, 2 * kJpegDevComp);
+                else WICCA_SYNC_LAUNCH(0, 2 * kJpegDevComp);
             }
 #undef WICCA_SYNC_LAUNCH
             return hipGetLastError();
@@ -2030,7 +2116,7 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
         if (P.max_tabs <= 4 && !force6)
             hipLaunchKernelGGL(jpeg_write_kernel<4>, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
         else
-            hipLaunchKernelGGL(jpeg_write_kernel<2 * kJpegMaxComp>, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
+            hipLaunchKernelGGL(jpeg_write_kernel<2 * kJpegDevComp>, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     } else if (sync_rounds) {
         *sync_rounds = 0;
@@ -2065,7 +2151,7 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
                 hipLaunchKernelGGL(jpeg_luma_color_kernel<false>, grid, dim3(256), 0, s, Q);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
-        return hipSuccess;
+        return cmyk_pass();
     }
     // one launch over the batch unless the images differ so much in size that
     // the padded grid would be mostly empty workgroups
@@ -2089,7 +2175,7 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
                            dim3(256), 0, s, Q);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    return hipSuccess;
+    return cmyk_pass();
 }
 
 }  // namespace wicca

@@ -108,7 +108,7 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
     if (n < 4 || d[0] != 0xFF || d[1] != 0xD8) return bad(-1, "not a JPEG file (no SOI marker)");
     size_t pos = 2;
     bool have_sof = false;
-    int scan_ids[kJpegMaxComp] = {0, 1, 2};
+    int scan_ids[kJpegMaxComp] = {0, 1, 2, 3};
     for (int c = 0; c < kJpegMaxComp; ++c) info->comp[c].latched = false;
     // A file cut inside a marker segment after its first scan: cv2.imread
     // reads through libjpeg's stdio source manager, which feeds a fake EOI
@@ -152,8 +152,8 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
             info->W = u16be(s + 3);
             info->ncomp = s[5];
             if (info->H <= 0 || info->W <= 0) return bad(-2, "JPEG with DNL height is not supported");
-            if (info->ncomp != 1 && info->ncomp != 3)
-                return bad(-2, "only grayscale and 3-component (YCbCr) JPEG is supported");
+            if (info->ncomp != 1 && info->ncomp != 3 && info->ncomp != 4)
+                return bad(-2, "only 1-, 3- and 4-component JPEG is supported");
             if (sl < 6 + 3 * info->ncomp) return bad(-1, "bad SOF");
             for (int c = 0; c < info->ncomp; ++c) {
                 JpegComponent& k = info->comp[c];
@@ -203,6 +203,13 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
         } else if (m == 0xE1) {  // APP1: EXIF orientation
             const int o = exif_orientation(s, (size_t)sl);
             if (o != 1) info->orientation = o;
+        } else if (m == 0xE0) {  // APP0: JFIF (jdmarker.c examine_app0: 14 bytes at least)
+            if (sl >= 14 && memcmp(s, "JFIF\0", 5) == 0) info->jfif = true;
+        } else if (m == 0xEE) {  // APP14: Adobe (examine_app14: 12 bytes at least), its colour transform
+            if (sl >= 12 && memcmp(s, "Adobe", 5) == 0) {
+                info->adobe = true;
+                info->adobe_transform = s[11];
+            }
         } else if (m == 0xDA) {  // SOS
             if (!have_sof) return bad(-1, "SOS before SOF");
             if (sl < 1) return bad(-1, "bad SOS");
@@ -311,7 +318,7 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
         info->slot_h[0] = info->slot_v[0] = 0;
     } else {
         int hmax = 1, vmax = 1;
-        for (int c = 0; c < 3; ++c) {
+        for (int c = 0; c < info->ncomp; ++c) {
             hmax = std::max(hmax, info->comp[c].h);
             vmax = std::max(vmax, info->comp[c].v);
         }
@@ -320,7 +327,7 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
         // the colour pass reads the Y plane at full resolution
         if (info->comp[0].h != hmax || info->comp[0].v != vmax)
             return bad(-2, "only full-resolution luma sampling is supported");
-        for (int c = 0; c < 3; ++c) {
+        for (int c = 0; c < info->ncomp; ++c) {
             const int fh = hmax / info->comp[c].h, fv = vmax / info->comp[c].v;
             if (hmax % info->comp[c].h || vmax % info->comp[c].v || fh > 2 || fv > 2 || (fh == 1 && fv == 2))
                 return bad(-2, "only 4:4:4, 4:2:2 and 4:2:0 sampling is supported");
@@ -328,7 +335,7 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
         info->mcux = (info->W + 8 * hmax - 1) / (8 * hmax);
         info->mcuy = (info->H + 8 * vmax - 1) / (8 * vmax);
         int slot = 0;
-        for (int i = 0; i < 3; ++i) {
+        for (int i = 0; i < info->ncomp; ++i) {
             const int c = scan_ids[i];
             JpegComponent& k = info->comp[c];
             k.bw = info->mcux * k.h;
@@ -345,6 +352,18 @@ int jpeg_parse(const uint8_t* d, size_t n, JpegInfo* info, std::string* err)
                 }
         }
         info->bpm = slot;
+    }
+    // colour space (jdapimin.c default_decompress_parms)
+    if (info->ncomp == 3) {
+        const int i0 = info->comp[0].id, i1 = info->comp[1].id, i2 = info->comp[2].id;
+        if (info->jfif)
+            info->xform = kJpegXformYcc;
+        else if (info->adobe)
+            info->xform = info->adobe_transform == 0 ? kJpegXformRgb : kJpegXformYcc;
+        else
+            info->xform = (i0 == 82 && i1 == 71 && i2 == 66) ? kJpegXformRgb : kJpegXformYcc;  // 'R' 'G' 'B'
+    } else if (info->ncomp == 4) {
+        info->xform = info->adobe && info->adobe_transform != 0 ? kJpegXformYcck : kJpegXformCmyk;
     }
     if (info->host_scans) {  // an interleaved scan may hold at most 10 blocks per MCU (jdinput.c)
         for (const JpegScan& sc : info->scans) {

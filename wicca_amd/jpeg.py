@@ -18,8 +18,8 @@ points sniff each file (``wicca_image_*``), so a batch may mix formats.
 (``cv2.imread`` returns None for every file it cannot read and
 ``validate_image`` then raises that message, validation.py:94-95) and
 returns ``None``; ``WICCA_LOAD_DETAIL=1`` prints the decoder's own reason
-instead.  Files no decoder here handles (CMYK JPEG, JPEG-compressed TIFF,
-ASCII PNM, ...) fail that way too — there is no CPU fallback behind it.
+instead.  Files no decoder here handles (arithmetic-coded JPEG,
+JPEG-compressed TIFF, ASCII PNM, ...) fail that way too — there is no CPU fallback behind it.
 """
 from __future__ import annotations
 
