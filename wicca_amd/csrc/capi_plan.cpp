@@ -65,6 +65,20 @@ int plan_copy_mode()
     return m;
 }
 
+// WICCA_PLAN_OVERLAP (default 1): the next asynchronous call's kernels start
+// after this call's decode, not after its plan kernels -- its latency-bound
+// Huffman passes beside this call's HBM / VALU-bound plan kernels: 11.1
+// against 12.3 ms per batch with two batches ahead (12.9 against 12.2 with
+// one, profiles/r05af_*)
+int plan_overlap()
+{
+    static const int m = [] {
+        const char* e = getenv("WICCA_PLAN_OVERLAP");
+        return e ? atoi(e) : 1;
+    }();
+    return m;
+}
+
 // Shapes per area-kernel launch (WICCA_PLAN_GROUP, 1..kPlanShapes; tuning)
 int plan_group_shapes()
 {
@@ -193,6 +207,11 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
             if (ws->copy_stream) (void)hipStreamSynchronize(ws->copy_stream);
         }
     } drain{ws};
+    // WICCA_PLAN_OVERLAP=1: the next asynchronous call's kernels may start
+    // once this call's decode is done (its latency-bound Huffman passes beside
+    // this call's plan kernels) instead of after the plan kernels
+    const bool early_serial = as && plan_overlap();
+    if (early_serial && (rc = jpeg_serial_record(dev, cs))) return rc;
     double t_decoded = 0;
     if (timing) {
         HIP_TRY(hipStreamSynchronize(cs));
@@ -600,7 +619,7 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
     if (copy_mode == 0) HIP_TRY(hipStreamWaitEvent(ws->copy_stream, icons_done, 0));
     // the next asynchronous call's kernels may start once these are done:
     // the copies below overlap them
-    if (as && (rc = jpeg_serial_record(dev, cs))) return rc;
+    if (as && !early_serial && (rc = jpeg_serial_record(dev, cs))) return rc;
     for (int s = 0; s < S; ++s) {
         const size_t bytes = (size_t)(n * ob[(size_t)s]);
         for (int d = 0; d < n_depths; ++d)
