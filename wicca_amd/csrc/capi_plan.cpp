@@ -268,7 +268,7 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
     // the vertical tables of each distinct (source height, shape) geometry
     // (plan_vertical; -1: not a plain downscale, per-image resize instead)
     struct VTab {
-        int H, dh, ky;
+        int H, dh, ky, band;
         double scale_y;
         std::vector<wicca::PlanVRow> rows;
         std::vector<wicca::PlanBand> bands;
@@ -276,26 +276,32 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         size_t o_rows = 0, o_bands = 0;
     };
     std::vector<VTab> vtabs;
-    auto vtab_of = [&](const wicca::ResizeParams& rp, int s, int64_t h) -> int {
+    auto vtab_of = [&](const wicca::ResizeParams& rp, int s, int64_t h, int band) -> int {
         const int ky = rp.mode == wicca::RS_AREA_FAST ? rp.ky : 0;
         const int dh = (int)shapes[(size_t)s].h;
         for (size_t k = 0; k < vtabs.size(); ++k)
-            if (vtabs[k].H == (int)h && vtabs[k].dh == dh && vtabs[k].ky == ky && vtabs[k].scale_y == rp.scale_y)
+            if (vtabs[k].H == (int)h && vtabs[k].dh == dh && vtabs[k].ky == ky && vtabs[k].band == band &&
+                vtabs[k].scale_y == rp.scale_y)
                 return vtabs[k].ok ? (int)k : -1;
         VTab v;
         v.H = (int)h;
         v.dh = dh;
         v.ky = ky;
+        v.band = band;
         v.scale_y = rp.scale_y;
-        v.ok = wicca::plan_vertical((int)h, dh, rp.scale_y, ky, v.rows, v.bands);
+        v.ok = wicca::plan_vertical((int)h, dh, rp.scale_y, ky, band, v.rows, v.bands);
         vtabs.push_back(std::move(v));
         return vtabs.back().ok ? (int)vtabs.size() - 1 : -1;
     };
-    auto area_rows_ok = [&](const wicca::ResizeParams& rp, int s, int64_t h, int64_t w) {
+    // bands: 64 rows for the sources, 32 for the icons (1080 rows and fewer:
+    // a 64-row band left the icon launch's few workgroups a long tail, 744
+    // against 652 us, profiles/r05ai_*)
+    constexpr int kSrcBand = wicca::kPlanBand, kIconBand = wicca::kPlanBand / 2;
+    auto area_rows_ok = [&](const wicca::ResizeParams& rp, int s, int64_t h, int64_t w, int band) {
         const bool fast = rp.mode == wicca::RS_AREA_FAST;
         return (rp.mode == wicca::RS_AREA || fast) &&
                wicca::plan_area_ok(shapes[(size_t)s].w, 3, fast ? rp.kx : 1, fast ? rp.ky : 1) &&
-               wicca::stage_row_ok(w, 3) && h <= 65535 && vtab_of(rp, s, h) >= 0;
+               wicca::stage_row_ok(w, 3) && h <= 65535 && vtab_of(rp, s, h, band) >= 0;
     };
     // 4. icon resizes: (shape s, depth slot u, image i)
     std::vector<wicca::ResizeParams> irp((size_t)S * U * n);
@@ -330,10 +336,10 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         std::vector<std::vector<wicca::PlanTask>> tasks;
         std::vector<size_t> task_off;
         size_t off = 0;
-        int rounds = 0, max_h = 0;
+        int rounds = 0, max_h = 0, band = wicca::kPlanBand;
     };
     // want(s, j): image j's resize to shape s comes from the area kernel; rp(s, j), dst(s, j)
-    auto make_groups = [&](const std::vector<RowSrc>& im, auto want, auto rp_of, auto dst_of) {
+    auto make_groups = [&](const std::vector<RowSrc>& im, int band, auto want, auto rp_of, auto dst_of) {
         const int64_t m = (int64_t)im.size();
         std::vector<AreaGroup> gs;
         AreaGroup g;
@@ -354,6 +360,7 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         }
         if (!g.shapes.empty()) gs.push_back(std::move(g));
         for (AreaGroup& gr : gs) {
+            gr.band = band;
             gr.imgs.resize((size_t)m);
             gr.vt.assign((size_t)m, {-1, -1, -1, -1});
             gr.tasks.resize((size_t)m);
@@ -373,7 +380,7 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                     wicca::append_plan_tasks((int)im[(size_t)j].W, (int)shapes[(size_t)s].w, rp.scale_x, fast, rp.kx,
                                              (int)q, gr.tasks[(size_t)j]);
                     e.dst[q] = dst_of(s, j);
-                    gr.vt[(size_t)j][q] = vtab_of(rp, s, im[(size_t)j].H);
+                    gr.vt[(size_t)j][q] = vtab_of(rp, s, im[(size_t)j].H, band);
                     e.ky[q] = fast ? rp.ky : 0;
                     e.kx[q] = fast ? rp.kx : 0;
                     e.area_scale[q] = rp.area_scale;
@@ -390,9 +397,10 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
     std::vector<bool> by_rows((size_t)S * n, false);
     for (int s = 0; s < S; ++s)
         for (int64_t i = 0; i < n; ++i)
-            by_rows[(size_t)(s * n + i)] = area_rows_ok(src_rp[(size_t)(s * n + i)], s, H[(size_t)i], W[(size_t)i]);
+            by_rows[(size_t)(s * n + i)] =
+                area_rows_ok(src_rp[(size_t)(s * n + i)], s, H[(size_t)i], W[(size_t)i], kSrcBand);
     std::vector<AreaGroup> groups = make_groups(
-        srcs, [&](int s, int64_t i) { return (bool)by_rows[(size_t)(s * n + i)]; },
+        srcs, kSrcBand, [&](int s, int64_t i) { return (bool)by_rows[(size_t)(s * n + i)]; },
         [&](int s, int64_t i) -> const wicca::ResizeParams& { return src_rp[(size_t)(s * n + i)]; },
         [&](int s, int64_t i) { return dout + res_off[(size_t)s] + i * ob[(size_t)s]; });
     // icons by rows: the icon planes of every depth slot with an area downscale to some shape
@@ -404,7 +412,7 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
             bool any = false;
             for (int s = 0; s < S; ++s) {
                 const size_t q = (size_t)((s * U + u) * n + i);
-                icon_by_rows[q] = area_rows_ok(irp[q], s, ih[j], iw[j]) && ico_pitch[j] % 16 == 0;
+                icon_by_rows[q] = area_rows_ok(irp[q], s, ih[j], iw[j], kIconBand) && ico_pitch[j] % 16 == 0;
                 any = any || icon_by_rows[q];
             }
             if (any) row_icon.push_back((int64_t)j);
@@ -419,7 +427,7 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         return (size_t)((s * U + (int)(ij % U)) * n + ij / U);
     };
     std::vector<AreaGroup> icon_groups = make_groups(
-        isrcs, [&](int s, int64_t j) { return (bool)icon_by_rows[irp_at(s, j)]; },
+        isrcs, kIconBand, [&](int s, int64_t j) { return (bool)icon_by_rows[irp_at(s, j)]; },
         [&](int s, int64_t j) -> const wicca::ResizeParams& { return irp[irp_at(s, j)]; },
         [&](int s, int64_t j) { return irp[irp_at(s, j)].dst; });
     // the other icon resizes: per shape, a compact descriptor list for the
@@ -575,7 +583,8 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                 pp.dw[q] = (int32_t)shapes[(size_t)g.shapes[q]].w;
                 pp.dh[q] = (int32_t)shapes[(size_t)g.shapes[q]].h;
             }
-            pp.bands = (g.max_h + wicca::kPlanBand - 1) / wicca::kPlanBand;
+            pp.band_rows = g.band;
+            pp.bands = (g.max_h + g.band - 1) / g.band;
             const hipError_t e = wicca::launch_plan_area(pp, (int64_t)g.imgs.size(), g.max_h, g.rounds, cs);
             if (e != hipSuccess) return e;
         }

@@ -52,7 +52,10 @@ inline bool stage_hsum_ok(int64_t dw, int64_t C) { return C == 3 && dw >= 1 && d
 // up to kPlanShapes classifier shapes from ONE read of each image, horizontal
 // and vertical passes in one kernel (plan_area_kernel, stage.hip).
 constexpr int kPlanShapes = 4;
-constexpr int kPlanBand = 64;    // source rows whose output rows one workgroup owns
+#ifndef WICCA_PLAN_BAND
+#define WICCA_PLAN_BAND 64
+#endif
+constexpr int kPlanBand = WICCA_PLAN_BAND;  // the most source rows whose output rows one workgroup owns
 constexpr int kPlanRounds = 6;   // task rounds per lane (<= 1536 tasks per image, 64-padded per shape)
 constexpr int kPlanVRows = 2 * kPlanBand;  // source rows a band reads (windows of at most kPlanBand rows)
 
@@ -133,11 +136,13 @@ struct PlanBand {
 };
 
 // The vertical tables of a shape for images of height H (plan_resize's
-// geometry: scale_y, ky > 0 for integer scales), kPlanBand-row bands.
+// geometry: scale_y, ky > 0 for integer scales), band_rows-row bands
+// (<= kPlanBand).
 // False when a row would sit in more than two windows, a window is empty (not
 // an INTER_AREA downscale) or spans more than kPlanBand rows (a downscale by
 // more than 64): the shape goes to the per-image resize.
-bool plan_vertical(int H, int dh, double scale_y, int ky, std::vector<PlanVRow>& rows, std::vector<PlanBand>& bands);
+bool plan_vertical(int H, int dh, double scale_y, int ky, int band_rows, std::vector<PlanVRow>& rows,
+                   std::vector<PlanBand>& bands);
 
 struct PlanImageDev {
     const uint8_t* src;   // HWC uint8 RGB, rows 16-B aligned, pitch >= round_up(W * 3, 16)
@@ -147,7 +152,7 @@ struct PlanImageDev {
     int32_t n_tasks, pad_;
     uint8_t* dst[kPlanShapes];  // (dh_s, dw_s, 3) dense: cv2.resize(image, (dw_s, dh_s), INTER_AREA), or nullptr
     const PlanVRow* vrows[kPlanShapes];  // H entries per shape
-    const PlanBand* bands[kPlanShapes];  // ceil(H / kPlanBand) entries per shape
+    const PlanBand* bands[kPlanShapes];  // ceil(H / band_rows) entries per shape
     int32_t ky[kPlanShapes];    // > 0: integer scale (RS_AREA_FAST) ky rows per output row
     int32_t kx[kPlanShapes];
     float area_scale[kPlanShapes];
@@ -157,7 +162,8 @@ struct PlanParams {
     const PlanImageDev* imgs;
     int32_t n_shapes, C;
     int32_t dw[kPlanShapes], dh[kPlanShapes];
-    int32_t bands;              // kPlanBand-row bands of the tallest image
+    int32_t bands;              // band_rows-row bands of the tallest image
+    int32_t band_rows;          // <= kPlanBand
 };
 
 // A shape the plan's area kernel takes: RGB, output rows of at most 1024

@@ -386,7 +386,7 @@ __global__ __launch_bounds__(kStThreads, WICCA_PLAN_AREA_OCC) void plan_area_ker
     const PlanImageDev& im = P.imgs[L / (uint32_t)P.bands];
     const int band = (int)(L % (uint32_t)P.bands);
     const int H = im.H, W = im.W;
-    if (band * kPlanBand >= H) return;  // uniform: the bands are counted for the tallest image
+    if (band * P.band_rows >= H) return;  // uniform: the bands are counted for the tallest image
     const int t = threadIdx.x;
     const int n_shapes = P.n_shapes;
 
@@ -591,8 +591,10 @@ void append_plan_tasks(int W, int dw, double scale_x, bool fast, int kx, int q, 
     while (out.size() % 64) out.push_back(PlanTask{0u, 0.f, 0.f, 0.f, (uint32_t)q << 16});
 }
 
-bool plan_vertical(int H, int dh, double scale_y, int ky, std::vector<PlanVRow>& rows, std::vector<PlanBand>& bands)
+bool plan_vertical(int H, int dh, double scale_y, int ky, int band_rows, std::vector<PlanVRow>& rows,
+                   std::vector<PlanBand>& bands)
 {
+    if (band_rows < 1 || band_rows > kPlanBand) return false;
     rows.assign((size_t)H, PlanVRow{-1, 0.f, 0.f, 0u});
     std::vector<int> wfirst((size_t)dh), wlast((size_t)dh);
     for (int dy = 0; dy < dh; ++dy) {
@@ -626,11 +628,11 @@ bool plan_vertical(int H, int dh, double scale_y, int ky, std::vector<PlanVRow>&
             }
         }
     }
-    const int nb = (H + kPlanBand - 1) / kPlanBand;
+    const int nb = (H + band_rows - 1) / band_rows;
     bands.assign((size_t)nb, PlanBand{0, 0, H, -1});
     int dy = 0;
     for (int b = 0; b < nb; ++b) {
-        const int y1 = std::min(H, (b + 1) * kPlanBand);
+        const int y1 = std::min(H, (b + 1) * band_rows);
         PlanBand& e = bands[(size_t)b];
         e.dlo = dy;
         while (dy < dh && (b == nb - 1 || wfirst[(size_t)dy] < y1)) ++dy;
@@ -647,7 +649,8 @@ hipError_t launch_plan_area(const PlanParams& p, int64_t n, int max_h, int round
 {
     if (n <= 0 || max_h <= 0) return hipSuccess;
     if (p.C != 3 || rounds < 1 || rounds > kPlanRounds || p.n_shapes < 1 || p.n_shapes > kPlanShapes ||
-        p.bands != (max_h + kPlanBand - 1) / kPlanBand || n * p.bands > INT32_MAX)
+        p.band_rows < 1 || p.band_rows > kPlanBand || p.bands != (max_h + p.band_rows - 1) / p.band_rows ||
+        n * p.bands > INT32_MAX)
         return hipErrorInvalidValue;
     const dim3 grid((uint32_t)(n * p.bands));
     switch (rounds) {
