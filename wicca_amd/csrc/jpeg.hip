@@ -361,31 +361,64 @@ __device__ __forceinline__ int extend(uint32_t v, int s)
 
 // What the Huffman passes need of an image, staged in LDS per workgroup (a
 // register copy of the whole JpegImageDev spilled 712 B per lane to scratch).
-struct DecGeom {
-    int64_t comp_block0[kJpegDevComp];
-    int32_t bpm, mcux;
-    int32_t slot_comp[kJpegMaxSlots], slot_h[kJpegMaxSlots], slot_v[kJpegMaxSlots];
-    int32_t comp_h[kJpegDevComp], comp_v[kJpegDevComp], comp_bw[kJpegDevComp];
-    int32_t dc_tab[kJpegDevComp], ac_tab[kJpegDevComp];  // LDS table slots
-    uint32_t slot_tab[kJpegMaxSlots];  // per MCU slot: dc_tab | ac_tab << 8 | component << 16
+// Per MCU slot s: the block index of the slot in MCU (mx, my) is
+// off + my * rs + mx * cs (one 16-B read per DC codeword; the per-component
+// form took two dependent LDS round trips), and its tables and component as
+// one byte of `tab`: dc_tab | ac_tab << 3 | component << 6 (table slots < 8).
+struct alignas(16) SlotGeom {
+    int64_t off;     // comp_block0 + slot_v * comp_bw + slot_h
+    int32_t rs, cs;  // comp_v * comp_bw, comp_h
 };
+struct DecGeom {
+    SlotGeom slot[kJpegMaxSlots];
+    int32_t bpm, mcux;
+    uint32_t tab[(kJpegMaxSlots + 3) / 4];
+};
+
+// The geometry a lane consults at every block end, in scalar registers, read
+// once per decode: in a wave of 64 independent decodes some lane ends a block
+// in nearly every iteration, so the two dependent LDS reads this replaces
+// (blocks per MCU, then the next slot's tables) sat on every iteration.
+struct GeomRegs {
+    uint32_t bpm, mcux;
+    uint64_t tab_lo, tab_hi;  // slots 0..7, 8..9: a byte each
+    __device__ __forceinline__ explicit GeomRegs(const DecGeom& im)
+    {
+        bpm = (uint32_t)__builtin_amdgcn_readfirstlane(im.bpm);
+        mcux = (uint32_t)__builtin_amdgcn_readfirstlane(im.mcux);
+        uint32_t t[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] = k < (kJpegMaxSlots + 3) / 4 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)im.tab[k]) : 0u;
+        tab_lo = (uint64_t)t[0] | ((uint64_t)t[1] << 32);
+        tab_hi = (uint64_t)t[2] | ((uint64_t)t[3] << 32);
+    }
+    __device__ __forceinline__ uint32_t slot_tab(uint32_t s) const
+    {
+        const uint64_t w = s < 8 ? tab_lo : tab_hi;
+        return (uint32_t)(w >> ((s & 7u) * 8u)) & 0xFFu;
+    }
+};
+static_assert(kJpegMaxSlots <= 16, "slot bytes in two 64-bit words");
+#ifndef WICCA_JPEG_SYNC_REGTAB
+#define WICCA_JPEG_SYNC_REGTAB 0  // 1: the sync passes take slot tables from registers too
+#endif
 
 // Position of a decode-order block: MCU column / row and slot, advanced
 // incrementally (one division per lane instead of three 64-bit ones per block).
 struct BlockPos {
     uint32_t mx, my, slot;
-    __device__ void init(const DecGeom& im, int64_t g)
+    __device__ void init(const GeomRegs& gr, int64_t g)
     {
-        const uint32_t gg = (uint32_t)g, bpm = (uint32_t)im.bpm, mcu = gg / bpm;
-        slot = gg - mcu * bpm;
-        my = mcu / (uint32_t)im.mcux;
-        mx = mcu - my * (uint32_t)im.mcux;
+        const uint32_t gg = (uint32_t)g, mcu = gg / gr.bpm;
+        slot = gg - mcu * gr.bpm;
+        my = mcu / gr.mcux;
+        mx = mcu - my * gr.mcux;
     }
-    __device__ void next(const DecGeom& im)
+    __device__ void next(const GeomRegs& gr)
     {
-        if (++slot == (uint32_t)im.bpm) {
+        if (++slot == gr.bpm) {
             slot = 0;
-            if (++mx == (uint32_t)im.mcux) {
+            if (++mx == gr.mcux) {
                 mx = 0;
                 ++my;
             }
@@ -393,10 +426,8 @@ struct BlockPos {
     }
     __device__ int64_t index(const DecGeom& im) const
     {
-        const int c = im.slot_comp[slot];
-        const int64_t bx = (int64_t)mx * im.comp_h[c] + im.slot_h[slot];
-        const int64_t by = (int64_t)my * im.comp_v[c] + im.slot_v[slot];
-        return im.comp_block0[c] + by * im.comp_bw[c] + bx;
+        const SlotGeom sg = im.slot[slot];
+        return sg.off + (int64_t)my * sg.rs + (int64_t)mx * sg.cs;
     }
 };
 
@@ -466,7 +497,8 @@ __device__ __forceinline__ void flush_blocks(bool done, int64_t blk, const WaveS
     if (done) ws.owner[__popcll(pend & below)] = (uint8_t)lane;
     wave_lds_sync();
     const int n_act = __popcll(act), n_chunks = 8 * __popcll(pend);
-    const int rounds = (n_chunks + n_act - 1) / n_act;
+    // one round unless more than 8 blocks wait per 64 lanes (no division then)
+    const int rounds = n_chunks <= n_act ? 1 : (n_chunks + n_act - 1) / n_act;
     int c = __popcll(act & below);
 #pragma unroll 1
     for (int t = 0; t < rounds; ++t, c += n_act) {
@@ -526,20 +558,29 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
     int64_t blk = -1;
     bool staged = false;
     int zk = 0;  // next zigzag position of a block written position by position (not staged)
+    const GeomRegs gr(im);
     BlockPos pos;
     int16_t* lb = nullptr;
     if (WRITE) {
         if (WICCA_JPEG_STAGE) lb = ws->blocks + (threadIdx.x & 63) * kLaneBlock;
-        pos.init(im, g < 0 ? 0 : g);
+        pos.init(gr, g < 0 ? 0 : g);
         if (g >= block_lo && g < block_end) blk = pos.index(im);
         zk = st.k;  // the block in progress at the start: this lane owns [st.k, ...)
     }
     // the current slot's component and tables, re-read when the slot advances
     // (one LDS read per block, not two dependent ones per codeword)
-    uint32_t sti = im.slot_tab[st.slot];
-    int c = (int)(sti >> 16);
-    const HT* tdc = &tabs[sti & 255];
-    const HT* tac = &tabs[(sti >> 8) & 255];
+    // the write pass takes a slot's tables from the scalar copy; the sync
+    // passes (8 waves per SIMD hide an LDS read, and they are issue-bound)
+    // from LDS: the 64-bit select and shift measured 7 % slower in the guess
+    // pass
+    auto slot_tab = [&](int32_t s) -> uint32_t {
+        if (WRITE || WICCA_JPEG_SYNC_REGTAB) return gr.slot_tab((uint32_t)s);
+        return reinterpret_cast<const uint8_t*>(im.tab)[s];
+    };
+    uint32_t sti = slot_tab(st.slot);
+    int c = (int)(sti >> 6);
+    const HT* tdc = &tabs[sti & 7];
+    const HT* tac = &tabs[(sti >> 3) & 7];
     // 32-bit positions relative to the reader's base inside the loop
     const int32_t stop_r = (int32_t)(stop - br.base);
     const int32_t ck_off = (int32_t)(br.base - ck_base);  // reader-relative -> checkpoint-relative
@@ -586,7 +627,7 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
             ++nstart;
             dc[c] += v;
             if (WRITE) {
-                if (g >= 0) pos.next(im);
+                if (g >= 0) pos.next(gr);
                 ++g;
                 blk = (g >= block_lo && g < block_end) ? pos.index(im) : -1;
                 if (blk >= 0) {
@@ -627,12 +668,12 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
             done = WRITE && staged;  // a whole block of this lane
             if (WRITE && !staged && blk >= 0) zero_zig(coef, ws->nat, blk, zk, 64);
             staged = false;
-            st.slot = st.slot + 1 == im.bpm ? 0 : st.slot + 1;
+            st.slot = st.slot + 1 == (int32_t)gr.bpm ? 0 : st.slot + 1;
             st.k = 0;
-            sti = im.slot_tab[st.slot];
-            c = (int)(sti >> 16);
-            tdc = &tabs[sti & 255];
-            tac = &tabs[(sti >> 8) & 255];
+            sti = slot_tab(st.slot);
+            c = (int)(sti >> 6);
+            tdc = &tabs[sti & 7];
+            tac = &tabs[(sti >> 3) & 7];
         }
         // every codeword: deferring the flush until 4 / 8 / 16 blocks wait (the
         // finished lanes idle meanwhile) measured 6.1 / 7.4 / 7.5 ms per 25 x 8K
@@ -656,13 +697,13 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
         if (seg_last) zero_zig(coef, ws->nat, blk, kend, 64);  // nobody decodes the rest
     }
     if (WRITE && seg_last) {  // blocks the segment's data never started
-        if (g >= 0) pos.next(im);
+        if (g >= 0) pos.next(gr);
         for (int64_t h = g + 1; h < block_end; ++h) {
             if (h >= block_lo) {
                 uint4* d = reinterpret_cast<uint4*>(coef + pos.index(im) * 64);
                 for (int q = 0; q < 8; ++q) d[q] = uint4{0, 0, 0, 0};
             }
-            pos.next(im);
+            pos.next(gr);
         }
     }
     st.p = br.p();
@@ -677,6 +718,7 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
 // image's subsequences to whole workgroups).
 template <int NS, typename HT = HuffDev>
 struct ImgTabs {
+    static_assert(NS <= 8, "table slots are 3-bit fields of DecGeom::tab");
     HT t[NS];
     DecGeom g;
 };
@@ -699,27 +741,21 @@ __device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageD
     const uint32_t* src = reinterpret_cast<const uint32_t*>(tables + first);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&lds.t[0]);
     for (int w = threadIdx.x; w < n * kWords; w += kJThreads) dst[w] = src[w];
+    if (threadIdx.x < kJpegMaxSlots) {  // one lane per MCU slot
+        const int k = threadIdx.x;
+        const int c = min(max(imp->slot_comp[k], 0), kJpegDevComp - 1);
+        SlotGeom& sgm = lds.g.slot[k];
+        sgm.off = imp->comp_block0[c] + (int64_t)imp->slot_v[k] * imp->comp_bw[c] + imp->slot_h[k];
+        sgm.rs = imp->comp_v[c] * imp->comp_bw[c];
+        sgm.cs = imp->comp_h[c];
+        const uint32_t dt = c < ncomp ? (uint32_t)(imp->dc_tab[c] - first) : 0u;
+        const uint32_t at = c < ncomp ? (uint32_t)(imp->ac_tab[c] - first) : 0u;
+        reinterpret_cast<uint8_t*>(lds.g.tab)[k] = (uint8_t)(dt | (at << 3) | ((uint32_t)c << 6));
+    }
     if (threadIdx.x == 0) {
-        DecGeom& g = lds.g;
-        g.bpm = imp->bpm;
-        g.mcux = imp->mcux;
-        for (int k = 0; k < kJpegMaxSlots; ++k) {
-            g.slot_comp[k] = imp->slot_comp[k];
-            g.slot_h[k] = imp->slot_h[k];
-            g.slot_v[k] = imp->slot_v[k];
-        }
-        for (int c = 0; c < kJpegDevComp; ++c) {
-            g.comp_block0[c] = imp->comp_block0[c];
-            g.comp_h[c] = imp->comp_h[c];
-            g.comp_v[c] = imp->comp_v[c];
-            g.comp_bw[c] = imp->comp_bw[c];
-            g.dc_tab[c] = c < ncomp ? imp->dc_tab[c] - first : 0;
-            g.ac_tab[c] = c < ncomp ? imp->ac_tab[c] - first : 0;
-        }
-        for (int k = 0; k < kJpegMaxSlots; ++k) {
-            const int c = min(max(g.slot_comp[k], 0), kJpegDevComp - 1);
-            g.slot_tab[k] = (uint32_t)g.dc_tab[c] | ((uint32_t)g.ac_tab[c] << 8) | ((uint32_t)c << 16);
-        }
+        lds.g.bpm = imp->bpm;
+        lds.g.mcux = imp->mcux;
+        for (int k = kJpegMaxSlots; k < 4 * (int)(sizeof(lds.g.tab) / 4); ++k) reinterpret_cast<uint8_t*>(lds.g.tab)[k] = 0;
     }
     __syncthreads();
 }
