@@ -550,13 +550,15 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
                           SyncCk* ck_rec = nullptr, int* n_rec = nullptr)
 {
     constexpr bool REC = CK == 1 || CK == 3, CMP = CK == 2 || CK == 3;
-    bool bad = false;  // WRITE: the true decode path meets damaged data (see JpegPlan::damage)
+    // bools carried around the divergent loop as VGPR ints: as i1 values each
+    // cost a lane-mask merge (3 scalar ops) per loop edge and iteration
+    uint32_t bad = 0;  // WRITE: the true decode path meets damaged data (see JpegPlan::damage)
     int nck = 0, hit = -1, nrec = 0;
     SyncCk* rec = CK == 3 ? ck_rec : ck;
     uint32_t cur = 0;  // CMP: pos_slot of checkpoint nck
     if (CMP && n_ck > 0) cur = ck[0].pos_slot;
     int64_t blk = -1;
-    bool staged = false;
+    uint32_t staged = 0;
     int zk = 0;  // next zigzag position of a block written position by position (not staged)
     const GeomRegs gr(im);
     BlockPos pos;
@@ -585,12 +587,12 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
     const int32_t stop_r = (int32_t)(stop - br.base);
     const int32_t ck_off = (int32_t)(br.base - ck_base);  // reader-relative -> checkpoint-relative
     int32_t nstart = 0;  // blocks started in this run
-    while (br.pr < stop_r) {
-        // the segment's last block is complete: the bits left are the encoder's
-        // fill (1-bits up to the byte boundary), which libjpeg never decodes
-        // (a single-code table, e.g. optimize=True on flat content, reads them
-        // as a code no table has)
-        if (WRITE && seg_last && st.k == 0 && g >= block_end - 1) break;
+    // WRITE, the segment's last lane: once the segment's last block is
+    // complete, the bits left are the encoder's fill (1-bits up to the byte
+    // boundary), which libjpeg never decodes (a single-code table, e.g.
+    // optimize=True on flat content, reads them as a code no table has).  One
+    // loop exit for the write pass.
+    while (br.pr < stop_r && !(WRITE && seg_last && st.k == 0 && g >= block_end - 1)) {
         if (REC && st.k == 0 && nrec < kSyncCk && br.pr + ck_off >= nrec * ck_step) {
             SyncCk e;
             e.pos_slot = (uint32_t)(br.pr + ck_off) | ((uint32_t)st.slot << 24);
@@ -619,7 +621,7 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
         const bool isdc = st.k == 0;
         const uint32_t e = huff_lookup(*(isdc ? tdc : tac), look);
         const int len = (int)(e >> 8), sym = (int)(e & 255);
-        if (WRITE) bad |= len > 16;
+        if (WRITE) bad |= (uint32_t)(len > 16);
         const int s = isdc ? min(sym, 16) : (sym & 15);  // a DC size > 11 only in corrupt streams
         const int v = s ? extend((look << len) >> (32 - s), s) : 0;
         br.skip(len + s);
@@ -633,7 +635,7 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
                 if (blk >= 0) {
                     if (WICCA_JPEG_STAGE) {
                         lb[0] = (int16_t)dc[c];
-                        staged = true;
+                        staged = 1;
                     } else {
                         coef[blk * 64] = (int16_t)dc[c];
                         zk = 1;
@@ -645,7 +647,7 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
             const int r = sym >> 4;
             if (s) {
                 st.k += r;
-                if (WRITE) bad |= st.k > 63;  // libjpeg writes these to coefficient 63
+                if (WRITE) bad |= (uint32_t)(st.k > 63);  // libjpeg writes these to coefficient 63
                 if (WRITE && blk >= 0 && st.k < 64) {
                     const int n = ws->nat[st.k];
                     if (staged) {
@@ -667,7 +669,7 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
         if (st.k >= 64) {
             done = WRITE && staged;  // a whole block of this lane
             if (WRITE && !staged && blk >= 0) zero_zig(coef, ws->nat, blk, zk, 64);
-            staged = false;
+            staged = 0;
             st.slot = st.slot + 1 == (int32_t)gr.bpm ? 0 : st.slot + 1;
             st.k = 0;
             sti = slot_tab(st.slot);
@@ -682,7 +684,7 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
     }
     // the segment's data ends before its last block does: libjpeg-turbo then
     // decodes the running MCU on from zero bits (jdhuff.c jpeg_fill_bit_buffer)
-    if (WRITE && seg_last) bad |= g < block_end - 1 || (g == block_end - 1 && st.k != 0);
+    if (WRITE && seg_last) bad |= (uint32_t)(g < block_end - 1 || (g == block_end - 1 && st.k != 0));
     if (WRITE && bad && damage) atomicOr(damage, 1);
     if (WRITE && blk >= 0 && st.k > 0) {  // the range ends inside block blk: this lane's part [.., st.k)
         const int kend = min(st.k, 64);
