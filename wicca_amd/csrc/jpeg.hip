@@ -621,6 +621,11 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
         const bool isdc = st.k == 0;
         const uint32_t e = huff_lookup(*(isdc ? tdc : tac), look);
         const int len = (int)(e >> 8), sym = (int)(e & 255);
+        // WRITE: the natural position of the coefficient this codeword would
+        // set, read as soon as the symbol is known (st.k <= 63 and the run <=
+        // 15, inside the 80-entry table), so its LDS latency overlaps the value
+        // extraction rather than stalling the staging write
+        const int nat_next = WRITE && WICCA_JPEG_STAGE ? ws->nat[st.k + (sym >> 4)] : 0;
         if (WRITE) bad |= (uint32_t)(len > 16);
         const int s = isdc ? min(sym, 16) : (sym & 15);  // a DC size > 11 only in corrupt streams
         const int v = s ? extend((look << len) >> (32 - s), s) : 0;
@@ -649,7 +654,7 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
                 st.k += r;
                 if (WRITE) bad |= (uint32_t)(st.k > 63);  // libjpeg writes these to coefficient 63
                 if (WRITE && blk >= 0 && st.k < 64) {
-                    const int n = ws->nat[st.k];
+                    const int n = WICCA_JPEG_STAGE ? nat_next : ws->nat[st.k];
                     if (staged) {
                         lb[n] = (int16_t)v;
                     } else {
