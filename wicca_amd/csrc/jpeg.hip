@@ -894,65 +894,160 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(J
 }
 
 // Segmented exclusive scan of (blocks started, DC sums) over each segment's
-// subsequences: one workgroup of 256 lanes per segment.
+// subsequences, in three launches over 256-subsequence chunks of the whole
+// call: a file without restart markers is ONE segment of ~20,000
+// subsequences, and one workgroup per segment (25 per call) left the chip
+// idle for 142 us.  1: every chunk scans itself (segment heads reset the sum;
+// padding lanes count as heads of nothing) and leaves its carry-out; 2: one
+// workgroup scans the chunks' carry-outs into carry-ins; 3: every chunk adds
+// its carry-in to the lanes before its first head.
 struct SubBase {
     int64_t block;
     int32_t dc[kJpegDevComp];
-    int32_t pad_;
+    int32_t pad_;  // scan 1 -> 3: 1 when a head lies in the chunk at or before this lane
+};
+constexpr int kScanChunk = 256;
+
+struct ScanVal {
+    uint32_t f;  // a segment head at or before this element (within the span summed)
+    int64_t b;
+    int32_t d[kJpegDevComp];
 };
 
-__global__ __launch_bounds__(256) void jpeg_scan_kernel(JpegPlan P, const SubResult* res, SubBase* base)
+// x = left ⊕ x: the segmented-scan operator
+__device__ __forceinline__ void scan_combine(const ScanVal& left, ScanVal& x)
 {
-    const JpegSegDev sg = P.segs[blockIdx.x];
-    const int64_t n = sg.n_sub;
-    __shared__ int64_t sb[256];
-    __shared__ int32_t sd[kJpegDevComp][256];
-    __shared__ int64_t carry_b;
-    __shared__ int32_t carry_d[kJpegDevComp];
-    const int t = threadIdx.x;
-    if (t == 0) {
-        carry_b = 0;
-        for (int c = 0; c < kJpegDevComp; ++c) carry_d[c] = 0;
+    if (!x.f) {
+        x.b += left.b;
+        for (int c = 0; c < kJpegDevComp; ++c) x.d[c] += left.d[c];
     }
+    x.f |= left.f;
+}
+
+__device__ __forceinline__ ScanVal scan_shfl_up(const ScanVal& v, int off)
+{
+    ScanVal o;
+    o.f = (uint32_t)__shfl_up((int)v.f, off, 64);
+    const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v.b, off, 64);
+    const uint32_t hi = (uint32_t)__shfl_up((int)(uint32_t)((uint64_t)v.b >> 32), off, 64);
+    o.b = (int64_t)(((uint64_t)hi << 32) | lo);
+    for (int c = 0; c < kJpegDevComp; ++c) o.d[c] = __shfl_up(v.d[c], off, 64);
+    return o;
+}
+
+// inclusive segmented scan over the workgroup (kScanChunk lanes); `tot`: the
+// whole chunk's (every lane gets it)
+__device__ __forceinline__ ScanVal scan_chunk(ScanVal x, ScanVal* lds_waves, ScanVal& tot)
+{
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const ScanVal l = scan_shfl_up(x, off);
+        if (lane >= off) scan_combine(l, x);
+    }
+    if (lane == 63) lds_waves[wv] = x;
     __syncthreads();
-    for (int64_t c0 = 0; c0 < n; c0 += 256) {
-        const int64_t i = c0 + t;
-        int64_t vb = 0;
-        int32_t vd[kJpegDevComp] = {0, 0, 0};
-        if (i < n) {
-            const SubResult& r = res[sg.sub0 + i];
-            vb = r.started;
-            for (int c = 0; c < kJpegDevComp; ++c) vd[c] = r.dc[c];
-        }
-        sb[t] = vb;
-        for (int c = 0; c < kJpegDevComp; ++c) sd[c][t] = vd[c];
-        __syncthreads();
-        for (int off = 1; off < 256; off <<= 1) {  // Hillis-Steele inclusive scan
-            int64_t ab = 0;
-            int32_t ad[kJpegDevComp] = {0, 0, 0};
-            if (t >= off) {
-                ab = sb[t - off];
-                for (int c = 0; c < kJpegDevComp; ++c) ad[c] = sd[c][t - off];
-            }
-            __syncthreads();
-            sb[t] += ab;
-            for (int c = 0; c < kJpegDevComp; ++c) sd[c][t] += ad[c];
-            __syncthreads();
-        }
-        if (i < n) {
-            SubBase b;
-            b.block = carry_b + sb[t] - vb;  // exclusive
-            for (int c = 0; c < kJpegDevComp; ++c) b.dc[c] = carry_d[c] + sd[c][t] - vd[c];
-            b.pad_ = 0;
-            base[sg.sub0 + i] = b;
-        }
-        __syncthreads();
-        if (t == 255) {
-            carry_b += sb[255];
-            for (int c = 0; c < kJpegDevComp; ++c) carry_d[c] += sd[c][255];
-        }
-        __syncthreads();
+    ScanVal carry{0, 0, {0, 0, 0}}, all{0, 0, {0, 0, 0}};  // the waves before this one; all waves
+#pragma unroll
+    for (int w = 0; w < kScanChunk / 64; ++w) {
+        ScanVal t = lds_waves[w];
+        scan_combine(all, t);
+        all = t;
+        if (w + 1 == wv) carry = all;
     }
+    scan_combine(carry, x);
+    tot = all;
+    return x;
+}
+
+__device__ __forceinline__ ScanVal scan_load(const JpegPlan& P, const SubResult* res, int64_t i)
+{
+    ScanVal v{1, 0, {0, 0, 0}};  // past the end / padding: a head of nothing
+    if (i < P.n_sub) {
+        const int32_t sgi = P.sub_seg[i];
+        if (sgi >= 0) {
+            const SubResult& r = res[i];
+            v.f = i == P.segs[sgi].sub0 ? 1u : 0u;
+            v.b = r.started;
+            for (int c = 0; c < kJpegDevComp; ++c) v.d[c] = r.dc[c];
+        }
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(kScanChunk) void jpeg_scan_local_kernel(JpegPlan P, const SubResult* res, SubBase* base,
+                                                                    SubBase* chunk_out)
+{
+    __shared__ ScanVal w[kScanChunk / 64];
+    const int64_t i = (int64_t)blockIdx.x * kScanChunk + threadIdx.x;
+    ScanVal tot;
+    const ScanVal x = scan_chunk(scan_load(P, res, i), w, tot);
+    if (i < P.n_sub) {
+        SubBase b;
+        b.block = x.b;
+        for (int c = 0; c < kJpegDevComp; ++c) b.dc[c] = x.d[c];
+        b.pad_ = (int32_t)x.f;
+        base[i] = b;  // inclusive within the chunk; finished by jpeg_scan_fix_kernel
+    }
+    if (threadIdx.x == 0) {
+        SubBase o;
+        o.block = tot.b;
+        for (int c = 0; c < kJpegDevComp; ++c) o.dc[c] = tot.d[c];
+        o.pad_ = (int32_t)tot.f;
+        chunk_out[blockIdx.x] = o;
+    }
+}
+
+// carry_in[k] = the sum of chunk k - 1's tail and, while no head intervenes,
+// the chunks before it (exclusive segmented scan of the carry-outs)
+__global__ __launch_bounds__(kScanChunk) void jpeg_scan_chunks_kernel(const SubBase* chunk_out, SubBase* carry_in,
+                                                                     int64_t n_chunks)
+{
+    __shared__ ScanVal w[kScanChunk / 64];
+    ScanVal run{0, 0, {0, 0, 0}};  // the scan of every earlier step's chunks
+    for (int64_t c0 = 0; c0 < n_chunks; c0 += kScanChunk) {
+        const int64_t k = c0 + threadIdx.x;
+        ScanVal v{0, 0, {0, 0, 0}};
+        if (k < n_chunks) {
+            const SubBase& o = chunk_out[k];
+            v.f = (uint32_t)o.pad_;
+            v.b = o.block;
+            for (int c = 0; c < kJpegDevComp; ++c) v.d[c] = o.dc[c];
+        }
+        ScanVal tot;
+        ScanVal x = scan_chunk(v, w, tot);
+        scan_combine(run, x);  // inclusive over chunks 0..k
+        // exclusive: chunk k + 1 takes chunk k's inclusive value
+        if (k + 1 < n_chunks) {
+            SubBase ci;
+            ci.block = x.b;
+            for (int c = 0; c < kJpegDevComp; ++c) ci.dc[c] = x.d[c];
+            ci.pad_ = 0;
+            carry_in[k + 1] = ci;
+        }
+        scan_combine(run, tot);
+        run = tot;
+        __syncthreads();  // w is reused by the next step
+    }
+    if (threadIdx.x == 0) {
+        SubBase z{0, {0, 0, 0}, 0};
+        carry_in[0] = z;
+    }
+}
+
+__global__ __launch_bounds__(kScanChunk) void jpeg_scan_fix_kernel(JpegPlan P, const SubResult* res, SubBase* base,
+                                                                  const SubBase* carry_in)
+{
+    const int64_t i = (int64_t)blockIdx.x * kScanChunk + threadIdx.x;
+    if (i >= P.n_sub || P.sub_seg[i] < 0) return;
+    SubBase b = base[i];
+    const SubResult& r = res[i];
+    const bool own = b.pad_ != 0;  // a head at or before i in this chunk: no carry-in
+    const SubBase& ci = carry_in[blockIdx.x];
+    b.block += (own ? 0 : ci.block) - r.started;  // exclusive
+    for (int c = 0; c < kJpegDevComp; ++c) b.dc[c] += (own ? 0 : ci.dc[c]) - r.dc[c];
+    b.pad_ = 0;
+    base[i] = b;
 }
 
 // Final pass: scatter coefficients (converged start states, scanned bases).
@@ -1970,6 +2065,7 @@ size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg)
 {
     (void)n_seg;
     return (size_t)n_sub * (5 * sizeof(SubResult) + sizeof(SubBase) + 2 * kSyncCk * sizeof(SyncCk)) + 256 +
+           2 * (size_t)((n_sub + kScanChunk - 1) / kScanChunk) * sizeof(SubBase) +
            kJpegMaxJobs * sizeof(IdctJob);
 }
 
@@ -1988,6 +2084,9 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     int* flags = (int*)(sb + P.n_sub);  // [0, kFlagRing): per-round "an end state changed"; then stats
     IdctJob* jobs = (IdctJob*)((uint8_t*)flags + 256);
     SyncCk* cks = (SyncCk*)(jobs + kJpegMaxJobs);
+    // the scan's per-chunk carry-outs and carry-ins
+    SubBase* chunk_out = reinterpret_cast<SubBase*>(cks + 2 * P.n_sub * kSyncCk);
+    SubBase* carry_in = chunk_out + (P.n_sub + kScanChunk - 1) / kScanChunk;
     // IDCT jobs: every (image, component); uploaded first, while the stream
     // still waits for the entropy-coded data
     // fused back end (default; WICCA_JPEG_FUSED=0: separate IDCT and colour
@@ -2154,7 +2253,14 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             for (int r = 0; r <= std::min(rounds, kStatRounds - 1); ++r) fprintf(stderr, " %d/%d", h[2 * r], h[2 * r + 1]);
             fprintf(stderr, "\n");
         }
-        hipLaunchKernelGGL(jpeg_scan_kernel, dim3((uint32_t)P.n_seg), dim3(256), 0, s, P, cur, sb);
+        {
+            const int64_t n_chunks = (P.n_sub + kScanChunk - 1) / kScanChunk;
+            hipLaunchKernelGGL(jpeg_scan_local_kernel, dim3((uint32_t)n_chunks), dim3(kScanChunk), 0, s, P, cur, sb,
+                               chunk_out);
+            hipLaunchKernelGGL(jpeg_scan_chunks_kernel, dim3(1), dim3(kScanChunk), 0, s, chunk_out, carry_in, n_chunks);
+            hipLaunchKernelGGL(jpeg_scan_fix_kernel, dim3((uint32_t)n_chunks), dim3(kScanChunk), 0, s, P, cur, sb,
+                               carry_in);
+        }
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (P.max_tabs <= 4 && !force6)
             hipLaunchKernelGGL(jpeg_write_kernel<4>, dim3(grid), dim3(kJThreads), 0, s, P, cur, sb);
