@@ -2005,43 +2005,63 @@ constexpr int kIlvWords = 32, kIlvSlotBytes = 160;  // words per workgroup row b
 __global__ __launch_bounds__(256) void jpeg_interleave_kernel(JpegPlan P)
 {
     __shared__ __attribute__((aligned(16))) uint8_t st[64 * kIlvSlotBytes];
-    __shared__ int64_t sb[64];  // slot's first byte of this block, -1: padding
+    __shared__ int64_t sb[64];  // slot's first byte (row block 0), -1: padding
     const int64_t g = blockIdx.x;
-    const int jb = (int)blockIdx.y, t = (int)threadIdx.x;
+    const int t = (int)threadIdx.x;
     if (t < 64) {
         const int64_t i = g * 64 + t;
         int64_t b = -1;
         if (i < P.n_sub && P.sub_seg[i] >= 0) {
             const JpegSegDev sg = P.segs[P.sub_seg[i]];
-            b = ((sg.bit0 + (i - sg.sub0) * (int64_t)P.sub_bits) >> 3) + 4 * (int64_t)kIlvWords * jb;
+            b = (sg.bit0 + (i - sg.sub0) * (int64_t)P.sub_bits) >> 3;
         }
         sb[t] = b;
     }
     __syncthreads();
-    constexpr int kChunks = kIlvSlotBytes / 16;
-    for (int c = t; c < 64 * kChunks; c += 256) {
-        const int l = c / kChunks, q = c - l * kChunks;
-        const int64_t b = sb[l];
-        uint4 v{0, 0, 0, 0};
-        if (b >= 0) {
-            const int64_t a = (b & ~(int64_t)15) + 16 * q;
-            if (a + 16 <= P.stream_bytes) v = *reinterpret_cast<const uint4*>(P.stream + a);
+    // the group's row blocks in turn (one workgroup per row block paid the
+    // slot lookups and a memory latency per 8 KB: 150 us per call); the next
+    // block's 16-B loads are in flight while this one's words leave
+    constexpr int kChunks = kIlvSlotBytes / 16, kPer = (64 * kChunks + 255) / 256;
+    const int n_jb = (P.ilv_sw + kIlvWords - 1) / kIlvWords;
+    uint4 v[kPer];
+    auto load = [&](int jb) {
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int c = t + 256 * k;
+            v[k] = uint4{0, 0, 0, 0};
+            if (c < 64 * kChunks) {
+                const int l = c / kChunks, q = c - l * kChunks;
+                const int64_t b = sb[l];
+                if (b >= 0) {
+                    const int64_t a = ((b + 4 * (int64_t)kIlvWords * jb) & ~(int64_t)15) + 16 * q;
+                    if (a + 16 <= P.stream_bytes) v[k] = *reinterpret_cast<const uint4*>(P.stream + a);
+                }
+            }
         }
-        *reinterpret_cast<uint4*>(st + l * kIlvSlotBytes + 16 * q) = v;
-    }
-    __syncthreads();
-    for (int o = t; o < 64 * kIlvWords; o += 256) {
-        const int jj = o >> 6, l = o & 63;
-        const int j = kIlvWords * jb + jj;
-        if (j >= P.ilv_sw) break;  // rows ascend with o
-        const int64_t b = sb[l];
-        uint32_t v = 0;
-        if (b >= 0) {
-            const int off = (int)(b & 15) + 4 * jj;
-            const uint32_t* w = reinterpret_cast<const uint32_t*>(st + l * kIlvSlotBytes + (off & ~3));
-            v = __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(off & 3));
+    };
+    load(0);
+    for (int jb = 0; jb < n_jb; ++jb) {
+        __syncthreads();  // the previous block's words have been read out of st
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int c = t + 256 * k;
+            if (c < 64 * kChunks) *reinterpret_cast<uint4*>(st + (c / kChunks) * kIlvSlotBytes + 16 * (c % kChunks)) = v[k];
         }
-        P.ilv[((g * P.ilv_sw + j) << 6) + l] = v;
+        __syncthreads();
+        if (jb + 1 < n_jb) load(jb + 1);
+        for (int o = t; o < 64 * kIlvWords; o += 256) {
+            const int jj = o >> 6, l = o & 63;
+            const int j = kIlvWords * jb + jj;
+            if (j >= P.ilv_sw) break;  // rows ascend with o
+            const int64_t b = sb[l];
+            uint32_t w = 0;
+            if (b >= 0) {
+                const int off = (int)((b + 4 * (int64_t)kIlvWords * jb) & 15) + 4 * jj;
+                const uint32_t* p = reinterpret_cast<const uint32_t*>(st + l * kIlvSlotBytes + (off & ~3));
+                w = __builtin_amdgcn_alignbyte(p[1], p[0], (uint32_t)(off & 3));
+            }
+            P.ilv[((g * P.ilv_sw + j) << 6) + l] = w;
+        }
     }
 }
 
@@ -2139,7 +2159,7 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     if (P.n_sub > 0) {
         const uint32_t grid = (uint32_t)((P.n_sub + kJThreads - 1) / kJThreads);
         if (P.ilv) {
-            const dim3 ig((uint32_t)((P.n_sub + 63) / 64), (uint32_t)((P.ilv_sw + kIlvWords - 1) / kIlvWords));
+            const dim3 ig((uint32_t)((P.n_sub + 63) / 64));
             hipLaunchKernelGGL(jpeg_interleave_kernel, ig, dim3(256), 0, s, P);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
