@@ -427,7 +427,8 @@ struct BlockPos {
     __device__ int64_t index(const DecGeom& im) const
     {
         const SlotGeom sg = im.slot[slot];
-        return sg.off + (int64_t)my * sg.rs + (int64_t)mx * sg.cs;
+        // the offset inside a component is below 2^32 (its blocks are)
+        return sg.off + (int64_t)(uint32_t)(my * (uint32_t)sg.rs + mx * (uint32_t)sg.cs);
     }
 };
 
@@ -471,12 +472,6 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ int64_t shfl64(int64_t v, int src)
-{
-    const int lo = __shfl((int)(uint32_t)v, src, 64), hi = __shfl((int)(uint32_t)((uint64_t)v >> 32), src, 64);
-    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-
 // Blocks completed by lanes of this wave in this iteration leave as full
 // 128-B blocks: the wave's active lanes deal the 8 16-B chunks of every such
 // block among themselves, so one store instruction writes up to 8 blocks
@@ -505,13 +500,14 @@ __device__ __forceinline__ void flush_blocks(bool done, int64_t blk, const WaveS
         const bool valid = c < n_chunks;
         const int bi = valid ? c >> 3 : 0, q = c & 7;
         const int o = ws.owner[bi];
-        const int64_t ob = shfl64(blk, o);
+        // a block index fits 32 bits (2^32 blocks of 128 B exceed any HBM)
+        const uint32_t ob = (uint32_t)__shfl((int)(uint32_t)blk, o, 64);
         if (valid) {
             uint4* chunk = reinterpret_cast<uint4*>(ws.blocks + o * kLaneBlock + q * 8);
             const uint4 v = *chunk;
             *chunk = uint4{0, 0, 0, 0};
 #ifndef WICCA_JPEG_ABLATE_STORES
-            *reinterpret_cast<uint4*>(coef + ob * 64 + q * 8) = v;
+            *reinterpret_cast<uint4*>(coef + (uint64_t)ob * 64 + q * 8) = v;
 #else
             asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w), "v"(ob));
 #endif
@@ -592,7 +588,8 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
     // boundary), which libjpeg never decodes (a single-code table, e.g.
     // optimize=True on flat content, reads them as a code no table has).  One
     // loop exit for the write pass.
-    while (br.pr < stop_r && !(WRITE && seg_last && st.k == 0 && g >= block_end - 1)) {
+    const int64_t g_stop = WRITE && seg_last ? block_end - 1 : INT64_MAX;  // (one compare per iteration)
+    while (br.pr < stop_r && !(WRITE && st.k == 0 && g >= g_stop)) {
         if (REC && st.k == 0 && nrec < kSyncCk && br.pr + ck_off >= nrec * ck_step) {
             SyncCk e;
             e.pos_slot = (uint32_t)(br.pr + ck_off) | ((uint32_t)st.slot << 24);
