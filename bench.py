@@ -61,8 +61,8 @@ def parse():
     ap.add_argument("--kernel-only", action="store_true",
                     help="--config jpeg / plan: only the synchronous calls (the kernel-trace child run)")
     ap.add_argument("--no-kernel-trace", action="store_true",
-                    help="--config jpeg / plan: skip the rocprofv3 --kernel-trace child run that times "
-                         "each kernel for the per-kernel roofline entries")
+                    help="skip the rocprofv3 --kernel-trace child run that times each kernel (batch: "
+                         "the headline launch and the sweep; jpeg / plan: the per-kernel roofline entries)")
     ap.add_argument("--interpolation", type=int, default=3, help="--config stage: cv2.INTER_*")
     ap.add_argument("--depths", default="1,2,3,4,5,6", help="depth list of --config multi")
     ap.add_argument("--steps", type=int, default=20)
@@ -82,6 +82,8 @@ def parse():
                     help="budget of the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true",
+                    help="batch config: skip the depth sweep 1..6 and the configs[1] leg")
     ap.add_argument("--no-live-pmc", action="store_true",
                     help="batch config at N=1: skip the two rocprofv3 --pmc child runs that "
                          "measure roofline.traffic live (the committed --pmc summary is used)")
@@ -208,7 +210,7 @@ def live_pmc(args, kernel: str, timeout_s: float = 150.0, extra=None):
             "rocprof" in os.environ.get("LD_PRELOAD", ""):
         return None
     child = [sys.executable, os.path.abspath(__file__), "--steps", "3", "--warmup", "1",
-             "--no-verify", "--no-cpu-baseline", "--no-live-pmc",
+             "--no-verify", "--no-cpu-baseline", "--no-live-pmc", "--no-sweep", "--no-kernel-trace",
              "--images", str(args.images), "--height", str(args.height), "--width", str(args.width),
              "--channels", str(args.channels), "--depth", str(args.depth),
              "--border", str(args.border), "--seed", str(args.seed)] + list(extra or [])
@@ -291,6 +293,124 @@ def kernel_trace_child(args, extra, timeout_s: float = 300.0):
                     durs.setdefault(row["Kernel_Name"], []).append(
                         int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
     return {k: (len(v), sum(v) / len(v) / 1e3) for k, v in durs.items()} if durs else None
+
+
+def kernel_trace_grid(args, extra, timeout_s: float = 240.0):
+    """The headline's kernel-trace child: this bench's workload (timed steps,
+    depth sweep, configs[1] leg) under rocprofv3 --kernel-trace, a child run
+    (this process has initialised the GPU).  {(kernel name, grid x): (launches,
+    mean duration in us)} -- the grid separates launches of one kernel on
+    different batches (configs[2] and configs[1] at depth 3); None when
+    rocprofv3 is absent, nested, or the run fails."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof) or any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ) or \
+            "rocprof" in os.environ.get("LD_PRELOAD", ""):
+        return None
+    child = [sys.executable, os.path.abspath(__file__), "--no-verify", "--no-cpu-baseline", "--no-live-pmc",
+             "--no-kernel-trace"] + list(extra)
+    env = dict(os.environ, TMPDIR="/tmp")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    with tempfile.TemporaryDirectory(prefix="wicca_kt_", dir="/tmp") as tmp:
+        try:
+            r = subprocess.run([prof, "--kernel-trace", "--output-format", "csv", "-d", tmp, "--"] + child,
+                               cwd="/tmp", env=env, timeout=timeout_s, stdout=subprocess.DEVNULL,
+                               stderr=subprocess.DEVNULL)
+        except (OSError, subprocess.TimeoutExpired):
+            return None
+        if r.returncode != 0:
+            return None
+        durs = {}
+        for path in glob.glob(os.path.join(tmp, "**", "*kernel_trace.csv"), recursive=True):
+            with open(path) as f:
+                for row in csv.DictReader(f):
+                    key = (row["Kernel_Name"], int(row.get("Grid_Size_X") or 0))
+                    t0, t1 = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
+                    durs.setdefault(key, []).append((t0, t1 - t0))
+    return {k: (len(v), sum(d for _, d in v) / len(v) / 1e3, min(t for t, _ in v))
+            for k, v in durs.items()} if durs else None
+
+
+def trace_lookup(stats, name, which=0):
+    """(launches, mean us) of the kernel-trace group (one kernel name
+    containing `name`, one grid) that ran `which`-th among that kernel's
+    groups (by first launch: 0 the first, -1 the last); None when absent."""
+    hits = sorted((t, n, us) for (k, _), (n, us, t) in (stats or {}).items() if name in k)
+    if not hits:
+        return None
+    _, n, us = hits[which]
+    return n, us
+
+
+def run_sweep(args, torch, lib, src, B, H, W, C, pitch, stream, sh, seed):
+    """BASELINE configs[2]'s transform_depth sweep 1..6 on the headline's
+    device-resident batch, and configs[1] (32 x 4K RGB, depth 3) on a batch of
+    its own: per entry one wicca_haar_ll_u8_uniform launch per step timed by
+    HIP events on the launch stream, algorithmic bytes (image read once, icon
+    written once) over that time, and -- unless --no-verify -- the first and
+    last image of the batch checked against the C oracle (oracle/haar_oracle.c,
+    pinned by the reference's goldens).  Returns the entries, one per leg, in
+    the order the legs run (configs[2] first)."""
+    from wicca_amd import _lib
+
+    steps = max(3, min(args.steps, 10))
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    out = []
+    legs = [("configs[2]", d, B, H, W) for d in range(1, 7)] + [("configs[1]", 3, 32, 2160, 3840)]
+    big = max(n * -(-h >> d) * ((-(-w >> d) * C + 15) // 16 * 16) for _, d, n, h, w in legs)
+    dst = torch.empty(big, dtype=torch.uint8, device="cuda")
+    src4k = None
+    for cfg, d, n, h, w in legs:
+        if cfg == "configs[1]":
+            p = (w * C + 15) // 16 * 16
+            src4k = torch.empty(n * h * p, dtype=torch.uint8, device="cuda")
+            _lib.check(lib.wicca_synth_u8(ctypes.c_void_p(src4k.data_ptr()), n, h, w, C, p, h * p,
+                                          seed + 7919, -1, sh))
+            s, sp, sd = src4k, p, seed + 7919
+        else:
+            s, sp, sd = src, pitch, seed
+        oh, ow = -(-h >> d), -(-w >> d)
+        op = (ow * C + 15) // 16 * 16
+
+        def launch():
+            _lib.check(lib.wicca_haar_ll_u8_uniform(
+                ctypes.c_void_p(s.data_ptr()), n, h, w, C, sp, h * sp, d, args.border, 0,
+                ctypes.c_void_p(dst.data_ptr()), op, oh * op, -1, sh))
+        launch()
+        torch.cuda.synchronize()
+        ev0.record(stream)
+        for _ in range(steps):
+            launch()
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        ms = ev0.elapsed_time(ev1) / steps
+        alg = n * (h * w * C + oh * ow * C)
+        e = {"config": cfg, "images": n, "height": h, "width": w, "depth": d,
+             "kernel": lib.wicca_kernel_name(d, C, 0).decode(), "launches": steps,
+             "kernel_ms": round(ms, 4), "alg_bytes_per_launch": alg,
+             "achieved": round(alg / (ms / 1e3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(alg / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+             "MP_per_s": round(n * h * w / 1e6 / (ms / 1e3), 1)}
+        if not args.no_verify:
+            from oracle import c_oracle
+            from wicca_amd.synth import synth_image
+            ok = True
+            for i in sorted({0, n - 1}):
+                ref = c_oracle.ll_int_block(synth_image(sd, i, h, w, C), d, args.border)[0]
+                got = dst[i * oh * op:(i + 1) * oh * op].view(oh, op)[:, :ow * C].cpu().numpy()
+                ok = ok and bool(np.array_equal(got.reshape(oh, ow, C), ref))
+            if not ok:
+                raise SystemExit(f"bench sweep verification FAILED: {cfg} depth {d}")
+            e["verified_images"] = sorted({0, n - 1})
+        out.append(e)
+    del src4k, dst
+    return out
 
 
 def kernel_rooflines(stats, table):
@@ -1441,6 +1561,23 @@ def main():
     # live HBM bytes: rank 0 (every rank runs the same per-GPU workload) starts
     # two single-process PMC child runs on its own device after the timed
     # region and the verification; the committed summary is only the fallback
+    sweep = None
+    if world == 1 and not args.no_sweep:
+        sweep = run_sweep(args, torch, lib, src, B, H, W, C, pitch, stream, sh, args.seed * 1000003 + rank)
+    del src, dst
+    torch.cuda.empty_cache()
+    # this run's rocprofv3 kernel trace of the same workload (a child run):
+    # the launch durations beside the HIP-event ones
+    trace = None
+    if world == 1 and not args.no_kernel_trace:
+        trace = kernel_trace_grid(args, ["--steps", "5", "--warmup", "1", "--images", str(B), "--height", str(H),
+                                         "--width", str(W), "--channels", str(C), "--depth", str(D),
+                                         "--border", str(args.border), "--seed", str(args.seed)]
+                                  + (["--no-sweep"] if sweep is None else []))
+    if sweep is not None:
+        for e in sweep:
+            hit = trace_lookup(trace, e["kernel"], -1 if e["config"] == "configs[1]" else 0)
+            e["rocprof_avg_us"] = round(hit[1], 1) if hit else None
     pmc = live_pmc(args, kernel) if not args.no_live_pmc else None
     pmc_source = ("live (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child runs of this per-GPU workload"
                   + (" on rank 0's device)" if world > 1 else ")")) if pmc else None
@@ -1480,12 +1617,20 @@ def main():
             "kernel_ms": round(kernel_ms, 4),
             "alg_bytes_per_launch": alg_bytes,
             "pmc_source": pmc_source,
+            "rocprof_avg_us": None,
+            "rocprof_launches": None,
         },
+        "sweep": sweep,
         "cpu_baseline": None,
         "verified_vs_numpy_port": verified,
         "verified_ranks": world if verified else None,
         "verified_images_per_rank": checked if verified else None,
     }
+    hit = trace_lookup(trace, kernel, 0)
+    if hit:
+        out["roofline"]["rocprof_launches"], out["roofline"]["rocprof_avg_us"] = hit[0], round(hit[1], 1)
+        out["roofline"]["rocprof_source"] = ("rocprofv3 --kernel-trace child run of this workload "
+                                             "(5 timed steps + the sweep's launches)")
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
     print(json.dumps(out), flush=True)

@@ -143,6 +143,35 @@ def test_plan_8k_batch_matches_per_call(tmp_path):
             assert np.array_equal(got[(s, d)][0], want[0]) and np.array_equal(got[(s, d)][1], want[1]), (s, d)
 
 
+def test_plan_8k_matches_oracle_at_demo_shapes(tmp_path):
+    """The benchmarked geometry against the oracles, not another product
+    kernel: 7680x4320 sources through plan_area_kernel's source launch at the
+    demo's shapes (area windows 23-34 pixels wide, the integer 32 x 18 scale of
+    240), and the depth 2-4 icons (1920x1080 .. 480x270: area downscales,
+    the plan's icon launch) plus the depth 5-6 icons (upscales) -- every
+    output equal to resize_cv(rgb) and resize_cv(oracle icon).  A JPEG scene
+    (its RGB from libjpeg-turbo, the decode pinned in test_gpu_jpeg.py) and a
+    noise BMP (raw pixels: every window sum at full entropy)."""
+    from PIL import Image
+    scene = J.test_image("scene", 4320, 7680, 61)
+    data = J.encode(scene, 90, 2)
+    p0 = tmp_path / "scene8k.jpg"
+    p0.write_bytes(data)
+    noise = np.random.default_rng(62).integers(0, 256, (4320, 7680, 3), dtype=np.uint8)
+    p1 = tmp_path / "noise8k.bmp"
+    Image.fromarray(noise).save(p1, "BMP")
+    paths, refs = [str(p0), str(p1)], [J.decode_rgb(data), noise]
+    depths = range(2, 7)
+    got = wicca_amd.get_img_matrix(paths, DEMO_SHAPES, depths)
+    for i, rgb in enumerate(refs):
+        icons = {d: _icon_oracle(rgb, d) for d in depths}
+        for s in DEMO_SHAPES:
+            want = R.resize(rgb, s, R.INTER_AREA)
+            for d in depths:
+                assert np.array_equal(got[(s, d)][0][i], want), (i, s, d)
+                assert np.array_equal(got[(s, d)][1][i], R.resize(icons[d], s, R.INTER_AREA)), (i, s, d)
+
+
 def test_plan_unreadable_file_fails_its_slot(tmp_path, capsys):
     paths, _ = _files(tmp_path, MIXED[:3])
     bad = tmp_path / "bad.jpg"
