@@ -90,15 +90,16 @@ const char* wicca_kernel_name(int depth, int64_t C, int ragged);
 int wicca_balance_ranges(const int64_t* weights, int64_t n, int n_ranges, int64_t* first);
 
 /* Device memory held by idle pooled workspaces of `device` (-1: all devices).
- * The pool keeps at most WICCA_WORKSPACE_CAP_MB (default: an eighth of device
- * 0's memory, at least 4096; 36 GB on an MI355X) idle per
+ * The pool keeps at most WICCA_WORKSPACE_CAP_MB (default: an eighth of each
+ * device's own memory, clamped to 4-16 GiB: 16 GiB on an MI355X) idle per
  * device: when a returned workspace takes the device above the cap, the least
  * recently used other workspaces free their buffers (the returned one keeps
  * its own, so a batch larger than the cap does not re-allocate every call). */
 int64_t wicca_workspace_bytes(int device);
 
-/* Set the idle-pool cap in bytes (bytes < 0: leave it); returns the previous
- * cap.  Overrides WICCA_WORKSPACE_CAP_MB. */
+/* Set the idle-pool cap in bytes for every device (bytes < 0: leave it);
+ * returns the previous cap (device 0's when none was set).  Overrides
+ * WICCA_WORKSPACE_CAP_MB. */
 int64_t wicca_set_workspace_cap(int64_t bytes);
 
 /* Free every idle pooled workspace (streams, events, buffers) of `device`
@@ -110,10 +111,16 @@ int wicca_release_workspaces(int device);
  * as a blit kernel that shares the GPU with the compute kernels.  *out gets
  * a block of at least `bytes`; wicca_host_free returns it to the pool (at most
  * WICCA_HOST_POOL_MB, default 4096, stay idle); wicca_host_pool_bytes: idle
- * pooled bytes. */
+ * pooled bytes.  Live blocks are capped (WICCA_HOST_PINNED_MB, default 3/8 of
+ * physical memory: pinned pages cannot be swapped out): past the cap
+ * wicca_host_alloc fails with WICCA_ERR_NOMEM and callers use pageable
+ * memory.  wicca_host_pinned_bytes: live bytes; wicca_set_host_pinned_cap:
+ * set the cap (bytes < 0: leave it), returns the previous one. */
 int wicca_host_alloc(int64_t bytes, void** out);
 int wicca_host_free(void* p);
 int64_t wicca_host_pool_bytes(void);
+int64_t wicca_host_pinned_bytes(void);
+int64_t wicca_set_host_pinned_cap(int64_t bytes);
 
 /* Output shape of get_small_copy for an (H, W) image at `depth`
  * (wicca/wavelet_coder.py:58 ratio = 2**depth; data_loader.py:107-110). */

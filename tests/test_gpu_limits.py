@@ -116,6 +116,31 @@ def test_workspace_pool_cap_and_release(coder):
         lib.wicca_set_workspace_cap(prev)
 
 
+def test_host_pinned_cap_falls_back_to_pageable():
+    """Live pinned output bytes are capped (WICCA_HOST_PINNED_MB): an
+    allocation past the cap gives an ordinary array, and freed blocks leave
+    the live count (callers may keep output arrays indefinitely)."""
+    import gc
+    lib = _lib.load()
+    prev = lib.wicca_set_host_pinned_cap(-1)
+    live = lib.wicca_host_pinned_bytes()
+    lib.wicca_set_host_pinned_cap(live + (1 << 20))
+    try:
+        a = _lib.pinned_empty((1 << 19,))  # fits: pinned, pooled by 4 KiB pages
+        assert lib.wicca_host_pinned_bytes() == live + (1 << 19)
+        assert a.base is not None
+        b = _lib.pinned_empty((1 << 20,))  # would pass the cap: pageable
+        assert b.base is None and b.shape == (1 << 20,)
+        assert lib.wicca_host_pinned_bytes() == live + (1 << 19)
+        a[:] = 7
+        assert int(a.sum()) == 7 << 19
+        del a
+        gc.collect()
+        assert lib.wicca_host_pinned_bytes() == live
+    finally:
+        lib.wicca_set_host_pinned_cap(prev)
+
+
 def _ragged_setup(shapes, C, D):
     r = 1 << D
     srcs, dsts, descs = [], [], (_lib.ImageDesc * len(shapes))()

@@ -50,6 +50,8 @@ SIGNATURES = {
     "wicca_host_alloc": (_int, [_i64, ctypes.POINTER(_p)]),
     "wicca_host_free": (_int, [_p]),
     "wicca_host_pool_bytes": (_i64, []),
+    "wicca_host_pinned_bytes": (_i64, []),
+    "wicca_set_host_pinned_cap": (_i64, [_i64]),
     "wicca_set_workspace_cap": (_i64, [_i64]),
     "wicca_icon_shape": (_int, [_i64, _i64, _int, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     "wicca_haar_ll_u8": (_int, [_p, _i64, _i64, _i64, _i64, _int, _int, _int, _p, _i64,
@@ -224,7 +226,8 @@ def pinned_empty(shape, dtype="uint8"):
     """An uninitialised numpy array in pinned host memory (wicca_host_alloc):
     device-to-host copies into it run by DMA.  The block goes back to the
     library's pool when the array (and every view of it) is gone.  Where the
-    runtime cannot pin memory (no device) the array is ordinary memory."""
+    runtime cannot pin memory (no device, or the live pinned bytes would pass
+    WICCA_HOST_PINNED_MB) the array is ordinary memory."""
     import weakref
 
     import numpy as np
@@ -237,5 +240,8 @@ def pinned_empty(shape, dtype="uint8"):
     if lib.wicca_host_alloc(n, ctypes.byref(p)) != WICCA_OK:  # no device / pinned memory exhausted:
         return np.empty(shape, dt)                            # pageable (copies into it are staged)
     buf = (ctypes.c_uint8 * n).from_address(p.value)
-    weakref.finalize(buf, lib.wicca_host_free, ctypes.c_void_p(p.value))
+    # not at interpreter exit: a block may still be the target of an
+    # asynchronous copy then; process teardown releases it after the native
+    # atexit drain has synchronised the streams
+    weakref.finalize(buf, lib.wicca_host_free, ctypes.c_void_p(p.value)).atexit = False
     return np.frombuffer(buf, dt, count=n // dt.itemsize).reshape(shape)

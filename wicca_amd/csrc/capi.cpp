@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <unistd.h>
 #include <chrono>
 #include <cstdarg>
 #include <functional>
@@ -60,31 +61,42 @@ void init_once()
 std::mutex g_pool_mu;
 std::vector<std::unique_ptr<Workspace>> g_pool;  // idle workspaces
 
-// Idle device memory the pool may keep per device (WICCA_WORKSPACE_CAP_MB,
-// default an eighth of device 0's memory, at least 4096 MiB: 36 GB on an
-// MI355X): a workspace returned while its device's idle pool already holds
-// that much gives its buffers back first.  Thirty-two threads on 8K inputs
-// otherwise pin ~3 GB each for the life of the process.  The stage plan's
-// workspace for 25 8K JPEG files holds ~7 GB (RGB, coefficients, row sums):
-// with a 4 GB cap, a loop keeping two batches in flight had one of its two
-// workspaces trimmed whenever both were idle, and the next batch re-allocated
-// it (hipFree synchronises the device) inside its issue, 20-45 ms.
-std::atomic<int64_t> g_pool_cap{-1};  // bytes; -1 = not read from the environment yet
+// Idle device memory the pool may keep per device (WICCA_WORKSPACE_CAP_MB;
+// default an eighth of THAT device's memory, clamped to [4, 16] GiB): a
+// workspace returned while its device's idle pool already holds that much
+// gives its buffers back first.  Thirty-two threads on 8K inputs otherwise
+// pin ~3 GB each for the life of the process.  The stage plan's workspace for
+// 25 8K JPEG files holds ~7 GB (RGB, coefficients, row sums): with a 4 GB cap,
+// a loop keeping two batches in flight had one of its two workspaces trimmed
+// whenever both were idle, and the next batch re-allocated it (hipFree
+// synchronises the device) inside its issue, 20-45 ms; 16 GiB keeps two such
+// workspaces and leaves the rest of the device to the models sharing it.
+std::atomic<int64_t> g_pool_cap{-1};  // bytes; -1 = no override (environment / wicca_set_workspace_cap)
 
-size_t pool_cap_bytes()
+size_t pool_cap_bytes(int device)
 {
     int64_t cap = g_pool_cap.load();
-    if (cap < 0) {
+    if (cap >= 0) return (size_t)cap;
+    static const int64_t env = [] {
         const char* e = getenv("WICCA_WORKSPACE_CAP_MB");
+        return e ? (int64_t)std::max<long long>(atoll(e), 0) << 20 : (int64_t)-1;
+    }();
+    if (env >= 0) return (size_t)env;
+    constexpr int kDev = 64;
+    static std::atomic<int64_t> per[kDev];
+    static std::once_flag once;
+    std::call_once(once, [] {
+        for (auto& p : per) p.store(-1);
+    });
+    const int d = device >= 0 && device < kDev ? device : 0;
+    int64_t c = per[d].load();
+    if (c < 0) {
         size_t total = 0;
-        const long long dflt =
-            hipDeviceTotalMem(&total, 0) == hipSuccess ? std::max<long long>(4096, (long long)(total >> 23)) : 4096;
-        const long long mb = e ? atoll(e) : dflt;
-        int64_t want = (int64_t)std::max<long long>(mb, 0) << 20;
-        g_pool_cap.compare_exchange_strong(cap, want);
-        cap = g_pool_cap.load();
+        const int64_t lo = (int64_t)4 << 30, hi = (int64_t)16 << 30;
+        c = hipDeviceTotalMem(&total, d) == hipSuccess ? std::min(hi, std::max(lo, (int64_t)(total >> 3))) : lo;
+        per[d].store(c);
     }
-    return (size_t)cap;
+    return (size_t)c;
 }
 
 size_t idle_bytes_locked(int device)
@@ -117,7 +129,7 @@ WorkspaceLease::~WorkspaceLease()
         std::lock_guard<std::mutex> g(g_pool_mu);
         g_pool.emplace_back(ws);
         size_t idle = idle_bytes_locked(ws->device);
-        for (size_t i = 0; i + 1 < g_pool.size() && idle > pool_cap_bytes();) {
+        for (size_t i = 0; i + 1 < g_pool.size() && idle > pool_cap_bytes(ws->device);) {
             Workspace* w = g_pool[i].get();
             if (w->device == ws->device && w->bytes() > 0) {
                 idle -= w->bytes();
@@ -591,7 +603,7 @@ int64_t wicca_workspace_bytes(int device)
 
 int64_t wicca_set_workspace_cap(int64_t bytes)
 {
-    const int64_t prev = (int64_t)pool_cap_bytes();
+    const int64_t prev = (int64_t)pool_cap_bytes(0);  // the override, else device 0's default
     if (bytes >= 0) g_pool_cap.store(bytes);
     return prev;
 }
@@ -619,12 +631,17 @@ int wicca_release_workspaces(int device)
 // buffer plus a host copy (in the stage plan, 21 such kernels per 25 x 8K
 // call shared the GPU with plan_rows_kernel and doubled its time).  Blocks
 // are pooled by size (a batch's outputs have the same sizes every call) up
-// to WICCA_HOST_POOL_MB (default 4096) of idle bytes.
+// to WICCA_HOST_POOL_MB (default 4096) of idle bytes.  Live (handed out)
+// bytes are capped too -- WICCA_HOST_PINNED_MB, default 3/8 of physical
+// memory: page-locked memory cannot be swapped out, and callers may keep their
+// output arrays as long as they like.  An allocation past the cap fails with
+// WICCA_ERR_NOMEM and the caller uses pageable memory instead.
 namespace {
 std::mutex g_host_mu;
 std::multimap<size_t, void*> g_host_idle;  // size -> idle block
 std::map<void*, size_t> g_host_live;       // block -> size
 size_t g_host_idle_bytes = 0;
+size_t g_host_live_bytes = 0;
 size_t host_pool_cap()
 {
     static const size_t cap = [] {
@@ -632,6 +649,23 @@ size_t host_pool_cap()
         return (size_t)(e ? std::max(0L, atol(e)) : 4096L) << 20;
     }();
     return cap;
+}
+std::atomic<int64_t> g_host_pinned_cap{-1};  // bytes; -1: not yet read from the environment
+size_t host_pinned_cap()
+{
+    int64_t c = g_host_pinned_cap.load();
+    if (c < 0) {
+        const char* e = getenv("WICCA_HOST_PINNED_MB");
+        if (e) {
+            c = (int64_t)std::max(0L, atol(e)) << 20;
+        } else {
+            const long pages = sysconf(_SC_PHYS_PAGES), page = sysconf(_SC_PAGESIZE);
+            c = pages > 0 && page > 0 ? (int64_t)pages * page / 8 * 3 : (int64_t)16 << 30;
+        }
+        int64_t expect = -1;
+        if (!g_host_pinned_cap.compare_exchange_strong(expect, c)) c = expect;
+    }
+    return (size_t)c;
 }
 }  // namespace
 
@@ -641,18 +675,26 @@ int wicca_host_alloc(int64_t bytes, void** out)
     const size_t n = (size_t)(bytes + 4095) & ~(size_t)4095;
     {
         std::lock_guard<std::mutex> g(g_host_mu);
+        if (g_host_live_bytes + n > host_pinned_cap())
+            return fail(WICCA_ERR_NOMEM, "host_alloc: %zu live pinned bytes + %zu would pass the cap of %zu "
+                        "(WICCA_HOST_PINNED_MB)", g_host_live_bytes, n, host_pinned_cap());
         auto it = g_host_idle.find(n);
         if (it != g_host_idle.end()) {
             *out = it->second;
             g_host_idle.erase(it);
             g_host_idle_bytes -= n;
             g_host_live[*out] = n;
+            g_host_live_bytes += n;
             return WICCA_OK;
         }
+        g_host_live_bytes += n;  // reserved while the allocation runs unlocked
     }
     void* p = nullptr;
-    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess || !p)
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess || !p) {
+        std::lock_guard<std::mutex> g(g_host_mu);
+        g_host_live_bytes -= n;
         return fail(WICCA_ERR_NOMEM, "hipHostMalloc of %zu bytes failed", n);
+    }
     std::lock_guard<std::mutex> g(g_host_mu);
     g_host_live[p] = n;
     *out = p;
@@ -669,6 +711,7 @@ int wicca_host_free(void* p)
         if (it == g_host_live.end()) return fail(WICCA_ERR_ARG, "host_free: not a wicca_host_alloc block");
         const size_t n = it->second;
         g_host_live.erase(it);
+        g_host_live_bytes -= n;
         g_host_idle.emplace(n, p);
         g_host_idle_bytes += n;
         while (g_host_idle_bytes > host_pool_cap() && !g_host_idle.empty()) {  // largest idle blocks first
@@ -686,6 +729,19 @@ int64_t wicca_host_pool_bytes(void)
 {
     std::lock_guard<std::mutex> g(g_host_mu);
     return (int64_t)g_host_idle_bytes;
+}
+
+int64_t wicca_host_pinned_bytes(void)
+{
+    std::lock_guard<std::mutex> g(g_host_mu);
+    return (int64_t)g_host_live_bytes;
+}
+
+int64_t wicca_set_host_pinned_cap(int64_t bytes)
+{
+    const int64_t prev = (int64_t)host_pinned_cap();
+    if (bytes >= 0) g_host_pinned_cap.store(bytes);
+    return prev;
 }
 
 int wicca_icon_shape(int64_t H, int64_t W, int depth, int64_t* out_h, int64_t* out_w)

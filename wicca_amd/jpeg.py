@@ -31,26 +31,60 @@ import numpy as np
 from . import _lib
 
 
-def read_files(paths: Sequence[str]) -> list:
-    """Each file's bytes as a read-only uint8 array over a memory map of the
-    file (no copy; the decoder's host threads fault the pages in in parallel
-    -- reading 25 x 10 MB files with f.read() took longer than the whole GPU
-    stage of the batch).  The maps close when the arrays are gone."""
+_READ_POOL = None
+
+
+def _read_pool():
+    global _READ_POOL
+    if _READ_POOL is None:
+        import os
+        from concurrent.futures import ThreadPoolExecutor
+        _READ_POOL = ThreadPoolExecutor(min(16, len(os.sched_getaffinity(0))), thread_name_prefix="wicca-read")
+    return _READ_POOL
+
+
+def _read_one(p: str) -> np.ndarray:
+    import os
+    with open(p, "rb", buffering=0) as f:
+        n = os.fstat(f.fileno()).st_size
+        buf = np.empty(n, np.uint8)
+        got = 0
+        mv = memoryview(buf)
+        while got < n:  # a file cut while it is read ends short, as cv2.imread reads it
+            k = f.readinto(mv[got:])
+            if not k:
+                break
+            got += k
+    return buf[:got]
+
+
+def _map_one(p: str) -> np.ndarray:
     import mmap
     import os
-    out = []
+    with open(p, "rb") as f:
+        if os.fstat(f.fileno()).st_size == 0:
+            return np.empty(0, np.uint8)
+        mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+    return np.frombuffer(mm, np.uint8)
+
+
+def read_files(paths: Sequence[str]) -> list:
+    """Each file's bytes as a uint8 array, read into memory of its own by a
+    pool of threads (serial f.read() of 25 x 10 MB files took longer than the
+    whole GPU stage of the batch).  WICCA_READ_MMAP=1 maps the files instead
+    (no copy), at a price: a file truncated or rewritten while it is mapped
+    raises SIGBUS when the decoder touches the missing pages, where a copy
+    (and cv2.imread) sees a short file."""
+    import os
     for p in paths:
         if not p:
             raise ValueError("File path cannot be empty")
-        with open(p, "rb") as f:
-            if os.fstat(f.fileno()).st_size == 0:
-                out.append(np.empty(0, np.uint8))
-                continue
-            mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
-        out.append(np.frombuffer(mm, np.uint8))
-    if not out:
+    if not paths:
         raise ValueError("need at least one array to stack")
-    return out
+    one = _map_one if os.environ.get("WICCA_READ_MMAP") == "1" else _read_one
+    if len(paths) == 1:
+        return [one(paths[0])]
+    return list(_read_pool().map(one, paths))
 
 
 def _buffers(blobs: Sequence[bytes]):
