@@ -359,7 +359,7 @@ def run_sweep(args, torch, lib, src, B, H, W, C, pitch, stream, sh, seed):
     the order the legs run (configs[2] first)."""
     from wicca_amd import _lib
 
-    steps = max(3, min(args.steps, 10))
+    steps = args.steps
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     out = []
     legs = [("configs[2]", d, B, H, W) for d in range(1, 7)] + [("configs[1]", 3, 32, 2160, 3840)]
@@ -382,7 +382,8 @@ def run_sweep(args, torch, lib, src, B, H, W, C, pitch, stream, sh, seed):
             _lib.check(lib.wicca_haar_ll_u8_uniform(
                 ctypes.c_void_p(s.data_ptr()), n, h, w, C, sp, h * sp, d, args.border, 0,
                 ctypes.c_void_p(dst.data_ptr()), op, oh * op, -1, sh))
-        launch()
+        for _ in range(max(1, args.warmup)):
+            launch()
         torch.cuda.synchronize()
         ev0.record(stream)
         for _ in range(steps):
