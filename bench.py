@@ -1129,14 +1129,22 @@ def run_plan(args, torch, rank):
 
 def plan_cpu_baseline(args, blobs, shapes, depths):
     """The reference's per-batch CPU cost, sampled: for one file, libjpeg-turbo's
-    decode (Pillow), the INTER_AREA source resize per classifier shape, the Haar
-    icon per depth and the icon resize per (shape, depth), with the NumPy ports
-    (oracle/resize_cv.py, oracle/haar_numpy.py -- much slower than OpenCV's C++
-    resize, which is absent here); extrapolated to the reference's structure,
-    which recomputes the whole chain for every file, classifier and depth."""
-    from oracle import haar_numpy, jpeg_pil
+    decode (Pillow: the library cv2.imread wraps), the INTER_AREA source resize
+    per classifier shape and the icon resize per (shape, depth) by
+    oracle/area_cpu.c (OpenCV's resize.cpp area tables and arithmetic order in
+    C at -O3, byte-identical to oracle/resize_cv.py -- cv2 itself is absent; the
+    icon upscales of the deep depths, OpenCV's bilinear path, through the NumPy
+    restatement: small images), and the Haar icon per depth by the NumPy port
+    (the reference's HaarCoder is NumPy); extrapolated to the reference's
+    structure, which recomputes the whole chain for every file, classifier and
+    depth (classifying_tools.py:312-323 under :339-346, :414-419, :546-551)."""
+    from oracle import c_oracle, haar_numpy, jpeg_pil
     from oracle import resize_cv as R
     B = len(blobs)
+
+    def area(img, sh):
+        out = c_oracle.area_resize(img, sh) if args.interpolation == R.INTER_AREA else None
+        return out if out is not None else R.resize(img, sh, args.interpolation)
     t = time.perf_counter()
     img = jpeg_pil.decode_rgb(blobs[0])
     t_dec = time.perf_counter() - t
@@ -1144,8 +1152,10 @@ def plan_cpu_baseline(args, blobs, shapes, depths):
     icons = {}
     for sh in shapes:
         t = time.perf_counter()
-        R.resize(img, sh, args.interpolation)
+        out = area(img, sh)
         t_src[sh] = time.perf_counter() - t
+        if sh == shapes[0] and not np.array_equal(out, R.resize(img, sh, args.interpolation)):
+            raise SystemExit("plan cpu baseline: compiled INTER_AREA differs from resize_cv")
     t_haar = {}
     for d in depths:
         t = time.perf_counter()
@@ -1154,17 +1164,22 @@ def plan_cpu_baseline(args, blobs, shapes, depths):
     for sh in shapes:
         for d in depths:
             t = time.perf_counter()
-            R.resize(icons[d], sh, args.interpolation)
+            area(icons[d], sh)
             t_ico[(sh, d)] = time.perf_counter() - t
     per_file = sum(t_dec + t_src[sh] + t_haar[d] + t_ico[(sh, d)] for sh in DEMO_CLASSIFIERS for d in depths)
     sampled = t_dec + sum(t_src.values()) + sum(t_haar.values()) + sum(t_ico.values())
     return {"value": round(per_file * B * 1e3, 1), "unit": "ms", "cores": 1, "kind": "port",
-            "sample": f"one {img.shape[1]}x{img.shape[0]} file: Pillow decode {t_dec * 1e3:.0f} ms, NumPy-port "
-                      f"INTER_AREA source resizes {sum(t_src.values()):.2f} s for {len(shapes)} shapes, "
-                      f"haar_numpy {sum(t_haar.values()):.2f} s for {len(depths)} depths, icon resizes "
-                      f"{sum(t_ico.values()):.2f} s ({sampled:.1f} s sampled); extrapolated to {B} files x "
+            "sample": f"one {img.shape[1]}x{img.shape[0]} file: Pillow decode {t_dec * 1e3:.0f} ms, INTER_AREA "
+                      f"source resizes in C (oracle/area_cpu.c, -O3, checked against resize_cv on this file) "
+                      f"{sum(t_src.values()) * 1e3:.0f} ms for {len(shapes)} shapes, haar_numpy "
+                      f"{sum(t_haar.values()) * 1e3:.0f} ms for {len(depths)} depths, icon resizes "
+                      f"{sum(t_ico.values()) * 1e3:.0f} ms ({sampled:.2f} s sampled); extrapolated to {B} files x "
                       f"{len(DEMO_CLASSIFIERS)} classifiers x {len(depths)} depths, single thread",
-            "per_file_ms": round(per_file * 1e3, 1)}
+            "per_file_ms": round(per_file * 1e3, 1),
+            "per_file_parts_ms": {"decode": round(t_dec * 1e3, 1),
+                                  "source_resize": {f"{w}x{h}": round(v * 1e3, 1) for (w, h), v in t_src.items()},
+                                  "haar": {str(d): round(v * 1e3, 1) for d, v in t_haar.items()},
+                                  "icon_resizes": round(sum(t_ico.values()) * 1e3, 1)}}
 
 
 def run_raster(args, torch, rank):

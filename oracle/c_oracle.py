@@ -80,3 +80,36 @@ def synth_u8(n: int, H: int, W: int, C: int, seed: int, first_image: int = 0) ->
     out = np.empty((n, H, W, C), np.uint8)
     lib().oracle_synth_u8(out.ctypes.data, n, H, W, C, seed, first_image)
     return out
+
+
+_AREA = None
+
+
+def area_resize(image: np.ndarray, dsize):
+    """cv2.resize(image, dsize, INTER_AREA) by oracle/area_cpu.c (compiled,
+    -O3): the downscales and copies; None where OpenCV takes its bilinear path
+    (an upscale in either direction)."""
+    global _AREA
+    if _AREA is None:
+        path = os.path.join(_HERE, "liboracle_area.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle`")
+        L = ctypes.CDLL(path)
+        L.oracle_area_resize_u8.argtypes = [_p, _i64, _i64, _i64, _i64, _p, _i64, _i64]
+        L.oracle_area_resize_u8.restype = ctypes.c_int
+        _AREA = L
+    img = np.asarray(image)
+    two_d = img.ndim == 2
+    if two_d:
+        img = img[:, :, None]
+    if img.strides[1] != img.shape[2] or img.strides[2] != 1:
+        img = np.ascontiguousarray(img)
+    H, W, C = img.shape
+    dw, dh = int(dsize[0]), int(dsize[1])
+    out = np.empty((dh, dw, C), np.uint8)
+    rc = _AREA.oracle_area_resize_u8(img.ctypes.data, H, W, C, img.strides[0], out.ctypes.data, dh, dw)
+    if rc == 1:
+        return None
+    if rc != 0:
+        raise ValueError("oracle_area_resize_u8 failed")
+    return out[:, :, 0] if out.shape[2] == 1 else out

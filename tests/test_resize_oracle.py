@@ -233,3 +233,23 @@ def test_engine_coefficient_tables_match_oracle(interp, K, src, dst):
     yo, yb = R.kernel_tables(H, dh, 1.0 / (dh / H), K)
     ref = np.concatenate([xo, xa.ravel(), yo, yb.ravel()])
     assert t.shape == ref.shape and np.array_equal(t, ref)
+
+
+@pytest.mark.parametrize("shape", [(300, 517, 3), (1081, 1919, 3), (448, 448, 3), (77, 61, 1), (240, 480, 4),
+                                   (135, 240, 3)])
+@pytest.mark.parametrize("dsize", [(224, 224), (331, 331), (299, 299), (240, 240), (112, 112), (30, 20)])
+def test_compiled_area_matches_numpy_restatement(shape, dsize):
+    """oracle/area_cpu.c (the plan bench's compiled CPU baseline) gives the
+    NumPy restatement's bytes for every INTER_AREA downscale and copy, and
+    declines the upscales (OpenCV's bilinear path)."""
+    from oracle import c_oracle
+    img = rng.integers(0, 256, shape, dtype=np.uint8)
+    got = c_oracle.area_resize(img, dsize)
+    if dsize[0] > shape[1] or dsize[1] > shape[0]:
+        assert got is None
+        return
+    want = R.resize(img, dsize, R.INTER_AREA)
+    assert np.array_equal(got, want)
+    view = np.zeros((shape[0], shape[1] + 5, shape[2]), np.uint8)[:, 2:2 + shape[1]]  # a strided view
+    view[...] = img
+    assert np.array_equal(c_oracle.area_resize(view, dsize), want)
