@@ -79,6 +79,18 @@ int plan_overlap()
     return m;
 }
 
+// WICCA_PLAN_WAVES=0: the plan's area resizes by plan_area_kernel (lanes over
+// every shape's columns) instead of plan_area_wave_kernel (a shape per wave,
+// its window mode specialised), for A/B runs
+bool plan_wave_kernel()
+{
+    static const bool on = [] {
+        const char* e = getenv("WICCA_PLAN_WAVES");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // Shapes per area-kernel launch (WICCA_PLAN_GROUP, 1..kPlanShapes; tuning)
 int plan_group_shapes()
 {
@@ -337,6 +349,7 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         std::vector<size_t> task_off;
         size_t off = 0;
         int rounds = 0, max_h = 0, band = wicca::kPlanBand;
+        bool wave_plans = true;  // every image has wave plans (wicca::plan_waves)
     };
     // want(s, j): image j's resize to shape s comes from the area kernel; rp(s, j), dst(s, j)
     auto make_groups = [&](const std::vector<RowSrc>& im, int band, auto want, auto rp_of, auto dst_of) {
@@ -386,6 +399,7 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                     e.area_scale[q] = rp.area_scale;
                 }
                 e.n_tasks = (int32_t)gr.tasks[(size_t)j].size();
+                if (gr.wave_plans && !wicca::plan_waves(gr.tasks[(size_t)j], e.kx, e)) gr.wave_plans = false;
                 gr.rounds = std::max(gr.rounds, (int)((e.n_tasks + 255) / 256));
                 gr.max_h = std::max(gr.max_h, (int)im[(size_t)j].H);
             }
@@ -584,6 +598,7 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                 pp.dh[q] = (int32_t)shapes[(size_t)g.shapes[q]].h;
             }
             pp.band_rows = g.band;
+            pp.wave_plans = g.wave_plans && plan_wave_kernel() ? 1 : 0;
             pp.bands = (g.max_h + g.band - 1) / g.band;
             const hipError_t e = wicca::launch_plan_area(pp, (int64_t)g.imgs.size(), g.max_h, g.rounds, cs);
             if (e != hipSuccess) return e;

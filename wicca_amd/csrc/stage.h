@@ -156,6 +156,12 @@ struct PlanImageDev {
     int32_t ky[kPlanShapes];    // > 0: integer scale (RS_AREA_FAST) ky rows per output row
     int32_t kx[kPlanShapes];
     float area_scale[kPlanShapes];
+    // plan_area_wave_kernel: the work of each of a workgroup's kPlanWaves
+    // waves -- one shape slot (wq), its window mode (wmode, plan_waves), and a
+    // run of that shape's 64-task chunks (wc0, wnc <= kPlanWaveRounds; wnc 0:
+    // the wave only stages rows)
+    uint8_t wq[8], wmode[8], wnc[8];
+    uint16_t wc0[8];
 };
 
 struct PlanParams {
@@ -164,7 +170,25 @@ struct PlanParams {
     int32_t dw[kPlanShapes], dh[kPlanShapes];
     int32_t bands;              // band_rows-row bands of the tallest image
     int32_t band_rows;          // <= kPlanBand
+    int32_t wave_plans;         // every image has wave plans (plan_waves): plan_area_wave_kernel
 };
+
+// Window modes of a wave (plan_area_wave_kernel): how its shape's columns sum
+// a staged row.  kModeGeneral: area_window_row (any window); 1..kModeMaxNgr:
+// the whole window read in one batch of 3 * mode + 3 dwords and summed over
+// `mode` 4-pixel groups (every task of the shape has len >> 2 in {mode - 2,
+// mode - 1}); kModeFastBase + G (G = 1..kModeMaxNgr): integer scale, kx >> 2 = G
+// 12-byte groups in one batch; kModeFast: area_fast_row.
+constexpr int kModeGeneral = 0, kModeMaxNgr = 10, kModeFastBase = 16, kModeFast = 32;
+// plan_area_wave_kernel's workgroup: 8 waves (one workgroup per CU, two waves
+// per SIMD), at most 3 chunks (64 columns each) per wave
+constexpr int kPlanWaves = 8, kPlanWaveRounds = 3;
+
+// The kPlanWaves wave plans of an image (shape slots with their modes and chunk
+// runs), from its task table (append_plan_tasks order) and each slot's
+// integer scale (kx[q] > 0) or general windows.  False when some wave would
+// need more than kPlanWaveRounds chunks (the launch then uses plan_area_kernel).
+bool plan_waves(const std::vector<PlanTask>& tasks, const int* kx, PlanImageDev& e);
 
 // A shape the plan's area kernel takes: RGB, output rows of at most 1024
 // pixels, and under an integer scale exact float sums (255 kx ky < 2^24).

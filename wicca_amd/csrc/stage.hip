@@ -524,7 +524,382 @@ __global__ __launch_bounds__(kStThreads, WICCA_PLAN_AREA_OCC) void plan_area_ker
     }
 }
 
+// ---------------------------------------------------------------------------
+// plan_area_wave_kernel: plan_area_kernel's rows, bands and vertical pass,
+// with each of the four waves owning ONE shape slot (a run of its 64-task
+// chunks, PlanImageDev::wq / wc0 / wnc) and that shape's window mode fixed for
+// the whole kernel (plan_waves, stage.h), so the horizontal sums are
+// specialised per mode:
+//   * general windows (NGR = mode groups): the window's first partial cell (2
+//     dwords) and its 4 * NGR following pixels (3 * NGR + 1 dwords) are read
+//     in ONE batch -- one LDS wait per column and row, where the per-group and
+//     per-pixel reads of area_window_row waited 6-7 times -- and summed with
+//     per-pixel weights: wm for whole groups, and for the last two groups
+//     weights fixed per column at kernel start (the column's last full cells,
+//     its partial cell wb, zeros past it: every column of the shape has len >>
+//     2 in {NGR - 2, NGR - 1}).  A zero weight adds +0: the float sums are
+//     area_window_row's, term by term in OpenCV's order;
+//   * integer scales (G = mode - kModeFastBase): all G 12-byte groups in one
+//     batch (in each lane's staggered bank order), v_dot4_u32_u8 sums.
+// The B channel's products are paired over two pixels (v_pk_mul_f32); the
+// sums stay serial per channel.
+// ---------------------------------------------------------------------------
+
+struct BatchW {
+    float wa, wm;
+    float ta[4], tb[4];  // weights of groups NGR - 2 and NGR - 1
+};
+
+__device__ __forceinline__ void batch_weights(uint32_t s1len, float wa, float wm, float wb, int ngr, BatchW& bw)
+{
+    const int len = (int)(s1len >> 16), G = len >> 2, rem = len & 3;
+    bw.wa = wa;
+    bw.wm = wm;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float tail = i < rem ? wm : (i == rem ? wb : 0.f);
+        const int ga = ngr - 2, gb = ngr - 1;
+        bw.ta[i] = ga < G ? wm : (ga == G ? tail : 0.f);
+        bw.tb[i] = gb < G ? wm : (gb == G ? tail : 0.f);
+    }
+}
+
+template <int NGR>
+__device__ __forceinline__ void area_batched_row(const uint8_t* b, uint32_t s1len, const BatchW& bw, float* h)
+{
+    const int s1 = (int)(s1len & 0xFFFFu);
+    const int ia = max(3 * s1 - 3, 0), base = 3 * s1;
+    const uint32_t* wf = reinterpret_cast<const uint32_t*>(b + (ia & ~3));
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(b + (base & ~3));
+    const uint32_t f0 = wf[0], f1 = wf[1];
+    uint32_t e[3 * NGR + 1];
+#pragma unroll
+    for (int i = 0; i < 3 * NGR + 1; ++i) e[i] = w[i];
+    // first partial cell (pixel s1 - 1; weight 0 without one)
+    const uint32_t r = __builtin_amdgcn_alignbyte(f1, f0, (uint32_t)(ia & 3));
+    f32x2 a01 = f32x2{ub(r, 0), ub(r, 1)} * f32x2{bw.wa, bw.wa};
+    float a2 = ub(r, 2) * bw.wa;
+    const uint32_t sh = (uint32_t)(base & 3);
+#pragma unroll
+    for (int g = 0; g < NGR; ++g) {
+        const uint32_t r0 = __builtin_amdgcn_alignbyte(e[3 * g + 1], e[3 * g], sh);
+        const uint32_t r1 = __builtin_amdgcn_alignbyte(e[3 * g + 2], e[3 * g + 1], sh);
+        const uint32_t r2 = __builtin_amdgcn_alignbyte(e[3 * g + 3], e[3 * g + 2], sh);
+        float w0 = bw.wm, w1 = bw.wm, w2 = bw.wm, w3 = bw.wm;
+        if (g == NGR - 1) {
+            w0 = bw.tb[0], w1 = bw.tb[1], w2 = bw.tb[2], w3 = bw.tb[3];
+        } else if (g == NGR - 2) {
+            w0 = bw.ta[0], w1 = bw.ta[1], w2 = bw.ta[2], w3 = bw.ta[3];
+        }
+        // pixel 0: r0.0 r0.1 r0.2 | 1: r0.3 r1.0 r1.1 | 2: r1.2 r1.3 r2.0 | 3: r2.1 r2.2 r2.3
+        const f32x2 b01 = f32x2{ub(r0, 2), ub(r1, 1)} * f32x2{w0, w1};
+        const f32x2 b23 = f32x2{ub(r2, 0), ub(r2, 3)} * f32x2{w2, w3};
+        a01 = a01 + f32x2{ub(r0, 0), ub(r0, 1)} * f32x2{w0, w0};
+        a2 = a2 + b01.x;
+        a01 = a01 + f32x2{ub(r0, 3), ub(r1, 0)} * f32x2{w1, w1};
+        a2 = a2 + b01.y;
+        a01 = a01 + f32x2{ub(r1, 2), ub(r1, 3)} * f32x2{w2, w2};
+        a2 = a2 + b23.x;
+        a01 = a01 + f32x2{ub(r2, 1), ub(r2, 2)} * f32x2{w3, w3};
+        a2 = a2 + b23.y;
+    }
+    h[0] = a01.x;
+    h[1] = a01.y;
+    h[2] = a2;
+}
+
+// RS_AREA_FAST, G = kx >> 2 groups read in one batch from group rot round
+// (the host's bank stagger, append_plan_tasks), then the kx & 3 last pixels
+template <int G>
+__device__ __forceinline__ void area_fast_batched_row(const uint8_t* b, int s1, int len, int rot, float* h)
+{
+    const int base = 3 * s1;
+    const uint32_t* w0 = reinterpret_cast<const uint32_t*>(b + (base & ~3));
+    const uint32_t sh = (uint32_t)(base & 3);
+    uint32_t e[G][4];
+    int j = rot;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+#pragma unroll
+        for (int m = 0; m < 4; ++m) e[k][m] = w0[3 * j + m];
+        j = j + 1 == G ? 0 : j + 1;
+    }
+    uint32_t R = 0, Gs = 0, B = 0;
+#pragma unroll
+    for (int k = 0; k < G; ++k) {
+        const uint32_t r0 = __builtin_amdgcn_alignbyte(e[k][1], e[k][0], sh);
+        const uint32_t r1 = __builtin_amdgcn_alignbyte(e[k][2], e[k][1], sh);
+        const uint32_t r2 = __builtin_amdgcn_alignbyte(e[k][3], e[k][2], sh);
+        R = __builtin_amdgcn_udot4(r0, 0x01000001u, R, false);
+        R = __builtin_amdgcn_udot4(r1, 0x00010000u, R, false);
+        R = __builtin_amdgcn_udot4(r2, 0x00000100u, R, false);
+        Gs = __builtin_amdgcn_udot4(r0, 0x00000100u, Gs, false);
+        Gs = __builtin_amdgcn_udot4(r1, 0x01000001u, Gs, false);
+        Gs = __builtin_amdgcn_udot4(r2, 0x00010000u, Gs, false);
+        B = __builtin_amdgcn_udot4(r0, 0x00010000u, B, false);
+        B = __builtin_amdgcn_udot4(r1, 0x00000100u, B, false);
+        B = __builtin_amdgcn_udot4(r2, 0x01000001u, B, false);
+    }
+    const uint8_t* q = b + base + 12 * G;
+    for (int i = 4 * G; i < len; ++i, q += 3) {
+        R += q[0];
+        Gs += q[1];
+        B += q[2];
+    }
+    h[0] = (float)R;
+    h[1] = (float)Gs;
+    h[2] = (float)B;
+}
+
+// One wave's share of a plan_area_wave_kernel workgroup: the band's rows
+// [ya, yb] staged cooperatively (every wave, one barrier per row, as
+// plan_area_kernel), its own shape's columns summed in MODE.
+constexpr int kWThreads = 64 * kPlanWaves;
+constexpr int kWChunks = (kStageRowMax / 16 + kWThreads - 1) / kWThreads;  // 16-B chunks of a row per lane (3)
+
+template <int MODE>
+__device__ __forceinline__ void plan_wave_rows(const PlanImageDev& im, const PlanParams& P, int band, int q, int c0,
+                                               int nc, int ya, int yb, uint8_t* buf0, uint8_t* buf1,
+                                               const PlanVRow* vtab)
+{
+    constexpr int NT = kPlanWaveRounds;
+    constexpr bool kBatched = MODE >= 1 && MODE <= kModeMaxNgr;
+    constexpr bool kFastB = MODE > kModeFastBase && MODE <= kModeFastBase + kModeMaxNgr;
+    constexpr bool kFast = kFastB || MODE == kModeFast;
+    const int t = threadIdx.x, lane = t & 63;
+    const int H = im.H, W = im.W;
+    // this lane's columns (one per chunk of the wave's run)
+    PlanTask tk[NT];
+    BatchW bw[kBatched ? NT : 1];
+    float acc[NT][3];
+#pragma unroll
+    for (int r = 0; r < NT; ++r) {
+        tk[r] = r < nc ? im.tasks[(c0 + r) * 64 + lane] : PlanTask{0u, 0.f, 0.f, 0.f, 0u};
+        if constexpr (kBatched) batch_weights(tk[r].s1len, tk[r].wa, tk[r].wm, tk[r].wb, MODE, bw[r]);
+        acc[r][0] = acc[r][1] = acc[r][2] = 0.f;
+    }
+    const PlanBand bq = nc > 0 ? im.bands[q][band] : PlanBand{0, 0, H, -1};
+    uint8_t* const dq = nc > 0 ? im.dst[q] : nullptr;
+    const int dwq = P.dw[q & (kPlanShapes - 1)];
+    const int kyq = im.ky[q & (kPlanShapes - 1)];
+    const float asq = im.area_scale[q & (kPlanShapes - 1)];
+    const bool halfq = im.kx[q & (kPlanShapes - 1)] == 2 && kyq == 2;
+
+    auto emit = [&](int r, int dy) {
+        if (!((tk[r].meta >> 24) & 1u)) return;
+        const int dx = (int)(tk[r].meta & 0xFFFFu);
+        __attribute__((address_space(1))) uint8_t* o =
+            (__attribute__((address_space(1))) uint8_t*)(dq + ((int64_t)dy * dwq + dx) * 3);
+        if constexpr (kFast) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                const int isum = (int)acc[r][c];
+                o[c] = halfq ? (uint8_t)((isum + 2) >> 2) : sat_u8(round_f32((float)isum * asq));
+            }
+        } else {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) o[c] = sat_u8(round_f32(acc[r][c]));
+        }
+    };
+
+    const uint8_t* const src = im.src;
+    const int64_t src_pitch = im.src_pitch;
+    const int nq = (W * 3 + 15) >> 4;
+    u32x4 va[kWChunks], vb[kWChunks];
+    auto load_row = [&](u32x4 (&v)[kWChunks], int y) {
+        const u32x4* row = reinterpret_cast<const u32x4*>(src + (int64_t)y * src_pitch);
+#pragma unroll
+        for (int m = 0; m < kWChunks; ++m) {
+            const int qq = t + m * kWThreads;
+            v[m] = qq < nq ? __builtin_nontemporal_load(row + qq) : u32x4{0, 0, 0, 0};
+        }
+    };
+    auto row_step = [&](u32x4 (&v)[kWChunks], int y, uint8_t* b) {
+#pragma unroll
+        for (int m = 0; m < kWChunks; ++m) {
+            const int qq = t + m * kWThreads;
+            if (qq < nq) reinterpret_cast<u32x4*>(b)[qq] = v[m];
+        }
+        if (y + 2 <= yb) load_row(v, y + 2);
+        __syncthreads();  // row y staged; the other buffer was last read before this
+        if (nc == 0 || y < bq.ya || y > bq.yb) return;  // wave-uniform
+        const PlanVRow vr = vtab[q * kPlanVRows + (y - ya)];
+        const bool w1 = vr.dy >= bq.dlo && vr.dy < bq.dhi;
+        const bool w2 = (vr.flags & kVTwo) && vr.dy + 1 >= bq.dlo && vr.dy + 1 < bq.dhi;
+        if (!w1 && !w2) return;
+#pragma unroll
+        for (int r = 0; r < NT; ++r) {
+            if (r >= nc) break;  // wave-uniform
+            float h[3];
+            if constexpr (kBatched)
+                area_batched_row<MODE>(b, tk[r].s1len, bw[r], h);
+            else if constexpr (kFastB)
+                area_fast_batched_row<MODE - kModeFastBase>(b, (int)(tk[r].s1len & 0xFFFFu), (int)(tk[r].s1len >> 16),
+                                                            (int)(tk[r].meta >> 25), h);
+            else if constexpr (MODE == kModeFast)
+                area_fast_row(b, (int)(tk[r].s1len & 0xFFFFu), (int)(tk[r].s1len >> 16), (int)(tk[r].meta >> 25), h);
+            else
+                area_window_row(b, tk[r].s1len, tk[r].wa, tk[r].wm, tk[r].wb, h);
+            if (w1) {  // the row's term in dy's window
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const float v1 = vr.b1 * h[c];
+                    acc[r][c] = (vr.flags & kVOpen1) ? v1 : acc[r][c] + v1;
+                }
+                if (vr.flags & kVClose1) emit(r, vr.dy);
+            }
+            if (w2) {  // ... and the first term of dy + 1's
+#pragma unroll
+                for (int c = 0; c < 3; ++c) acc[r][c] = vr.b2 * h[c];
+                if (vr.flags & kVClose2) emit(r, vr.dy + 1);
+            }
+        }
+    };
+    load_row(va, ya);
+    if (ya + 1 <= yb) load_row(vb, ya + 1);
+    for (int y = ya; y <= yb; y += 2) {
+        row_step(va, y, buf0);
+        if (y + 1 <= yb) row_step(vb, y + 1, buf1);
+    }
+}
+
+__global__ __launch_bounds__(kWThreads, 1) void plan_area_wave_kernel(PlanParams P)
+{
+    constexpr int kRowBuf = kStageRowMax + 64;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kRowBuf + kPlanShapes * kPlanVRows * sizeof(PlanVRow)];
+    uint8_t* const buf0 = lds;
+    uint8_t* const buf1 = lds + kRowBuf;
+    PlanVRow* const vtab = reinterpret_cast<PlanVRow*>(lds + 2 * kRowBuf);
+    uint32_t L = blockIdx.x;
+    const uint32_t per = gridDim.x / 8;
+    if (L < per * 8) L = (L % 8) * per + L / 8;
+    const PlanImageDev& im = P.imgs[L / (uint32_t)P.bands];
+    const int band = (int)(L % (uint32_t)P.bands);
+    const int H = im.H;
+    if (band * P.band_rows >= H) return;  // uniform
+    const int t = threadIdx.x;
+    const int n_shapes = P.n_shapes;
+    int ya = H, yb = -1;
+    for (int q = 0; q < n_shapes; ++q) {
+        if (im.dst[q] == nullptr) continue;
+        const PlanBand b = im.bands[q][band];
+        if (b.dlo < b.dhi) {
+            ya = min(ya, b.ya);
+            yb = max(yb, b.yb);
+        }
+    }
+    if (yb < ya) return;  // uniform
+    const int nrows = yb - ya + 1;
+    for (int e = t; e < n_shapes * nrows; e += kWThreads) {
+        const int q = e / nrows, j = e - q * nrows;
+        if (im.dst[q] != nullptr) vtab[q * kPlanVRows + j] = im.vrows[q][ya + j];
+    }
+    // this wave's plan (plan_waves pairs a heavy plan with a light one on
+    // waves w and w + 4)
+    const int p = t >> 6;
+    const int q = __builtin_amdgcn_readfirstlane((int)im.wq[p]);
+    const int mode = __builtin_amdgcn_readfirstlane((int)im.wmode[p]);
+    const int c0 = __builtin_amdgcn_readfirstlane((int)im.wc0[p]);
+    const int nc = __builtin_amdgcn_readfirstlane((int)im.wnc[p]);
+#define WICCA_WAVE(M) \
+    case M: plan_wave_rows<M>(im, P, band, q, c0, nc, ya, yb, buf0, buf1, vtab); break;
+    switch (nc == 0 ? kModeGeneral : mode) {
+        WICCA_WAVE(1) WICCA_WAVE(2) WICCA_WAVE(3) WICCA_WAVE(4) WICCA_WAVE(5)
+        WICCA_WAVE(6) WICCA_WAVE(7) WICCA_WAVE(8) WICCA_WAVE(9) WICCA_WAVE(10)
+        WICCA_WAVE(17) WICCA_WAVE(18) WICCA_WAVE(19) WICCA_WAVE(20) WICCA_WAVE(21)
+        WICCA_WAVE(22) WICCA_WAVE(23) WICCA_WAVE(24) WICCA_WAVE(25) WICCA_WAVE(26)
+        WICCA_WAVE(kModeFast)
+    default: plan_wave_rows<kModeGeneral>(im, P, band, q, c0, nc, ya, yb, buf0, buf1, vtab); break;
+    }
+#undef WICCA_WAVE
+}
+
 }  // namespace
+
+bool plan_waves(const std::vector<PlanTask>& tasks, const int* kx, PlanImageDev& e)
+{
+    memset(e.wq, 0, sizeof(e.wq));
+    memset(e.wmode, 0, sizeof(e.wmode));
+    memset(e.wnc, 0, sizeof(e.wnc));
+    memset(e.wc0, 0, sizeof(e.wc0));
+    // each shape slot's chunk run, mode and cost per chunk (VALU per row)
+    struct Slot {
+        int q, c0 = -1, n = 0, mode = kModeGeneral, waves = 0;
+        double cost = 0;
+    };
+    std::vector<Slot> slots;
+    const size_t nch = tasks.size() / 64;
+    for (size_t c = 0; c < nch; ++c) {
+        const int q = (int)((tasks[c * 64].meta >> 16) & 0xFu);
+        if (slots.empty() || slots.back().q != q) {
+            for (const Slot& s : slots)
+                if (s.q == q) return false;  // a slot's chunks not contiguous: not append_plan_tasks order
+            Slot s;
+            s.q = q;
+            s.c0 = (int)c;
+            slots.push_back(s);
+        }
+        slots.back().n++;
+    }
+    if (slots.empty() || (int)slots.size() > kPlanWaves) return false;
+    for (Slot& s : slots) {
+        int gmin = 1 << 30, gmax = -1, lmax = 0;
+        for (int c = s.c0; c < s.c0 + s.n; ++c)
+            for (int i = 0; i < 64; ++i) {
+                const PlanTask& k = tasks[(size_t)c * 64 + (size_t)i];
+                if (!((k.meta >> 24) & 1u)) continue;
+                const int len = (int)(k.s1len >> 16);
+                gmin = std::min(gmin, len >> 2);
+                gmax = std::max(gmax, len >> 2);
+                lmax = std::max(lmax, len);
+            }
+        if (gmax < 0) gmax = gmin = 0;
+        if (kx[s.q] > 0) {
+            const int G = kx[s.q] >> 2;
+            s.mode = G >= 1 && G <= kModeMaxNgr ? kModeFastBase + G : kModeFast;
+            s.cost = 3.0 * (lmax + 1);
+        } else {
+            const int ngr = gmax + 1;
+            s.mode = gmax - gmin <= 1 && ngr <= kModeMaxNgr ? ngr : kModeGeneral;
+            s.cost = 7.25 * (lmax + 2);
+        }
+        s.waves = (s.n + kPlanWaveRounds - 1) / kPlanWaveRounds;  // at most kPlanWaveRounds chunks a wave
+    }
+    int used = 0;
+    for (const Slot& s : slots) used += s.waves;
+    if (used > kPlanWaves) return false;
+    // the other waves to the slots with the most work per wave
+    for (int w = used; w < kPlanWaves; ++w) {
+        Slot* best = nullptr;
+        for (Slot& s : slots)
+            if (s.waves < s.n && (!best || s.cost * s.n / s.waves > best->cost * best->n / best->waves)) best = &s;
+        if (!best) break;
+        best->waves++;
+    }
+    struct Plan {
+        int q, mode, c0, nc;
+        double cost;
+    };
+    std::vector<Plan> plans;
+    for (const Slot& s : slots)
+        for (int k = 0; k < s.waves; ++k) {
+            const int a = s.c0 + s.n * k / s.waves, b = s.c0 + s.n * (k + 1) / s.waves;
+            if (b - a > kPlanWaveRounds) return false;
+            plans.push_back(Plan{s.q, s.mode, a, b - a, s.cost * (b - a)});
+        }
+    while ((int)plans.size() < kPlanWaves) plans.push_back(Plan{0, kModeGeneral, 0, 0, 0.0});
+    // waves w and w + 4 share a SIMD: the heaviest plans on 0..3, each paired
+    // with the lightest left
+    std::sort(plans.begin(), plans.end(), [](const Plan& a, const Plan& b) { return a.cost > b.cost; });
+    for (int i = 0; i < kPlanWaves / 2; ++i) {
+        const Plan& hi = plans[(size_t)i];
+        const Plan& lo = plans[(size_t)(kPlanWaves - 1 - i)];
+        e.wq[i] = (uint8_t)hi.q, e.wmode[i] = (uint8_t)hi.mode, e.wc0[i] = (uint16_t)hi.c0, e.wnc[i] = (uint8_t)hi.nc;
+        const int j = i + kPlanWaves / 2;
+        e.wq[j] = (uint8_t)lo.q, e.wmode[j] = (uint8_t)lo.mode, e.wc0[j] = (uint16_t)lo.c0, e.wnc[j] = (uint8_t)lo.nc;
+    }
+    return true;
+}
 
 void append_area_tasks(int W, int dw, double scale_x, bool fast, int kx, uint32_t out0, std::vector<AreaTask>& tasks)
 {
@@ -653,6 +1028,10 @@ hipError_t launch_plan_area(const PlanParams& p, int64_t n, int max_h, int round
         n * p.bands > INT32_MAX)
         return hipErrorInvalidValue;
     const dim3 grid((uint32_t)(n * p.bands));
+    if (p.wave_plans) {
+        hipLaunchKernelGGL(plan_area_wave_kernel, grid, dim3(kWThreads), 0, s, p);
+        return hipGetLastError();
+    }
     switch (rounds) {
     case 1: hipLaunchKernelGGL(plan_area_kernel<1>, grid, dim3(kStThreads), 0, s, p); break;
     case 2: hipLaunchKernelGGL(plan_area_kernel<2>, grid, dim3(kStThreads), 0, s, p); break;
