@@ -160,8 +160,8 @@ struct PlanImageDev {
     // waves -- one shape slot (wq), its window mode (wmode, plan_waves), and a
     // run of that shape's 64-task chunks (wc0, wnc <= kPlanWaveRounds; wnc 0:
     // the wave only stages rows)
-    uint8_t wq[8], wmode[8], wnc[8];
-    uint16_t wc0[8];
+    uint8_t wq[16], wmode[16], wnc[16];
+    uint16_t wc0[16];
 };
 
 struct PlanParams {
@@ -179,10 +179,18 @@ struct PlanParams {
 // `mode` 4-pixel groups (every task of the shape has len >> 2 in {mode - 2,
 // mode - 1}); kModeFastBase + G (G = 1..kModeMaxNgr): integer scale, kx >> 2 = G
 // 12-byte groups in one batch; kModeFast: area_fast_row.
-constexpr int kModeGeneral = 0, kModeMaxNgr = 10, kModeFastBase = 16, kModeFast = 32;
-// plan_area_wave_kernel's workgroup: 8 waves (one workgroup per CU, two waves
-// per SIMD), at most 3 chunks (64 columns each) per wave
-constexpr int kPlanWaves = 8, kPlanWaveRounds = 3;
+constexpr int kModeGeneral = 0, kModeMaxNgr = 9, kModeFastBase = 16, kModeFast = 32;
+// plan_area_wave_kernel's workgroup: kPlanWaves waves (16: one workgroup per
+// CU, four waves per SIMD), at most kPlanWaveRounds chunks (64 columns each)
+// per wave
+#ifndef WICCA_PLAN_WAVES_N
+#define WICCA_PLAN_WAVES_N 16
+#endif
+#ifndef WICCA_PLAN_WAVE_ROUNDS
+#define WICCA_PLAN_WAVE_ROUNDS 2
+#endif
+constexpr int kPlanWaves = WICCA_PLAN_WAVES_N, kPlanWaveRounds = WICCA_PLAN_WAVE_ROUNDS;
+static_assert(kPlanWaves == 8 || kPlanWaves == 16, "wave plans: 8 or 16 waves");
 
 // The kPlanWaves wave plans of an image (shape slots with their modes and chunk
 // runs), from its task table (append_plan_tasks order) and each slot's

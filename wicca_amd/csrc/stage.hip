@@ -43,6 +43,12 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float ub(uint32_t v, int k) { return (float)((v >> (8 * k)) & 0xFFu); }
 
+// A 16-B nontemporal load through a global (not flat) pointer: a flat load
+// counts on the LDS counter too, so every LDS wait of a row's sums would also
+// wait for the next rows' loads in flight
+typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+__device__ __forceinline__ u32x4 gload16_nt(const void* p) { return __builtin_nontemporal_load((gu32x4*)p); }
+
 // One AreaTask (stage.h) on one staged RGB row b (LDS, 64 B of slack past the
 // row): the output column's three channel sums in OpenCV's order — the first
 // partial cell, the full cells left to right, the last partial cell (a weight
@@ -220,7 +226,7 @@ stage_rows_kernel(StageParams P)
 #pragma unroll
         for (int m = 0; m < kStChunks; ++m) {
             const int q = t + m * kStThreads;
-            v[m] = q < nq ? __builtin_nontemporal_load(row + q) : u32x4{0, 0, 0, 0};
+            v[m] = q < nq ? gload16_nt(row + q) : u32x4{0, 0, 0, 0};
         }
     };
     // rows the block sums take: real rows, and under REPLICATE the clamped
@@ -471,7 +477,7 @@ __global__ __launch_bounds__(kStThreads, WICCA_PLAN_AREA_OCC) void plan_area_ker
 #pragma unroll
         for (int m = 0; m < kStChunks; ++m) {
             const int q = t + m * kStThreads;
-            v[m] = q < nq ? __builtin_nontemporal_load(row + q) : u32x4{0, 0, 0, 0};
+            v[m] = q < nq ? gload16_nt(row + q) : u32x4{0, 0, 0, 0};
         }
     };
     auto row_step = [&](auto& v, int y, uint8_t* b) {
@@ -564,6 +570,36 @@ __device__ __forceinline__ void batch_weights(uint32_t s1len, float wa, float wm
     }
 }
 
+// One 4-pixel group of area_batched_row: pixels 0..3 of the realigned dwords
+// r0 r1 r2 (pixel 0: r0.0 r0.1 r0.2 | 1: r0.3 r1.0 r1.1 | 2: r1.2 r1.3 r2.0 |
+// 3: r2.1 r2.2 r2.3) with weights w0..w3, into the channel sums in order.
+// Scalar f32 operations: a packed multiply or add issues in the cycles of two
+// scalar ones, and its operand pairs cost moves and registers.
+__device__ __forceinline__ void area_group4(uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3, uint32_t sh, float w0,
+                                            float w1, float w2, float w3, float& aR, float& aG, float& aB)
+{
+    const uint32_t r0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    const uint32_t r1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    const uint32_t r2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+    aR = aR + ub(r0, 0) * w0;
+    aG = aG + ub(r0, 1) * w0;
+    aB = aB + ub(r0, 2) * w0;
+    aR = aR + ub(r0, 3) * w1;
+    aG = aG + ub(r1, 0) * w1;
+    aB = aB + ub(r1, 1) * w1;
+    aR = aR + ub(r1, 2) * w2;
+    aG = aG + ub(r1, 3) * w2;
+    aB = aB + ub(r2, 0) * w2;
+    aR = aR + ub(r2, 1) * w3;
+    aG = aG + ub(r2, 2) * w3;
+    aB = aB + ub(r2, 3) * w3;
+}
+
+// The window in steps of up to kStepG groups (3 * kStepG + 1 dwords a step),
+// the next step's reads issued before this step's sums (two steps of
+// registers: with four waves a SIMD the other waves hide the rest)
+constexpr int kStepG = 4;
+
 template <int NGR>
 __device__ __forceinline__ void area_batched_row(const uint8_t* b, uint32_t s1len, const BatchW& bw, float* h)
 {
@@ -572,40 +608,40 @@ __device__ __forceinline__ void area_batched_row(const uint8_t* b, uint32_t s1le
     const uint32_t* wf = reinterpret_cast<const uint32_t*>(b + (ia & ~3));
     const uint32_t* w = reinterpret_cast<const uint32_t*>(b + (base & ~3));
     const uint32_t f0 = wf[0], f1 = wf[1];
-    uint32_t e[3 * NGR + 1];
+    constexpr int kSteps = (NGR + kStepG - 1) / kStepG;
+    uint32_t e[2][3 * kStepG + 1];
+    auto fetch = [&](int st, uint32_t (&d)[3 * kStepG + 1]) {
+        const int g0 = st * kStepG, ng = min(kStepG, NGR - g0);
 #pragma unroll
-    for (int i = 0; i < 3 * NGR + 1; ++i) e[i] = w[i];
-    // first partial cell (pixel s1 - 1; weight 0 without one)
+        for (int i = 0; i < 3 * kStepG + 1; ++i)
+            if (i < 3 * ng + 1) d[i] = w[3 * g0 + i];
+    };
+    fetch(0, e[0]);
+    // first partial cell (pixel s1 - 1; weight 0 without one): 0 + p = p
     const uint32_t r = __builtin_amdgcn_alignbyte(f1, f0, (uint32_t)(ia & 3));
-    f32x2 a01 = f32x2{ub(r, 0), ub(r, 1)} * f32x2{bw.wa, bw.wa};
-    float a2 = ub(r, 2) * bw.wa;
+    float aR = ub(r, 0) * bw.wa, aG = ub(r, 1) * bw.wa, aB = ub(r, 2) * bw.wa;
     const uint32_t sh = (uint32_t)(base & 3);
 #pragma unroll
-    for (int g = 0; g < NGR; ++g) {
-        const uint32_t r0 = __builtin_amdgcn_alignbyte(e[3 * g + 1], e[3 * g], sh);
-        const uint32_t r1 = __builtin_amdgcn_alignbyte(e[3 * g + 2], e[3 * g + 1], sh);
-        const uint32_t r2 = __builtin_amdgcn_alignbyte(e[3 * g + 3], e[3 * g + 2], sh);
-        float w0 = bw.wm, w1 = bw.wm, w2 = bw.wm, w3 = bw.wm;
-        if (g == NGR - 1) {
-            w0 = bw.tb[0], w1 = bw.tb[1], w2 = bw.tb[2], w3 = bw.tb[3];
-        } else if (g == NGR - 2) {
-            w0 = bw.ta[0], w1 = bw.ta[1], w2 = bw.ta[2], w3 = bw.ta[3];
+    for (int st = 0; st < kSteps; ++st) {
+        if (st + 1 < kSteps) fetch(st + 1, e[(st + 1) & 1]);
+        const uint32_t(&d)[3 * kStepG + 1] = e[st & 1];
+#pragma unroll
+        for (int k = 0; k < kStepG; ++k) {
+            const int g = st * kStepG + k;
+            if (g >= NGR) break;
+            float w0 = bw.wm, w1 = bw.wm, w2 = bw.wm, w3 = bw.wm;
+            if (g == NGR - 1) {
+                w0 = bw.tb[0], w1 = bw.tb[1], w2 = bw.tb[2], w3 = bw.tb[3];
+            } else if (g == NGR - 2) {
+                w0 = bw.ta[0], w1 = bw.ta[1], w2 = bw.ta[2], w3 = bw.ta[3];
+            }
+            area_group4(d[3 * k], d[3 * k + 1], d[3 * k + 2], d[3 * k + 3], sh, w0, w1, w2, w3, aR, aG, aB);
         }
-        // pixel 0: r0.0 r0.1 r0.2 | 1: r0.3 r1.0 r1.1 | 2: r1.2 r1.3 r2.0 | 3: r2.1 r2.2 r2.3
-        const f32x2 b01 = f32x2{ub(r0, 2), ub(r1, 1)} * f32x2{w0, w1};
-        const f32x2 b23 = f32x2{ub(r2, 0), ub(r2, 3)} * f32x2{w2, w3};
-        a01 = a01 + f32x2{ub(r0, 0), ub(r0, 1)} * f32x2{w0, w0};
-        a2 = a2 + b01.x;
-        a01 = a01 + f32x2{ub(r0, 3), ub(r1, 0)} * f32x2{w1, w1};
-        a2 = a2 + b01.y;
-        a01 = a01 + f32x2{ub(r1, 2), ub(r1, 3)} * f32x2{w2, w2};
-        a2 = a2 + b23.x;
-        a01 = a01 + f32x2{ub(r2, 1), ub(r2, 2)} * f32x2{w3, w3};
-        a2 = a2 + b23.y;
+        __builtin_amdgcn_sched_barrier(0);
     }
-    h[0] = a01.x;
-    h[1] = a01.y;
-    h[2] = a2;
+    h[0] = aR;
+    h[1] = aG;
+    h[2] = aB;
 }
 
 // RS_AREA_FAST, G = kx >> 2 groups read in one batch from group rot round
@@ -654,12 +690,24 @@ __device__ __forceinline__ void area_fast_batched_row(const uint8_t* b, int s1, 
 // One wave's share of a plan_area_wave_kernel workgroup: the band's rows
 // [ya, yb] staged cooperatively (every wave, one barrier per row, as
 // plan_area_kernel), its own shape's columns summed in MODE.
+#ifndef WICCA_PLAN_WAVE_OCC
+#define WICCA_PLAN_WAVE_OCC 1  // workgroups per CU the register budget is sized for (2: 4 waves per SIMD, spills)
+#endif
+#ifndef WICCA_PLAN_WAVE_FENCE
+#define WICCA_PLAN_WAVE_FENCE 1  // no scheduling across a wave's columns (register budget)
+#endif
+#ifndef WICCA_PLAN_WAVE_REWEIGH
+#define WICCA_PLAN_WAVE_REWEIGH 1  // batched windows' last-group weights formed per row, not held
+#endif
+#ifndef WICCA_PLAN_WAVE_GLDS
+#define WICCA_PLAN_WAVE_GLDS 1  // rows staged by LDS-DMA into three buffers (0: through registers, two buffers)
+#endif
 constexpr int kWThreads = 64 * kPlanWaves;
 constexpr int kWChunks = (kStageRowMax / 16 + kWThreads - 1) / kWThreads;  // 16-B chunks of a row per lane (3)
 
 template <int MODE>
 __device__ __forceinline__ void plan_wave_rows(const PlanImageDev& im, const PlanParams& P, int band, int q, int c0,
-                                               int nc, int ya, int yb, uint8_t* buf0, uint8_t* buf1,
+                                               int nc, int ya, int yb, uint8_t* buf0, uint8_t* buf1, uint8_t* buf2,
                                                const PlanVRow* vtab)
 {
     constexpr int NT = kPlanWaveRounds;
@@ -670,12 +718,15 @@ __device__ __forceinline__ void plan_wave_rows(const PlanImageDev& im, const Pla
     const int H = im.H, W = im.W;
     // this lane's columns (one per chunk of the wave's run)
     PlanTask tk[NT];
-    BatchW bw[kBatched ? NT : 1];
+    BatchW bw[kBatched && !WICCA_PLAN_WAVE_REWEIGH ? NT : 1];
+    (void)bw;
     float acc[NT][3];
 #pragma unroll
     for (int r = 0; r < NT; ++r) {
         tk[r] = r < nc ? im.tasks[(c0 + r) * 64 + lane] : PlanTask{0u, 0.f, 0.f, 0.f, 0u};
+#if !WICCA_PLAN_WAVE_REWEIGH
         if constexpr (kBatched) batch_weights(tk[r].s1len, tk[r].wa, tk[r].wm, tk[r].wb, MODE, bw[r]);
+#endif
         acc[r][0] = acc[r][1] = acc[r][2] = 0.f;
     }
     const PlanBand bq = nc > 0 ? im.bands[q][band] : PlanBand{0, 0, H, -1};
@@ -705,23 +756,8 @@ __device__ __forceinline__ void plan_wave_rows(const PlanImageDev& im, const Pla
     const uint8_t* const src = im.src;
     const int64_t src_pitch = im.src_pitch;
     const int nq = (W * 3 + 15) >> 4;
-    u32x4 va[kWChunks], vb[kWChunks];
-    auto load_row = [&](u32x4 (&v)[kWChunks], int y) {
-        const u32x4* row = reinterpret_cast<const u32x4*>(src + (int64_t)y * src_pitch);
-#pragma unroll
-        for (int m = 0; m < kWChunks; ++m) {
-            const int qq = t + m * kWThreads;
-            v[m] = qq < nq ? __builtin_nontemporal_load(row + qq) : u32x4{0, 0, 0, 0};
-        }
-    };
-    auto row_step = [&](u32x4 (&v)[kWChunks], int y, uint8_t* b) {
-#pragma unroll
-        for (int m = 0; m < kWChunks; ++m) {
-            const int qq = t + m * kWThreads;
-            if (qq < nq) reinterpret_cast<u32x4*>(b)[qq] = v[m];
-        }
-        if (y + 2 <= yb) load_row(v, y + 2);
-        __syncthreads();  // row y staged; the other buffer was last read before this
+    // the row's sums of this wave (after row y is in b)
+    auto row_sums = [&](int y, const uint8_t* b) {
         if (nc == 0 || y < bq.ya || y > bq.yb) return;  // wave-uniform
         const PlanVRow vr = vtab[q * kPlanVRows + (y - ya)];
         const bool w1 = vr.dy >= bq.dlo && vr.dy < bq.dhi;
@@ -731,8 +767,15 @@ __device__ __forceinline__ void plan_wave_rows(const PlanImageDev& im, const Pla
         for (int r = 0; r < NT; ++r) {
             if (r >= nc) break;  // wave-uniform
             float h[3];
-            if constexpr (kBatched)
+            if constexpr (kBatched) {
+#if WICCA_PLAN_WAVE_REWEIGH
+                BatchW bwr;  // the column's weights again (registers: 8 fewer per column held)
+                batch_weights(tk[r].s1len, tk[r].wa, tk[r].wm, tk[r].wb, MODE, bwr);
+                area_batched_row<MODE>(b, tk[r].s1len, bwr, h);
+#else
                 area_batched_row<MODE>(b, tk[r].s1len, bw[r], h);
+#endif
+            }
             else if constexpr (kFastB)
                 area_fast_batched_row<MODE - kModeFastBase>(b, (int)(tk[r].s1len & 0xFFFFu), (int)(tk[r].s1len >> 16),
                                                             (int)(tk[r].meta >> 25), h);
@@ -753,7 +796,85 @@ __device__ __forceinline__ void plan_wave_rows(const PlanImageDev& im, const Pla
                 for (int c = 0; c < 3; ++c) acc[r][c] = vr.b2 * h[c];
                 if (vr.flags & kVClose2) emit(r, vr.dy + 1);
             }
+#if WICCA_PLAN_WAVE_FENCE
+            // one column's window in registers at a time (the scheduler would
+            // hoist every round's window reads, ~30 VGPRs each, past the
+            // 128-register budget of four waves per SIMD)
+            __builtin_amdgcn_sched_barrier(0);
+#endif
         }
+    };
+#if WICCA_PLAN_WAVE_GLDS
+    // Rows land in LDS by LDS-DMA (global_load_lds_dwordx4: 1 KiB per wave
+    // instruction, lane-linear), three buffers, two rows in flight: wave w
+    // issues the row's pieces w, w + 8, w + 16.  At row y each wave waits for
+    // its own pieces of row y (vmcnt: only row y + 1's may stay in flight;
+    // loads retire in order, the output stores between them do not matter),
+    // then the barrier makes every wave's pieces visible and tells that row
+    // y - 1 is done everywhere, so row y + 2 may go into its buffer.
+    const int lane16 = lane * 16;
+    const int npieces = (nq * 16 + 1023) >> 10;
+    const int wv = t >> 6;
+    const int cw = wv < npieces ? (npieces - 1 - wv) / kPlanWaves + 1 : 0;  // pieces per row of this wave
+    auto issue_row = [&](int y, uint8_t* b) {
+        const uint8_t* row = src + (int64_t)y * src_pitch;
+#pragma unroll
+        for (int k = 0; k < (kStageRowMax / 1024 + kPlanWaves - 1) / kPlanWaves; ++k) {
+            const int p = wv + k * kPlanWaves;
+            if (p < npieces) {  // wave-uniform; lanes past the row re-read its last chunk into the slack
+                const int off = min(p * 1024 + lane16, (nq - 1) * 16);
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(row + off),
+                                                 (__attribute__((address_space(3))) void*)(b + p * 1024), 16, 0, 0);
+            }
+        }
+    };
+    auto wait_row = [&](bool next_in_flight) {
+        if (!next_in_flight || cw == 0)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else if (cw == 1)
+            asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        else if (cw == 2)
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    };
+    // buffer k at buf0 + k * (buf1 - buf0) (arithmetic, so the compiler
+    // keeps the LDS address space: an array of the three pointers made every
+    // window read a flat load)
+    const int stride = (int)(buf1 - buf0);
+    (void)buf2;
+    issue_row(ya, buf0);
+    if (ya + 1 <= yb) issue_row(ya + 1, buf1);
+    int i0 = 0;  // (y - ya) % 3
+    for (int y = ya; y <= yb; ++y) {
+        wait_row(y + 1 <= yb);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        const int i2 = i0 == 0 ? 2 : i0 - 1;  // (y + 2 - ya) % 3
+        if (y + 2 <= yb) issue_row(y + 2, buf0 + i2 * stride);
+        row_sums(y, buf0 + i0 * stride);
+        i0 = i0 == 2 ? 0 : i0 + 1;
+    }
+#else
+    u32x4 va[kWChunks], vb[kWChunks];
+    auto load_row = [&](u32x4 (&v)[kWChunks], int y) {
+        const u32x4* row = reinterpret_cast<const u32x4*>(src + (int64_t)y * src_pitch);
+#pragma unroll
+        for (int m = 0; m < kWChunks; ++m) {
+            const int qq = t + m * kWThreads;
+            v[m] = qq < nq ? gload16_nt(row + qq) : u32x4{0, 0, 0, 0};
+        }
+    };
+    auto row_step = [&](u32x4 (&v)[kWChunks], int y, uint8_t* b) {
+#pragma unroll
+        for (int m = 0; m < kWChunks; ++m) {
+            const int qq = t + m * kWThreads;
+            if (qq < nq) reinterpret_cast<u32x4*>(b)[qq] = v[m];
+        }
+        if (y + 2 <= yb) load_row(v, y + 2);
+        __syncthreads();  // row y staged; the other buffer was last read before this
+        row_sums(y, b);
     };
     load_row(va, ya);
     if (ya + 1 <= yb) load_row(vb, ya + 1);
@@ -761,15 +882,23 @@ __device__ __forceinline__ void plan_wave_rows(const PlanImageDev& im, const Pla
         row_step(va, y, buf0);
         if (y + 1 <= yb) row_step(vb, y + 1, buf1);
     }
+#endif
 }
 
-__global__ __launch_bounds__(kWThreads, 1) void plan_area_wave_kernel(PlanParams P)
+__global__ __attribute__((amdgpu_flat_work_group_size(1, kWThreads),
+                          amdgpu_waves_per_eu(WICCA_PLAN_WAVE_OCC * kPlanWaves / 4))) void
+plan_area_wave_kernel(PlanParams P)
 {
-    constexpr int kRowBuf = kStageRowMax + 64;
-    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kRowBuf + kPlanShapes * kPlanVRows * sizeof(PlanVRow)];
+    // [row buffers | the band's vertical table]: the window reads past a
+    // row's end (at most ~40 B, weighted 0) land in the next buffer or the
+    // table; three buffers of 24 KiB + 8 KiB = 80 KiB, two workgroups a CU
+    constexpr int kRowBuf = WICCA_PLAN_WAVE_GLDS ? kStageRowMax : kStageRowMax + 64;
+    constexpr int kBufs = WICCA_PLAN_WAVE_GLDS ? 3 : 2;
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kBufs * kRowBuf + kPlanShapes * kPlanVRows * sizeof(PlanVRow)];
     uint8_t* const buf0 = lds;
     uint8_t* const buf1 = lds + kRowBuf;
-    PlanVRow* const vtab = reinterpret_cast<PlanVRow*>(lds + 2 * kRowBuf);
+    uint8_t* const buf2 = lds + 2 * kRowBuf;  // (unused with two buffers)
+    PlanVRow* const vtab = reinterpret_cast<PlanVRow*>(lds + kBufs * kRowBuf);
     uint32_t L = blockIdx.x;
     const uint32_t per = gridDim.x / 8;
     if (L < per * 8) L = (L % 8) * per + L / 8;
@@ -794,23 +923,29 @@ __global__ __launch_bounds__(kWThreads, 1) void plan_area_wave_kernel(PlanParams
         const int q = e / nrows, j = e - q * nrows;
         if (im.dst[q] != nullptr) vtab[q * kPlanVRows + j] = im.vrows[q][ya + j];
     }
-    // this wave's plan (plan_waves pairs a heavy plan with a light one on
-    // waves w and w + 4)
+    // this wave's plan (plan_waves balances the plans over the SIMDs)
     const int p = t >> 6;
     const int q = __builtin_amdgcn_readfirstlane((int)im.wq[p]);
     const int mode = __builtin_amdgcn_readfirstlane((int)im.wmode[p]);
     const int c0 = __builtin_amdgcn_readfirstlane((int)im.wc0[p]);
     const int nc = __builtin_amdgcn_readfirstlane((int)im.wnc[p]);
 #define WICCA_WAVE(M) \
-    case M: plan_wave_rows<M>(im, P, band, q, c0, nc, ya, yb, buf0, buf1, vtab); break;
+    case M: plan_wave_rows<M>(im, P, band, q, c0, nc, ya, yb, buf0, buf1, buf2, vtab); break;
+#ifdef WICCA_PLAN_WAVE_ONLY  // register-budget experiments: one mode compiled
+    switch (nc == 0 ? kModeGeneral : mode) {
+        WICCA_WAVE(WICCA_PLAN_WAVE_ONLY)
+    default: break;
+    }
+#else
     switch (nc == 0 ? kModeGeneral : mode) {
         WICCA_WAVE(1) WICCA_WAVE(2) WICCA_WAVE(3) WICCA_WAVE(4) WICCA_WAVE(5)
-        WICCA_WAVE(6) WICCA_WAVE(7) WICCA_WAVE(8) WICCA_WAVE(9) WICCA_WAVE(10)
+        WICCA_WAVE(6) WICCA_WAVE(7) WICCA_WAVE(8) WICCA_WAVE(9)
         WICCA_WAVE(17) WICCA_WAVE(18) WICCA_WAVE(19) WICCA_WAVE(20) WICCA_WAVE(21)
-        WICCA_WAVE(22) WICCA_WAVE(23) WICCA_WAVE(24) WICCA_WAVE(25) WICCA_WAVE(26)
+        WICCA_WAVE(22) WICCA_WAVE(23) WICCA_WAVE(24) WICCA_WAVE(25)
         WICCA_WAVE(kModeFast)
-    default: plan_wave_rows<kModeGeneral>(im, P, band, q, c0, nc, ya, yb, buf0, buf1, vtab); break;
+    default: plan_wave_rows<kModeGeneral>(im, P, band, q, c0, nc, ya, yb, buf0, buf1, buf2, vtab); break;
     }
+#endif
 #undef WICCA_WAVE
 }
 
@@ -888,15 +1023,17 @@ bool plan_waves(const std::vector<PlanTask>& tasks, const int* kx, PlanImageDev&
             plans.push_back(Plan{s.q, s.mode, a, b - a, s.cost * (b - a)});
         }
     while ((int)plans.size() < kPlanWaves) plans.push_back(Plan{0, kModeGeneral, 0, 0, 0.0});
-    // waves w and w + 4 share a SIMD: the heaviest plans on 0..3, each paired
-    // with the lightest left
+    // waves w, w + 4, w + 8, ... share SIMD w % 4: the plans dealt to the
+    // SIMDs heaviest first in snake order (0 1 2 3 3 2 1 0 ...), so each SIMD
+    // gets a similar sum of work
     std::sort(plans.begin(), plans.end(), [](const Plan& a, const Plan& b) { return a.cost > b.cost; });
-    for (int i = 0; i < kPlanWaves / 2; ++i) {
-        const Plan& hi = plans[(size_t)i];
-        const Plan& lo = plans[(size_t)(kPlanWaves - 1 - i)];
-        e.wq[i] = (uint8_t)hi.q, e.wmode[i] = (uint8_t)hi.mode, e.wc0[i] = (uint16_t)hi.c0, e.wnc[i] = (uint8_t)hi.nc;
-        const int j = i + kPlanWaves / 2;
-        e.wq[j] = (uint8_t)lo.q, e.wmode[j] = (uint8_t)lo.mode, e.wc0[j] = (uint16_t)lo.c0, e.wnc[j] = (uint8_t)lo.nc;
+    int slot[4] = {0, 0, 0, 0};
+    for (int k = 0; k < kPlanWaves; ++k) {
+        const int lap = k / 4, pos = k % 4;
+        const int simd = lap % 2 ? 3 - pos : pos;
+        const int w = slot[simd]++ * 4 + simd;
+        const Plan& p = plans[(size_t)k];
+        e.wq[w] = (uint8_t)p.q, e.wmode[w] = (uint8_t)p.mode, e.wc0[w] = (uint16_t)p.c0, e.wnc[w] = (uint8_t)p.nc;
     }
     return true;
 }
