@@ -696,6 +696,12 @@ __device__ __forceinline__ void area_fast_batched_row(const uint8_t* b, int s1, 
 #ifndef WICCA_PLAN_WAVE_FENCE
 #define WICCA_PLAN_WAVE_FENCE 1  // no scheduling across a wave's columns (register budget)
 #endif
+#ifndef WICCA_PLAN_WAVE_PRIO
+#define WICCA_PLAN_WAVE_PRIO 0
+#endif
+#ifndef WICCA_PLAN_WAVE_ABL
+#define WICCA_PLAN_WAVE_ABL 0  // timing-only ablations (1: no sums, 2: no row barrier, 4: no output stores)
+#endif
 #ifndef WICCA_PLAN_WAVE_REWEIGH
 #define WICCA_PLAN_WAVE_REWEIGH 1  // batched windows' last-group weights formed per row, not held
 #endif
@@ -737,6 +743,10 @@ __device__ __forceinline__ void plan_wave_rows(const PlanImageDev& im, const Pla
     const bool halfq = im.kx[q & (kPlanShapes - 1)] == 2 && kyq == 2;
 
     auto emit = [&](int r, int dy) {
+        if (WICCA_PLAN_WAVE_ABL & 4) {  // timing-only ablation: the sums without their stores
+            asm volatile("" ::"v"(acc[r][0]), "v"(acc[r][1]), "v"(acc[r][2]));
+            return;
+        }
         if (!((tk[r].meta >> 24) & 1u)) return;
         const int dx = (int)(tk[r].meta & 0xFFFFu);
         __attribute__((address_space(1))) uint8_t* o =
@@ -758,6 +768,7 @@ __device__ __forceinline__ void plan_wave_rows(const PlanImageDev& im, const Pla
     const int nq = (W * 3 + 15) >> 4;
     // the row's sums of this wave (after row y is in b)
     auto row_sums = [&](int y, const uint8_t* b) {
+        if (WICCA_PLAN_WAVE_ABL & 1) return;  // timing-only ablation: staging and barriers alone
         if (nc == 0 || y < bq.ya || y > bq.yb) return;  // wave-uniform
         const PlanVRow vr = vtab[q * kPlanVRows + (y - ya)];
         const bool w1 = vr.dy >= bq.dlo && vr.dy < bq.dhi;
@@ -848,7 +859,7 @@ __device__ __forceinline__ void plan_wave_rows(const PlanImageDev& im, const Pla
     int i0 = 0;  // (y - ya) % 3
     for (int y = ya; y <= yb; ++y) {
         wait_row(y + 1 <= yb);
-        __builtin_amdgcn_s_barrier();
+        if (!(WICCA_PLAN_WAVE_ABL & 2)) __builtin_amdgcn_s_barrier();  // ablation 2: no barrier (races; timing only)
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         const int i2 = i0 == 0 ? 2 : i0 - 1;  // (y + 2 - ya) % 3
@@ -929,6 +940,12 @@ plan_area_wave_kernel(PlanParams P)
     const int mode = __builtin_amdgcn_readfirstlane((int)im.wmode[p]);
     const int c0 = __builtin_amdgcn_readfirstlane((int)im.wc0[p]);
     const int nc = __builtin_amdgcn_readfirstlane((int)im.wnc[p]);
+#if WICCA_PLAN_WAVE_PRIO
+    // the waves with two columns a lane issue first: the SIMD's lighter
+    // waves fill in behind them instead of leaving a heavy wave alone at the
+    // end of every row
+    if (nc > 1) __builtin_amdgcn_s_setprio(2);
+#endif
 #define WICCA_WAVE(M) \
     case M: plan_wave_rows<M>(im, P, band, q, c0, nc, ya, yb, buf0, buf1, buf2, vtab); break;
 #ifdef WICCA_PLAN_WAVE_ONLY  // register-budget experiments: one mode compiled
