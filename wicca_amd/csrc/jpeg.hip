@@ -1522,6 +1522,9 @@ constexpr int kFuseRows = 1;  // block rows per workgroup (the launch grid's y u
 #ifndef WICCA_LUMA_NT
 #define WICCA_LUMA_NT 0  // 1: non-temporal coefficient loads and RGB stores
 #endif
+#ifndef WICCA_LUMA_PAIR16
+#define WICCA_LUMA_PAIR16 0  // 1: neighbouring lanes' RGB bytes leave as 16-B stores, 2 + 1 a lane pair (measured 1.75 vs 1.58 ms, profiles/r06j_*)
+#endif
 #ifndef WICCA_LUMA_WAVES
 #define WICCA_LUMA_WAVES 0  // > 0: amdgpu_waves_per_eu for the fused kernel
 #endif
@@ -1802,6 +1805,28 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
             asm volatile("" ::"v"(w[0]), "v"(w[1]), "v"(w[2]), "v"(w[3]), "v"(w[4]), "v"(w[5]));
             return;
         }
+#if WICCA_LUMA_PAIR16
+        // lanes lb and lb ^ 1 (same row r, lane id ^ 8: DPP row_ror:8) hold the
+        // row's 48 contiguous bytes of two neighbouring blocks: the even lane
+        // stores bytes 0-31 and the odd one 32-47 as 16-B stores (3 per pair
+        // instead of 6 of 8 B; the "store16" probe streams 1.2x the 8-B-piece rate)
+        if ((((uintptr_t)im.dst | (uintptr_t)im.dst_pitch) & 15) == 0) {  // uniform
+            const uint32_t o0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[0], 0x128, 0xF, 0xF, false);
+            const uint32_t o1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[1], 0x128, 0xF, 0xF, false);
+            const int xe = x & ~15;  // the pair's first pixel (x0 is a multiple of 256)
+            if (px_live && xe + 16 <= im.W) {
+                uint8_t* d = im.dst + (int64_t)y * im.dst_pitch + (int64_t)x * 3;
+                if (!(lb & 1)) {
+                    uint4* d4 = reinterpret_cast<uint4*>(d);
+                    d4[0] = uint4{w[0], w[1], w[2], w[3]};
+                    d4[1] = uint4{w[4], w[5], o0, o1};
+                } else {
+                    *reinterpret_cast<uint4*>(d + 8) = uint4{w[2], w[3], w[4], w[5]};
+                }
+                return;
+            }
+        }
+#endif
         if (px_live) {
             uint8_t* d = im.dst + (int64_t)y * im.dst_pitch + (int64_t)x * 3;
             if (x + 8 <= im.W) {

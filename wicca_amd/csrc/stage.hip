@@ -709,7 +709,7 @@ __device__ __forceinline__ void area_fast_batched_row(const uint8_t* b, int s1, 
 #define WICCA_PLAN_WAVE_GLDS 1  // rows staged by LDS-DMA into three buffers (0: through registers, two buffers)
 #endif
 constexpr int kWThreads = 64 * kPlanWaves;
-constexpr int kWChunks = (kStageRowMax / 16 + kWThreads - 1) / kWThreads;  // 16-B chunks of a row per lane (3)
+[[maybe_unused]] constexpr int kWChunks = (kStageRowMax / 16 + kWThreads - 1) / kWThreads;  // 16-B chunks of a row per lane (3)
 
 template <int MODE>
 __device__ __forceinline__ void plan_wave_rows(const PlanImageDev& im, const PlanParams& P, int band, int q, int c0,
