@@ -1081,7 +1081,7 @@ def run_plan(args, torch, rank):
     kernels = kernel_rooflines(kstats, [
         ("haar_multi_ragged_kernel (icons, every depth)", "haar_multi_ragged_kernel", img_b + icon_b,
          "decoded images read once + every depth's icons written"),
-        ("plan_area_kernel (INTER_AREA resizes: icon launch + source launch)", "plan_area_kernel",
+        ("plan_area_wave_kernel (INTER_AREA resizes: icon launch + source launch)", "plan_area",
          img_b + out_src_b + icon_read_b + icon_out_b,
          "decoded images and the downscaled depths' icons read once, every area resize written", 2),
     ])
