@@ -145,7 +145,7 @@ def test_plan_8k_batch_matches_per_call(tmp_path):
 
 def test_plan_8k_matches_oracle_at_demo_shapes(tmp_path):
     """The benchmarked geometry against the oracles, not another product
-    kernel: 7680x4320 sources through plan_area_kernel's source launch at the
+    kernel: 7680x4320 sources through the plan's area kernel (source launch) at the
     demo's shapes (area windows 23-34 pixels wide, the integer 32 x 18 scale of
     240), and the depth 2-4 icons (1920x1080 .. 480x270: area downscales,
     the plan's icon launch) plus the depth 5-6 icons (upscales) -- every
@@ -268,6 +268,8 @@ def test_plan_async_damaged_file_redone(tmp_path):
     lib = _lib.load()
     before = lib.wicca_jpeg_damaged_redone()
     got = wicca_amd.get_img_matrix(paths, [(224, 224), (299, 299)], (2, 3, 4))
+    # counted once: the asynchronous wait redoes the batch, whose decode counts the file
+    assert lib.wicca_jpeg_damaged_redone() - before in (0, 1)
     want = _matrix_sync(paths, [(224, 224), (299, 299)], (2, 3, 4))
     for key in want:
         assert np.array_equal(got[key][0], want[key][0]), key

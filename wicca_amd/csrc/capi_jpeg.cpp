@@ -1474,7 +1474,7 @@ int wicca_image_stage_wait(int64_t ticket)
         HIP_TRY(hipMemcpyAsync(dmg.data(), st->damage, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost,
                                st->stream));
         HIP_TRY(hipStreamSynchronize(st->stream));
-        for (int64_t i = 0; i < n; ++i) g_jpeg_redone += dmg[(size_t)i] != 0;
+        // not counted here: the synchronous redo decodes them again and counts them
         for (int64_t i = 0; i < n && converged; ++i) converged = dmg[(size_t)i] == 0;
     }
     if (!converged) {  // rare: the whole stage again, synchronously, with the host looking at every round
@@ -1555,7 +1555,7 @@ int jpeg_async_result(hipStream_t stream, const int* flags, const int32_t* damag
         std::vector<int32_t> dmg((size_t)n, 0);
         HIP_TRY(hipMemcpyAsync(dmg.data(), damage, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost, stream));
         HIP_TRY(hipStreamSynchronize(stream));
-        for (int64_t i = 0; i < n; ++i) g_jpeg_redone += dmg[(size_t)i] != 0;
+        // not counted here: a flagged batch is redone synchronously (the caller), whose decode counts them
         for (int64_t i = 0; i < n && converged; ++i) converged = dmg[(size_t)i] == 0;
     }
     *ok = converged;

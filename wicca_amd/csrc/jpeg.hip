@@ -1651,8 +1651,15 @@ __device__ __forceinline__ void rgb8_pack(uint2 yv, const int (&g)[8], const int
 // each wave touching ~4 partial lines per instruction) ran at 0.78 TB/s on
 // their own in the probe (tools/luma_probe.hip chroma12, profiles/r05g_*).
 constexpr int kCwinRows = 6, kCwinWords = 10, kCwinPlane = kCwinRows * kCwinWords, kCwin = 2 * kCwinPlane;
+// WICCA_LUMA_CWIN 2: one window per workgroup (256 x 8 pixels: chroma columns
+// x0/2 - 16 .. x0/2 + 143, 10 16-B chunks a row, 6 rows, 2 planes), loaded by
+// 120 lanes with one 16-B load each and shared through LDS after one
+// workgroup barrier
+constexpr int kCwinChunks = 10, kCwinWords2 = 4 * kCwinChunks;
+static_assert(2 * kCwinRows * kCwinWords2 <= 4 * kCwin, "the workgroup window fits the per-wave windows' LDS");
+__device__ __forceinline__ int c_of(int x) { return x >> 1; }
 #ifndef WICCA_LUMA_CWIN
-#define WICCA_LUMA_CWIN 1  // 0: every lane loads its own 12-byte chroma windows (A/B)
+#define WICCA_LUMA_CWIN 2  // 0: every lane loads its own 12-byte chroma windows; 1: one window per wave (1.58 vs 1.56 ms, profiles/r06l_*)
 #endif
 
 template <int FMT, bool SAME>
@@ -1683,6 +1690,7 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
     const uint8_t* pb = P.planes + im.comp_plane0[1];
     const uint8_t* pr = P.planes + im.comp_plane0[2];
     uint32_t cw[2] = {0, 0};  // SAME: this lane's words of the wave's chroma window (loads in flight)
+    uint4 cw4{0, 0, 0, 0};    // SAME, WICCA_LUMA_CWIN 2: this lane's 16 B of the workgroup's window
     if constexpr (FMT == kJpegFmtH2V2) {
         // Cb and Cr planes alike, under 2^31 bytes (the host's conditions)
         const int dw = im.comp_dw[1], dh = im.comp_dh[1];
@@ -1692,6 +1700,22 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
         interior = px_live && c >= 4 && c + 5 <= dw;  // then c + 8 <= sb too (sb: a multiple of 8 >= dw)
         if (P.abl & 2) {
             ab = bb = ar = br = uint3{(uint32_t)x, (uint32_t)y, 7u};
+        } else if (SAME && WICCA_LUMA_CWIN == 2) {
+            // the workgroup's window: chunk q of 120 = plane q / 60, row (q % 60) / 10, 16-B column q % 10
+            // from byte x0 / 2 - 16 (16-B aligned: x0 is a multiple of 256)
+            const int q = (int)threadIdx.x;
+            if (q < 2 * kCwinRows * kCwinChunks) {
+                const int pl = q >= kCwinRows * kCwinChunks ? 1 : 0, rem = q - pl * kCwinRows * kCwinChunks;
+                const int row = rem / kCwinChunks, col = (x0 >> 1) - 16 + 16 * (rem - row * kCwinChunks);
+                const int ry = min(max((y0 >> 1) - 1 + row, 0), dh - 1);
+                const uint8_t* src = (pl ? pr : pb) + __umul24((uint32_t)ry, sb);
+                if (col >= 0 && col + 16 <= (int)sb) {
+                    cw4 = *reinterpret_cast<const uint4*>(src + col);
+                } else if (col >= 0 && col + 8 <= (int)sb) {
+                    const uint2 h = *reinterpret_cast<const uint2*>(src + col);
+                    cw4 = uint4{h.x, h.y, 0u, 0u};
+                }
+            }
         } else if (SAME && WICCA_LUMA_CWIN) {
             // the wave's window: word q of 120 = plane q / 60, row (q % 60) / 10, column word q % 10
             const int lane = (int)(threadIdx.x & 63);
@@ -1732,7 +1756,12 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
         if (blive) *reinterpret_cast<uint2*>(ytile + r * kYPitch + lb * 8) = pack8(px);
         __syncthreads();  // ytile complete
     }
-    if constexpr (SAME && FMT == kJpegFmtH2V2 && WICCA_LUMA_CWIN) {
+    if constexpr (SAME && FMT == kJpegFmtH2V2 && WICCA_LUMA_CWIN == 2) {
+        if (!(P.abl & 2)) {
+            if (threadIdx.x < 2 * kCwinRows * kCwinChunks) reinterpret_cast<uint4*>(cwin)[threadIdx.x] = cw4;
+            __syncthreads();  // the workgroup's window complete
+        }
+    } else if constexpr (SAME && FMT == kJpegFmtH2V2 && WICCA_LUMA_CWIN) {
         if (!(P.abl & 2)) {
             const int lane = (int)(threadIdx.x & 63);
             cwin[lane] = cw[0];
@@ -1754,7 +1783,18 @@ __device__ __forceinline__ void luma_color_tile(const JpegPlan& P, const JpegIma
             int cbm[8], crm[8];
             if constexpr (FMT == kJpegFmtH2V2) {
                 if (interior) {
-                    if (SAME && WICCA_LUMA_CWIN && !(P.abl & 2)) {  // this lane's windows from the wave's LDS copy
+                    if (SAME && WICCA_LUMA_CWIN == 2 && !(P.abl & 2)) {  // from the workgroup's LDS copy
+                        const int iy0 = y0 >> 1, iy = y >> 1;
+                        const int oy = (y & 1) ? min(iy + 1, im.comp_dh[1] - 1) : max(iy - 1, 0);
+                        const int w0 = ((c_of(x) - (x0 >> 1)) >> 2) + 3;  // word of byte c - 4 (window from x0/2 - 16)
+                        const uint32_t* n0 = cwin + (iy - iy0 + 1) * kCwinWords2 + w0;
+                        const uint32_t* f0 = cwin + (oy - iy0 + 1) * kCwinWords2 + w0;
+                        constexpr int kPl = kCwinRows * kCwinWords2;
+                        ab = uint3{n0[0], n0[1], n0[2]};
+                        bb = uint3{f0[0], f0[1], f0[2]};
+                        ar = uint3{n0[kPl], n0[kPl + 1], n0[kPl + 2]};
+                        br = uint3{f0[kPl], f0[kPl + 1], f0[kPl + 2]};
+                    } else if (SAME && WICCA_LUMA_CWIN && !(P.abl & 2)) {  // this lane's windows from the wave's LDS copy
                         const int iy0 = y0 >> 1, iy = y >> 1;
                         const int oy = (y & 1) ? min(iy + 1, im.comp_dh[1] - 1) : max(iy - 1, 0);
                         const int w0 = (lb & 7);  // the window's words c-4 .. c+7 start at word lb mod 8
@@ -1884,8 +1924,8 @@ void jpeg_luma_color_kernel(JpegPlan P)
     __shared__ int32_t tr[kFuseBlocks * kTrBlock];
     __shared__ __attribute__((aligned(16))) uint8_t ytile[8 * kYPitch];
     __shared__ __attribute__((aligned(16))) uint32_t stage[8 * kFuseRowBytes / 4];
-    __shared__ uint32_t cwin_all[4 * kCwin];  // per wave: its h2v2 chroma window (direct-store path)
-    uint32_t* cwin = cwin_all + (threadIdx.x >> 6) * kCwin;
+    __shared__ __attribute__((aligned(16))) uint32_t cwin_all[4 * kCwin];  // per wave: its h2v2 chroma window (direct-store path)
+    uint32_t* cwin = WICCA_LUMA_CWIN == 2 ? cwin_all : cwin_all + (threadIdx.x >> 6) * kCwin;
     int tx = blockIdx.x, ty = blockIdx.y, tz = blockIdx.z;
     if constexpr (XCD) {
         const uint32_t gx = gridDim.x, gxy = gx * gridDim.y, n = gxy * gridDim.z;
