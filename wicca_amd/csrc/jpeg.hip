@@ -98,6 +98,9 @@ struct SyncCk {
 #ifndef WICCA_JPEG_ILV
 #define WICCA_JPEG_ILV 1  // the lane-interleaved stream copy (runtime switch WICCA_JPEG_ILV=0: the plain stream)
 #endif
+#ifndef WICCA_JPEG_CK_PRELOAD
+#define WICCA_JPEG_CK_PRELOAD 1  // 0: the first checkpoint's load left pending into the decode loop
+#endif
 struct BitReader {
     const uint32_t* w;  // the word in nx
     int64_t base;       // absolute bit position of the first word read
@@ -553,6 +556,13 @@ __device__ int decode_run(const DecGeom& im, const HT* tabs, BR& br, int64_t sto
     SyncCk* rec = CK == 3 ? ck_rec : ck;
     uint32_t cur = 0;  // CMP: pos_slot of checkpoint nck
     if (CMP && n_ck > 0) cur = ck[0].pos_slot;
+#if WICCA_JPEG_CK_PRELOAD
+    // waited for here: left pending into the loop, its first use at a block
+    // start compiled to a vmcnt(0) on every iteration, which also waited for
+    // the reader's next word (loaded one refill ahead) at nearly every block
+    // start -- a full memory latency per block for a lone lane of rounds >= 2
+    if (CMP) asm volatile("" ::"v"(cur));
+#endif
     int64_t blk = -1;
     uint32_t staged = 0;
     int zk = 0;  // next zigzag position of a block written position by position (not staged)
@@ -727,9 +737,10 @@ struct ImgTabs {
     DecGeom g;
 };
 
-template <int NS, typename HT>
+template <int NS, typename HT, int NT = kJThreads>
 __device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageDev* imp, ImgTabs<NS, HT>& lds)
 {
+    static_assert(NT >= kJpegMaxSlots, "one lane per MCU slot");
     constexpr int kWords = sizeof(HT) / 4;
     static_assert(sizeof(HT) % 4 == 0, "word copy");
     const int ncomp = imp->ncomp;
@@ -744,7 +755,7 @@ __device__ __forceinline__ void stage_tables(const JpegPlan& P, const JpegImageD
     else tables = P.huff;
     const uint32_t* src = reinterpret_cast<const uint32_t*>(tables + first);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&lds.t[0]);
-    for (int w = threadIdx.x; w < n * kWords; w += kJThreads) dst[w] = src[w];
+    for (int w = threadIdx.x; w < n * kWords; w += NT) dst[w] = src[w];
     if (threadIdx.x < kJpegMaxSlots) {  // one lane per MCU slot
         const int k = threadIdx.x;
         const int c = min(max(imp->slot_comp[k], 0), kJpegDevComp - 1);
@@ -888,6 +899,285 @@ __global__ __launch_bounds__(kJThreads, NS <= 4 ? 8 : 5) void jpeg_sync_kernel(J
     for (int c = 0; c < kJpegDevComp; ++c) r.dc[c] = dc[c];
     if (round > 0 && !same_state(prev[i].end, st)) *changed = 1;
     next[i] = r;
+}
+
+// ---------------------------------------------------------------------------
+// Sync rounds >= WICCA_JPEG_TAIL (default 2): one WAVE per decoding lane.
+// After round 1 only a few lanes still decode (12,716 -> 316 -> 5 of 499,712
+// on 25 x 8K photos), and a lone lane's serial decode in jpeg_sync_kernel ran
+// at ~70 ns per bit whatever the memory path (a plain-stream reader, or the
+// first checkpoint's load waited for before the loop, measured the same:
+// profiles/r06m_*): ~130 dependent vector instructions and two LDS round
+// trips per codeword.  Here the 64 lanes of a wave look up, in parallel, the
+// codeword (and for DC its value) at each of 64 consecutive bit offsets of a
+// window, for the current component's DC and AC tables; the decode state
+// (position, MCU slot, coefficient index, DC sums, checkpoints) lives in
+// scalar registers and steps from codeword to codeword by reading the
+// window's lane at its offset (v_readlane).  Same decode, same results as
+// decode_run<false, 3>: the same tables, the same bits, the same rules for a
+// code no table has (17 bits, symbol 0) and for DC sizes past 11.
+// jpeg_sync_mark_kernel lists the lanes whose start state moved (the rest
+// repeat their result, as in jpeg_sync_kernel); jpeg_sync_tail_kernel's
+// waves take listed lanes in turn.
+// ---------------------------------------------------------------------------
+// The list is cut into kTailRegions regions, one per residue of the mark
+// kernel's workgroup index, each with its own counter on its own cache line:
+// one counter took an atomic from every wave with a decoding lane (~2,000 in
+// round 2) at one address, 80 us of serialised atomics.  Two counter sets
+// alternate between rounds; round r's mark kernel clears round r + 1's.
+constexpr int kTailRegions = 64, kTailCntPitch = 32;  // counters 128 B apart
+__host__ __device__ inline int64_t tail_region_cap(int64_t n_sub)  // list entries per region
+{
+    return ((n_sub + kJThreads - 1) / kJThreads + kTailRegions - 1) / kTailRegions * kJThreads;
+}
+
+__global__ __launch_bounds__(256) void jpeg_sync_mark_kernel(JpegPlan P, const SubResult* prev, SubResult* next,
+                                                             int round, const SubResult* older, int* list,
+                                                             int* cnt, int* cnt_next, int* stats,
+                                                             const int* prev_changed)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < kTailRegions) cnt_next[threadIdx.x * kTailCntPitch] = 0;
+    if (prev_changed && *prev_changed == 0) {  // the last round moved nothing: repeat it
+        if (i < P.n_sub) next[i] = prev[i];
+        return;
+    }
+    bool decode = false;
+    if (i < P.n_sub && P.sub_seg[i] >= 0) {
+        const JpegSegDev& sg = P.segs[P.sub_seg[i]];
+        const int64_t j = i - sg.sub0;
+        if (j > 0) {  // a segment's first lane starts exactly, in every round
+            const DecState st = prev[i - 1].end;
+            DecState before;
+            if (round == 1) {
+                before.p = sg.bit0 + j * P.sub_bits;
+                before.slot = 0;
+                before.k = 0;
+            } else {
+                before = older[i - 1].end;
+            }
+            decode = !same_state(st, before);
+        }
+        if (!decode) next[i] = prev[i];
+    }
+    const uint64_t m = __ballot(decode);
+    if (m == 0) return;
+    const int lane = (int)(threadIdx.x & 63), lead = __ffsll((long long)m) - 1;
+    const int reg = (int)(blockIdx.x % kTailRegions);
+    int base = 0;
+    if (lane == lead) {
+        base = atomicAdd(cnt + reg * kTailCntPitch, __popcll(m));
+        if (stats) atomicAdd(stats, __popcll(m));
+    }
+    base = __shfl(base, lead, 64);
+    if (decode) list[reg * tail_region_cap(P.n_sub) + base + __popcll(m & ((1ull << lane) - 1))] = (int)i;
+}
+
+constexpr int kTailWords = 256;  // stream words staged per wave (8192 bits; restaged as the decode moves on)
+#ifndef WICCA_JPEG_TAIL_GRID
+#define WICCA_JPEG_TAIL_GRID 8192  // waves of jpeg_sync_tail_kernel (a multiple of kTailRegions)
+#endif
+static_assert(WICCA_JPEG_TAIL_GRID % kTailRegions == 0, "whole waves per region");
+// Packed window entries.  DC: (bits consumed) | value << 8, from the lookup
+// result e at bits `look`.
+__device__ __forceinline__ uint32_t tail_pack_dc(uint32_t e, uint32_t look)
+{
+    const int l = (int)(e >> 8), sz = min((int)(e & 255), 16);
+    const int v = sz ? extend((look << l) >> (32 - sz), sz) : 0;
+    return (uint32_t)(l + sz) | ((uint32_t)v << 8);
+}
+// AC runs: bits | coefficient advance << 8 | (ends in an EOB) << 16.  The run
+// at offset L extended by the run where it ends (offset L + bits, within the
+// 64-bit window), unless it ends in an EOB: runs of 1 -> 2 -> 4 codewords.
+__device__ __forceinline__ uint32_t tail_jump(uint32_t j, int lane)
+{
+    const int nx = lane + (int)(j & 255u);
+    const uint32_t n = (uint32_t)__builtin_amdgcn_ds_bpermute(min(nx, 63) << 2, (int)j);
+    if ((j & 0x10000u) || nx >= 64) return j;
+    return ((j & 255u) + (n & 255u)) | ((((j >> 8) & 255u) + ((n >> 8) & 255u)) << 8) | (n & 0x10000u);
+}
+
+template <int NS>
+__global__ __launch_bounds__(64) void jpeg_sync_tail_kernel(JpegPlan P, const SubResult* prev, SubResult* next,
+                                                            int* changed, SyncCk* cks, int* stats, SubResult* r0res,
+                                                            const int* list, const int* cnt)
+{
+    __shared__ ImgTabs<NS> tabs;  // the write pass's 9-bit tables with second-level lookups
+    __shared__ uint32_t words[kTailWords + 2];  // byte-swapped stream words from word `sw` of the lane
+    const int lane = (int)threadIdx.x;
+    const int reg = (int)(blockIdx.x % kTailRegions), per = (int)(gridDim.x / kTailRegions);
+    const int n = cnt[reg * kTailCntPitch];
+    const int* rlist = list + reg * tail_region_cap(P.n_sub);
+    int staged_img = -1;
+    const uint32_t* stream32 = reinterpret_cast<const uint32_t*>(P.stream);
+    const int64_t n_words = (P.stream_bytes + 64) / 4;  // the host pads the streams with 64 zero bytes
+#pragma unroll 1
+    for (int item = (int)(blockIdx.x / kTailRegions); item < n; item += per) {
+        const int64_t i = __builtin_amdgcn_readfirstlane(rlist[item]);
+        const int img = __builtin_amdgcn_readfirstlane(P.sub_img[i / kJThreads]);
+        if (img != staged_img) {
+            __syncthreads();  // the last item's lookups are done with the old tables
+            stage_tables<NS, HuffDev, 64>(P, P.imgs + img, tabs);
+            staged_img = img;
+        }
+        const DecGeom& im = tabs.g;
+        const JpegSegDev& sg = P.segs[P.sub_seg[i]];
+        const int64_t j = i - sg.sub0;
+        const int64_t b0 = sg.bit0 + j * P.sub_bits;
+        const int64_t b1 = min(b0 + P.sub_bits, sg.bit0 + sg.bits);
+        DecState st = prev[i - 1].end;  // listed lanes have j > 0
+        const int o_nck = r0res[i].n_ck;
+        const int set = (o_nck >> 16) & 1, n_ck = o_nck & 0xFFFF;
+        SyncCk* ck = cks + i * kSyncCk;
+        const SyncCk* cur_ck = ck + (set ? P.n_sub * kSyncCk : 0);
+        SyncCk* new_ck = ck + (set ? 0 : P.n_sub * kSyncCk);
+        // this lane's checkpoints' positions, one per lane (checkpoint order)
+        const uint32_t ckv = lane < n_ck ? cur_ck[lane].pos_slot : 0xFFFFFFFFu;
+        const int32_t ck_step = P.sub_bits / kSyncCk;
+        // positions relative to rb (st.p's word), 32-bit
+        const int64_t rb = st.p & ~(int64_t)31;
+        int32_t p = (int32_t)(st.p - rb);
+        const int32_t stop = (int32_t)(b1 - rb);
+        const int32_t ck_off = (int32_t)(rb - b0);  // relative -> checkpoint position
+        int32_t sw = INT32_MIN / 2;  // staged window's first word (relative), none yet
+        int32_t w0 = INT32_MIN / 2;  // lookup window's first bit; its look for this lane
+        uint32_t look = 0;
+        int32_t tag_dc = -1, tag_ac = -1;  // the tables the window's DC / AC entries are for
+        uint32_t res_dc = 0, jump1 = 0, jump2 = 0, jump4 = 0;
+        int32_t slot = st.slot, k = st.k;
+        const uint8_t* slot_tabs = reinterpret_cast<const uint8_t*>(im.tab);
+        uint32_t sti = (uint32_t)__builtin_amdgcn_readfirstlane((int)slot_tabs[slot]);
+        const int32_t bpm = im.bpm;
+        int32_t nstart = 0, dc0 = 0, dc1 = 0, dc2 = 0;
+        int nck = 0, hit = -1, nrec = 0;
+        uint32_t cur = (uint32_t)__builtin_amdgcn_readlane((int)ckv, 0);
+#pragma unroll 1
+        while (p < stop) {
+            if (k == 0) {  // a block starts: record, then look for a checkpoint (decode_run's order)
+                const int32_t here = p + ck_off;
+                if (nrec < kSyncCk && here >= nrec * ck_step) {
+                    if (lane == 0) {
+                        SyncCk e;
+                        e.pos_slot = (uint32_t)here | ((uint32_t)slot << 24);
+                        e.started = nstart;
+                        e.dc[0] = dc0;
+                        e.dc[1] = dc1;
+                        e.dc[2] = dc2;
+                        e.pad_ = 0;
+                        new_ck[nrec] = e;
+                    }
+                    ++nrec;
+                }
+                if (nck < n_ck) {
+                    while ((cur & 0xFFFFFFu) < (uint32_t)here) {
+                        if (++nck == n_ck) break;
+                        cur = (uint32_t)__builtin_amdgcn_readlane((int)ckv, nck);
+                    }
+                    if (nck < n_ck && cur == ((uint32_t)here | ((uint32_t)slot << 24))) {
+                        hit = nck;
+                        break;
+                    }
+                }
+            }
+            if ((uint32_t)(p - w0) >= 64u) {  // a new window from here
+                w0 = p;
+                tag_dc = tag_ac = -1;
+                // staged words must reach the window's last lookup: bits w0 + 63 .. w0 + 95, + 1 word
+                if ((w0 >> 5) < sw || ((w0 + 95) >> 5) + 1 >= sw + kTailWords) {
+                    sw = w0 >> 5;
+                    __syncthreads();  // (one wave) earlier reads of `words` are done
+#pragma unroll
+                    for (int q = 0; q < (kTailWords + 2) / 64 + 1; ++q) {
+                        const int idx = lane + 64 * q;
+                        if (idx < kTailWords + 2) {
+                            const int64_t a = (rb >> 5) + sw + idx;
+                            words[idx] = a < n_words ? __builtin_bswap32(stream32[a]) : 0u;
+                        }
+                    }
+                    __syncthreads();
+                }
+                const int32_t q = w0 + lane - 32 * sw;  // this lane's bit in the staged words
+                const uint64_t two = ((uint64_t)words[q >> 5] << 32) | words[(q >> 5) + 1];
+                look = (uint32_t)((two << (q & 31)) >> 32);
+            }
+            // the table's codeword at every offset of the window at once (DC:
+            // its bits and value; AC: its bits and symbol, and the run of up
+            // to 2 / 4 AC codewords from there: bits, coefficient advance,
+            // ending in an EOB), when not yet looked up for this window
+            const int32_t o = p - w0;
+            if (k == 0) {
+                const int32_t t = (int32_t)(sti & 7u);
+                if (t != tag_dc) {
+                    tag_dc = t;
+                    res_dc = tail_pack_dc(huff_lookup(tabs.t[t], look), look);
+                }
+                const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)res_dc, o);
+                p += (int32_t)(x & 63u);
+                const int v = (int32_t)x >> 8;
+                const int c = (int)(sti >> 6);
+                dc0 += c == 0 ? v : 0;
+                dc1 += c == 1 ? v : 0;
+                dc2 += c == 2 ? v : 0;
+                ++nstart;
+                k = 1;
+            } else {
+                const int32_t t = (int32_t)((sti >> 3) & 7u);
+                if (t != tag_ac) {
+                    tag_ac = t;
+                    const uint32_t e = huff_lookup(tabs.t[t], look);
+                    const uint32_t r = (e >> 4) & 15u, sz = e & 15u;
+                    // one codeword: bits | advance << 8 | EOB << 16
+                    const uint32_t j1 = ((e >> 8) + sz) | ((sz ? r + 1 : (r == 15 ? 16u : 0u)) << 8) |
+                                        ((sz == 0 && r != 15) ? 0x10000u : 0u);
+                    jump1 = j1;
+                    jump2 = tail_jump(j1, lane);
+                    jump4 = tail_jump(jump2, lane);
+                }
+                // the longest run from here that stays inside the block (every
+                // coefficient index before its last codeword < 64) and inside
+                // the lane's range (it ends by `stop`: no codeword of it starts
+                // past the range; a single codeword is always this lane's)
+                uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)jump4, o);
+                if ((int32_t)((x >> 8) & 255u) + k >= 64 || p + (int32_t)(x & 255u) > stop) {
+                    x = (uint32_t)__builtin_amdgcn_readlane((int)jump2, o);
+                    if ((int32_t)((x >> 8) & 255u) + k >= 64 || p + (int32_t)(x & 255u) > stop)
+                        x = (uint32_t)__builtin_amdgcn_readlane((int)jump1, o);
+                }
+                p += (int32_t)(x & 255u);
+                k = (x & 0x10000u) ? 64 : k + (int32_t)((x >> 8) & 255u);
+            }
+            if (k >= 64) {
+                slot = slot + 1 == bpm ? 0 : slot + 1;
+                k = 0;
+                sti = (uint32_t)__builtin_amdgcn_readfirstlane((int)slot_tabs[slot]);
+            }
+        }
+        SubResult r;
+        r.end.p = rb + p;
+        r.end.slot = slot;
+        r.end.k = k;
+        r.started = nstart;
+        r.dc[0] = dc0;
+        r.dc[1] = dc1;
+        r.dc[2] = dc2;
+        r.n_ck = 0;
+        if (hit >= 0) {  // the rest is the recorded decode's from checkpoint `hit`
+            const SyncCk h = cur_ck[hit];
+            const SubResult o = r0res[i];
+            r.end = o.end;
+            r.started += o.started - h.started;
+            for (int c = 0; c < kJpegDevComp; ++c) r.dc[c] += o.dc[c] - h.dc[c];
+            if (stats && lane == 0) atomicAdd(stats + 1, 1);
+        } else if (lane == 0) {  // a full decode from a new start: its checkpoints replace the old ones
+            SubResult f = r;
+            f.n_ck = nrec | ((set ^ 1) << 16);
+            r0res[i] = f;
+        }
+        if (lane == 0) {
+            if (!same_state(prev[i].end, r.end)) *changed = 1;
+            next[i] = r;
+        }
+    }
 }
 
 // Segmented exclusive scan of (blocks started, DC sums) over each segment's
@@ -2147,8 +2437,8 @@ size_t jpeg_scratch_bytes(int64_t n_sub, int64_t n_seg)
 {
     (void)n_seg;
     return (size_t)n_sub * (5 * sizeof(SubResult) + sizeof(SubBase) + 2 * kSyncCk * sizeof(SyncCk)) + 256 +
-           2 * (size_t)((n_sub + kScanChunk - 1) / kScanChunk) * sizeof(SubBase) +
-           kJpegMaxJobs * sizeof(IdctJob);
+           2 * (size_t)((n_sub + kScanChunk - 1) / kScanChunk) * sizeof(SubBase) + kJpegMaxJobs * sizeof(IdctJob) +
+           (size_t)(kTailRegions * tail_region_cap(n_sub) + 2 * kTailRegions * kTailCntPitch) * sizeof(int32_t);
 }
 
 hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* scratch, int64_t n_images,
@@ -2169,6 +2459,10 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
     // the scan's per-chunk carry-outs and carry-ins
     SubBase* chunk_out = reinterpret_cast<SubBase*>(cks + 2 * P.n_sub * kSyncCk);
     SubBase* carry_in = chunk_out + (P.n_sub + kScanChunk - 1) / kScanChunk;
+    // the tail rounds' lists of lanes to decode (kTailRegions regions) and
+    // their two counter sets
+    int* tail_list = reinterpret_cast<int*>(carry_in + (P.n_sub + kScanChunk - 1) / kScanChunk);
+    int* tail_cnt = tail_list + kTailRegions * tail_region_cap(P.n_sub);
     // IDCT jobs: every (image, component); uploaded first, while the stream
     // still waits for the entropy-coded data
     // fused back end (default; WICCA_JPEG_FUSED=0: separate IDCT and colour
@@ -2243,6 +2537,16 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             return e ? atoi(e) : 2;
         }();
         static const bool stats_on = getenv("WICCA_JPEG_TIMING") != nullptr;
+        static const int tail_plain = [] {  // WICCA_JPEG_TAIL_PLAIN=r: rounds >= r on the plain stream (0: none)
+            const char* e = getenv("WICCA_JPEG_TAIL_PLAIN");
+            return e ? atoi(e) : 0;
+        }();
+        // WICCA_JPEG_TAIL=r: rounds >= r by the wave-per-lane tail kernels
+        // (0: every round by jpeg_sync_kernel); checkpoint refresh mode only
+        static const int tail_from = [] {
+            const char* e = getenv("WICCA_JPEG_TAIL");
+            return e ? atoi(e) : 2;
+        }();
         constexpr int kStatRounds = 6;
         constexpr int kFlagRing = 16, kSpec = 4;  // flag slots (a ring), rounds launched per host look
         int* stats = flags + kFlagRing;  // [round][decoding lanes, checkpoint hits]
@@ -2259,8 +2563,15 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
                         int* st) {
             int* changed = flags + round % kFlagRing;
             const int* prev_changed = round >= 2 ? flags + (round - 1) % kFlagRing : nullptr;
+            // rounds >= tail_plain read the plain stream: their few decoding
+            // lanes each walk a whole subsequence alone, and in the
+            // interleaved copy every one of a lone lane's words is its own
+            // 128-B line (a miss per refill); in the plain stream 32
+            // consecutive words share one
+            JpegPlan Q = P;
+            if (tail_plain > 0 && round >= tail_plain) Q.ilv = nullptr;
 #define WICCA_SYNC_LAUNCH(CKV, NSV)                                                                        \
-    hipLaunchKernelGGL((jpeg_sync_kernel<CKV, NSV>), dim3(grid), dim3(kJThreads), 0, s, P, prev, next, round, \
+    hipLaunchKernelGGL((jpeg_sync_kernel<CKV, NSV>), dim3(grid), dim3(kJThreads), 0, s, Q, prev, next, round, \
                        changed, older, cks, st, ckres, prev_changed)
             if (ns4) {
                 if (ck == 1) WICCA_SYNC_LAUNCH(1, 4);
@@ -2276,8 +2587,29 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
 #undef WICCA_SYNC_LAUNCH
             return hipGetLastError();
         };
+        // tail rounds: round r's lists count in counter set r % 2; its mark
+        // kernel clears set (r + 1) % 2 for the next round
+        const bool tail_on = ck_mode == 2 && tail_from > 0;
+        auto tail = [&](const SubResult* prev, SubResult* next, int round, const SubResult* older, int* st) {
+            int* changed = flags + round % kFlagRing;
+            const int* prev_changed = round >= 2 ? flags + (round - 1) % kFlagRing : nullptr;
+            int* cnt = tail_cnt + (round & 1) * kTailRegions * kTailCntPitch;
+            int* cnt_next = tail_cnt + ((round + 1) & 1) * kTailRegions * kTailCntPitch;
+            hipLaunchKernelGGL(jpeg_sync_mark_kernel, dim3(grid), dim3(kJThreads), 0, s, P, prev, next, round, older,
+                               tail_list, cnt, cnt_next, st, prev_changed);
+            const uint32_t tg = WICCA_JPEG_TAIL_GRID;
+            if (ns4)
+                hipLaunchKernelGGL(jpeg_sync_tail_kernel<4>, dim3(tg), dim3(64), 0, s, P, prev, next, changed, cks,
+                                   st, ckres, (const int*)tail_list, (const int*)cnt);
+            else
+                hipLaunchKernelGGL(jpeg_sync_tail_kernel<2 * kJpegDevComp>, dim3(tg), dim3(64), 0, s, P, prev, next,
+                                   changed, cks, st, ckres, (const int*)tail_list, (const int*)cnt);
+            return hipGetLastError();
+        };
         e = sync(ck_mode ? 1 : 0, r0, r0, 0, nullptr, stats_on ? stats : nullptr);
         if (e != hipSuccess) return e;
+        if (tail_on && (e = hipMemsetAsync(tail_cnt, 0, 2 * kTailRegions * kTailCntPitch * sizeof(int), s)) != hipSuccess)
+            return e;
         // the checkpoints' results start as round 0's (checkpoint set 0)
         if (ck_mode && (e = hipMemcpyAsync(ckres, r0, (size_t)P.n_sub * sizeof(SubResult), hipMemcpyDeviceToDevice,
                                            s)) != hipSuccess)
@@ -2304,7 +2636,9 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             for (int r = launched + 1; r <= launched + batch; ++r) {
                 SubResult* nxt = bufs[(r - 1) % 3];
                 int* st_r = stats_on && r < kStatRounds ? stats + 2 * r : nullptr;
-                if ((e = sync(ck_mode == 0 ? 0 : ck_mode == 1 ? 2 : 3, cur, nxt, r, older, st_r)) != hipSuccess) return e;
+                if (tail_on && r >= tail_from) e = tail(cur, nxt, r, older, st_r);
+                else e = sync(ck_mode == 0 ? 0 : ck_mode == 1 ? 2 : 3, cur, nxt, r, older, st_r);
+                if (e != hipSuccess) return e;
                 older = cur;
                 cur = nxt;
             }
