@@ -85,3 +85,29 @@ def test_workspace_controls_without_device():
     assert lib.wicca_set_workspace_cap(-1) == 123 << 20  # query leaves it
     lib.wicca_set_workspace_cap(prev)
     assert lib.wicca_release_workspaces(-1) == 0
+
+
+def test_read_buffer_pool_recycles(tmp_path):
+    """read_files(pooled=True) reads into recycled 1 MiB-granule buffers that
+    release_buffers hands back (the stage plan's asynchronous calls); the
+    bytes read are the file's, and a released buffer is reused."""
+    import numpy as np
+
+    from wicca_amd import jpeg
+    data = [bytes(np.random.default_rng(i).integers(0, 256, n, dtype=np.uint8)) for i, n in
+            enumerate((5, 1 << 20, (1 << 20) + 3))]
+    paths = []
+    for i, d in enumerate(data):
+        p = tmp_path / f"f{i}.bin"
+        p.write_bytes(d)
+        paths.append(str(p))
+    got = jpeg.read_files(paths, pooled=True)
+    assert [bytes(g) for g in got] == data
+    bases = [g.base for g in got]
+    assert [b.nbytes for b in bases] == [1 << 20, 1 << 20, 2 << 20]
+    jpeg.release_buffers(got)
+    again = jpeg.read_files(paths[:1], pooled=True)
+    assert bytes(again[0]) == data[0]
+    assert any(again[0].base is b for b in bases)
+    plain = jpeg.read_files(paths[:1])
+    assert plain[0].base is None or plain[0].base.nbytes == len(data[0])

@@ -975,9 +975,18 @@ __global__ __launch_bounds__(256) void jpeg_sync_mark_kernel(JpegPlan P, const S
 
 constexpr int kTailWords = 256;  // stream words staged per wave (8192 bits; restaged as the decode moves on)
 #ifndef WICCA_JPEG_TAIL_GRID
-#define WICCA_JPEG_TAIL_GRID 8192  // waves of jpeg_sync_tail_kernel (a multiple of kTailRegions)
+#define WICCA_JPEG_TAIL_GRID 1024  // waves of jpeg_sync_tail_kernel (a multiple of kTailRegions; 8192 slowed the plan pipeline, profiles/r06t_*)
 #endif
 static_assert(WICCA_JPEG_TAIL_GRID % kTailRegions == 0, "whole waves per region");
+int tail_grid()  // WICCA_JPEG_TAIL_GRID (runtime): waves of the tail kernel, rounded to whole regions
+{
+    static const int g = [] {
+        const char* e = getenv("WICCA_JPEG_TAIL_GRID");
+        const int v = e ? atoi(e) : WICCA_JPEG_TAIL_GRID;
+        return std::max(kTailRegions, v / kTailRegions * kTailRegions);
+    }();
+    return g;
+}
 // Packed window entries.  DC: (bits consumed) | value << 8, from the lookup
 // result e at bits `look`.
 __device__ __forceinline__ uint32_t tail_pack_dc(uint32_t e, uint32_t look)
@@ -2597,7 +2606,7 @@ hipError_t jpeg_decode_device(const JpegPlan& P, const JpegImageDev* ims, void* 
             int* cnt_next = tail_cnt + ((round + 1) & 1) * kTailRegions * kTailCntPitch;
             hipLaunchKernelGGL(jpeg_sync_mark_kernel, dim3(grid), dim3(kJThreads), 0, s, P, prev, next, round, older,
                                tail_list, cnt, cnt_next, st, prev_changed);
-            const uint32_t tg = WICCA_JPEG_TAIL_GRID;
+            const uint32_t tg = (uint32_t)tail_grid();
             if (ns4)
                 hipLaunchKernelGGL(jpeg_sync_tail_kernel<4>, dim3(tg), dim3(64), 0, s, P, prev, next, changed, cks,
                                    st, ckres, (const int*)tail_list, (const int*)cnt);

@@ -43,11 +43,48 @@ def _read_pool():
     return _READ_POOL
 
 
-def _read_one(p: str) -> np.ndarray:
+class _BufferPool:
+    """Recycled read buffers (1 MiB granules, at most WICCA_READ_POOL_MB idle,
+    default 1024): a fresh np.empty per 10 MB file was mapped and page-faulted
+    by 16 threads at once and unmapped again after the batch (TLB shootdowns
+    across every CPU the process ran on), and the StagePlan's host issue of a
+    batch took 10 to 34 ms from one batch to the next (tools/
+    plan_variance_probe.py).  Only callers that hand the buffers back
+    (:func:`release_buffers`, the stage plan's asynchronous calls) use it."""
+
+    def __init__(self):
+        import os
+        import threading
+        self._lock = threading.Lock()
+        self._idle: dict[int, list] = {}
+        self._bytes = 0
+        self._cap = int(os.environ.get("WICCA_READ_POOL_MB", "1024")) << 20
+
+    def take(self, n: int) -> np.ndarray:
+        size = max(1, (n + (1 << 20) - 1) >> 20) << 20
+        with self._lock:
+            lst = self._idle.get(size)
+            if lst:
+                self._bytes -= size
+                return lst.pop()
+        return np.empty(size, np.uint8)
+
+    def give(self, buf: np.ndarray) -> None:
+        size = buf.nbytes
+        with self._lock:
+            if self._bytes + size <= self._cap:
+                self._idle.setdefault(size, []).append(buf)
+                self._bytes += size
+
+
+_BUFFERS = _BufferPool()
+
+
+def _read_into(p: str, pooled: bool) -> np.ndarray:
     import os
     with open(p, "rb", buffering=0) as f:
         n = os.fstat(f.fileno()).st_size
-        buf = np.empty(n, np.uint8)
+        buf = _BUFFERS.take(n) if pooled else np.empty(n, np.uint8)
         got = 0
         mv = memoryview(buf)
         while got < n:  # a file cut while it is read ends short, as cv2.imread reads it
@@ -56,6 +93,23 @@ def _read_one(p: str) -> np.ndarray:
                 break
             got += k
     return buf[:got]
+
+
+def _read_one(p: str) -> np.ndarray:
+    return _read_into(p, False)
+
+
+def _read_pooled(p: str) -> np.ndarray:
+    return _read_into(p, True)
+
+
+def release_buffers(blobs) -> None:
+    """Hand the buffers of :func:`read_files` (pooled=True) back for reuse;
+    the caller must be done with them (and with every view of them)."""
+    for b in blobs:
+        base = b.base if isinstance(b, np.ndarray) and b.base is not None else None
+        if isinstance(base, np.ndarray) and base.ndim == 1 and base.nbytes % (1 << 20) == 0:
+            _BUFFERS.give(base)
 
 
 def _map_one(p: str) -> np.ndarray:
@@ -68,7 +122,7 @@ def _map_one(p: str) -> np.ndarray:
     return np.frombuffer(mm, np.uint8)
 
 
-def read_files(paths: Sequence[str]) -> list:
+def read_files(paths: Sequence[str], pooled: bool = False) -> list:
     """Each file's bytes as a uint8 array, read into memory of its own by a
     pool of threads (serial f.read() of 25 x 10 MB files took longer than the
     whole GPU stage of the batch).  WICCA_READ_MMAP=1 maps the files instead
@@ -81,7 +135,7 @@ def read_files(paths: Sequence[str]) -> list:
             raise ValueError("File path cannot be empty")
     if not paths:
         raise ValueError("need at least one array to stack")
-    one = _map_one if os.environ.get("WICCA_READ_MMAP") == "1" else _read_one
+    one = _map_one if os.environ.get("WICCA_READ_MMAP") == "1" else _read_pooled if pooled else _read_one
     if len(paths) == 1:
         return [one(paths[0])]
     return list(_read_pool().map(one, paths))

@@ -63,12 +63,12 @@ def _norm_depths(depths) -> tuple[int, ...]:
     return (_depth_index(depths),)
 
 
-def _read(paths: Sequence) -> list:
+def _read(paths: Sequence, pooled: bool = False) -> list:
     from .jpeg import read_files
-    return read_files(paths)
+    return read_files(paths, pooled=pooled)
 
 
-def _matrix_args(file_paths, shapes, depths, interpolation, border_type, border_constant, device):
+def _matrix_args(file_paths, shapes, depths, interpolation, border_type, border_constant, device, pooled=False):
     from .coder import _border_value
     shp = []
     for s in shapes:
@@ -80,7 +80,7 @@ def _matrix_args(file_paths, shapes, depths, interpolation, border_type, border_
     dep = _norm_depths(depths)
     if not dep:
         raise ValueError("need at least one depth")
-    blobs = _read(file_paths)
+    blobs = _read(file_paths, pooled)
     n = len(blobs)
     keep = [np.frombuffer(b, np.uint8) for b in blobs]
     # pinned host outputs: the device-to-host copies run by DMA, not as blit
@@ -115,6 +115,11 @@ class MatrixCall:
             ticket, self._ticket = self._ticket, None
             try:
                 _lib.check(_lib.load().wicca_image_stage_plan_wait(ticket))
+                # the native side is done with the file bytes: their read
+                # buffers go back to the pool (only after a clean wait)
+                from .jpeg import release_buffers
+                blobs, self._keep = self._keep[0], None
+                release_buffers(blobs)
             finally:
                 self._keep = None
         return self._out
@@ -136,7 +141,7 @@ def get_img_matrix_async(file_paths: Sequence, shapes: Iterable, depths, interpo
     asynchronous call's, so a loop that issues batch k+1 before waiting for
     batch k overlaps k+1's host work and k's output copies with the kernels."""
     blobs, keep, args, out = _matrix_args(file_paths, shapes, depths, interpolation, border_type,
-                                          border_constant, device)
+                                          border_constant, device, pooled=True)
     if args[2] == 0:
         return MatrixCall(None, None, out)
     ticket = ctypes.c_int64(0)
