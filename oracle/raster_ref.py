@@ -431,20 +431,23 @@ def _tiff_rows(samples: np.ndarray, bits: int) -> np.ndarray:
 
 def encode_tiff(samples: np.ndarray, photometric: int, bits: int = 8, compression: int = 1, predictor: int = 1,
                 tile=None, rows_per_strip: int = 8, big_endian: bool = False, colormap=None,
-                extra_samples=None) -> bytes:
+                extra_samples=None, planar: int = 1) -> bytes:
     """A TIFF file of (H, W[, spp]) samples: compression 1 none / 8 Deflate /
     32773 PackBits, predictor 2 (8-bit), strips of rows_per_strip rows or
-    tiles (tw, th), either byte order; colormap (2**bits, 3) 16-bit values."""
+    tiles (tw, th), either byte order; colormap (2**bits, 3) 16-bit values;
+    planar 2: each sample's plane stored on its own (PlanarConfiguration 2,
+    plane 0's strips / tiles first)."""
     samples = np.asarray(samples)
     if samples.ndim == 2:
         samples = samples[..., None]
     h, w, spp = samples.shape
     e = ">" if big_endian else "<"
+    planes = [samples[..., c:c + 1] for c in range(spp)] if planar == 2 else [samples]
 
     def code(seg_samples):
         rows = _tiff_rows(seg_samples, bits).astype(np.uint8)
         if predictor == 2:
-            r = rows.astype(np.int64).reshape(rows.shape[0], -1, spp)
+            r = rows.astype(np.int64).reshape(rows.shape[0], -1, seg_samples.shape[2])
             d = r.copy()
             d[:, 1:] = r[:, 1:] - r[:, :-1]
             rows = (d & 255).astype(np.uint8).reshape(rows.shape[0], -1)
@@ -456,17 +459,18 @@ def encode_tiff(samples: np.ndarray, photometric: int, bits: int = 8, compressio
         return raw
 
     segs = []
-    if tile:
-        tw, th = tile
-        for ty in range(0, h, th):
-            for tx in range(0, w, tw):
-                t = np.zeros((th, tw, spp), samples.dtype)
-                blk = samples[ty:ty + th, tx:tx + tw]
-                t[:blk.shape[0], :blk.shape[1]] = blk
-                segs.append(code(t))
-    else:
-        for y in range(0, h, rows_per_strip):
-            segs.append(code(samples[y:y + rows_per_strip]))
+    for pl in planes:
+        if tile:
+            tw, th = tile
+            for ty in range(0, h, th):
+                for tx in range(0, w, tw):
+                    t = np.zeros((th, tw, pl.shape[2]), samples.dtype)
+                    blk = pl[ty:ty + th, tx:tx + tw]
+                    t[:blk.shape[0], :blk.shape[1]] = blk
+                    segs.append(code(t))
+        else:
+            for y in range(0, h, rows_per_strip):
+                segs.append(code(pl[y:y + rows_per_strip]))
     body = bytearray(b"MM\x00*" if big_endian else b"II*\x00") + b"\0\0\0\0"
     offs = []
     for sgm in segs:
@@ -496,7 +500,7 @@ def encode_tiff(samples: np.ndarray, photometric: int, bits: int = 8, compressio
     if not tile:
         entries.append((278, 4, [rows_per_strip]))
         entries.append((279, 4, [len(x) for x in segs]))
-    entries.append((284, 3, [1]))
+    entries.append((284, 3, [planar]))
     if predictor != 1:
         entries.append((317, 3, [predictor]))
     if colormap is not None:

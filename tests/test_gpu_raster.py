@@ -430,23 +430,71 @@ def test_rle_bmp_corrupt_rules():
     assert np.array_equal(WJ.decode(deep), pal[want])
 
 
+def _plain_pnm(img: np.ndarray, rng) -> bytes:
+    """A plain (ASCII) P2 / P3 file of `img`: tokens split over lines of
+    random length, runs of whitespace, comments between samples."""
+    gray = img.ndim == 2
+    h, w = img.shape[:2]
+    out = [b"P2" if gray else b"P3", b"# plain\n", b"%d %d\n255\n" % (w, h)]
+    line = []
+    for v in img.reshape(-1).tolist():
+        line.append(b"%d" % v)
+        if rng.random() < 0.05:
+            out.append(b" ".join(line) + (b"  # note 12 34\n" if rng.random() < 0.3 else b"\n\t"))
+            line = []
+    out.append(b" ".join(line) + b"\n")
+    return b"".join(out)
+
+
 def test_pnm_vs_pillow(tmp_path, capsys):
-    """Binary PGM / PPM at maxval 255 (load_image, file stage); other PNM
-    kinds fail their slot as unsupported."""
+    """PGM / PPM at maxval 255, binary (P5 / P6) and plain (P2 / P3: tokens,
+    whitespace and comments), and P4 bitmaps (load_image, file stage), pinned
+    to Pillow; plain P1 bitmaps and other maxvals fail their slot as
+    unsupported."""
+    from PIL import Image
     rng = np.random.default_rng(8)
     gray = rng.integers(0, 256, (61, 93), dtype=np.uint8)
     rgb = rng.integers(0, 256, (480, 640, 3), dtype=np.uint8)
-    blobs = [rr.encode_pnm(gray), rr.encode_pnm(rgb, comment=False)]
+    bits = rng.integers(0, 2, (37, 75), dtype=np.uint8)
+    buf = io.BytesIO()
+    Image.fromarray((bits * 255).astype(np.uint8)).convert("1").save(buf, format="PPM")
+    pbm = buf.getvalue()
+    assert pbm[:2] == b"P4"
+    blobs = [rr.encode_pnm(gray), rr.encode_pnm(rgb, comment=False), _plain_pnm(gray, rng),
+             _plain_pnm(rgb[:97, :133], rng), pbm]
     got = WJ.decode_batch(blobs)
     assert np.array_equal(got[0], np.repeat(gray[..., None], 3, axis=2))
     assert np.array_equal(got[1], rgb)
+    assert np.array_equal(got[2], got[0])
+    assert np.array_equal(got[3], rgb[:97, :133])
+    assert np.array_equal(got[4], np.repeat((bits * 255)[..., None], 3, axis=2))
     for i, data in enumerate(blobs):
-        assert np.array_equal(got[i], rr.pillow_rgb(data))
-    ascii_pgm = b"P2\n2 2\n255\n0 1 2 3\n"
+        assert np.array_equal(got[i], rr.pillow_rgb(data)), i
+    plain_pbm = b"P1\n2 2\n0 1 1 0\n"
     wide = b"P5\n2 2\n65535\n" + bytes(8)
-    assert WJ.decode_batch([ascii_pgm, wide, blobs[0]], errors="none")[:2] == [None, None]
+    short = b"P2\n2 2\n255\n0 1 2\n"
+    bad_token = b"P3\n1 1\n255\n1 x 3\n"
+    assert WJ.decode_batch([plain_pbm, wide, short, bad_token, blobs[0]], errors="none")[:4] == [None] * 4
     p = tmp_path / "x.ppm"
     p.write_bytes(blobs[1])
     imgs, icons = wicca_amd.get_img_batch([str(p)], (224, 224), 3)
     assert np.array_equal(imgs[0], R.resize(rgb, (224, 224), R.INTER_AREA))
     assert np.array_equal(icons[0], R.resize(c_oracle.ll_int_block(rgb, 3)[0], (224, 224), R.INTER_AREA))
+
+
+@pytest.mark.parametrize("spp,photometric,extra", [(3, 2, None), (4, 2, 2), (2, 1, 2)])
+@pytest.mark.parametrize("layout", ["strips", "tiles", "deflate_pred"])
+def test_tiff_separate_planes_vs_pillow(spp, photometric, extra, layout):
+    """PlanarConfiguration 2 (8-bit RGB, RGBA unassociated, gray + alpha):
+    each plane's strips / tiles, interleaved on the host; pinned to Pillow
+    (libtiff 4.7.1) and equal to the same image stored chunky."""
+    rng = np.random.default_rng(spp * 7 + len(layout))
+    img = rng.integers(0, 256, (45, 70, spp), dtype=np.uint8)
+    kw = dict(tile=(32, 16)) if layout == "tiles" else dict(rows_per_strip=7)
+    if layout == "deflate_pred":
+        kw.update(compression=8, predictor=2)
+    sep = rr.encode_tiff(img, photometric, extra_samples=extra, planar=2, **kw)
+    chunky = rr.encode_tiff(img, photometric, extra_samples=extra, **kw)
+    got = WJ.decode_batch([sep, chunky])
+    assert np.array_equal(got[0], got[1])
+    assert np.array_equal(got[0], rr.pillow_rgb(sep))

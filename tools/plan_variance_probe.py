@@ -5,7 +5,7 @@ when its issue started / ended (host read, parse, de-stuffing, uploads queued)
 and when its wait returned (device work and output copies done), relative to
 the loop start.  A slow loop then shows whether one batch stalled or every
 batch slowed, and in which phase.
-Usage: python tools/plan_variance_probe.py [loops] [batches]"""
+Usage: python tools/plan_variance_probe.py [loops] [batches] [aheads, e.g. 2,3]"""
 import argparse
 import os
 import shutil
@@ -52,6 +52,7 @@ def main():
     from wicca_amd import plan as P
     loops = int(sys.argv[1]) if len(sys.argv) > 1 else 6
     nb = int(sys.argv[2]) if len(sys.argv) > 2 else 12
+    aheads = [int(a) for a in (sys.argv[3] if len(sys.argv) > 3 else "2").split(",")]
     args = argparse.Namespace(quality=90)
     B, H, W = 25, 4320, 7680
     depths = [2, 3, 4, 5, 6]
@@ -75,6 +76,16 @@ def main():
         call.wait = wait
         return call
     P.get_img_matrix_async = timed_async
+    reads = []
+    orig_read = P._read
+
+    def timed_read(*a, **kw):
+        t1 = time.perf_counter()
+        r = orig_read(*a, **kw)
+        with lock:
+            reads.append(time.perf_counter() - t1)
+        return r
+    P._read = timed_read
     try:
         batches = []
         for b in range(nb):
@@ -86,11 +97,13 @@ def main():
                 paths.append(p)
             batches.append(paths)
         print(f"cgroup cpu quota: {cpu_quota()}; affinity {len(os.sched_getaffinity(0))} CPUs", flush=True)
-        for rep in range(loops + 1):
+        for rep in range(loops * len(aheads) + 1):
+            ahead = aheads[(rep - 1) % len(aheads)] if rep else aheads[0]
             log.clear()
+            reads.clear()
             st0 = cgroup_stat()
             ru0 = resource.getrusage(resource.RUSAGE_SELF)
-            sp = P.StagePlan(bench.DEMO_CLASSIFIERS, depths, batches=batches, ahead=2, copy=False)
+            sp = P.StagePlan(bench.DEMO_CLASSIFIERS, depths, batches=batches, ahead=ahead, copy=False)
             t0 = time.perf_counter()
             for d in depths:
                 def classify(shape):
@@ -107,13 +120,15 @@ def main():
             ev = sorted((a - t0, b - t0, c - t0) for a, b, c, _ in log)
             done = sorted(c for _, _, c in ev)
             steady = (done[-1] - done[0]) / (len(done) - 1) if len(done) > 1 else 0.0
-            tag = "warm" if rep == 0 else f"loop {rep}"
+            tag = "warm" if rep == 0 else f"loop {rep} ahead {ahead}"
             print(f"{tag}: {1e3 * wall / nb:.2f} ms per batch, steady {1e3 * steady:.2f}; CPU {cpu_s / wall:.1f} cores; "
                   f"{thr}; "
                   f"issue ms {' '.join(f'{1e3 * (b - a):.1f}' for a, b, _ in ev)}; "
+                  f"of which file reads ms {' '.join(f'{1e3 * r:.1f}' for r in reads)}; "
                   f"done gaps ms {' '.join(f'{1e3 * (y - x):.1f}' for x, y in zip(done, done[1:]))}", flush=True)
     finally:
         P.get_img_matrix_async = orig_async
+        P._read = orig_read
         shutil.rmtree(tmp, ignore_errors=True)
 
 

@@ -65,7 +65,7 @@ int raster_decode_to_device(Workspace* ws, const uint8_t* const* data, const int
             for (int64_t i; (i = next.fetch_add(1)) < n;) {
                 const size_t a = (size_t)off[(size_t)i];
                 if ((info[(size_t)i].kind == wicca::RK_BMP && !info[(size_t)i].rle) ||
-                    info[(size_t)i].kind == wicca::RK_PNM) {
+                    (info[(size_t)i].kind == wicca::RK_PNM && !info[(size_t)i].pnm_plain)) {
                     // the pixel array as stored: straight from the caller's bytes (a pageable copy
                     // runs at the DMA rate and skips the host copy into pinned staging)
                     if (hipMemcpyAsync(raw + a, data[i] + info[(size_t)i].data_off, (size_t)lay[(size_t)i].bytes,

@@ -20,7 +20,8 @@
 //       palette entry 0; a run past the row's end fails the file, a delta
 //       past the bottom ends the bitmap -- corrupt-data rules restated from
 //       OpenCV's BmpDecoder, parity unpinned: Pillow clips such runs).
-//   PNM (OpenCV's PxMDecoder): binary P5 gray / P6 RGB at maxval 255.
+//   PNM (OpenCV's PxMDecoder): P5 gray / P6 RGB (binary) and P2 / P3 (plain
+//       ASCII) at maxval 255; P4 bitmaps (1 = black).
 //
 // Why the row reconstruction is on the host: deflate is a serial bit stream
 // (no resynchronisation points), so inflate runs on host threads, one file
@@ -82,10 +83,13 @@ struct RasterInfo {
     int64_t stride = 0;
     bool bottom_up = false;
     int rle = 0;
+    // PNM: plain (ASCII) P2 / P3 samples, tokenised on the host into 8-bit rows
+    bool pnm_plain = false;
     // TIFF (first IFD): strips or tiles (offset, byte count), layout, coding
     int flags = 0;                 // kRasterInvert / kRasterPremul
     int spp = 1;                   // samples per pixel
     int compression = 1;           // 1 none, 5 LZW, 8 / 32946 Deflate, 32773 PackBits
+    bool separate = false;         // PlanarConfiguration 2: one plane per sample (8-bit), strips / tiles plane by plane
     int predictor = 1;             // 1 none, 2 horizontal differencing
     int64_t rows_per_strip = 0;
     int64_t tile_w = 0, tile_h = 0;  // 0: strips

@@ -25,9 +25,10 @@
 // (v * a + 127) / 255, then dropped), palette (1/2/4/8-bit indices, a 16-bit
 // ColorMap taken >> 8 unless every entry is < 256); strips or tiles,
 // chunky samples, compression none / LZW (with the early code-width change)
-// / Deflate / PackBits, horizontal predictor.  16-bit samples, planar
-// configuration 2, JPEG / CCITT compression, CMYK / YCbCr / Lab and
-// orientations other than top-left are reported unsupported.
+// / Deflate / PackBits, horizontal predictor; 8-bit samples in separate
+// planes (PlanarConfiguration 2: each plane's strips / tiles, then the planes
+// interleaved on the host).  16-bit samples, JPEG / CCITT compression, CMYK /
+// YCbCr / Lab and orientations other than top-left are reported unsupported.
 // GIF (87a / 89a; cv2.imread reads the first frame): the first image's LZW
 // codes (LSB-first, code width growing when the next code reaches 2^width,
 // 12-bit table without a forced clear) decoded into palette colours (local
@@ -296,28 +297,46 @@ int unpack_bmp_rle(const uint8_t* d, size_t n, const RasterInfo& f, uint8_t* out
 }
 
 // ----------------------------------------------------------------------------- PNM
-// Binary PGM (P5) / PPM (P6) at maxval 255: the header's whitespace and '#'
-// comments, then the raster (one whitespace byte after maxval).
+// Netpbm headers: magic, then width, height (and maxval, except for P4), each
+// after whitespace and '#' comments.  Decoded: P5 gray / P6 RGB (binary,
+// one whitespace byte before the raster) and P2 / P3 (plain: the samples as
+// decimal tokens, whitespace and comments between them) at maxval 255, and
+// P4 bitmaps (rows of MSB-first bits, 1 = black) as a two-entry palette.
+// Pinned to Pillow (tests/test_gpu_raster.py::test_pnm_vs_pillow), which
+// agrees with OpenCV's PxMDecoder there.  Not decoded (the slot fails):
+// plain P1 bitmaps (Pillow reads "0101" as four bits; whether OpenCV's
+// number reader does is not pinned here) and maxval other than 255 (Pillow
+// rounds value * 255 / maxval, OpenCV's PxMDecoder truncates; 16-bit samples
+// likewise differ).
+namespace {
+size_t pnm_skip_space(const uint8_t* d, size_t n, size_t p)
+{
+    for (;;) {
+        if (p >= n) return p;
+        if (d[p] == '#') {
+            while (p < n && d[p] != '\n' && d[p] != '\r') ++p;
+        } else if (d[p] == ' ' || d[p] == '\t' || d[p] == '\n' || d[p] == '\r' || d[p] == '\v' || d[p] == '\f') {
+            ++p;
+        } else {
+            return p;
+        }
+    }
+}
+}  // namespace
+
 int parse_pnm(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
 {
     info->kind = RK_PNM;
     if (n < 3 || d[0] != 'P') return bad(err, -1, "PNM: bad magic");
     const int type = d[1] - '0';
     if (type < 1 || type > 6) return bad(err, -1, "PNM: bad magic");
-    if (type != 5 && type != 6) return bad(err, -2, "PNM: only binary P5 / P6 are decoded");
+    if (type == 1) return bad(err, -2, "PNM: plain P1 bitmaps are not decoded");
+    const bool bitmap = type == 4, plain = type == 2 || type == 3;
     size_t p = 2;
-    int64_t v[3];
-    for (int k = 0; k < 3; ++k) {
-        for (;;) {  // whitespace and comments
-            if (p >= n) return bad(err, -1, "PNM: truncated header");
-            if (d[p] == '#') {
-                while (p < n && d[p] != '\n' && d[p] != '\r') ++p;
-            } else if (d[p] == ' ' || d[p] == '\t' || d[p] == '\n' || d[p] == '\r' || d[p] == '\v' || d[p] == '\f') {
-                ++p;
-            } else {
-                break;
-            }
-        }
+    int64_t v[3] = {0, 0, 1};
+    for (int k = 0; k < (bitmap ? 2 : 3); ++k) {
+        p = pnm_skip_space(d, n, p);
+        if (p >= n) return bad(err, -1, "PNM: truncated header");
         if (d[p] < '0' || d[p] > '9') return bad(err, -1, "PNM: bad header number");
         int64_t x = 0;
         while (p < n && d[p] >= '0' && d[p] <= '9') {
@@ -327,18 +346,58 @@ int parse_pnm(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
         }
         v[k] = x;
     }
-    if (p >= n) return bad(err, -1, "PNM: truncated header");
-    ++p;  // the single whitespace byte before the raster
     if (v[0] <= 0 || v[1] <= 0) return bad(err, -1, "PNM: invalid image size");
-    if (v[2] != 255) return bad(err, -2, "PNM: only maxval 255 is decoded");
+    if (!bitmap && v[2] != 255) return bad(err, -2, "PNM: only maxval 255 is decoded");
     if (v[0] > kMaxDim || v[1] > kMaxDim) return bad(err, -2, "PNM: image larger than 65535 pixels");
     info->W = v[0];
     info->H = v[1];
-    info->bits = 8;
-    info->fmt = type == 5 ? RF_GRAY : RF_RGB;
-    info->stride = info->W * (type == 5 ? 1 : 3);
+    const bool gray = type == 2 || type == 5;
+    if (plain) {  // the tokens start after maxval (unpack_pnm_plain skips the whitespace)
+        info->pnm_plain = true;
+        info->bits = 8;
+        info->fmt = gray ? RF_GRAY : RF_RGB;
+        info->stride = info->W * (gray ? 1 : 3);
+        info->data_off = p;
+        if (p >= n) return bad(err, -1, "PNM: truncated raster");
+        return 0;
+    }
+    if (p >= n) return bad(err, -1, "PNM: truncated header");
+    ++p;  // the single whitespace byte before the raster
+    if (bitmap) {
+        info->bits = 1;
+        info->fmt = RF_PAL;
+        info->npal = 2;
+        memset(info->pal, 0, sizeof(info->pal));
+        memset(info->pal[0], 255, 3);  // 0 = white, 1 = black
+        info->stride = (info->W + 7) / 8;
+    } else {
+        info->bits = 8;
+        info->fmt = gray ? RF_GRAY : RF_RGB;
+        info->stride = info->W * (gray ? 1 : 3);
+    }
     info->data_off = p;
     if ((uint64_t)(n - p) < (uint64_t)info->stride * (uint64_t)info->H) return bad(err, -1, "PNM: truncated raster");
+    return 0;
+}
+
+// Plain P2 / P3 samples into 8-bit rows.  A token past maxval is clamped to
+// it, as OpenCV's PxMDecoder does (Pillow raises instead: unpinned); a
+// non-digit where a token starts, or data that ends early, fails the file.
+int unpack_pnm_plain(const uint8_t* d, size_t n, const RasterInfo& f, uint8_t* out, std::string* err)
+{
+    const int64_t total = f.stride * f.H;
+    size_t p = f.data_off;
+    for (int64_t k = 0; k < total; ++k) {
+        p = pnm_skip_space(d, n, p);
+        if (p >= n) return bad(err, -1, "PNM: truncated raster");
+        if (d[p] < '0' || d[p] > '9') return bad(err, -1, "PNM: bad sample token");
+        int64_t x = 0;
+        while (p < n && d[p] >= '0' && d[p] <= '9') {
+            x = std::min<int64_t>(x * 10 + (d[p] - '0'), 1 << 20);
+            ++p;
+        }
+        out[k] = (uint8_t)std::min<int64_t>(x, 255);
+    }
     return 0;
 }
 
@@ -434,7 +493,9 @@ int parse_tiff(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
     }
     if (!seen[262]) photo = spp >= 3 ? 2 : 1;  // libtiff's guess when the tag is missing
     else if (!get(262, 1, &photo)) return bad(err, -1, "TIFF: malformed PhotometricInterpretation");
-    if (planar != 1) return bad(err, -2, "TIFF: planar configuration 2 is not decoded");
+    if (planar != 1 && planar != 2) return bad(err, -1, "TIFF: invalid PlanarConfiguration");
+    const bool separate = planar == 2 && spp > 1;
+    if (separate && bits != 8) return bad(err, -2, "TIFF: separate planes are decoded for 8-bit samples only");
     if (orient != 1) return bad(err, -2, "TIFF: orientations other than top-left are not decoded");
     if (!(comp == 1 || comp == 5 || comp == 8 || comp == 32946 || comp == 32773))
         return bad(err, -2, "TIFF: compression scheme not decoded (none, LZW, Deflate, PackBits are)");
@@ -500,6 +561,8 @@ int parse_tiff(const uint8_t* d, size_t n, RasterInfo* info, std::string* err)
         info->rows_per_strip = (int64_t)std::min<uint64_t>(rps, H);
         nseg = (H + info->rows_per_strip - 1) / info->rows_per_strip;
     }
+    info->separate = separate;
+    if (separate) nseg *= spp;  // plane 0's strips / tiles, then plane 1's, ...
     if (tag[off_tag].count < nseg || tag[cnt_tag].count < nseg) return bad(err, -1, "TIFF: too few strips / tiles");
     info->segs.resize((size_t)nseg);
     for (uint64_t k = 0; k < nseg; ++k) {
@@ -642,9 +705,52 @@ void tiff_undiff(uint8_t* p, int64_t rows, int64_t pitch, int64_t w, int spp)
     }
 }
 
+// One plane of a PlanarConfiguration 2 file (8-bit samples): strips or tiles
+// [k0, k0 + per_plane) into `plane` (W x H bytes), then sample s of every
+// pixel of `out` (chunky rows of `pitch` bytes, spp samples a pixel).
+int unpack_tiff_plane(const uint8_t* data, const RasterInfo& f, size_t k0, uint8_t* plane, std::string* err)
+{
+    const size_t per_plane = f.segs.size() / (size_t)f.spp;
+    if (!f.tile_w) {
+        for (size_t k = 0; k < per_plane; ++k) {
+            const int64_t y0 = (int64_t)k * f.rows_per_strip, rows = std::min(f.rows_per_strip, f.H - y0);
+            uint8_t* dst = plane + y0 * f.W;
+            if (!tiff_segment(f, data + f.segs[k0 + k].first, (size_t)f.segs[k0 + k].second, dst, (size_t)(rows * f.W)))
+                return bad(err, -1, "TIFF: corrupt or short strip data");
+            if (f.predictor == 2) tiff_undiff(dst, rows, f.W, f.W, 1);
+        }
+        return 0;
+    }
+    std::vector<uint8_t> tile((size_t)(f.tile_w * f.tile_h));
+    const int64_t across = (f.W + f.tile_w - 1) / f.tile_w;
+    for (size_t k = 0; k < per_plane; ++k) {
+        const int64_t tx = (int64_t)k % across, ty = (int64_t)k / across;
+        if (!tiff_segment(f, data + f.segs[k0 + k].first, (size_t)f.segs[k0 + k].second, tile.data(), tile.size()))
+            return bad(err, -1, "TIFF: corrupt or short tile data");
+        if (f.predictor == 2) tiff_undiff(tile.data(), f.tile_h, f.tile_w, f.tile_w, 1);
+        const int64_t w = std::min(f.tile_w, f.W - tx * f.tile_w);
+        for (int64_t r = 0; r < f.tile_h && ty * f.tile_h + r < f.H; ++r)
+            memcpy(plane + (ty * f.tile_h + r) * f.W + tx * f.tile_w, tile.data() + r * f.tile_w, (size_t)w);
+    }
+    return 0;
+}
+
 int unpack_tiff(const uint8_t* data, const RasterInfo& f, const RasterLayout& lay, uint8_t* out, std::string* err)
 {
     const int64_t pitch = lay.pass_pitch[0];
+    if (f.separate) {  // planes in turn, each interleaved into the chunky rows
+        std::vector<uint8_t> plane((size_t)(f.W * f.H));
+        const size_t per_plane = f.segs.size() / (size_t)f.spp;
+        for (int s = 0; s < f.spp; ++s) {
+            if (int rc = unpack_tiff_plane(data, f, (size_t)s * per_plane, plane.data(), err)) return rc;
+            for (int64_t y = 0; y < f.H; ++y) {
+                const uint8_t* src = plane.data() + y * f.W;
+                uint8_t* dst = out + y * pitch + s;
+                for (int64_t x = 0; x < f.W; ++x) dst[x * f.spp] = src[x];
+            }
+        }
+        return 0;
+    }
     if (!f.tile_w) {
         for (size_t k = 0; k < f.segs.size(); ++k) {
             const int64_t y0 = (int64_t)k * f.rows_per_strip, rows = std::min(f.rows_per_strip, f.H - y0);
@@ -1009,6 +1115,7 @@ int raster_unpack(const uint8_t* data, size_t size, const RasterInfo& info, cons
                   std::string* err)
 {
     if (info.kind == RK_BMP && info.rle) return unpack_bmp_rle(data, size, info, out, err);
+    if (info.kind == RK_PNM && info.pnm_plain) return unpack_pnm_plain(data, size, info, out, err);
     if (info.kind == RK_BMP || info.kind == RK_PNM) {
         memcpy(out, data + info.data_off, (size_t)lay.bytes);
         return 0;

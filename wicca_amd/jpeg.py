@@ -19,7 +19,7 @@ points sniff each file (``wicca_image_*``), so a batch may mix formats.
 ``validate_image`` then raises that message, validation.py:94-95) and
 returns ``None``; ``WICCA_LOAD_DETAIL=1`` prints the decoder's own reason
 instead.  Files no decoder here handles (arithmetic-coded JPEG,
-JPEG-compressed TIFF, ASCII PNM, ...) fail that way too — there is no CPU fallback behind it.
+JPEG-compressed TIFF, plain PBM, 16-bit PNM, ...) fail that way too — there is no CPU fallback behind it.
 """
 from __future__ import annotations
 
