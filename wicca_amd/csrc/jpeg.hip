@@ -974,8 +974,11 @@ __global__ __launch_bounds__(256) void jpeg_sync_mark_kernel(JpegPlan P, const S
 }
 
 constexpr int kTailWords = 256;  // stream words staged per wave (8192 bits; restaged as the decode moves on)
+#ifndef WICCA_JPEG_TAIL_J8
+#define WICCA_JPEG_TAIL_J8 1  // AC runs of up to 8 codewords (0: up to 4)
+#endif
 #ifndef WICCA_JPEG_TAIL_GRID
-#define WICCA_JPEG_TAIL_GRID 1024  // waves of jpeg_sync_tail_kernel (a multiple of kTailRegions; 8192 slowed the plan pipeline, profiles/r06t_*)
+#define WICCA_JPEG_TAIL_GRID 4096  // waves of jpeg_sync_tail_kernel (a multiple of kTailRegions): round 2 670 / 420 / 275 us at 1024 / 2048 / 4096, the plan loop alike at 1024 and 4096 (profiles/r06zb_*)
 #endif
 static_assert(WICCA_JPEG_TAIL_GRID % kTailRegions == 0, "whole waves per region");
 int tail_grid()  // WICCA_JPEG_TAIL_GRID (runtime): waves of the tail kernel, rounded to whole regions
@@ -1052,7 +1055,8 @@ __global__ __launch_bounds__(64) void jpeg_sync_tail_kernel(JpegPlan P, const Su
         int32_t w0 = INT32_MIN / 2;  // lookup window's first bit; its look for this lane
         uint32_t look = 0;
         int32_t tag_dc = -1, tag_ac = -1;  // the tables the window's DC / AC entries are for
-        uint32_t res_dc = 0, jump1 = 0, jump2 = 0, jump4 = 0;
+        uint32_t res_dc = 0, jump1 = 0, jump2 = 0, jump4 = 0, jump8 = 0;
+        (void)jump8;
         int32_t slot = st.slot, k = st.k;
         const uint8_t* slot_tabs = reinterpret_cast<const uint8_t*>(im.tab);
         uint32_t sti = (uint32_t)__builtin_amdgcn_readfirstlane((int)slot_tabs[slot]);
@@ -1141,12 +1145,21 @@ __global__ __launch_bounds__(64) void jpeg_sync_tail_kernel(JpegPlan P, const Su
                     jump1 = j1;
                     jump2 = tail_jump(j1, lane);
                     jump4 = tail_jump(jump2, lane);
+#if WICCA_JPEG_TAIL_J8
+                    jump8 = tail_jump(jump4, lane);
+#endif
                 }
                 // the longest run from here that stays inside the block (every
                 // coefficient index before its last codeword < 64) and inside
                 // the lane's range (it ends by `stop`: no codeword of it starts
                 // past the range; a single codeword is always this lane's)
+#if WICCA_JPEG_TAIL_J8
+                uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)jump8, o);
+                if ((int32_t)((x >> 8) & 255u) + k >= 64 || p + (int32_t)(x & 255u) > stop)
+                    x = (uint32_t)__builtin_amdgcn_readlane((int)jump4, o);
+#else
                 uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)jump4, o);
+#endif
                 if ((int32_t)((x >> 8) & 255u) + k >= 64 || p + (int32_t)(x & 255u) > stop) {
                     x = (uint32_t)__builtin_amdgcn_readlane((int)jump2, o);
                     if ((int32_t)((x >> 8) & 255u) + k >= 64 || p + (int32_t)(x & 255u) > stop)
