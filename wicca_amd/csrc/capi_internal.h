@@ -288,6 +288,8 @@ int image_file_probe(const uint8_t* data, int64_t size, int64_t i, int64_t* H, i
 int image_files_screen(const uint8_t* const* data, const int64_t* sizes, int64_t n, int* status,
                        std::vector<int64_t>* good);
 bool timing_on();      // WICCA_JPEG_TIMING set: per-call phase timings on stderr
+bool issue_timing_on();  // WICCA_ISSUE_TIMING set: host phase times of each asynchronous plan issue on stderr
+extern thread_local double t_issue_destuff, t_issue_tables, t_issue_kernels;  // the last async JPEG issue's phases (ms)
 double timing_now_ms();
 int image_files_decode(Workspace* ws, const uint8_t* const* data, const int64_t* sizes, int64_t n,
                        uint8_t* const* dst, const int64_t* dpitch, hipStream_t stream, int* late);

@@ -355,6 +355,9 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     }
     if (upload_err) return fail(WICCA_ERR_HIP, "JPEG stream upload failed");
     const double t_destuffed = now_ms();
+    if (async_rounds > 0 && issue_timing_on()) {
+        t_issue_destuff = t_destuffed - t_start;
+    }
     int64_t total_bits = 0;
     for (int64_t i = 0; i < n; ++i) total_bits += seg_off[(size_t)i].back() * 8;
     const int64_t S = jpeg_sub_bits(total_bits);
@@ -563,6 +566,10 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     HIP_TRY(wicca::jpeg_decode_device(P, ims.data(), ws->jscratch.ptr, n, &rounds, stream, async_rounds,
                                       async_flags, ws->jtab.ptr + jobs_off));
     if (rounds_out) *rounds_out = rounds;
+    if (async_rounds > 0 && issue_timing_on()) {
+        t_issue_tables = t_upload - t_destuffed;
+        t_issue_kernels = now_ms() - t_upload;
+    }
     for (int64_t i = 0; i < n; ++i)
         if (tmp_off[(size_t)i] >= 0)
             HIP_TRY(wicca::launch_orient(ims[(size_t)i].dst, ims[(size_t)i].dst_pitch, info[(size_t)i].W,
@@ -1513,6 +1520,12 @@ int image_files_decode(Workspace* ws, const uint8_t* const* data, const int64_t*
 }
 
 bool timing_on() { return jpeg_timing(); }
+bool issue_timing_on()
+{
+    static const bool on = getenv("WICCA_ISSUE_TIMING") != nullptr;
+    return on;
+}
+thread_local double t_issue_destuff = 0, t_issue_tables = 0, t_issue_kernels = 0;
 double timing_now_ms() { return now_ms(); }
 
 int image_file_is_jpeg(const uint8_t* data, int64_t size, int64_t i, bool* jpeg)

@@ -140,6 +140,7 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
                uint8_t* const* icons, int device, int* late_status, PlanCall* as = nullptr)
 {
     const int S = (int)shapes.size();
+    const double t_issue0 = timing_now_ms();
     // distinct depths: each is computed once, repeated entries are copied out
     std::vector<int> ud;
     std::vector<int> slot_of((size_t)n_depths);
@@ -202,11 +203,13 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
     } leave;
     const bool timing = timing_on() && !as;
     const double t0 = timing_now_ms();
+    const bool itiming = as && issue_timing_on();
     if (as)
         rc = jpeg_files_decode_async(ws, data, sizes, n, img.data(), pitch.data(), cs, &as->flags, &as->damage);
     else
         rc = image_files_decode(ws, data, sizes, n, img.data(), pitch.data(), cs, late_status ? late.data() : nullptr);
     if (rc) return rc;
+    const double t_after_decode = timing_now_ms();
     // the pinned staging and descriptors, and the copies into the caller's
     // arrays, are in use until both streams are done: an error return waits
     struct Drain {
@@ -664,6 +667,12 @@ int plan_batch(const uint8_t* const* data, const int64_t* sizes, int64_t n, cons
         as->stream = cs;
         as->copy_stream = ws->copy_stream;
         drain.active = false;
+        if (itiming) {
+            fprintf(stderr, "[wicca plan issue] %lld files: probe+lease %.2f, parse+destuff+uploads %.2f, tables %.2f, "
+                    "decode launches %.2f, plan launches + copies %.2f, total %.2f ms\n", (long long)n, t0 - t_issue0,
+                    t_issue_destuff, t_issue_tables, t_issue_kernels, timing_now_ms() - t_after_decode,
+                    timing_now_ms() - t_issue0);
+        }
         return WICCA_OK;
     }
     HIP_TRY(hipStreamSynchronize(ws->copy_stream));

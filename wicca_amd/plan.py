@@ -68,7 +68,8 @@ def _read(paths: Sequence, pooled: bool = False) -> list:
     return read_files(paths, pooled=pooled)
 
 
-def _matrix_args(file_paths, shapes, depths, interpolation, border_type, border_constant, device, pooled=False):
+def _matrix_args(file_paths, shapes, depths, interpolation, border_type, border_constant, device, pooled=False,
+                 after_read=None):
     from .coder import _border_value
     shp = []
     for s in shapes:
@@ -81,6 +82,8 @@ def _matrix_args(file_paths, shapes, depths, interpolation, border_type, border_
     if not dep:
         raise ValueError("need at least one depth")
     blobs = _read(file_paths, pooled)
+    if after_read is not None:
+        after_read()
     n = len(blobs)
     keep = [np.frombuffer(b, np.uint8) for b in blobs]
     # pinned host outputs: the device-to-host copies run by DMA, not as blit
@@ -134,18 +137,26 @@ class MatrixCall:
 
 def get_img_matrix_async(file_paths: Sequence, shapes: Iterable, depths, interpolation: int = 3,
                          border_type: int = 1, border_constant: int = 0,
-                         device: int | None = None) -> MatrixCall:
+                         device: int | None = None, _after_read=None, _issue_gate=None) -> MatrixCall:
     """:func:`get_img_matrix` (errors "raise") without waiting for the device:
     the batch's host work, decode, plan kernels and output copies are queued
     (``wicca_image_stage_plan_async``) and its kernels run after the previous
     asynchronous call's, so a loop that issues batch k+1 before waiting for
-    batch k overlaps k+1's host work and k's output copies with the kernels."""
+    batch k overlaps k+1's host work and k's output copies with the kernels.
+    (StagePlan's hooks: ``_after_read()`` once the files are read,
+    ``_issue_gate`` = (enter, leave) around the native issue.)"""
     blobs, keep, args, out = _matrix_args(file_paths, shapes, depths, interpolation, border_type,
-                                          border_constant, device, pooled=True)
+                                          border_constant, device, pooled=True, after_read=_after_read)
     if args[2] == 0:
         return MatrixCall(None, None, out)
     ticket = ctypes.c_int64(0)
-    _lib.check(_lib.load().wicca_image_stage_plan_async(*args, ctypes.byref(ticket)))
+    if _issue_gate is not None:
+        _issue_gate[0]()
+    try:
+        _lib.check(_lib.load().wicca_image_stage_plan_async(*args, ctypes.byref(ticket)))
+    finally:
+        if _issue_gate is not None:
+            _issue_gate[1]()
     return MatrixCall(ticket.value, (blobs, keep, args), out)
 
 
@@ -258,6 +269,13 @@ class StagePlan:
         self._retired = set()  # batches every expected request was served from (never prefetched again)
         self._matrix = get_img_matrix  # the native call (tests inject a stand-in)
         self.stats = collections.Counter()
+        # native issues in the order the computations started (tickets): the
+        # next batch starts (and reads its files) once this batch's files are
+        # read, so its read overlaps this batch's native issue, and issues
+        # after it
+        self._gate = threading.Condition()
+        self._ticket_next = 0
+        self._ticket_turn = 0
 
     @staticmethod
     def _key(paths) -> tuple:
@@ -277,19 +295,45 @@ class StagePlan:
         return self.devices[idx % len(self.devices)]
 
     def _compute(self, key, entry: _Entry, device, issued=None) -> None:
-        """Compute `entry`; `issued()` runs once the batch's native work is
-        queued (its host parse, de-stuffing and uploads done): the owner starts
-        the next batch's prefetch there, so the two batches' host work does
-        not compete and this batch's kernels go first."""
+        """Compute `entry`; `issued()` runs once the batch's files are read
+        (the asynchronous native path) or its native work is queued: the
+        owner starts the next batch's prefetch there.  The native issues go
+        in ticket order (a batch's kernels before the next one's), so the
+        next batch's file reads overlap this batch's parse, de-stuffing and
+        uploads, not its kernels' order."""
         paths, depth = key
         depths = self.depths if depth is None else (depth,)
+        native = self._matrix is get_img_matrix and self.errors == "raise"
+        if native:
+            with self._gate:
+                my = self._ticket_next
+                self._ticket_next += 1
+        gate = {"entered": False, "left": not native}
+
+        def enter():
+            with self._gate:
+                while self._ticket_turn != my:
+                    self._gate.wait()
+            gate["entered"] = True
+
+        def leave():
+            if not gate["left"]:
+                gate["left"] = True
+                with self._gate:
+                    self._ticket_turn += 1
+                    self._gate.notify_all()
+
+        def after_read():
+            nonlocal issued
+            if issued is not None:
+                cb, issued = issued, None
+                cb()
         try:
-            if self._matrix is get_img_matrix and self.errors == "raise":
+            if native:
                 call = get_img_matrix_async(list(paths), self.shapes, depths, self.interpolation, self.border_type,
-                                            self.border_constant, device)
-                if issued is not None:
-                    issued()
-                    issued = None
+                                            self.border_constant, device, _after_read=after_read,
+                                            _issue_gate=(enter, leave))
+                after_read()  # (no files: nothing was read)
                 entry.result = call.wait()
             else:
                 if issued is not None:
@@ -306,6 +350,10 @@ class StagePlan:
         except BaseException as e:  # the requesters waiting now see the failure ...
             entry.error = e
         finally:
+            if not gate["left"]:  # this ticket's turn passes even when it never issued
+                if not gate["entered"]:
+                    enter()
+                leave()
             if issued is not None:  # the issue failed: the prefetch still starts
                 try:
                     issued()
