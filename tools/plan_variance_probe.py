@@ -65,17 +65,19 @@ def main():
     def timed_async(*a, **kw):
         t1 = time.perf_counter()
         call = orig_async(*a, **kw)
-        t2 = time.perf_counter()
-        inner = call.wait
-
-        def wait():
-            r = inner()
-            with lock:
-                log.append((t1, t2, time.perf_counter(), threading.get_ident()))
-            return r
-        call.wait = wait
+        call._probe_t = (t1, time.perf_counter())  # plain attributes: no reference cycle keeps the outputs alive
         return call
+    orig_wait = P.MatrixCall.wait
+
+    def timed_wait(self):
+        r = orig_wait(self)
+        t = getattr(self, "_probe_t", None)
+        if t is not None:
+            with lock:
+                log.append((t[0], t[1], time.perf_counter(), threading.get_ident()))
+        return r
     P.get_img_matrix_async = timed_async
+    P.MatrixCall.wait = timed_wait
     reads = []
     orig_read = P._read
 
@@ -128,6 +130,7 @@ def main():
                   f"done gaps ms {' '.join(f'{1e3 * (y - x):.1f}' for x, y in zip(done, done[1:]))}", flush=True)
     finally:
         P.get_img_matrix_async = orig_async
+        P.MatrixCall.wait = orig_wait
         P._read = orig_read
         shutil.rmtree(tmp, ignore_errors=True)
 

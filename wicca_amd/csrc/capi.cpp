@@ -690,7 +690,12 @@ int wicca_host_alloc(int64_t bytes, void** out)
         g_host_live_bytes += n;  // reserved while the allocation runs unlocked
     }
     void* p = nullptr;
-    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess || !p) {
+    const double t_alloc = issue_timing_on() ? timing_now_ms() : 0.0;
+    const hipError_t he = hipHostMalloc(&p, n, hipHostMallocDefault);
+    if (issue_timing_on())
+        fprintf(stderr, "[wicca host_alloc] pool miss: hipHostMalloc of %zu bytes took %.2f ms\n", n,
+                timing_now_ms() - t_alloc);
+    if (he != hipSuccess || !p) {
         std::lock_guard<std::mutex> g(g_host_mu);
         g_host_live_bytes -= n;
         return fail(WICCA_ERR_NOMEM, "hipHostMalloc of %zu bytes failed", n);

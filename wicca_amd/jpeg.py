@@ -122,11 +122,12 @@ def _map_one(p: str) -> np.ndarray:
     return np.frombuffer(mm, np.uint8)
 
 
-def read_files(paths: Sequence[str], pooled: bool = False) -> list:
+def read_files(paths: Sequence[str], pooled: bool = False, mapped: bool = False) -> list:
     """Each file's bytes as a uint8 array, read into memory of its own by a
     pool of threads (serial f.read() of 25 x 10 MB files took longer than the
-    whole GPU stage of the batch).  WICCA_READ_MMAP=1 maps the files instead
-    (no copy), at a price: a file truncated or rewritten while it is mapped
+    whole GPU stage of the batch).  mapped=True (the stage plan's default) or
+    WICCA_READ_MMAP=1 maps the files instead (no copy; WICCA_READ_MMAP=0 forces
+    copies), at a price: a file truncated or rewritten while it is mapped
     raises SIGBUS when the decoder touches the missing pages, where a copy
     (and cv2.imread) sees a short file."""
     import os
@@ -135,7 +136,9 @@ def read_files(paths: Sequence[str], pooled: bool = False) -> list:
             raise ValueError("File path cannot be empty")
     if not paths:
         raise ValueError("need at least one array to stack")
-    one = _map_one if os.environ.get("WICCA_READ_MMAP") == "1" else _read_pooled if pooled else _read_one
+    env = os.environ.get("WICCA_READ_MMAP")
+    mapped = env == "1" or (mapped and env != "0")
+    one = _map_one if mapped else _read_pooled if pooled else _read_one
     if len(paths) == 1:
         return [one(paths[0])]
     return list(_read_pool().map(one, paths))

@@ -63,13 +63,13 @@ def _norm_depths(depths) -> tuple[int, ...]:
     return (_depth_index(depths),)
 
 
-def _read(paths: Sequence, pooled: bool = False) -> list:
+def _read(paths: Sequence, pooled: bool = False, mapped: bool = False) -> list:
     from .jpeg import read_files
-    return read_files(paths, pooled=pooled)
+    return read_files(paths, pooled=pooled, mapped=mapped)
 
 
 def _matrix_args(file_paths, shapes, depths, interpolation, border_type, border_constant, device, pooled=False,
-                 after_read=None):
+                 after_read=None, mapped=False):
     from .coder import _border_value
     shp = []
     for s in shapes:
@@ -81,7 +81,7 @@ def _matrix_args(file_paths, shapes, depths, interpolation, border_type, border_
     dep = _norm_depths(depths)
     if not dep:
         raise ValueError("need at least one depth")
-    blobs = _read(file_paths, pooled)
+    blobs = _read(file_paths, pooled, mapped)
     if after_read is not None:
         after_read()
     n = len(blobs)
@@ -137,26 +137,47 @@ class MatrixCall:
 
 def get_img_matrix_async(file_paths: Sequence, shapes: Iterable, depths, interpolation: int = 3,
                          border_type: int = 1, border_constant: int = 0,
-                         device: int | None = None, _after_read=None, _issue_gate=None) -> MatrixCall:
+                         device: int | None = None, _after_read=None, _issue_gate=None,
+                         _mapped: bool = False) -> MatrixCall:
     """:func:`get_img_matrix` (errors "raise") without waiting for the device:
     the batch's host work, decode, plan kernels and output copies are queued
     (``wicca_image_stage_plan_async``) and its kernels run after the previous
     asynchronous call's, so a loop that issues batch k+1 before waiting for
     batch k overlaps k+1's host work and k's output copies with the kernels.
     (StagePlan's hooks: ``_after_read()`` once the files are read,
-    ``_issue_gate`` = (enter, leave) around the native issue.)"""
+    ``_issue_gate`` = (enter, leave) around the native issue, ``_mapped``:
+    the files memory-mapped instead of copied.)"""
+    import os
+    import time
+    timing = os.environ.get("WICCA_ISSUE_TIMING") is not None
+    marks = [time.perf_counter()]
+
+    def after_read():
+        marks.append(time.perf_counter())
+        if _after_read is not None:
+            _after_read()
     blobs, keep, args, out = _matrix_args(file_paths, shapes, depths, interpolation, border_type,
-                                          border_constant, device, pooled=True, after_read=_after_read)
+                                          border_constant, device, pooled=True, after_read=after_read,
+                                          mapped=_mapped)
     if args[2] == 0:
         return MatrixCall(None, None, out)
     ticket = ctypes.c_int64(0)
+    marks.append(time.perf_counter())
     if _issue_gate is not None:
         _issue_gate[0]()
+    marks.append(time.perf_counter())
     try:
         _lib.check(_lib.load().wicca_image_stage_plan_async(*args, ctypes.byref(ticket)))
     finally:
         if _issue_gate is not None:
             _issue_gate[1]()
+    if timing:  # WICCA_ISSUE_TIMING: the Python side of the issue (the native side prints its own phases)
+        marks.append(time.perf_counter())
+        d = [1e3 * (b - a) for a, b in zip(marks, marks[1:])]
+        if len(d) == 4:
+            import sys
+            print(f"[wicca plan py] read {d[0]:.2f}, outputs + args {d[1]:.2f}, gate wait {d[2]:.2f}, "
+                  f"native call {d[3]:.2f} ms", file=sys.stderr, flush=True)
     return MatrixCall(ticket.value, (blobs, keep, args), out)
 
 
@@ -224,6 +245,15 @@ class StagePlan:
         per depth instead -- every shape of that depth from one decode, the
         14x saving across classifiers kept -- and the working set is a few
         batches of one depth;
+    mapped_files: True (default) memory-maps the batch's files instead of
+        copying them out of the page cache: 25 x 10 MB copies took 4-17 ms
+        per batch on the host, and with them the loop's issue chain (read +
+        parse / de-stuffing / uploads ~7 ms) outran the device's ~11 ms per
+        batch now and then -- steady 12.5-16 ms per batch, against 12.1-12.6
+        mapped (profiles/r06ze_*, r06zf_*).  A file truncated or rewritten while
+        its batch is being decoded then raises SIGBUS (a copy, like
+        cv2.imread, would see a short file): pass False for folders that may
+        change during the run (WICCA_READ_MMAP=0 forces copies everywhere);
     copy: True (default) hands each request its own writable arrays, as the
         reference's ``np.stack`` does; False hands every classifier the one
         cached pair, READ-ONLY (a classifier writing into its batch raises
@@ -237,7 +267,7 @@ class StagePlan:
     def __init__(self, shapes: Iterable, depths, interpolation: int = 3, border_type: int = 1,
                  border_constant: int = 0, *, batches: Sequence[Sequence] | None = None,
                  device: int | None = None, devices: Sequence[int] | None = None, errors: str = "raise",
-                 cache_bytes: int | None = None, copy: bool = True, ahead: int = 2):
+                 cache_bytes: int | None = None, copy: bool = True, ahead: int = 2, mapped_files: bool = True):
         self.expected = collections.Counter(_norm_shape(s) for s in shapes)
         if not self.expected:
             raise ValueError("need at least one shape")
@@ -251,6 +281,7 @@ class StagePlan:
         self.errors = errors
         self.cache_bytes = int(cache_bytes) if cache_bytes is not None else _default_cache_bytes()
         self.copy = copy
+        self.mapped_files = bool(mapped_files)
         self.ahead = max(0, int(ahead))
         self._order = {}
         self._batches = [list(b) for b in batches] if batches is not None else None
@@ -332,7 +363,7 @@ class StagePlan:
             if native:
                 call = get_img_matrix_async(list(paths), self.shapes, depths, self.interpolation, self.border_type,
                                             self.border_constant, device, _after_read=after_read,
-                                            _issue_gate=(enter, leave))
+                                            _issue_gate=(enter, leave), _mapped=self.mapped_files)
                 after_read()  # (no files: nothing was read)
                 entry.result = call.wait()
             else:
