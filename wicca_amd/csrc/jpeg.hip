@@ -1503,10 +1503,59 @@ constexpr int kTrPitch = 9, kTrBlock = 8 * kTrPitch;
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
+#ifndef WICCA_IDCT_LEAN
+#define WICCA_IDCT_LEAN 1  // 0: the ac_zero select on every value and live-guarded transposes (the round-5 form)
+#endif
+
 __device__ __forceinline__ void idct8_lane_v(uint4 v, const uint16_t* qt, int r, bool live, int32_t* t,
                                              uint8_t (&px)[8])
 {
     auto at = [&](int i, int j) { return i * kTrPitch + j; };
+#if WICCA_IDCT_LEAN
+    // Lanes of blocks past the image (live false) run the transposes on
+    // their own block's LDS area like the others (no branches around the LDS
+    // accesses); their results are never stored.
+    {  // dequantised row r: the low 16 bits of each product, two per v_pk_mul_lo_u16
+        const uint4 qv = *reinterpret_cast<const uint4*>(qt + r * 8);
+        const uint32_t cw[4] = {v.x, v.y, v.z, v.w}, qw[4] = {qv.x, qv.y, qv.z, qv.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t pr = __builtin_bit_cast(uint32_t, __builtin_bit_cast(ushort2_t, cw[k]) *
+                                                                 __builtin_bit_cast(ushort2_t, qw[k]));
+            t[at(r, 2 * k)] = sext16((int32_t)pr);
+            t[at(r, 2 * k + 1)] = (int32_t)pr >> 16;
+        }
+    }
+    wave_lds_sync();
+    int32_t in[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) in[k] = t[at(k, r)];  // pass 1: column r
+    int32_t p1[8];
+    {
+        uint32_t o[8];
+        islow_simd(in, 1u << (kConstBits - kPass1Bits - 1), o);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) p1[k] = min(max((int32_t)o[k] >> (kConstBits - kPass1Bits), -32768), 32767);
+        // pass 1's shortcut (a block whose coefficient rows 1..7 are all zero
+        // takes the 16-bit in0 << PASS1_BITS for every row) differs from the
+        // saturated butterfly -- which is in0 * 4 there -- only where in0 * 4
+        // leaves int16: the vote runs only when some lane's in0 does
+        if (__ballot((uint32_t)(in[0] + 8192) >= 16384u)) {
+            const bool nz = r != 0 && (v.x | v.y | v.z | v.w) != 0;
+            const uint64_t vote = __ballot(nz);
+            if (((vote >> (threadIdx.x & 56)) & 0xFFu) == 0) {
+                const int32_t dc = sext16(in[0] << kPass1Bits);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) p1[k] = dc;
+            }
+        }
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[at(k, r)] = p1[k];
+    wave_lds_sync();
+    if (!live) return;
+#else
     // pass 1's shortcut: the block's coefficient rows 1..7 all zero (lane r
     // holds row r; a wave holds 8 blocks, 8 lanes each)
     const bool nz = r != 0 && (v.x | v.y | v.z | v.w) != 0;
@@ -1543,6 +1592,7 @@ __device__ __forceinline__ void idct8_lane_v(uint4 v, const uint16_t* qt, int r,
     }
     wave_lds_sync();
     if (!live) return;
+#endif
 #pragma unroll
     for (int k = 0; k < 8; ++k) in[k] = t[at(r, k)];  // pass 2: row r
     constexpr int sh = kConstBits + kPass1Bits + 3;
