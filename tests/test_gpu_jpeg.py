@@ -760,3 +760,26 @@ def test_cmyk_file_caller_stage(tmp_path):
         assert np.array_equal(imgs[i], R.resize(rgb, (224, 224), R.INTER_AREA)), p
         icon = c_oracle.ll_int_block(rgb, 3, 1, 0)[0]
         assert np.array_equal(icons[i], R.resize(icon, (224, 224), R.INTER_AREA)), p
+
+
+@pytest.mark.gpu
+def test_truncated_mapping_in_plan_batch(tmp_path):
+    """StagePlan maps its files: a file truncated under the mapping between
+    the header parse and the de-stuffing makes the batch fail with an error
+    (the library's SIGBUS guard), and the process goes on."""
+    from oracle import jpeg_pil as J
+    from wicca_amd import plan as P
+    data = J.encode(J.test_image("scene", 720, 1280, 5), 90)
+    paths = []
+    for i in range(3):
+        p = tmp_path / f"{i}.jpg"
+        p.write_bytes(data)
+        paths.append(str(p))
+    blobs = P._read(paths, mapped=True)
+    os.truncate(paths[1], 1024)  # the header stays, the scan's pages go
+    keep = [np.frombuffer(b, np.uint8) for b in blobs]
+    with pytest.raises(Exception, match="truncated"):
+        WJ.decode_batch(keep)
+    del keep, blobs
+    got = P.get_img_matrix([paths[0], paths[2]], [(224, 224)], [3])
+    assert got[((224, 224), 3)][0].shape == (2, 224, 224, 3)

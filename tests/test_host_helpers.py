@@ -2,6 +2,7 @@
 the kernel-name report bench.py uses for its roofline line, and the
 workspace-pool controls."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -111,3 +112,37 @@ def test_read_buffer_pool_recycles(tmp_path):
     assert any(again[0].base is b for b in bases)
     plain = jpeg.read_files(paths[:1])
     assert plain[0].base is None or plain[0].base.nbytes == len(data[0])
+
+
+def _jpeg_with_big_header():
+    """A small JPEG with a 20 KB comment segment after SOI: its markers span
+    several pages, so a mapping of it truncated to a few bytes faults."""
+    from oracle import jpeg_pil as J
+    data = J.encode(J.test_image("scene", 64, 96, 1), 90)
+    com = b"\xff\xfe" + (20002).to_bytes(2, "big") + bytes(20000)
+    return data[:2] + com + data[2:]
+
+
+def test_truncated_mapping_fails_cleanly(tmp_path):
+    """A file truncated while it is memory-mapped (StagePlan maps its files):
+    the header parse touches a page past the new end -- SIGBUS, which the
+    library's guard turns into an ordinary error instead of killing the
+    process."""
+    import mmap
+
+    import numpy as np
+
+    from wicca_amd import jpeg
+    data = _jpeg_with_big_header()
+    p = tmp_path / "t.jpg"
+    p.write_bytes(data)
+    h, w, c, _ = jpeg.info(data)
+    assert (h, w) == (64, 96)
+    with open(p, "rb") as f:
+        mm = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+    arr = np.frombuffer(mm, np.uint8)
+    os.truncate(p, 16)
+    with pytest.raises(Exception, match="was truncated while it was read"):
+        jpeg.info(arr)
+    del arr
+    mm.close()

@@ -29,6 +29,9 @@
 #include <thread>
 #include <vector>
 
+#include <csetjmp>
+#include <csignal>
+
 #include "capi_internal.h"
 
 namespace wicca_capi {
@@ -1174,3 +1177,54 @@ int wicca_synth_band_u8(uint8_t* dst, int64_t rows, int64_t W, int64_t C, int64_
 }
 
 }  // extern "C"
+
+namespace wicca_capi {
+namespace {
+thread_local sigjmp_buf* t_bus_jmp = nullptr;
+struct sigaction g_prev_bus;
+std::once_flag g_bus_once;
+
+void bus_handler(int sig, siginfo_t* si, void* uc)
+{
+    if (t_bus_jmp) siglongjmp(*t_bus_jmp, 1);  // a guarded read of a truncated mapping
+    if (g_prev_bus.sa_flags & SA_SIGINFO) {
+        if (g_prev_bus.sa_sigaction) {
+            g_prev_bus.sa_sigaction(sig, si, uc);
+            return;
+        }
+    } else if (g_prev_bus.sa_handler != SIG_DFL && g_prev_bus.sa_handler != SIG_IGN) {
+        g_prev_bus.sa_handler(sig);
+        return;
+    }
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+}  // namespace
+
+bool bus_guarded(const std::function<void()>& fn)
+{
+    std::call_once(g_bus_once, [] {
+        struct sigaction sa;
+        memset(&sa, 0, sizeof(sa));
+        sa.sa_sigaction = bus_handler;
+        sa.sa_flags = SA_SIGINFO;
+        sigemptyset(&sa.sa_mask);
+        sigaction(SIGBUS, &sa, &g_prev_bus);
+    });
+    sigjmp_buf jb;
+    sigjmp_buf* const outer = t_bus_jmp;
+    if (sigsetjmp(jb, 1) != 0) {  // (the signal mask is restored with the jump)
+        t_bus_jmp = outer;
+        return false;
+    }
+    t_bus_jmp = &jb;
+    try {
+        fn();
+    } catch (...) {
+        t_bus_jmp = outer;
+        throw;
+    }
+    t_bus_jmp = outer;
+    return true;
+}
+}  // namespace wicca_capi

@@ -287,6 +287,14 @@ int raster_decode_to_device(Workspace* ws, const uint8_t* const* data, const int
 int image_file_probe(const uint8_t* data, int64_t size, int64_t i, int64_t* H, int64_t* W);
 int image_files_screen(const uint8_t* const* data, const int64_t* sizes, int64_t n, int* status,
                        std::vector<int64_t>* good);
+// Host reads of caller file bytes, which may be memory-mapped (StagePlan maps
+// a batch's files): a file truncated under its mapping raises SIGBUS when a
+// page past its new end is touched.  bus_guarded runs fn with a SIGBUS
+// handler armed for this thread and returns false if fn touched such a page
+// (the caller then fails the file or the call, as for a short file); other
+// SIGBUS signals go to the handler that was installed before.  fn must not
+// hold locks or leave objects half-built across the byte reads it guards.
+bool bus_guarded(const std::function<void()>& fn);
 bool timing_on();      // WICCA_JPEG_TIMING set: per-call phase timings on stderr
 bool issue_timing_on();  // WICCA_ISSUE_TIMING set: host phase times of each asynchronous plan issue on stderr
 extern thread_local double t_issue_destuff, t_issue_tables, t_issue_kernels;  // the last async JPEG issue's phases (ms)

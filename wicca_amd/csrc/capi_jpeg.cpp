@@ -52,7 +52,9 @@ int parse_one(const uint8_t* data, int64_t size, wicca::JpegInfo* info, int64_t 
 {
     if (!data || size <= 0) return fail(WICCA_ERR_NULL_IMAGE, "Image didn't found. Please check your input.");
     std::string err;
-    const int rc = wicca::jpeg_parse(data, (size_t)size, info, &err);
+    int rc = -1;
+    if (!bus_guarded([&] { rc = wicca::jpeg_parse(data, (size_t)size, info, &err); }))
+        return fail(WICCA_ERR_DECODE, "image %lld: the file was truncated while it was read", (long long)i);
     if (rc == -2) return fail(WICCA_ERR_UNSUPPORTED, "image %lld: %s", (long long)i, err.c_str());
     if (rc) return fail(WICCA_ERR_DECODE, "image %lld: %s", (long long)i, err.c_str());
     if (info->H > 65535 || info->W > 65535) return fail(WICCA_ERR_UNSUPPORTED, "image %lld too large", (long long)i);
@@ -68,11 +70,19 @@ int probe_file(const uint8_t* data, int64_t size, int64_t i, bool any, bool orie
                int* kind = nullptr)
 {
     if (any && data && size > 0) {
-        const int rk = wicca::raster_kind(data, (size_t)size);
+        int rk = wicca::RK_NONE;
+        bool jpeg_magic = false;
+        if (!bus_guarded([&] {
+                rk = wicca::raster_kind(data, (size_t)size);
+                jpeg_magic = size >= 2 && data[0] == 0xFF && data[1] == 0xD8;
+            }))
+            return fail(WICCA_ERR_DECODE, "image %lld: the file was truncated while it was read", (long long)i);
         if (rk != wicca::RK_NONE) {
             wicca::RasterInfo r;
             std::string err;
-            const int rc = wicca::raster_parse(data, (size_t)size, &r, &err);
+            int rc = -1;
+            if (!bus_guarded([&] { rc = wicca::raster_parse(data, (size_t)size, &r, &err); }))
+                return fail(WICCA_ERR_DECODE, "image %lld: the file was truncated while it was read", (long long)i);
             if (rc == -2) return fail(WICCA_ERR_UNSUPPORTED, "image %lld: %s", (long long)i, err.c_str());
             if (rc) return fail(WICCA_ERR_DECODE, "image %lld: %s", (long long)i, err.c_str());
             *H = r.H;
@@ -80,7 +90,7 @@ int probe_file(const uint8_t* data, int64_t size, int64_t i, bool any, bool orie
             if (kind) *kind = rk == wicca::RK_PNG ? 2 : rk == wicca::RK_BMP ? 3 : rk == wicca::RK_TIFF ? 4 : rk == wicca::RK_GIF ? 5 : 6;
             return WICCA_OK;
         }
-        if (size < 2 || data[0] != 0xFF || data[1] != 0xD8)
+        if (!jpeg_magic)
             return fail(WICCA_ERR_DECODE, "image %lld: unrecognised image format (JPEG, PNG, BMP, TIFF, GIF and PNM are decoded)",
                         (long long)i);
     }
@@ -317,12 +327,13 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
     std::vector<std::vector<int64_t>> seg_off((size_t)n);
     std::vector<char> rst_ok((size_t)n, 1);  // RSTn markers in sequence (else: a damaged file)
     std::atomic<int> upload_err{0};
+    std::atomic<int64_t> truncated{-1};  // a file whose (mapped) bytes vanished while it was read
     {
         const int nt = (int)std::min<int64_t>(n, 16);
         std::atomic<int64_t> next{0};
         auto work = [&] {
             for (int64_t i; (i = next.fetch_add(1)) < n;)
-            {
+            if (!bus_guarded([&] {
                 if (info[(size_t)i].host_scans) {
                     const wicca::JpegInfo& f = info[(size_t)i];
                     int16_t* hc = (int16_t*)ws->jhcoef.ptr + hoff[(size_t)i] * 64;
@@ -335,7 +346,7 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
                     if (hipMemcpyAsync((int16_t*)ws->jcoef.ptr + coef0[(size_t)i] * 64, hc, (size_t)blocks * 128,
                                        hipMemcpyHostToDevice, stream) != hipSuccess)
                         upload_err = 1;
-                    continue;
+                    return;
                 }
                 bool in_order = true;
                 const size_t got = wicca::jpeg_destuff_into(info[(size_t)i], stream_h + img_off[(size_t)i],
@@ -346,7 +357,8 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
                 if (hipMemcpyAsync(stream_d + a, stream_h + a, (size_t)len, hipMemcpyHostToDevice, stream) !=
                     hipSuccess)
                     upload_err = 1;
-            }
+            }))
+                truncated = i;
         };
         std::vector<std::thread> th;
         for (int t = 1; t < nt; ++t) th.emplace_back(work);
@@ -354,6 +366,8 @@ int jpeg_decode_to_device(Workspace* ws, const uint8_t* const* data, const int64
         for (auto& t : th) t.join();
     }
     if (upload_err) return fail(WICCA_ERR_HIP, "JPEG stream upload failed");
+    if (truncated >= 0)
+        return fail(WICCA_ERR_DECODE, "image %lld: the file was truncated while it was read", (long long)truncated.load());
     const double t_destuffed = now_ms();
     if (async_rounds > 0 && issue_timing_on()) {
         t_issue_destuff = t_destuffed - t_start;
@@ -1150,7 +1164,8 @@ int wicca_jpeg_host_coefficients(const uint8_t* data, int64_t size, int force_ho
     memset(out, 0, (size_t)b * 128);
     int64_t rel[wicca::kJpegMaxComp] = {0, 0, 0};
     for (int c = 1; c < f.ncomp; ++c) rel[c] = rel[c - 1] + (int64_t)f.comp[c - 1].bw * f.comp[c - 1].bh;
-    wicca::jpeg_host_decode(f, out, rel);
+    if (!bus_guarded([&] { wicca::jpeg_host_decode(f, out, rel); }))
+        return fail(WICCA_ERR_DECODE, "the file was truncated while it was read");
     return WICCA_OK;
 }
 

@@ -37,7 +37,11 @@ int raster_decode_to_device(Workspace* ws, const uint8_t* const* data, const int
     std::vector<int64_t> off((size_t)n + 1, 0);
     for (int64_t i = 0; i < n; ++i) {
         std::string err;
-        const int rc = wicca::raster_parse(data[i], (size_t)sizes[i], &info[(size_t)i], &err);
+        int rc = -1;
+        if (!bus_guarded([&] { rc = wicca::raster_parse(data[i], (size_t)sizes[i], &info[(size_t)i], &err); })) {
+            rc = -1;
+            err = "the file was truncated while it was read";
+        }
         if (rc == -2) return fail(WICCA_ERR_UNSUPPORTED, "image %lld: %s", (long long)i, err.c_str());
         if (rc) return fail(WICCA_ERR_DECODE, "image %lld: %s", (long long)i, err.c_str());
         wicca::raster_layout(info[(size_t)i], &lay[(size_t)i]);
@@ -75,8 +79,13 @@ int raster_decode_to_device(Workspace* ws, const uint8_t* const* data, const int
                 }
                 int urc;
                 try {  // no exception may leave a worker thread (host scratch: IDAT join, TIFF tiles)
-                    urc = wicca::raster_unpack(data[i], (size_t)sizes[i], info[(size_t)i], lay[(size_t)i], host + a,
-                                               &errs[(size_t)i]);
+                    if (!bus_guarded([&] {
+                            urc = wicca::raster_unpack(data[i], (size_t)sizes[i], info[(size_t)i], lay[(size_t)i],
+                                                       host + a, &errs[(size_t)i]);
+                        })) {
+                        urc = -1;
+                        errs[(size_t)i] = "the file was truncated while it was read";
+                    }
                 } catch (const std::exception&) {
                     errs[(size_t)i] = "out of host memory";
                     urc = -1;

@@ -250,10 +250,13 @@ class StagePlan:
         per batch on the host, and with them the loop's issue chain (read +
         parse / de-stuffing / uploads ~7 ms) outran the device's ~11 ms per
         batch now and then -- steady 12.5-16 ms per batch, against 12.1-12.6
-        mapped (profiles/r06ze_*, r06zf_*).  A file truncated or rewritten while
-        its batch is being decoded then raises SIGBUS (a copy, like
-        cv2.imread, would see a short file): pass False for folders that may
-        change during the run (WICCA_READ_MMAP=0 forces copies everywhere);
+        mapped (profiles/r06ze_*, r06zf_*).  A file truncated while its
+        batch is being decoded faults (SIGBUS) on the pages past its new end:
+        the library's reads of file bytes run under a SIGBUS guard, so the
+        batch then fails with an error, as a short file would fail its slot
+        under cv2.imread -- except uncompressed BMP / PNM rows, which the HIP
+        runtime copies straight from the mapping.  Pass False for folders that
+        may change during the run (WICCA_READ_MMAP=0 forces copies everywhere);
     copy: True (default) hands each request its own writable arrays, as the
         reference's ``np.stack`` does; False hands every classifier the one
         cached pair, READ-ONLY (a classifier writing into its batch raises
